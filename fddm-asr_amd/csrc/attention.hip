@@ -1,0 +1,466 @@
+// Flash-style multi-head attention for gfx950 (head_dim 64), forward + backward.
+//
+// Covers the three attention sites of the train step:
+//  * decoder self-attention  (models/denoise_decoder.py:129,164 -> nn.MultiheadAttention):
+//      key-padding mask (~x_mask), dropout p on the attention probabilities;
+//  * decoder cross-attention (models/denoise_decoder.py:130,169-174): no mask, dropout p;
+//  * WavLM gated relative-position attention (HF modeling_wavlm.py:152-200), forward only:
+//      score += gate[b,h,q] * table[h][key - q + Lk - 1]  (bucketed rel-pos bias gathered from a
+//      per-head table instead of the reference's materialised [B*H,S,S] bias).
+//
+// Structure ("swapped" products so a lane owns one query (fwd, dQ) or one key (dK/dV) end to end):
+//   S^T = K Q^T  (16x16 MFMA tiles, C layout: lane l holds rows 4*(l>>4)+j, column l&15)
+//   O^T = V^T P^T  — P^T is the lane's own softmax values (no LDS round trip); V^T fragments come
+//                    from a [key][d] LDS image through ds_read_b64_tr_b16 (hardware transpose).
+// Work split: 4 waves x 16 rows = 64 rows per workgroup; K/V (or Q/dO) tiles of 64 rows in LDS.
+// T = bf16 (mfma_f32_16x16x32_bf16) or f32 (mfma_f32_16x16x4f32, exact fp32 parity mode).
+#include "common.h"
+
+namespace fddm {
+namespace attn {
+
+constexpr int DH = 64;
+
+template <typename T> struct Cfg;
+template <> struct Cfg<bf16_t> { static constexpr int RB = 128, NSUB = 2, ECH = 8; };
+template <> struct Cfg<float> { static constexpr int RB = 256, NSUB = 4, ECH = 4; };
+
+__device__ __forceinline__ int kc_off(int RB, int r, int c) { return r * RB + ((c ^ ((r >> 1) & 7)) << 4); }
+__device__ __forceinline__ int hatt(int k) { return ((k >> 1) & 3) << 2; }
+
+template <typename T>
+__device__ __forceinline__ void mma(f32x4_t& c, const uint4& a, const uint4& b);
+template <> __device__ __forceinline__ void mma<bf16_t>(f32x4_t& c, const uint4& a, const uint4& b) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
+}
+template <> __device__ __forceinline__ void mma<float>(f32x4_t& c, const uint4& a, const uint4& b) {
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.x), __uint_as_float(b.x), c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.y), __uint_as_float(b.y), c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.z), __uint_as_float(b.z), c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.w), __uint_as_float(b.w), c, 0, 0, 0);
+}
+
+// Stage a 64-row x 64-col tile (rows row0.., `nvalid` valid) into LDS as a KC image (row reads)
+// and/or an MC image (transposed reads).
+template <typename T>
+__device__ __forceinline__ void stage(unsigned char* kc, unsigned char* mc, const T* base, long stride, int row0,
+                                      int nvalid) {
+  constexpr int RB = Cfg<T>::RB, ECH = Cfg<T>::ECH, CPR = RB / 16;
+  for (int idx = threadIdx.x; idx < 64 * CPR; idx += 256) {
+    const int r = idx / CPR, c = idx % CPR;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (r < nvalid) v = *(const uint4*)(base + (long)(row0 + r) * stride + c * ECH);
+    if (kc) *(uint4*)(kc + kc_off(RB, r, c)) = v;
+    if (mc) {
+      if constexpr (sizeof(T) == 2) *(uint4*)(mc + r * 128 + (((2 * c) ^ hatt(r)) << 3)) = v;
+      else *(uint4*)(mc + r * 256 + c * 16) = v;
+    }
+  }
+}
+
+// lane's register fragments of its own row (16-B chunk sub*4+g of row `row`) from global
+template <typename T>
+__device__ __forceinline__ void row_frags(uint4 (&f)[Cfg<T>::NSUB], const T* base, long stride, long row, bool valid,
+                                          int lane) {
+  const int g = lane >> 4;
+#pragma unroll
+  for (int s = 0; s < Cfg<T>::NSUB; ++s)
+    f[s] = valid ? *(const uint4*)(base + row * stride + (s * 4 + g) * Cfg<T>::ECH) : make_uint4(0, 0, 0, 0);
+}
+
+// acc[kb] = sum_sub  A(img rows kb*16..+15, KC) x B(lane fragment)
+template <typename T>
+__device__ __forceinline__ void rows_times_frag(f32x4_t (&acc)[4], const unsigned char* img, const uint4 (&f)[Cfg<T>::NSUB],
+                                                int lane) {
+  constexpr int RB = Cfg<T>::RB;
+  const int g = lane >> 4, i = lane & 15;
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb) {
+    acc[kb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < Cfg<T>::NSUB; ++s) {
+      const uint4 a = *(const uint4*)(img + kc_off(RB, kb * 16 + i, s * 4 + g));
+      mma<T>(acc[kb], a, f[s]);
+    }
+  }
+}
+
+__device__ __forceinline__ unsigned pk(float a, float b) { return (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16); }
+
+// out[db] += sum_rows  A(MC image transposed: [col d][row]) x B(lane-owned values v[kb][j] at row kb*16+4g+j)
+template <typename T>
+__device__ __forceinline__ void trans_times_vals(f32x4_t (&out)[4], const unsigned char* img, const float (&v)[4][4],
+                                                 int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  if constexpr (sizeof(T) == 2) {
+    const int q = i >> 2, p = i & 3;
+    typedef __attribute__((address_space(3))) s16x4_t* lp;
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) {
+      uint4 b;
+      b.x = pk(v[2 * ss][0], v[2 * ss][1]);
+      b.y = pk(v[2 * ss][2], v[2 * ss][3]);
+      b.z = pk(v[2 * ss + 1][0], v[2 * ss + 1][1]);
+      b.w = pk(v[2 * ss + 1][2], v[2 * ss + 1][3]);
+      const int k1 = 32 * ss + 4 * g + q, k2 = k1 + 16;
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        const int u = db * 4 + p;
+        const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(img + k1 * 128 + ((u ^ hatt(k1)) << 3)));
+        const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(img + k2 * 128 + ((u ^ hatt(k2)) << 3)));
+        uint4 a;
+        a.x = (unsigned)(unsigned short)lo[0] | ((unsigned)(unsigned short)lo[1] << 16);
+        a.y = (unsigned)(unsigned short)lo[2] | ((unsigned)(unsigned short)lo[3] << 16);
+        a.z = (unsigned)(unsigned short)hi[0] | ((unsigned)(unsigned short)hi[1] << 16);
+        a.w = (unsigned)(unsigned short)hi[2] | ((unsigned)(unsigned short)hi[3] << 16);
+        mma<bf16_t>(out[db], a, b);
+      }
+    }
+  } else {
+    const float* f = (const float*)img;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        uint4 a, b;
+        a.x = __float_as_uint(f[(kb * 16 + 4 * g + 0) * 64 + db * 16 + i]);
+        a.y = __float_as_uint(f[(kb * 16 + 4 * g + 1) * 64 + db * 16 + i]);
+        a.z = __float_as_uint(f[(kb * 16 + 4 * g + 2) * 64 + db * 16 + i]);
+        a.w = __float_as_uint(f[(kb * 16 + 4 * g + 3) * 64 + db * 16 + i]);
+        b = make_uint4(__float_as_uint(v[kb][0]), __float_as_uint(v[kb][1]), __float_as_uint(v[kb][2]),
+                       __float_as_uint(v[kb][3]));
+        mma<float>(out[db], a, b);
+      }
+    }
+  }
+}
+
+struct AttnArgs {
+  const void *Q, *K, *V, *O, *dO;
+  void *Out, *dQ, *dK, *dV;
+  float* lse;
+  float* delta;  // [B*H][Lq] workspace: rowsum(dO*O), written by dq_kernel
+  long sq, sk, sv, so, sdo, sdq, sdk, sdv;
+  const unsigned char* key_keep;  // [B][Lk] or null
+  const float* gate;              // [B*H][Lq] or null (WavLM)
+  const float* table;             // [H][2*Lk-1]
+  int B, H, Lq, Lk;
+  float scale;
+  uint64_t seed, stream;
+  unsigned thr16;
+  float drop_scale;
+};
+
+__device__ __forceinline__ bool key_ok(const AttnArgs& a, int b, int key) {
+  return key < a.Lk && (a.key_keep == nullptr || a.key_keep[(long)b * a.Lk + key]);
+}
+
+// ------------------------------------------------------------------------------------------- fwd
+template <typename T>
+__global__ void __launch_bounds__(256) fwd_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int RB = Cfg<T>::RB;
+  unsigned char* kimg = smem;
+  unsigned char* vimg = smem + 64 * RB;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, i = lane & 15;
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int q = blockIdx.x * 64 + w * 16 + i;
+  const bool qv = q < a.Lq;
+  const T* Qb = (const T*)a.Q + (long)b * a.Lq * a.sq + h * DH;
+  const T* Kb = (const T*)a.K + (long)b * a.Lk * a.sk + h * DH;
+  const T* Vb = (const T*)a.V + (long)b * a.Lk * a.sv + h * DH;
+  uint4 qf[Cfg<T>::NSUB];
+  row_frags<T>(qf, Qb, a.sq, qv ? q : 0, qv, lane);
+  const float gate = (a.gate && qv) ? a.gate[(long)bh * a.Lq + q] : 0.f;
+  const float* tab = a.table ? a.table + (long)h * (2 * a.Lk - 1) + (a.Lk - 1) - q : nullptr;
+
+  float m = -INFINITY, l = 0.f;
+  f32x4_t o[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) o[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  for (int k0 = 0; k0 < a.Lk; k0 += 64) {
+    const int nv = min(64, a.Lk - k0);
+    __syncthreads();
+    stage<T>(kimg, nullptr, Kb, a.sk, k0, nv);
+    stage<T>(nullptr, vimg, Vb, a.sv, k0, nv);
+    __syncthreads();
+    f32x4_t s[4];
+    rows_times_frag<T>(s, kimg, qf, lane);
+    float p[4][4];
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int key = k0 + kb * 16 + 4 * g + j;
+        float x = s[kb][j] * a.scale;
+        if (tab && qv && key < a.Lk) x += gate * tab[key];
+        if (!key_ok(a, b, key)) x = -INFINITY;
+        p[kb][j] = x;
+        tmax = fmaxf(tmax, x);
+      }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float mn = fmaxf(m, tmax);
+    const float alpha = (mn == -INFINITY) ? 1.f : __expf(m - mn);
+    float ls = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float e = (mn == -INFINITY) ? 0.f : __expf(p[kb][j] - mn);
+        ls += e;
+        if (a.thr16) {
+          const int key = k0 + kb * 16 + 4 * g + j;
+          const uint64_t idx = ((uint64_t)bh * a.Lq + q) * a.Lk + key;
+          e = drop_keep(a.seed, a.stream, idx, a.thr16) ? e * a.drop_scale : 0.f;
+        }
+        p[kb][j] = e;
+      }
+    l = l * alpha + ls;
+    m = mn;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) o[d] *= alpha;
+    trans_times_vals<T>(o, vimg, p, lane);
+  }
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  if (!qv) return;
+  const float inv = (l > 0.f) ? 1.f / l : NAN;  // fully masked row -> NaN like softmax(all -inf)
+  T* Ob = (T*)a.Out + ((long)b * a.Lq + q) * a.so + h * DH;
+#pragma unroll
+  for (int d = 0; d < 4; ++d)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) st<T>(Ob + d * 16 + 4 * g + j, o[d][j] * inv);
+  if (a.lse && g == 0) a.lse[(long)bh * a.Lq + q] = (l > 0.f) ? m + __logf(l) : NAN;
+}
+
+// ------------------------------------------------------------------------------------------- dQ
+// query-owned: recompute S^T, dP^T = V dO^T; dS = P (dP - delta); dQ^T = K^T dS^T
+template <typename T>
+__global__ void __launch_bounds__(256) dq_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int RB = Cfg<T>::RB;
+  unsigned char* kimg = smem;             // K rows (KC)
+  unsigned char* ktimg = smem + 64 * RB;  // K transposed reads (MC)
+  unsigned char* vimg = smem + 128 * RB;  // V rows (KC)
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, i = lane & 15;
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int q = blockIdx.x * 64 + w * 16 + i;
+  const bool qv = q < a.Lq;
+  const int qq = qv ? q : 0;
+  const T* Qb = (const T*)a.Q + (long)b * a.Lq * a.sq + h * DH;
+  const T* Ob = (const T*)a.O + (long)b * a.Lq * a.so + h * DH;
+  const T* dOb = (const T*)a.dO + (long)b * a.Lq * a.sdo + h * DH;
+  const T* Kb = (const T*)a.K + (long)b * a.Lk * a.sk + h * DH;
+  const T* Vb = (const T*)a.V + (long)b * a.Lk * a.sv + h * DH;
+  uint4 qf[Cfg<T>::NSUB], dof[Cfg<T>::NSUB], of[Cfg<T>::NSUB];
+  row_frags<T>(qf, Qb, a.sq, qq, qv, lane);
+  row_frags<T>(dof, dOb, a.sdo, qq, qv, lane);
+  row_frags<T>(of, Ob, a.so, qq, qv, lane);
+  // delta = rowsum(dO * O) over this lane's chunks, then across the 4 lane groups
+  float delta = 0.f;
+#pragma unroll
+  for (int s = 0; s < Cfg<T>::NSUB; ++s) {
+    const T* x = (const T*)&dof[s];
+    const T* y = (const T*)&of[s];
+#pragma unroll
+    for (int e = 0; e < Cfg<T>::ECH; ++e) delta += ld<T>(x + e) * ld<T>(y + e);
+  }
+  delta += __shfl_xor(delta, 16, 64);
+  delta += __shfl_xor(delta, 32, 64);
+  if (qv && g == 0) a.delta[(long)bh * a.Lq + q] = delta;
+  const float lse = qv ? a.lse[(long)bh * a.Lq + q] : 0.f;
+
+  f32x4_t dq[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) dq[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  for (int k0 = 0; k0 < a.Lk; k0 += 64) {
+    const int nv = min(64, a.Lk - k0);
+    __syncthreads();
+    stage<T>(kimg, ktimg, Kb, a.sk, k0, nv);
+    stage<T>(vimg, nullptr, Vb, a.sv, k0, nv);
+    __syncthreads();
+    f32x4_t s[4], dp[4];
+    rows_times_frag<T>(s, kimg, qf, lane);
+    rows_times_frag<T>(dp, vimg, dof, lane);
+    float ds[4][4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int key = k0 + kb * 16 + 4 * g + j;
+        float pr = 0.f;
+        if (key_ok(a, b, key) && qv) pr = __expf(s[kb][j] * a.scale - lse);
+        float dpv = dp[kb][j];
+        if (a.thr16) {
+          const uint64_t idx = ((uint64_t)bh * a.Lq + q) * a.Lk + key;
+          dpv = drop_keep(a.seed, a.stream, idx, a.thr16) ? dpv * a.drop_scale : 0.f;
+        }
+        ds[kb][j] = pr * (dpv - delta);
+      }
+    trans_times_vals<T>(dq, ktimg, ds, lane);
+  }
+  if (!qv) return;
+  T* dQb = (T*)a.dQ + ((long)b * a.Lq + q) * a.sdq + h * DH;
+#pragma unroll
+  for (int d = 0; d < 4; ++d)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) st<T>(dQb + d * 16 + 4 * g + j, dq[d][j] * a.scale);
+}
+
+// ------------------------------------------------------------------------------------------- dK dV
+// key-owned: S = Q K^T (lane = key), dP = dO V^T, dV^T = dO^T P_drop, dK^T = Q^T dS
+template <typename T>
+__global__ void __launch_bounds__(256) dkv_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int RB = Cfg<T>::RB;
+  unsigned char* qimg = smem;
+  unsigned char* qtimg = smem + 64 * RB;
+  unsigned char* doimg = smem + 128 * RB;
+  unsigned char* dotimg = smem + 192 * RB;
+  float* lse_s = (float*)(smem + 256 * RB);
+  float* del_s = lse_s + 64;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, i = lane & 15;
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int key = blockIdx.x * 64 + w * 16 + i;
+  const bool kv = key < a.Lk;
+  const bool kok = key_ok(a, b, kv ? key : 0) && kv;
+  const T* Qb = (const T*)a.Q + (long)b * a.Lq * a.sq + h * DH;
+  const T* dOb = (const T*)a.dO + (long)b * a.Lq * a.sdo + h * DH;
+  const T* Kb = (const T*)a.K + (long)b * a.Lk * a.sk + h * DH;
+  const T* Vb = (const T*)a.V + (long)b * a.Lk * a.sv + h * DH;
+  uint4 kf[Cfg<T>::NSUB], vf[Cfg<T>::NSUB];
+  row_frags<T>(kf, Kb, a.sk, kv ? key : 0, kv, lane);
+  row_frags<T>(vf, Vb, a.sv, kv ? key : 0, kv, lane);
+
+  f32x4_t dk[4], dv[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) dk[d] = dv[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  for (int q0 = 0; q0 < a.Lq; q0 += 64) {
+    const int nv = min(64, a.Lq - q0);
+    __syncthreads();
+    stage<T>(qimg, qtimg, Qb, a.sq, q0, nv);
+    stage<T>(doimg, dotimg, dOb, a.sdo, q0, nv);
+    if (threadIdx.x < 64) {
+      const int qq = q0 + threadIdx.x;
+      float lv = 0.f, dl = 0.f;
+      if (qq < a.Lq) {
+        lv = a.lse[(long)bh * a.Lq + qq];
+        dl = a.delta[(long)bh * a.Lq + qq];
+      }
+      lse_s[threadIdx.x] = lv;
+      del_s[threadIdx.x] = dl;
+    }
+    __syncthreads();
+    f32x4_t s[4], dp[4];
+    rows_times_frag<T>(s, qimg, kf, lane);    // S[q = qb*16+4g+j][key = lane]
+    rows_times_frag<T>(dp, doimg, vf, lane);  // dP[q][key]
+    float pd[4][4], ds[4][4];
+#pragma unroll
+    for (int qb = 0; qb < 4; ++qb)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int ql = qb * 16 + 4 * g + j;
+        const int qq = q0 + ql;
+        float pr = 0.f;
+        if (kok && qq < a.Lq) pr = __expf(s[qb][j] * a.scale - lse_s[ql]);
+        float keep = 1.f;
+        if (a.thr16) {
+          const uint64_t idx = ((uint64_t)bh * a.Lq + qq) * a.Lk + key;
+          keep = drop_keep(a.seed, a.stream, idx, a.thr16) ? a.drop_scale : 0.f;
+        }
+        pd[qb][j] = pr * keep;
+        ds[qb][j] = pr * (dp[qb][j] * keep - del_s[ql]);
+      }
+    trans_times_vals<T>(dv, dotimg, pd, lane);
+    trans_times_vals<T>(dk, qtimg, ds, lane);
+  }
+  if (!kv) return;
+  T* dKb = (T*)a.dK + ((long)b * a.Lk + key) * a.sdk + h * DH;
+  T* dVb = (T*)a.dV + ((long)b * a.Lk + key) * a.sdv + h * DH;
+#pragma unroll
+  for (int d = 0; d < 4; ++d)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      st<T>(dKb + d * 16 + 4 * g + j, dk[d][j] * a.scale);
+      st<T>(dVb + d * 16 + 4 * g + j, dv[d][j]);
+    }
+}
+
+template <typename T>
+static int run(int which, AttnArgs& a, hipStream_t s) {
+  constexpr int RB = Cfg<T>::RB;
+  if (which == 0) {
+    dim3 grid((a.Lq + 63) / 64, a.B * a.H);
+    hipLaunchKernelGGL(fwd_kernel<T>, grid, dim3(256), 128 * RB, s, a);
+  } else if (which == 1) {
+    dim3 grid((a.Lq + 63) / 64, a.B * a.H);
+    hipLaunchKernelGGL(dq_kernel<T>, grid, dim3(256), 192 * RB, s, a);
+  } else {
+    dim3 grid((a.Lk + 63) / 64, a.B * a.H);
+    hipLaunchKernelGGL(dkv_kernel<T>, grid, dim3(256), 256 * RB + 512, s, a);
+  }
+  return (int)hipGetLastError();
+}
+
+static bool aligned_ok(const void* p, long stride, int ech) {
+  return p == nullptr || (((uintptr_t)p & 15) == 0 && stride % ech == 0);
+}
+
+}  // namespace attn
+}  // namespace fddm
+
+using namespace fddm;
+using namespace fddm::attn;
+
+static int attn_dispatch(int which, int dtype, AttnArgs& a, float drop_p, void* hs) {
+  if (a.B <= 0 || a.H <= 0 || a.Lq <= 0 || a.Lk <= 0) return 0;
+  const int ech = dtype == FDDM_BF16 ? 8 : 4;
+  if (!aligned_ok(a.Q, a.sq, ech) || !aligned_ok(a.K, a.sk, ech) || !aligned_ok(a.V, a.sv, ech) ||
+      !aligned_ok(a.O, a.so, ech) || !aligned_ok(a.dO, a.sdo, ech))
+    return (int)hipErrorInvalidValue;
+  a.thr16 = 0;
+  a.drop_scale = 1.f;
+  if (drop_p > 0.f) {
+    a.thr16 = (unsigned)llrintf(drop_p * 65536.f);
+    a.drop_scale = 1.f / (1.f - drop_p);
+  }
+  if (dtype == FDDM_BF16) return run<bf16_t>(which, a, (hipStream_t)hs);
+  if (dtype == FDDM_F32) return run<float>(which, a, (hipStream_t)hs);
+  return (int)hipErrorInvalidValue;
+}
+
+// Forward. Q/K/V/O: element (b, pos, h, d) at base + (b*L + pos)*stride + h*64 + d.
+FDDM_API int fddm_attn_fwd(int dtype, const void* Q, long sq, const void* K, long sk, const void* V, long sv, void* O,
+                           long so, float* lse, const unsigned char* key_keep, const float* gate, const float* table,
+                           int B, int H, int Lq, int Lk, float scale, float drop_p, unsigned long long seed,
+                           unsigned long long stream, void* hs) {
+  AttnArgs a{};
+  a.Q = Q; a.K = K; a.V = V; a.Out = O; a.lse = lse;
+  a.sq = sq; a.sk = sk; a.sv = sv; a.so = so;
+  a.key_keep = key_keep; a.gate = gate; a.table = table;
+  a.B = B; a.H = H; a.Lq = Lq; a.Lk = Lk; a.scale = scale; a.seed = seed; a.stream = stream;
+  return attn_dispatch(0, dtype, a, drop_p, hs);
+}
+
+// Backward: dQ (query-owned kernel) and dK/dV (key-owned kernel). lse from the forward.
+FDDM_API int fddm_attn_bwd(int dtype, const void* Q, long sq, const void* K, long sk, const void* V, long sv,
+                           const void* O, long so, const void* dO, long sdo, const float* lse, void* dQ, long sdq,
+                           void* dK, long sdk, void* dV, long sdv, float* delta_ws, const unsigned char* key_keep,
+                           int B, int H, int Lq, int Lk, float scale, float drop_p, unsigned long long seed,
+                           unsigned long long stream, void* hs) {
+  AttnArgs a{};
+  a.delta = delta_ws;
+  a.Q = Q; a.K = K; a.V = V; a.O = O; a.dO = dO; a.lse = (float*)lse;
+  a.dQ = dQ; a.dK = dK; a.dV = dV;
+  a.sq = sq; a.sk = sk; a.sv = sv; a.so = so; a.sdo = sdo; a.sdq = sdq; a.sdk = sdk; a.sdv = sdv;
+  a.key_keep = key_keep;
+  a.B = B; a.H = H; a.Lq = Lq; a.Lk = Lk; a.scale = scale; a.seed = seed; a.stream = stream;
+  int e = attn_dispatch(1, dtype, a, drop_p, hs);
+  if (e) return e;
+  return attn_dispatch(2, dtype, a, drop_p, hs);
+}

@@ -1,0 +1,360 @@
+// MFMA GEMM for gfx950:  C[m][n] = alpha * sum_k A(m,k) * B(n,k)  (+ fused epilogue)
+//
+// Each operand is either K-contiguous ("KC": A stored [M][K], B stored [N][K]) or M/N-contiguous
+// ("MC": A stored [K][M], B stored [K][N]). That covers every GEMM of the train step without
+// materialised transposes:
+//   forward  Y  = X  W^T : A=X  KC, B=W  KC        (also the WavLM conv feature extractor as an
+//                                                 implicit GEMM: the A row of output frame t is the
+//                                                 window x[s*t .. s*t+k) of a channels-last input,
+//                                                 i.e. lda = s*C < K, overlapping rows)
+//   backward dX = dY W   : A=dY KC, B=W  MC
+//   backward dW = dY^T X : A=dY MC, B=X  MC
+// A rows are batched for the conv case: A(m,k) at A + (m / Mi)*sAb + (m % Mi)*lda + k.
+//
+// Tile 128x128, 256 threads = 4 waves in 2x2, each wave 64x64 = 4x4 tiles of 16x16.
+// A K-step moves 128 bytes of the compute type per tile row (bf16: 64 k, 2 x mfma_f32_16x16x32_bf16;
+// f32: 32 k, 8 x mfma_f32_16x16x4f32 — exact fp32, the parity mode).
+// LDS images (16 KB per operand per stage, double-buffered):
+//   KC: [128 rows][128 B], 16-B chunk c of row r at r*128 + ((c ^ ((r>>1)&7))<<4)  -> ds_read_b128
+//   MC: [K-step rows][128 elems]; bf16 8-B unit u of row k at k*256 + ((u ^ h(k))<<3),
+//       h(k) = ((k&3)<<2) | (((k>>3)&1)<<4) -> conflict-free ds_read_b64_tr_b16 (hardware transpose)
+//       f32: plain rows of 512 B, scalar reads.
+// Register-staged prefetch of step k+1 is issued before the MFMAs of step k (one barrier per step).
+// A may be stored in f32 while the MFMA runs in bf16 (TA=float, T=bf16): converted while staging.
+#include "common.h"
+
+namespace fddm {
+
+enum { EPI_STORE = 0, EPI_GELU = 1, EPI_ACC_F32 = 2, EPI_GELU_ONLY = 3, EPI_DGELU = 4 };
+
+// implicit-conv addressing of a KC A operand: A(m,k) = A + (m/Mi)*sAb + (t*cstride - cpad + k/Cg)*lda + k%Cg,
+// t = m%Mi, zero outside 0 <= time < Tin (WavLM conv feature extractor and grouped positional conv)
+struct ConvGeo { long Cg, cstride, cpad, Tin; };
+
+constexpr int GBM = 128, GBN = 128;
+constexpr int GTILE_BYTES = 16384;  // per operand per stage
+
+__device__ __forceinline__ int swz_kc(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
+__device__ __forceinline__ int hk(int k) { return ((k & 3) << 2) | (((k >> 3) & 1) << 4); }
+
+template <typename T> struct Mma;
+template <> struct Mma<bf16_t> {
+  static constexpr int KSTEP = 64, ECH = 8;
+  __device__ __forceinline__ static void mma(f32x4_t& c, const uint4& a, const uint4& b) {
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c, 0,
+                                                0, 0);
+  }
+};
+template <> struct Mma<float> {
+  static constexpr int KSTEP = 32, ECH = 4;
+  __device__ __forceinline__ static void mma(f32x4_t& c, const uint4& a, const uint4& b) {
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.x), __uint_as_float(b.x), c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.y), __uint_as_float(b.y), c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.z), __uint_as_float(b.z), c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.w), __uint_as_float(b.w), c, 0, 0, 0);
+  }
+};
+
+__device__ __forceinline__ unsigned pack_bf2(float a, float b) { return (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16); }
+
+// load one 16-B chunk of compute type T (ECH elements) from storage type TS
+template <typename T, typename TS>
+__device__ __forceinline__ uint4 load_chunk(const TS* p) {
+  if constexpr (sizeof(T) == sizeof(TS)) {
+    return *(const uint4*)p;
+  } else {  // TS = float, T = bf16: 8 floats -> 8 bf16
+    const float4 a = *(const float4*)p;
+    const float4 b = *(const float4*)(p + 4);
+    return make_uint4(pack_bf2(a.x, a.y), pack_bf2(a.z, a.w), pack_bf2(b.x, b.y), pack_bf2(b.z, b.w));
+  }
+}
+
+// Operand stager/reader. ROWS = M (or N) extent of the tile = 128.
+template <typename T, typename TS, bool KC, bool CONV = false>
+struct Operand {
+  static constexpr int KSTEP = Mma<T>::KSTEP, ECH = Mma<T>::ECH;
+  static constexpr int CPR = KC ? 8 : (128 / ECH);  // chunks per LDS row
+  const TS* src[4];
+  bool ok[4];
+  int lds_off[4];
+  long ld, dim_ext, K;
+  int kk[4];  // KC: chunk k offset (elements); MC: row k within the step
+  long tpos[4];
+  ConvGeo cg;
+  uint4 r[4];
+
+  // dim0: first row (m or n) of the tile; batched KC addressing via (Mi, sb)
+  __device__ __forceinline__ void init(const TS* base, long ld_, long Mi, long sb, long dim0, long dim_ext_, long K_,
+                                       ConvGeo geo = ConvGeo{1, 0, 0, 0}) {
+    ld = ld_; dim_ext = dim_ext_; K = K_; cg = geo;
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + 256 * i;
+      if (KC) {
+        const int row = c >> 3, cc = c & 7;
+        const long m = dim0 + row;
+        ok[i] = m < dim_ext;
+        const long mm = ok[i] ? m : 0;
+        if (CONV) {
+          src[i] = base + (mm / Mi) * sb;
+          tpos[i] = (mm % Mi) * cg.cstride - cg.cpad;
+        } else {
+          src[i] = base + (mm / Mi) * sb + (mm % Mi) * ld + cc * ECH;
+        }
+        kk[i] = cc * ECH;
+        lds_off[i] = swz_kc(row, cc);
+      } else {
+        const int k = c / CPR, mc = c % CPR;
+        const long m = dim0 + (long)mc * ECH;
+        ok[i] = m < dim_ext;  // dim_ext % ECH == 0 (checked on host)
+        src[i] = base + (long)k * ld + (ok[i] ? m : 0);
+        kk[i] = k;
+        if constexpr (sizeof(T) == 2) lds_off[i] = k * 256 + (((2 * mc) ^ hk(k)) << 3);
+        else lds_off[i] = k * 512 + mc * 16;
+      }
+    }
+  }
+  __device__ __forceinline__ void gload(long kt) {
+    const long k0 = kt * KSTEP;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (KC && CONV) {
+        const long k = k0 + kk[i];
+        const long tap = k / cg.Cg, c = k - tap * cg.Cg;
+        const long tm = tpos[i] + tap;
+        const bool in = ok[i] && (k < K) && tm >= 0 && tm < cg.Tin;
+        r[i] = in ? load_chunk<T, TS>(src[i] + tm * ld + c) : make_uint4(0, 0, 0, 0);
+      } else if (KC) {
+        const bool in = ok[i] && (k0 + kk[i] < K);
+        r[i] = in ? load_chunk<T, TS>(src[i] + k0) : make_uint4(0, 0, 0, 0);
+      } else {
+        const bool in = ok[i] && (k0 + kk[i] < K);
+        r[i] = in ? load_chunk<T, TS>(src[i] + k0 * ld) : make_uint4(0, 0, 0, 0);
+      }
+    }
+  }
+  __device__ __forceinline__ void lstore(unsigned char* s) const {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *(uint4*)(s + lds_off[i]) = r[i];
+  }
+  // fragment for the 16-row tile starting at rb, sub-step sub (0/1)
+  __device__ __forceinline__ static uint4 frag(const unsigned char* s, int rb, int sub, int lane) {
+    const int g = lane >> 4, i = lane & 15;
+    if constexpr (KC) {
+      return *(const uint4*)(s + swz_kc(rb + i, sub * 4 + g));
+    } else if constexpr (sizeof(T) == 2) {
+      const int q = i >> 2, p = i & 3;
+      const int k = sub * 32 + 8 * g + q;
+      const int u = (rb >> 2) + p;
+      typedef __attribute__((address_space(3))) s16x4_t* lp;
+      const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(s + k * 256 + ((u ^ hk(k)) << 3)));
+      const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(s + (k + 4) * 256 + ((u ^ hk(k + 4)) << 3)));
+      uint4 o;
+      o.x = (unsigned)(unsigned short)lo[0] | ((unsigned)(unsigned short)lo[1] << 16);
+      o.y = (unsigned)(unsigned short)lo[2] | ((unsigned)(unsigned short)lo[3] << 16);
+      o.z = (unsigned)(unsigned short)hi[0] | ((unsigned)(unsigned short)hi[1] << 16);
+      o.w = (unsigned)(unsigned short)hi[2] | ((unsigned)(unsigned short)hi[3] << 16);
+      return o;
+    } else {
+      const int k = sub * 16 + 4 * g;
+      const float* f = (const float*)s;
+      uint4 o;
+      o.x = __float_as_uint(f[(k + 0) * 128 + rb + i]);
+      o.y = __float_as_uint(f[(k + 1) * 128 + rb + i]);
+      o.z = __float_as_uint(f[(k + 2) * 128 + rb + i]);
+      o.w = __float_as_uint(f[(k + 3) * 128 + rb + i]);
+      return o;
+    }
+  }
+};
+
+struct GemmArgs {
+  const void* A; long lda, Mi, sAb;
+  const void* B; long ldb;
+  void* C; long ldc; void* C2;
+  const float* bias; float alpha;
+  long M, N, K;
+  uint64_t seed, stream; unsigned thr16; float drop_scale;
+  ConvGeo geo;
+  long sAz, sBz, sCz, sbiasz;  // per-blockIdx.z offsets (grouped conv)
+};
+
+template <typename T, typename TA, bool AKC, bool BKC, int EPI, typename OT, bool CONV>
+__global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int KSTEP = Mma<T>::KSTEP;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const long m0 = (long)blockIdx.y * GBM, n0 = (long)blockIdx.x * GBN;
+
+  const long z = blockIdx.z;
+  Operand<T, TA, AKC, CONV> opa;
+  Operand<T, T, BKC> opb;
+  opa.init((const TA*)g.A + z * g.sAz, g.lda, g.Mi, g.sAb, m0, g.M, g.K, g.geo);
+  opb.init((const T*)g.B + z * g.sBz, g.ldb, 1L << 62, 0, n0, g.N, g.K);
+  OT* Cz = (OT*)g.C + z * g.sCz;
+  const float* biasz = g.bias ? g.bias + z * g.sbiasz : nullptr;
+
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const long nk = (g.K + KSTEP - 1) / KSTEP;
+  opa.gload(0);
+  opb.gload(0);
+  opa.lstore(smem);
+  opb.lstore(smem + GTILE_BYTES);
+  __syncthreads();
+  for (long kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) {
+      opa.gload(kt + 1);
+      opb.gload(kt + 1);
+    }
+    const unsigned char* sa = smem + buf * 2 * GTILE_BYTES;
+    const unsigned char* sb = sa + GTILE_BYTES;
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      uint4 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = Operand<T, TA, AKC, CONV>::frag(sa, wr * 64 + i * 16, sub, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = Operand<T, T, BKC>::frag(sb, wc * 64 + j * 16, sub, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) Mma<T>::mma(acc[i][j], af[i], bfr[j]);
+    }
+    if (kt + 1 < nk) {
+      unsigned char* na = smem + (buf ^ 1) * 2 * GTILE_BYTES;
+      opa.lstore(na);
+      opb.lstore(na + GTILE_BYTES);
+    }
+    __syncthreads();
+  }
+
+  // epilogue: acc[i][j][e] -> row m0 + wr*64 + i*16 + 4*fg + e, col n0 + wc*64 + j*16 + fr
+  const int fr = lane & 15, fg = lane >> 4;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const long n = n0 + wc * 64 + j * 16 + fr;
+    if (n >= g.N) continue;
+    const float bv = biasz ? biasz[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const long m = m0 + wr * 64 + i * 16 + 4 * fg + e;
+        if (m >= g.M) continue;
+        const float v = acc[i][j][e] * g.alpha + bv;
+        if constexpr (EPI == EPI_STORE) {
+          st<OT>(Cz + m * g.ldc + n, v);
+        } else if constexpr (EPI == EPI_GELU) {
+          st<OT>(Cz + m * g.ldc + n, v);  // pre-activation, saved for backward
+          float a = gelu_f(v);
+          if (g.thr16) a = drop_keep(g.seed, g.stream, (uint64_t)(m * g.N + n), g.thr16) ? a * g.drop_scale : 0.f;
+          st<OT>((OT*)g.C2 + m * g.ldc + n, a);
+        } else if constexpr (EPI == EPI_GELU_ONLY) {
+          st<OT>(Cz + m * g.ldc + n, gelu_f(v));
+        } else if constexpr (EPI == EPI_DGELU) {
+          float dv = v * gelu_grad(ld<OT>((const OT*)g.C2 + m * g.ldc + n));
+          if (g.thr16) dv = drop_keep(g.seed, g.stream, (uint64_t)(m * g.N + n), g.thr16) ? dv * g.drop_scale : 0.f;
+          st<OT>(Cz + m * g.ldc + n, dv);
+        } else {
+          float* c = (float*)Cz + m * g.ldc + n;
+          *c += v;
+        }
+      }
+    }
+  }
+}
+
+template <typename T, typename TA, bool AKC, bool BKC, int EPI, typename OT, bool CONV = false>
+static int launch(const GemmArgs& g, hipStream_t s, int nz) {
+  dim3 grid((unsigned)((g.N + GBN - 1) / GBN), (unsigned)((g.M + GBM - 1) / GBM), (unsigned)nz);
+  hipLaunchKernelGGL((gemm_kernel<T, TA, AKC, BKC, EPI, OT, CONV>), grid, dim3(256), 4 * GTILE_BYTES, s, g);
+  return (int)hipGetLastError();
+}
+
+template <typename T, typename TA, bool AKC, bool BKC>
+static int dispatch_epi(int epi, int out_dtype, const GemmArgs& g, hipStream_t s, int nz) {
+  if (epi == EPI_STORE) {
+    if (out_dtype == FDDM_F32) return launch<T, TA, AKC, BKC, EPI_STORE, float>(g, s, nz);
+    if constexpr (sizeof(T) == 2) return launch<T, TA, AKC, BKC, EPI_STORE, bf16_t>(g, s, nz);
+  } else if (epi == EPI_GELU) {
+    return launch<T, TA, AKC, BKC, EPI_GELU, T>(g, s, nz);
+  } else if (epi == EPI_ACC_F32) {
+    return launch<T, TA, AKC, BKC, EPI_ACC_F32, float>(g, s, nz);
+  } else if (epi == EPI_DGELU) {
+    return launch<T, TA, AKC, BKC, EPI_DGELU, T>(g, s, nz);
+  } else if (epi == EPI_GELU_ONLY) {
+    return launch<T, TA, AKC, BKC, EPI_GELU_ONLY, T>(g, s, nz);
+  }
+  return (int)hipErrorInvalidValue;
+}
+
+template <typename T, typename TA>
+static int dispatch_layout(int a_kc, int b_kc, int epi, int out_dtype, const GemmArgs& g, hipStream_t s) {
+  if (a_kc && b_kc) return dispatch_epi<T, TA, true, true>(epi, out_dtype, g, s, 1);
+  if (a_kc && !b_kc) return dispatch_epi<T, TA, true, false>(epi, out_dtype, g, s, 1);
+  if (!a_kc && !b_kc) return dispatch_epi<T, TA, false, false>(epi, out_dtype, g, s, 1);
+  return dispatch_epi<T, TA, false, true>(epi, out_dtype, g, s, 1);
+}
+
+}  // namespace fddm
+
+using namespace fddm;
+
+FDDM_API int fddm_gemm(int dtype, int a_dtype, int a_kc, int b_kc, int epi, int out_dtype, const void* A, long lda,
+                       long Mi, long sAb, const void* B, long ldb, void* C, long ldc, void* C2, const float* bias,
+                       float alpha, long M, long N, long K, unsigned long long seed, unsigned long long stream,
+                       float drop_p, void* hip_stream) {
+  if (M <= 0 || N <= 0) return 0;
+  const int ech = dtype == FDDM_BF16 ? 8 : 4;
+  // layout preconditions (16-B chunks never straddle a row end or the tile edge)
+  if (a_kc ? (K % ech || lda % ech || sAb % ech) : (M % ech || lda % ech)) return (int)hipErrorInvalidValue;
+  if (b_kc ? (K % ech || ldb % ech) : (N % ech || ldb % ech)) return (int)hipErrorInvalidValue;
+  if (((uintptr_t)A & 15) || ((uintptr_t)B & 15)) return (int)hipErrorInvalidValue;
+  if (!a_kc && Mi > 0 && Mi != M) return (int)hipErrorInvalidValue;
+  if (Mi <= 0) Mi = 1L << 62;
+  GemmArgs g{A, lda, Mi, sAb, B, ldb, C, ldc, C2, bias, alpha, M, N, K, seed, stream, 0u, 1.f, ConvGeo{1, 0, 0, 0}, 0, 0, 0, 0};
+  if ((epi == EPI_GELU || epi == EPI_DGELU) && drop_p > 0.f) {
+    g.thr16 = (unsigned)llrintf(drop_p * 65536.f);
+    g.drop_scale = 1.f / (1.f - drop_p);
+  }
+  hipStream_t s = (hipStream_t)hip_stream;
+  if (dtype == FDDM_BF16) {
+    if (a_dtype == FDDM_BF16) return dispatch_layout<bf16_t, bf16_t>(a_kc, b_kc, epi, out_dtype, g, s);
+    if (a_dtype == FDDM_F32) return dispatch_layout<bf16_t, float>(a_kc, b_kc, epi, out_dtype, g, s);
+  } else if (dtype == FDDM_F32 && a_dtype == FDDM_F32) {
+    return dispatch_layout<float, float>(a_kc, b_kc, epi, out_dtype, g, s);
+  }
+  return (int)hipErrorInvalidValue;
+}
+
+// Implicit-GEMM 1-D convolution over a channels-last input x[b][time][lda] (KC A operand):
+//   out[b*Tout + t][z*N + n] = act( sum_{tap,c} x[b][t*cstride - cpad + tap][z*Cg + c] * W[z][n][tap*Cg + c] + bias )
+// for each group z < groups (gridDim.z). W is [groups][N][K = taps*Cg] (K-contiguous), out row stride ldc.
+// epi: EPI_STORE or EPI_GELU_ONLY.  Sites: HF modeling_wavlm.py:675-693 (conv layers 1..6, groups=1) and
+// 37-90 (positional grouped conv, groups=16, pad 64).
+FDDM_API int fddm_conv1d_gemm(int dtype, int epi, const void* x, long lda, long sAb, long Tin, long Cg, long cstride,
+                              long cpad, const void* W, void* out, long ldc, const float* bias, long Bn, long Tout,
+                              long N, long K, int groups, void* hip_stream) {
+  const int ech = dtype == FDDM_BF16 ? 8 : 4;
+  if (Bn <= 0 || Tout <= 0) return 0;
+  if (K % ech || Cg % ech || lda % ech || sAb % ech || ((uintptr_t)x & 15) || ((uintptr_t)W & 15))
+    return (int)hipErrorInvalidValue;
+  GemmArgs g{x, lda, Tout, sAb, W, K, out, ldc, nullptr, bias, 1.f, Bn * Tout, N, K, 0, 0, 0u, 1.f,
+             ConvGeo{Cg, cstride, cpad, Tin}, Cg, N * K, N, N};
+  hipStream_t s = (hipStream_t)hip_stream;
+  if (dtype == FDDM_BF16) {
+    if (epi == EPI_GELU_ONLY) return launch<bf16_t, bf16_t, true, true, EPI_GELU_ONLY, bf16_t, true>(g, s, groups);
+    return launch<bf16_t, bf16_t, true, true, EPI_STORE, bf16_t, true>(g, s, groups);
+  } else {
+    if (epi == EPI_GELU_ONLY) return launch<float, float, true, true, EPI_GELU_ONLY, float, true>(g, s, groups);
+    return launch<float, float, true, true, EPI_STORE, float, true>(g, s, groups);
+  }
+}

@@ -1,0 +1,279 @@
+// Discrete-diffusion kernels:
+//  * fddm_sample_q      — SchedulerAdapter.sample_q (train.py:180-188): closed-form two-valued
+//                         inverse CDF over the q_sample distribution, counter-based RNG (bit-exact
+//                         with oracle.sample_xt).
+//  * fddm_kl_fwd/_bwd   — SchedulerAdapter.kl_term (train.py:190-255): per-token categorical KL
+//                         q(x_{t-1}|x_t,x0) || p(x_{t-1}|x_t,softmax(z)) and its exact gradient,
+//                         one workgroup per token, the V-row held in registers (one HBM read,
+//                         one write). Closed form: SURVEY §8(a) "KL closed form".
+//  * fddm_softmax_rows / fddm_softmax_bwd_rows — TextEmbedding (models/projection.py:41-47).
+#include "common.h"
+
+namespace fddm {
+
+__global__ void sample_q_kernel(const long* __restrict__ x0, const long* __restrict__ t,
+                                const unsigned* __restrict__ thr, long* __restrict__ xt, long B, long L,
+                                long K, uint64_t seed, uint64_t stream) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= B * L) return;
+  const long b = e / L;
+  const uint64_t h = mix64(seed, stream, (uint64_t)e);
+  const unsigned r1 = (unsigned)(h >> 32), r2 = (unsigned)(h & 0xffffffffu);
+  const long x = x0[e];
+  const long tv = t[b];
+  if (r1 < thr[tv - 1]) {
+    xt[e] = x;
+  } else {
+    const long j = (long)(((uint64_t)r2 * (uint64_t)(K - 1)) >> 32);
+    xt[e] = j + (j >= x ? 1 : 0);
+  }
+}
+
+struct KlRow {
+  float a_t, b_t, a_p, b_p, dq, inv_dq;
+};
+
+__device__ __forceinline__ KlRow kl_consts(const float* betas, long tv, long xt, long x0, float K) {
+  KlRow c;
+  const float bt = betas[tv - 1];
+  const float bp = (tv == 1) ? 0.f : betas[tv - 2];
+  c.a_t = 1.f - bt;
+  c.b_t = bt / K;
+  c.a_p = 1.f - bp;
+  c.b_p = bp / K;
+  c.dq = c.b_t + c.a_t * (x0 == xt ? 1.f : 0.f);
+  c.inv_dq = 1.f / (c.dq + 1e-8f);
+  return c;
+}
+
+// NPT = row elements held per thread (V <= 256 * NPT)
+template <int NPT, bool BWD, typename OT>
+__global__ void __launch_bounds__(256) kl_kernel(const float* __restrict__ logits, const long* __restrict__ xt_,
+                                                 const long* __restrict__ x0_, const long* __restrict__ t_,
+                                                 const float* __restrict__ betas, const float* __restrict__ w,
+                                                 const float* __restrict__ gscale, float* __restrict__ kl_tok,
+                                                 OT* __restrict__ dz, long L, long V) {
+  __shared__ float red[8];
+  const long row = blockIdx.x;
+  const int tid = threadIdx.x;
+  const float* z = logits + row * V;
+  const long xt = xt_[row], x0 = x0_[row], tv = t_[row / L];
+  const float eps = 1e-8f;
+  const KlRow c = kl_consts(betas, tv, xt, x0, (float)V);
+
+  float v[NPT];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < NPT; ++i) {
+    const long k = tid + 256L * i;
+    v[i] = k < V ? z[k] : -INFINITY;
+    mx = fmaxf(mx, v[i]);
+  }
+  mx = block_max(mx, red);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NPT; ++i) {
+    v[i] = __expf(v[i] - mx);  // exp(-inf) = 0 for padding lanes
+    s += v[i];
+  }
+  s = block_sum(s, red);
+  const float inv_s = 1.f / s;
+  const float xhat_xt = __expf(z[xt] - mx) * inv_s;
+  const float dp = c.b_t + c.a_t * xhat_xt;
+  const float inv_dp = 1.f / (dp + eps);
+  // pass over the row: KL, S1 = sum Q P/(P+eps), G0 = sum g0 xhat
+  float kl = 0.f, s1 = 0.f, g0s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NPT; ++i) {
+    const long k = tid + 256L * i;
+    if (k < V) {
+      const float xh = v[i] * inv_s;
+      const float M = c.b_t + (k == xt ? c.a_t : 0.f);
+      const float Q = M * ((k == x0 ? c.a_p : 0.f) + c.b_p) * c.inv_dq;
+      const float P = M * (c.a_p * xh + c.b_p) * inv_dp;
+      const float rP = 1.f / (P + eps);
+      kl += Q * (__logf(Q + eps) - __logf(P + eps));
+      s1 += Q * P * rP;
+      if (BWD) g0s += -Q * M * c.a_p * rP * inv_dp * xh;
+      v[i] = xh;
+    }
+  }
+  if (!BWD) {
+    kl = block_sum(kl, red);
+    if (tid == 0) kl_tok[row] = kl;
+    return;
+  }
+  s1 = block_sum(s1, red);
+  g0s = block_sum(g0s, red);
+  const float gxt = c.a_t * s1 * inv_dp;
+  const float G = g0s + xhat_xt * gxt;
+  const float wr = w[row] * (gscale ? gscale[0] : 1.f);
+  OT* out = dz + row * V;
+#pragma unroll
+  for (int i = 0; i < NPT; ++i) {
+    const long k = tid + 256L * i;
+    if (k < V) {
+      const float xh = v[i];
+      const float M = c.b_t + (k == xt ? c.a_t : 0.f);
+      const float Q = M * ((k == x0 ? c.a_p : 0.f) + c.b_p) * c.inv_dq;
+      const float P = M * (c.a_p * xh + c.b_p) * inv_dp;
+      float g = -Q * M * c.a_p / (P + eps) * inv_dp + (k == xt ? gxt : 0.f);
+      st<OT>(out + k, wr * xh * (g - G));
+    }
+  }
+}
+
+// softmax over rows of length V (fp32 in) -> T out
+template <int NPT, typename OT>
+__global__ void __launch_bounds__(256) softmax_rows_kernel(const float* __restrict__ x, OT* __restrict__ y, long V) {
+  __shared__ float red[8];
+  const long row = blockIdx.x;
+  const int tid = threadIdx.x;
+  const float* z = x + row * V;
+  float v[NPT];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < NPT; ++i) {
+    const long k = tid + 256L * i;
+    v[i] = k < V ? z[k] : -INFINITY;
+    mx = fmaxf(mx, v[i]);
+  }
+  mx = block_max(mx, red);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NPT; ++i) {
+    v[i] = __expf(v[i] - mx);
+    s += v[i];
+  }
+  s = block_sum(s, red);
+  const float inv = 1.f / s;
+#pragma unroll
+  for (int i = 0; i < NPT; ++i) {
+    const long k = tid + 256L * i;
+    if (k < V) st<OT>(y + row * V + k, v[i] * inv);
+  }
+}
+
+// dz = y * (dy - sum(y*dy)); y, dy in T; dz written as T or accumulated into f32
+template <int NPT, typename T, typename OT>
+__global__ void __launch_bounds__(256) softmax_bwd_kernel(const T* __restrict__ y, const T* __restrict__ dy,
+                                                          OT* __restrict__ dz, long V, int accumulate) {
+  __shared__ float red[8];
+  const long row = blockIdx.x;
+  const int tid = threadIdx.x;
+  float yv[NPT], dv[NPT];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NPT; ++i) {
+    const long k = tid + 256L * i;
+    yv[i] = k < V ? ld<T>(y + row * V + k) : 0.f;
+    dv[i] = k < V ? ld<T>(dy + row * V + k) : 0.f;
+    s += yv[i] * dv[i];
+  }
+  s = block_sum(s, red);
+#pragma unroll
+  for (int i = 0; i < NPT; ++i) {
+    const long k = tid + 256L * i;
+    if (k < V) {
+      float r = yv[i] * (dv[i] - s);
+      OT* o = dz + row * V + k;
+      if (accumulate) r += ld<OT>(o);
+      st<OT>(o, r);
+    }
+  }
+}
+
+}  // namespace fddm
+
+using namespace fddm;
+
+FDDM_API int fddm_sample_q(const long* x0, const long* t, const unsigned* thr, long* xt, long B, long L, long K,
+                           unsigned long long seed, unsigned long long stream, void* hs) {
+  const long n = B * L;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(sample_q_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)hs, x0, t, thr,
+                     xt, B, L, K, (uint64_t)seed, (uint64_t)stream);
+  return (int)hipGetLastError();
+}
+
+#define KL_DISPATCH(NPT)                                                                                            \
+  if (V <= 256L * NPT) {                                                                                           \
+    if (!bwd) {                                                                                                    \
+      hipLaunchKernelGGL((kl_kernel<NPT, false, float>), dim3((unsigned)N), dim3(256), 0, s, logits, xt, x0, t,   \
+                         betas, w, gscale, kl_tok, (float*)nullptr, L, V);                                         \
+    } else if (dz_dtype == FDDM_BF16) {                                                                            \
+      hipLaunchKernelGGL((kl_kernel<NPT, true, bf16_t>), dim3((unsigned)N), dim3(256), 0, s, logits, xt, x0, t,   \
+                         betas, w, gscale, kl_tok, (bf16_t*)dz, L, V);                                             \
+    } else {                                                                                                       \
+      hipLaunchKernelGGL((kl_kernel<NPT, true, float>), dim3((unsigned)N), dim3(256), 0, s, logits, xt, x0, t,    \
+                         betas, w, gscale, kl_tok, (float*)dz, L, V);                                              \
+    }                                                                                                              \
+    return (int)hipGetLastError();                                                                                 \
+  }
+
+static int kl_launch(int bwd, const float* logits, const long* xt, const long* x0, const long* t, const float* betas,
+                     const float* w, const float* gscale, float* kl_tok, void* dz, int dz_dtype, long N, long L,
+                     long V, void* hs) {
+  if (N <= 0) return 0;
+  hipStream_t s = (hipStream_t)hs;
+  KL_DISPATCH(4)
+  KL_DISPATCH(16)
+  KL_DISPATCH(32)
+  KL_DISPATCH(64)
+  return (int)hipErrorInvalidValue;
+}
+
+FDDM_API int fddm_kl_fwd(const float* logits, const long* xt, const long* x0, const long* t, const float* betas,
+                         float* kl_tok, long N, long L, long V, void* hs) {
+  return kl_launch(0, logits, xt, x0, t, betas, nullptr, nullptr, kl_tok, nullptr, FDDM_F32, N, L, V, hs);
+}
+
+FDDM_API int fddm_kl_bwd(const float* logits, const long* xt, const long* x0, const long* t, const float* betas,
+                         const float* w, const float* gscale, void* dz, int dz_dtype, long N, long L, long V,
+                         void* hs) {
+  return kl_launch(1, logits, xt, x0, t, betas, w, gscale, nullptr, dz, dz_dtype, N, L, V, hs);
+}
+
+#define SM_DISPATCH(NPT)                                                                                 \
+  if (V <= 256L * NPT) {                                                                                \
+    if (out_dtype == FDDM_BF16)                                                                         \
+      hipLaunchKernelGGL((softmax_rows_kernel<NPT, bf16_t>), dim3((unsigned)N), dim3(256), 0, s, x,   \
+                         (bf16_t*)y, V);                                                                \
+    else                                                                                                \
+      hipLaunchKernelGGL((softmax_rows_kernel<NPT, float>), dim3((unsigned)N), dim3(256), 0, s, x,    \
+                         (float*)y, V);                                                                 \
+    return (int)hipGetLastError();                                                                      \
+  }
+
+FDDM_API int fddm_softmax_rows(const float* x, void* y, int out_dtype, long N, long V, void* hs) {
+  if (N <= 0) return 0;
+  hipStream_t s = (hipStream_t)hs;
+  SM_DISPATCH(4)
+  SM_DISPATCH(16)
+  SM_DISPATCH(32)
+  SM_DISPATCH(64)
+  return (int)hipErrorInvalidValue;
+}
+
+#define SMB_DISPATCH(NPT)                                                                                        \
+  if (V <= 256L * NPT) {                                                                                        \
+    if (dtype == FDDM_BF16)                                                                                     \
+      hipLaunchKernelGGL((softmax_bwd_kernel<NPT, bf16_t, float>), dim3((unsigned)N), dim3(256), 0, s,         \
+                         (const bf16_t*)y, (const bf16_t*)dy, dz, V, accumulate);                               \
+    else                                                                                                        \
+      hipLaunchKernelGGL((softmax_bwd_kernel<NPT, float, float>), dim3((unsigned)N), dim3(256), 0, s,          \
+                         (const float*)y, (const float*)dy, dz, V, accumulate);                                 \
+    return (int)hipGetLastError();                                                                              \
+  }
+
+// dz (f32) = y*(dy - sum(y*dy)) [+ dz if accumulate]
+FDDM_API int fddm_softmax_bwd_rows(const void* y, const void* dy, float* dz, int dtype, long N, long V, int accumulate,
+                                   void* hs) {
+  if (N <= 0) return 0;
+  hipStream_t s = (hipStream_t)hs;
+  SMB_DISPATCH(4)
+  SMB_DISPATCH(16)
+  SMB_DISPATCH(32)
+  SMB_DISPATCH(64)
+  return (int)hipErrorInvalidValue;
+}

@@ -1,0 +1,109 @@
+// L_fd cross-modal feature decorrelation (losses/fddm_losses.py:18-58) — the non-GEMM parts.
+// The [D x D] cross-correlation C = za~^T zb~ / (B*T) and its two backward products run on the MFMA
+// GEMM (MC operands, no transposes); these kernels do the batch-dim standardisation and the loss.
+#include "common.h"
+
+namespace fddm {
+
+// per column c of z [B][C] (C = T*D): mean / biased var over B, z~ = (z - mean)/sqrt(var + eps)
+template <typename OT>
+__global__ void lfd_std_fwd_kernel(const float* __restrict__ z, OT* __restrict__ zt, float* __restrict__ inv_std, long B,
+                                   long C, float eps) {
+  const long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float m = 0.f;
+  for (long b = 0; b < B; ++b) m += z[b * C + c];
+  m /= (float)B;
+  float v = 0.f;
+  for (long b = 0; b < B; ++b) {
+    const float t = z[b * C + c] - m;
+    v += t * t;
+  }
+  v /= (float)B;
+  const float is = 1.f / sqrtf(v + eps);
+  inv_std[c] = is;
+  for (long b = 0; b < B; ++b) st<OT>(zt + b * C + c, (z[b * C + c] - m) * is);
+}
+
+// dz = (dz~ - mean_b(dz~) - z~ * mean_b(dz~ * z~)) * inv_std
+template <typename T>
+__global__ void lfd_std_bwd_kernel(const float* __restrict__ dzt, const T* __restrict__ zt, const float* __restrict__ inv_std,
+                                   float* __restrict__ dz, long B, long C) {
+  const long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float m1 = 0.f, m2 = 0.f;
+  for (long b = 0; b < B; ++b) {
+    const float g = dzt[b * C + c];
+    m1 += g;
+    m2 += g * ld<T>(zt + b * C + c);
+  }
+  m1 /= (float)B;
+  m2 /= (float)B;
+  const float is = inv_std[c];
+  for (long b = 0; b < B; ++b) dz[b * C + c] = (dzt[b * C + c] - m1 - ld<T>(zt + b * C + c) * m2) * is;
+}
+
+// loss = sum_j (1 - C_jj)^2 + lambda * sum_{j!=k} C_jk^2   (single block)
+__global__ void __launch_bounds__(256) lfd_loss_kernel(const float* __restrict__ Cm, float* __restrict__ loss, long D,
+                                                       float lam) {
+  __shared__ float red[4];
+  float acc = 0.f;
+  for (long e = threadIdx.x; e < D * D; e += 256) {
+    const long j = e / D, k = e % D;
+    const float c = Cm[e];
+    acc += (j == k) ? (1.f - c) * (1.f - c) : lam * c * c;
+  }
+  acc = block_sum(acc, red);
+  if (threadIdx.x == 0) loss[0] = acc;
+}
+
+// dC = g * d loss / dC
+template <typename OT>
+__global__ void lfd_dloss_kernel(const float* __restrict__ Cm, const float* __restrict__ gscale, OT* __restrict__ dC, long D,
+                                 float lam) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= D * D) return;
+  const long j = e / D, k = e % D;
+  const float c = Cm[e];
+  const float g = gscale ? gscale[0] : 1.f;
+  st<OT>(dC + e, g * ((j == k) ? -2.f * (1.f - c) : 2.f * lam * c));
+}
+
+}  // namespace fddm
+
+using namespace fddm;
+
+FDDM_API int fddm_lfd_std_fwd(int out_dtype, const float* z, void* zt, float* inv_std, long B, long C, float eps, void* hs) {
+  if (C <= 0) return 0;
+  dim3 g((unsigned)((C + 255) / 256));
+  if (out_dtype == FDDM_BF16)
+    hipLaunchKernelGGL((lfd_std_fwd_kernel<bf16_t>), g, dim3(256), 0, (hipStream_t)hs, z, (bf16_t*)zt, inv_std, B, C, eps);
+  else
+    hipLaunchKernelGGL((lfd_std_fwd_kernel<float>), g, dim3(256), 0, (hipStream_t)hs, z, (float*)zt, inv_std, B, C, eps);
+  return (int)hipGetLastError();
+}
+
+FDDM_API int fddm_lfd_std_bwd(int zt_dtype, const float* dzt, const void* zt, const float* inv_std, float* dz, long B,
+                              long C, void* hs) {
+  if (C <= 0) return 0;
+  dim3 g((unsigned)((C + 255) / 256));
+  if (zt_dtype == FDDM_BF16)
+    hipLaunchKernelGGL((lfd_std_bwd_kernel<bf16_t>), g, dim3(256), 0, (hipStream_t)hs, dzt, (const bf16_t*)zt, inv_std, dz, B, C);
+  else
+    hipLaunchKernelGGL((lfd_std_bwd_kernel<float>), g, dim3(256), 0, (hipStream_t)hs, dzt, (const float*)zt, inv_std, dz, B, C);
+  return (int)hipGetLastError();
+}
+
+FDDM_API int fddm_lfd_loss(const float* Cm, float* loss, long D, float lam, void* hs) {
+  hipLaunchKernelGGL(lfd_loss_kernel, dim3(1), dim3(256), 0, (hipStream_t)hs, Cm, loss, D, lam);
+  return (int)hipGetLastError();
+}
+
+FDDM_API int fddm_lfd_dloss(int out_dtype, const float* Cm, const float* gscale, void* dC, long D, float lam, void* hs) {
+  dim3 g((unsigned)((D * D + 255) / 256));
+  if (out_dtype == FDDM_BF16)
+    hipLaunchKernelGGL((lfd_dloss_kernel<bf16_t>), g, dim3(256), 0, (hipStream_t)hs, Cm, gscale, (bf16_t*)dC, D, lam);
+  else
+    hipLaunchKernelGGL((lfd_dloss_kernel<float>), g, dim3(256), 0, (hipStream_t)hs, Cm, gscale, (float*)dC, D, lam);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,176 @@
+// HBM-bound helper kernels of the train step: RoPE, token embedding, column sums, casts.
+#include "common.h"
+
+namespace fddm {
+
+// RoPE (models/denoise_decoder.py:42-53), applied to the full-width block input:
+//   out[i]   = x[2i]*cos[p][2i] - x[2i+1]*sin[p][2i+1]
+//   out[h+i] = x[2i]*sin[p][2i] + x[2i+1]*cos[p][2i+1]       (h = d/2, p = position)
+// cos/sin tables [L][d] are the reference's emb.cos()/emb.sin() (computed once on the host).
+template <typename OT>
+__global__ void rope_fwd_kernel(const float* __restrict__ x, const float* __restrict__ cs, const float* __restrict__ sn,
+                                OT* __restrict__ out, long N, long L, long d) {
+  const long h = d / 2;
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= N * h) return;
+  const long r = e / h, i = e % h, p = r % L;
+  const float x1 = x[r * d + 2 * i], x2 = x[r * d + 2 * i + 1];
+  const float* C = cs + p * d;
+  const float* S = sn + p * d;
+  st<OT>(out + r * d + i, x1 * C[2 * i] - x2 * S[2 * i + 1]);
+  st<OT>(out + r * d + h + i, x1 * S[2 * i] + x2 * C[2 * i + 1]);
+}
+
+// dx += RoPE^T(dy)
+__global__ void rope_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ cs, const float* __restrict__ sn,
+                                float* __restrict__ dx, long N, long L, long d) {
+  const long h = d / 2;
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= N * h) return;
+  const long r = e / h, i = e % h, p = r % L;
+  const float a = dy[r * d + i], b = dy[r * d + h + i];
+  const float* C = cs + p * d;
+  const float* S = sn + p * d;
+  dx[r * d + 2 * i] += a * C[2 * i] + b * S[2 * i];
+  dx[r * d + 2 * i + 1] += -a * S[2 * i + 1] + b * C[2 * i + 1];
+}
+
+// x[r] = E[tok[r]] + tbias[r / L]   (models/denoise_decoder.py:254, 272-274)
+template <typename OT>
+__global__ void embed_fwd_kernel(const long* __restrict__ tok, const float* __restrict__ E,
+                                 const float* __restrict__ tbias, float* __restrict__ out, OT* __restrict__ out_t, long N,
+                                 long L, long d) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= N * d) return;
+  const long r = e / d, c = e % d;
+  float v = E[tok[r] * d + c];
+  if (tbias) v += tbias[(r / L) * d + c];
+  if (out) out[e] = v;
+  if (out_t) st<OT>(out_t + e, v);
+}
+
+// dE[tok[r]] += dx[r] (skip padding_idx rows), dtb[b] += sum_l dx[b,l]  — caller zeroes outputs
+__global__ void embed_bwd_kernel(const long* __restrict__ tok, const float* __restrict__ dx, float* __restrict__ dE,
+                                 float* __restrict__ dtb, long N, long L, long d, long pad_id) {
+  // one block = 32 rows x d columns (threads stride columns)
+  const long r0 = (long)blockIdx.x * 32;
+  for (long c = threadIdx.x; c < d; c += blockDim.x) {
+    float acc = 0.f;
+    long cur_b = r0 / L;
+    for (long r = r0; r < min(r0 + 32, N); ++r) {
+      const float g = dx[r * d + c];
+      const long t = tok[r];
+      if (dE && t != pad_id) atomicAdd(dE + t * d + c, g);
+      if (dtb) {
+        const long b = r / L;
+        if (b != cur_b) {
+          atomicAdd(dtb + cur_b * d + c, acc);
+          acc = 0.f;
+          cur_b = b;
+        }
+        acc += g;
+      }
+    }
+    if (dtb) atomicAdd(dtb + cur_b * d + c, acc);
+  }
+}
+
+// out[n] (+)= sum_m X[m][n]   (bias gradients); caller zeroes `out` when accumulate=0 is not used
+template <typename T>
+__global__ void colsum_kernel(const T* __restrict__ X, float* __restrict__ out, long M, long N, long ldx, long rows_per_block) {
+  const long n = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  const long m0 = (long)blockIdx.y * rows_per_block;
+  const long m1 = min(M, m0 + rows_per_block);
+  float acc = 0.f;
+  for (long m = m0; m < m1; ++m) acc += ld<T>(X + m * ldx + n);
+  atomicAdd(out + n, acc);
+}
+
+__global__ void cast_f32_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, long n) {
+  const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i + 3 < n) {
+    const float4 v = *(const float4*)(x + i);
+    y[i] = f2bf(v.x); y[i + 1] = f2bf(v.y); y[i + 2] = f2bf(v.z); y[i + 3] = f2bf(v.w);
+  } else {
+    for (long j = i; j < n; ++j) y[j] = f2bf(x[j]);
+  }
+}
+
+__global__ void cast_bf16_f32_kernel(const bf16_t* __restrict__ x, float* __restrict__ y, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = bf2f(x[i]);
+}
+
+}  // namespace fddm
+
+using namespace fddm;
+
+static inline dim3 g1(long n, int bs = 256) { return dim3((unsigned)((n + bs - 1) / bs)); }
+
+FDDM_API int fddm_rope_fwd(int out_dtype, const float* x, const float* cs, const float* sn, void* out, long N, long L,
+                           long d, void* hs) {
+  if (N <= 0) return 0;
+  if (d % 2) return (int)hipErrorInvalidValue;
+  const long n = N * (d / 2);
+  if (out_dtype == FDDM_BF16)
+    hipLaunchKernelGGL((rope_fwd_kernel<bf16_t>), g1(n), dim3(256), 0, (hipStream_t)hs, x, cs, sn, (bf16_t*)out, N, L, d);
+  else
+    hipLaunchKernelGGL((rope_fwd_kernel<float>), g1(n), dim3(256), 0, (hipStream_t)hs, x, cs, sn, (float*)out, N, L, d);
+  return (int)hipGetLastError();
+}
+
+FDDM_API int fddm_rope_bwd(const float* dy, const float* cs, const float* sn, float* dx, long N, long L, long d,
+                           void* hs) {
+  if (N <= 0) return 0;
+  const long n = N * (d / 2);
+  hipLaunchKernelGGL(rope_bwd_kernel, g1(n), dim3(256), 0, (hipStream_t)hs, dy, cs, sn, dx, N, L, d);
+  return (int)hipGetLastError();
+}
+
+FDDM_API int fddm_embed_fwd(int out_dtype, const long* tok, const float* E, const float* tbias, float* out, void* out_t,
+                            long N, long L, long d, void* hs) {
+  if (N <= 0) return 0;
+  if (out_dtype == FDDM_BF16)
+    hipLaunchKernelGGL((embed_fwd_kernel<bf16_t>), g1(N * d), dim3(256), 0, (hipStream_t)hs, tok, E, tbias, out,
+                       (bf16_t*)out_t, N, L, d);
+  else
+    hipLaunchKernelGGL((embed_fwd_kernel<float>), g1(N * d), dim3(256), 0, (hipStream_t)hs, tok, E, tbias, out,
+                       (float*)out_t, N, L, d);
+  return (int)hipGetLastError();
+}
+
+FDDM_API int fddm_embed_bwd(const long* tok, const float* dx, float* dE, float* dtb, long N, long L, long d, long pad_id,
+                            void* hs) {
+  if (N <= 0) return 0;
+  hipLaunchKernelGGL(embed_bwd_kernel, dim3((unsigned)((N + 31) / 32)), dim3(256), 0, (hipStream_t)hs, tok, dx, dE, dtb,
+                     N, L, d, pad_id);
+  return (int)hipGetLastError();
+}
+
+FDDM_API int fddm_colsum(int dtype, const void* X, float* out, long M, long N, long ldx, void* hs) {
+  if (M <= 0 || N <= 0) return 0;
+  const long rpb = 64;
+  dim3 grid((unsigned)((N + 255) / 256), (unsigned)((M + rpb - 1) / rpb));
+  if (dtype == FDDM_BF16)
+    hipLaunchKernelGGL((colsum_kernel<bf16_t>), grid, dim3(256), 0, (hipStream_t)hs, (const bf16_t*)X, out, M, N, ldx, rpb);
+  else
+    hipLaunchKernelGGL((colsum_kernel<float>), grid, dim3(256), 0, (hipStream_t)hs, (const float*)X, out, M, N, ldx, rpb);
+  return (int)hipGetLastError();
+}
+
+FDDM_API int fddm_cast(int src_dtype, int dst_dtype, const void* x, void* y, long n, void* hs) {
+  if (n <= 0) return 0;
+  if (src_dtype == FDDM_F32 && dst_dtype == FDDM_BF16)
+    hipLaunchKernelGGL(cast_f32_bf16_kernel, g1((n + 3) / 4), dim3(256), 0, (hipStream_t)hs, (const float*)x,
+                       (bf16_t*)y, n);
+  else if (src_dtype == FDDM_BF16 && dst_dtype == FDDM_F32)
+    hipLaunchKernelGGL(cast_bf16_f32_kernel, g1(n), dim3(256), 0, (hipStream_t)hs, (const bf16_t*)x, (float*)y, n);
+  else
+    return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}
+
+FDDM_API const char* fddm_error_string(int code) { return hipGetErrorString((hipError_t)code); }
+
+FDDM_API int fddm_abi_version() { return 1; }

@@ -1,0 +1,94 @@
+// Fused clip_grad_norm_(5.0) + AdamW over all trainable tensors in two launches (train.py:411-423):
+//   1) sum of squares of every gradient (multi-tensor, chunked) -> one fp32 accumulator
+//   2) per element: g' = g * min(1, max_norm / (sqrt(total) + 1e-6));
+//      p *= (1 - lr*wd); m = lerp(m, g', 1-b1); v = b2 v + (1-b2) g'^2;
+//      p -= (lr/bc1) * m / (sqrt(v)/sqrt(bc2) + eps)          (torch.optim.AdamW single-tensor form)
+//      and optionally a bf16 copy of p for the next forward's MFMA operands.
+// No host synchronisation: the clip coefficient is read on the device. Tensors whose grad is None
+// are simply not in the list (set_to_none semantics, train.py:400).
+#include "common.h"
+
+namespace fddm {
+
+struct MTTable {
+  const long* chunk_tensor;  // [nchunks]
+  const long* chunk_start;   // [nchunks]
+  const long* numel;         // [ntensors]
+  float* const* p;
+  const float* const* g;
+  float* const* m;
+  float* const* v;
+  bf16_t* const* pbf;        // entries may be null
+  const float* step_size;    // [ntensors] lr / bc1
+  const float* bc2_sqrt;     // [ntensors]
+};
+
+constexpr long MT_CHUNK = 65536;
+
+__global__ void __launch_bounds__(256) sumsq_kernel(MTTable t, float* total) {
+  __shared__ float red[4];
+  const long ci = blockIdx.x;
+  const long ti = t.chunk_tensor[ci], s0 = t.chunk_start[ci];
+  const long n = min(MT_CHUNK, t.numel[ti] - s0);
+  const float* g = t.g[ti] + s0;
+  float acc = 0.f;
+  for (long i = threadIdx.x; i < n; i += 256) {
+    const float x = g[i];
+    acc += x * x;
+  }
+  acc = block_sum(acc, red);
+  if (threadIdx.x == 0) atomicAdd(total, acc);
+}
+
+__global__ void __launch_bounds__(256) adamw_kernel(MTTable t, const float* total, float max_norm, float lr_wd, float b1,
+                                                    float b2, float eps) {
+  const long ci = blockIdx.x;
+  const long ti = t.chunk_tensor[ci], s0 = t.chunk_start[ci];
+  const long n = min(MT_CHUNK, t.numel[ti] - s0);
+  float coef = 1.f;
+  if (total) {
+    coef = max_norm / (sqrtf(total[0]) + 1e-6f);
+    coef = fminf(coef, 1.f);
+  }
+  float* p = t.p[ti] + s0;
+  const float* g = t.g[ti] + s0;
+  float* m = t.m[ti] + s0;
+  float* v = t.v[ti] + s0;
+  bf16_t* pb = t.pbf[ti] ? t.pbf[ti] + s0 : nullptr;
+  const float ss = t.step_size[ti], bc2s = t.bc2_sqrt[ti];
+  for (long i = threadIdx.x; i < n; i += 256) {
+    const float gg = g[i] * coef;
+    float pp = p[i] * (1.f - lr_wd);
+    const float mm = m[i] + (1.f - b1) * (gg - m[i]);
+    const float vv = v[i] * b2 + (1.f - b2) * gg * gg;
+    const float denom = sqrtf(vv) / bc2s + eps;
+    pp = pp - ss * (mm / denom);
+    p[i] = pp;
+    m[i] = mm;
+    v[i] = vv;
+    if (pb) pb[i] = f2bf(pp);
+  }
+}
+
+}  // namespace fddm
+
+using namespace fddm;
+
+FDDM_API int fddm_grad_sumsq(const long* chunk_tensor, const long* chunk_start, const long* numel, const float* const* g,
+                             long nchunks, float* total, void* hs) {
+  if (nchunks <= 0) return 0;
+  MTTable t{chunk_tensor, chunk_start, numel, nullptr, g, nullptr, nullptr, nullptr, nullptr, nullptr};
+  hipLaunchKernelGGL(sumsq_kernel, dim3((unsigned)nchunks), dim3(256), 0, (hipStream_t)hs, t, total);
+  return (int)hipGetLastError();
+}
+
+FDDM_API int fddm_adamw(const long* chunk_tensor, const long* chunk_start, const long* numel, float* const* p,
+                        const float* const* g, float* const* m, float* const* v, bf16_t* const* pbf,
+                        const float* step_size, const float* bc2_sqrt, long nchunks, const float* total, float max_norm,
+                        float lr_wd, float b1, float b2, float eps, void* hs) {
+  if (nchunks <= 0) return 0;
+  MTTable t{chunk_tensor, chunk_start, numel, p, g, m, v, pbf, step_size, bc2_sqrt};
+  hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)nchunks), dim3(256), 0, (hipStream_t)hs, t, total, max_norm, lr_wd, b1,
+                     b2, eps);
+  return (int)hipGetLastError();
+}

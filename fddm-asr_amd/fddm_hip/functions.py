@@ -1,0 +1,343 @@
+"""torch.autograd.Functions of the train step. Each forward/backward is a fixed sequence of
+libfddm_hip launches on the current stream; activations are saved in the compute dtype (bf16 / f32)
+with the residual stream, LayerNorm statistics and softmax log-sum-exps in fp32.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import ops, runtime as rt
+
+F32 = torch.float32
+
+
+def _t(x):
+    """compute-dtype view/copy of an activation"""
+    cd = rt.compute_dtype()
+    return x if x.dtype == cd else ops.cast(x.contiguous(), cd)
+
+
+# ------------------------------------------------------------------------------- generic Linear
+class LinearFn(torch.autograd.Function):
+    """y = x W^T + b (f32 out) — SpeechProjector / TextProjector / encoder proj (models/projection.py)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        shp = x.shape
+        x2 = _t(x.reshape(-1, shp[-1]).contiguous())
+        w = rt.wt(weight)
+        y = ops.linear(x2, w, bias, out_dtype=F32)
+        ctx.save_for_backward(x2, weight, bias)
+        ctx.shp = shp
+        return y.view(*shp[:-1], weight.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, weight, bias = ctx.saved_tensors
+        dy2 = dy.reshape(-1, weight.shape[0]).contiguous()
+        dyt = _t(dy2)
+        dx = dW = db = None
+        if ctx.needs_input_grad[0]:
+            dx = ops.linear_dx(dyt, rt.wt(weight)).view(ctx.shp)
+        if ctx.needs_input_grad[1]:
+            dW = ops.linear_dw(dyt, x2)
+        if bias is not None and ctx.needs_input_grad[2]:
+            db = ops.colsum(dy2)
+        return dx, dW, db
+
+
+def linear(x, weight, bias=None):
+    return LinearFn.apply(x, weight, bias)
+
+
+# ------------------------------------------------------------------------------ token embedding
+class EmbedFn(torch.autograd.Function):
+    """x = tok_emb[xt] + t_bias[b]   (models/denoise_decoder.py:254, 274). Returns (x f32, x_T)."""
+
+    @staticmethod
+    def forward(ctx, xt, E, tbias, pad_id):
+        B, L = xt.shape
+        d = E.shape[1]
+        x = torch.empty(B * L, d, device=E.device, dtype=F32)
+        cd = rt.compute_dtype()
+        xT = torch.empty(B * L, d, device=E.device, dtype=cd)
+        ops.embed_fwd(xt.contiguous(), E.detach(), tbias.detach().contiguous(), x, xT, L)
+        ctx.save_for_backward(xt)
+        ctx.pad_id, ctx.L, ctx.V = pad_id, L, E.shape[0]
+        ctx.mark_non_differentiable(xT)
+        return x, xT
+
+    @staticmethod
+    def backward(ctx, dx, _dxT):
+        (xt,) = ctx.saved_tensors
+        d = dx.shape[1]
+        B = xt.shape[0]
+        dE = torch.zeros(ctx.V, d, device=dx.device, dtype=F32)
+        dtb = torch.zeros(B, d, device=dx.device, dtype=F32)
+        ops.embed_bwd(xt.contiguous(), dx.contiguous(), dE, dtb, ctx.L, ctx.pad_id)
+        return None, dE, dtb, None
+
+
+# -------------------------------------------------------------------------------- decoder block
+def _film_split(fs):
+    return fs.contiguous()
+
+
+class DecoderBlockFn(torch.autograd.Function):
+    """DecoderBlock.forward (models/denoise_decoder.py:147-192) as one fused sequence:
+    RoPE -> self-attn (kpm, dropout) -> +drop -> LN1 -> cross-attn -> +drop -> LN2 -> FiLM ->
+    FF(GELU, dropout) -> +drop -> LN3.  Inputs: x (f32 [N,d], differentiable), xT (compute dtype copy),
+    cT (cond, compute dtype [B*S,d], no grad), key_keep (u8 [B,L]), film scale/shift [B,d] (diff.),
+    then the 18 block parameters. Dropout sites use rng streams 6*layer + {1..6}."""
+
+    @staticmethod
+    def forward(ctx, x, xT, cT, key_keep, fscale, fshift, meta, *params):
+        (sa_w, sa_b, so_w, so_b, ca_w, ca_b, co_w, co_b, f0_w, f0_b, f3_w, f3_b,
+         n1w, n1b, n2w, n2b, n3w, n3b) = params
+        B, L, S, H, layer, p, seed, cos, sin = meta
+        N, d = x.shape
+        dev = x.device
+        cd = rt.compute_dtype()
+        st = 6 * layer
+        W = {k: rt.wt(v) for k, v in (("sa", sa_w), ("so", so_w), ("ca", ca_w), ("co", co_w), ("f0", f0_w),
+                                       ("f3", f3_w))}
+        # 1. RoPE on the block input (q = k = rope(x), v = x)
+        xr = torch.empty(N, d, device=dev, dtype=cd)
+        ops.rope_fwd(x, cos, sin, xr, L)
+        qk = ops.linear(xr, W["sa"][: 2 * d], sa_b[: 2 * d], out_dtype=cd)
+        v = ops.linear(xT, W["sa"][2 * d:], sa_b[2 * d:], out_dtype=cd)
+        o = torch.empty(N, d, device=dev, dtype=cd)
+        lse = torch.empty(B * H, L, device=dev, dtype=F32)
+        ops.attn_fwd(qk, qk[:, d:], v, o, lse, B, H, L, L, key_keep=key_keep, drop_p=p, seed=seed, rng_stream=st + 1)
+        y = ops.linear(o, W["so"], so_b, out_dtype=cd)
+        s1 = torch.empty(N, d, device=dev, dtype=F32)
+        m1 = torch.empty(N, device=dev, dtype=F32)
+        r1 = torch.empty(N, device=dev, dtype=F32)
+        x1 = torch.empty(N, d, device=dev, dtype=F32)
+        x1T = torch.empty(N, d, device=dev, dtype=cd) if cd != F32 else x1
+        ops.ln_fwd(x, y, n1w, n1b, out_f32=x1, out_t=x1T if cd != F32 else None, save_s=s1, mean=m1, rstd=r1,
+                   drop_p=p, seed=seed, rng_stream=st + 2)
+        # 2. cross-attention to the acoustic condition
+        qc = ops.linear(x1T, W["ca"][:d], ca_b[:d], out_dtype=cd)
+        kvc = ops.linear(cT, W["ca"][d:], ca_b[d:], out_dtype=cd)
+        oc = torch.empty(N, d, device=dev, dtype=cd)
+        lsec = torch.empty(B * H, L, device=dev, dtype=F32)
+        ops.attn_fwd(qc, kvc, kvc[:, d:], oc, lsec, B, H, L, S, drop_p=p, seed=seed, rng_stream=st + 3)
+        yc = ops.linear(oc, W["co"], co_b, out_dtype=cd)
+        s2 = torch.empty(N, d, device=dev, dtype=F32)
+        m2 = torch.empty(N, device=dev, dtype=F32)
+        r2 = torch.empty(N, device=dev, dtype=F32)
+        x2 = torch.empty(N, d, device=dev, dtype=F32)
+        x2T = torch.empty(N, d, device=dev, dtype=cd) if cd != F32 else x2
+        fsc, fsh = fscale.detach().contiguous(), fshift.detach().contiguous()
+        ops.ln_fwd(x1, yc, n2w, n2b, out_f32=x2, out_t=x2T if cd != F32 else None, save_s=s2, mean=m2, rstd=r2,
+                   film=(fsc, fsh), rows_per_batch=L, drop_p=p, seed=seed, rng_stream=st + 4)
+        # 3. feed-forward
+        FF = f0_w.shape[0]
+        hpre = torch.empty(N, FF, device=dev, dtype=cd)
+        hact = torch.empty(N, FF, device=dev, dtype=cd)
+        ops.linear(x2T, W["f0"], f0_b, out=hpre, epi=ops.EPI_GELU, C2=hact, drop_p=p, seed=seed, rng_stream=st + 5)
+        y3 = ops.linear(hact, W["f3"], f3_b, out_dtype=cd)
+        s3 = torch.empty(N, d, device=dev, dtype=F32)
+        m3 = torch.empty(N, device=dev, dtype=F32)
+        r3 = torch.empty(N, device=dev, dtype=F32)
+        x3 = torch.empty(N, d, device=dev, dtype=F32)
+        x3T = torch.empty(N, d, device=dev, dtype=cd)
+        ops.ln_fwd(x2, y3, n3w, n3b, out_f32=x3, out_t=x3T, save_s=s3, mean=m3, rstd=r3,
+                   drop_p=p, seed=seed, rng_stream=st + 6)
+        ctx.save_for_backward(xT, xr, qk, v, o, lse, s1, m1, r1, x1T, qc, kvc, oc, lsec, s2, m2, r2, x2T, hpre, hact,
+                              s3, m3, r3, cT, key_keep, fsc, *params)
+        ctx.meta = meta
+        ctx.mark_non_differentiable(x3T)
+        return x3, x3T
+
+    @staticmethod
+    def backward(ctx, dx3, _dx3T):
+        (xT, xr, qk, v, o, lse, s1, m1, r1, x1T, qc, kvc, oc, lsec, s2, m2, r2, x2T, hpre, hact, s3, m3, r3, cT,
+         key_keep, fsc, *params) = ctx.saved_tensors
+        (sa_w, sa_b, so_w, so_b, ca_w, ca_b, co_w, co_b, f0_w, f0_b, f3_w, f3_b,
+         n1w, n1b, n2w, n2b, n3w, n3b) = params
+        B, L, S, H, layer, p, seed, cos, sin = ctx.meta
+        st = 6 * layer
+        N, d = dx3.shape
+        dev = dx3.device
+        cd = rt.compute_dtype()
+        W = {k: rt.wt(v_) for k, v_ in (("sa", sa_w), ("so", so_w), ("ca", ca_w), ("co", co_w), ("f0", f0_w),
+                                         ("f3", f3_w))}
+        g = {}
+        dx3 = dx3.contiguous()
+        # LN3
+        dx2 = torch.empty(N, d, device=dev, dtype=F32)
+        dy3 = torch.empty(N, d, device=dev, dtype=cd)
+        g["n3w"] = torch.zeros(d, device=dev, dtype=F32)
+        g["n3b"] = torch.zeros(d, device=dev, dtype=F32)
+        ops.ln_bwd(dx3, s3, m3, r3, n3w, n3b, dres=dx2, dy_t=dy3, dgamma=g["n3w"], dbeta=g["n3b"], drop_p=p,
+                   seed=seed, rng_stream=st + 6)
+        # FF
+        g["f3w"] = ops.linear_dw(dy3, hact)
+        g["f3b"] = ops.colsum(dy3)
+        FF = f0_w.shape[0]
+        dh = torch.empty(N, FF, device=dev, dtype=cd)
+        ops.linear_dx(dy3, W["f3"], out=dh, epi=ops.EPI_DGELU, C2=hpre, drop_p=p, seed=seed, rng_stream=st + 5)
+        g["f0w"] = ops.linear_dw(dh, x2T)
+        g["f0b"] = ops.colsum(dh)
+        ops.linear_dx(dh, W["f0"], out=dx2, accumulate=True)
+        # LN2 + FiLM
+        dx1 = torch.empty(N, d, device=dev, dtype=F32)
+        dyc = torch.empty(N, d, device=dev, dtype=cd)
+        g["n2w"] = torch.zeros(d, device=dev, dtype=F32)
+        g["n2b"] = torch.zeros(d, device=dev, dtype=F32)
+        dfs = torch.zeros(B, d, device=dev, dtype=F32)
+        dfh = torch.zeros(B, d, device=dev, dtype=F32)
+        ops.ln_bwd(dx2, s2, m2, r2, n2w, n2b, dres=dx1, dy_t=dyc, dgamma=g["n2w"], dbeta=g["n2b"], film_scale=fsc,
+                   dfilm=(dfs, dfh), rows_per_batch=L, drop_p=p, seed=seed, rng_stream=st + 4)
+        # cross out-proj + attention
+        g["cow"] = ops.linear_dw(dyc, oc)
+        g["cob"] = ops.colsum(dyc)
+        doc = ops.linear_dx(dyc, W["co"], out_dtype=cd)
+        dqc = torch.empty(N, d, device=dev, dtype=cd)
+        dkvc = torch.empty(B * S, 2 * d, device=dev, dtype=cd)
+        ops.attn_bwd(qc, kvc, kvc[:, d:], oc, doc, lsec, dqc, dkvc, dkvc[:, d:], B, H, L, S, drop_p=p, seed=seed,
+                     rng_stream=st + 3)
+        gca_w = torch.empty(3 * d, d, device=dev, dtype=F32)
+        ops.linear_dw(dqc, x1T, out=gca_w[:d])
+        ops.linear_dw(dkvc, cT, out=gca_w[d:])
+        gca_b = torch.empty(3 * d, device=dev, dtype=F32)
+        ops.colsum(dqc, out=gca_b[:d])
+        ops.colsum(dkvc, out=gca_b[d:])
+        ops.linear_dx(dqc, W["ca"][:d], out=dx1, accumulate=True)
+        # LN1
+        dx = torch.empty(N, d, device=dev, dtype=F32)
+        dy = torch.empty(N, d, device=dev, dtype=cd)
+        g["n1w"] = torch.zeros(d, device=dev, dtype=F32)
+        g["n1b"] = torch.zeros(d, device=dev, dtype=F32)
+        ops.ln_bwd(dx1, s1, m1, r1, n1w, n1b, dres=dx, dy_t=dy, dgamma=g["n1w"], dbeta=g["n1b"], drop_p=p, seed=seed,
+                   rng_stream=st + 2)
+        # self out-proj + attention
+        g["sow"] = ops.linear_dw(dy, o)
+        g["sob"] = ops.colsum(dy)
+        do = ops.linear_dx(dy, W["so"], out_dtype=cd)
+        dqk = torch.empty(N, 2 * d, device=dev, dtype=cd)
+        dv = torch.empty(N, d, device=dev, dtype=cd)
+        ops.attn_bwd(qk, qk[:, d:], v, o, do, lse, dqk, dqk[:, d:], dv, B, H, L, L, key_keep=key_keep, drop_p=p,
+                     seed=seed, rng_stream=st + 1)
+        gsa_w = torch.empty(3 * d, d, device=dev, dtype=F32)
+        ops.linear_dw(dqk, xr, out=gsa_w[: 2 * d])
+        ops.linear_dw(dv, xT, out=gsa_w[2 * d:])
+        gsa_b = torch.empty(3 * d, device=dev, dtype=F32)
+        ops.colsum(dqk, out=gsa_b[: 2 * d])
+        ops.colsum(dv, out=gsa_b[2 * d:])
+        ops.linear_dx(dv, W["sa"][2 * d:], out=dx, accumulate=True)
+        dxr = ops.linear_dx(dqk, W["sa"][: 2 * d])
+        ops.rope_bwd(dxr, cos, sin, dx, L)
+        grads = (gsa_w, gsa_b, g["sow"], g["sob"], gca_w, gca_b, g["cow"], g["cob"], g["f0w"], g["f0b"], g["f3w"],
+                 g["f3b"], g["n1w"], g["n1b"], g["n2w"], g["n2b"], g["n3w"], g["n3b"])
+        return (dx, None, None, None, dfs, dfh, None) + grads
+
+
+# --------------------------------------------------------------------------------------- head
+class HeadFn(torch.autograd.Function):
+    """logits = h W^T + b in fp32 (models/denoise_decoder.py:286)."""
+
+    @staticmethod
+    def forward(ctx, x, xT, weight, bias):
+        w = rt.wt(weight)
+        logits = ops.linear(xT, w, bias, out_dtype=F32)
+        ctx.save_for_backward(xT, weight)
+        return logits
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        xT, weight = ctx.saved_tensors
+        dl = dlogits.contiguous()
+        w = rt.wt(weight)
+        dx = ops.linear_dx(dl, w)                 # A = dlogits (f32, converted while staging)
+        dW = ops.linear_dw(dl, xT)
+        db = ops.colsum(dl)
+        return dx, None, dW, db
+
+
+# -------------------------------------------------------------------------------------- KL term
+class KLFn(torch.autograd.Function):
+    """SchedulerAdapter.kl_term (train.py:190-255): fused closed-form KL; the exact gradient is
+    produced in backward by a second fused pass that reads the upstream scalar on the device."""
+
+    @staticmethod
+    def forward(ctx, logits, xt, x0, t, w, betas):
+        B, L, V = logits.shape
+        l2 = logits.reshape(B * L, V)
+        kl_tok = ops.kl_fwd(l2, xt.reshape(-1).contiguous(), x0.reshape(-1).contiguous(), t.contiguous(), betas, L)
+        loss = (kl_tok * w).sum()
+        ctx.save_for_backward(l2, xt, x0, t, w, betas)
+        ctx.shape = (B, L, V)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        l2, xt, x0, t, w, betas = ctx.saved_tensors
+        B, L, V = ctx.shape
+        gs = g.reshape(1).to(F32).contiguous()
+        dz = ops.kl_bwd(l2, xt.reshape(-1).contiguous(), x0.reshape(-1).contiguous(), t.contiguous(), betas, w, gs, L)
+        return dz.view(B, L, V), None, None, None, None, None
+
+
+# ------------------------------------------------------------------------------- TextEmbedding
+class TextEmbedFn(torch.autograd.Function):
+    """softmax(logits) @ W^T (models/projection.py:41-47), K = vocab."""
+
+    @staticmethod
+    def forward(ctx, logits, weight):
+        shp = logits.shape
+        V = shp[-1]
+        l2 = logits.reshape(-1, V).contiguous()
+        cd = rt.compute_dtype()
+        xhat = ops.softmax_rows(l2, cd)
+        z = ops.linear(xhat, rt.wt(weight), None, out_dtype=F32)
+        ctx.save_for_backward(xhat, weight)
+        ctx.shp = shp
+        return z.view(*shp[:-1], weight.shape[0])
+
+    @staticmethod
+    def backward(ctx, dz):
+        xhat, weight = ctx.saved_tensors
+        dz2 = dz.reshape(-1, weight.shape[0]).contiguous()
+        cd = rt.compute_dtype()
+        dxhat = ops.linear_dx(dz2, rt.wt(weight), out_dtype=cd)
+        dlogits = ops.softmax_bwd_rows(xhat, dxhat)
+        dW = ops.linear_dw(_t(dz2), xhat)
+        return dlogits.view(ctx.shp), dW
+
+
+# ---------------------------------------------------------------------------------------- L_fd
+class LfdFn(torch.autograd.Function):
+    """lfd_loss (losses/fddm_losses.py:29-58): batch-dim standardisation + C = za~^T zb~ /(B T)."""
+
+    @staticmethod
+    def forward(ctx, z_a, z_b, lam, eps):
+        B, T, D = z_a.shape
+        cd = rt.compute_dtype()
+        za, isa = ops.lfd_std_fwd(z_a.reshape(B, T * D).float().contiguous(), cd, eps)
+        zb, isb = ops.lfd_std_fwd(z_b.reshape(B, T * D).float().contiguous(), cd, eps)
+        za2, zb2 = za.view(B * T, D), zb.view(B * T, D)
+        Cm = torch.empty(D, D, device=z_a.device, dtype=F32)
+        ops.gemm(za2, zb2, Cm, D, D, B * T, a_kc=False, b_kc=False, lda=D, ldb=D, ldc=D, alpha=1.0 / (B * T))
+        loss = ops.lfd_loss(Cm, lam)
+        ctx.save_for_backward(za, zb, isa, isb, Cm)
+        ctx.args = (B, T, D, lam)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        za, zb, isa, isb, Cm = ctx.saved_tensors
+        B, T, D, lam = ctx.args
+        cd = rt.compute_dtype()
+        dC = ops.lfd_dloss(Cm, g.reshape(1).to(F32).contiguous(), lam, cd)
+        za2, zb2 = za.view(B * T, D), zb.view(B * T, D)
+        dza = torch.empty(B * T, D, device=za.device, dtype=F32)
+        dzb = torch.empty(B * T, D, device=za.device, dtype=F32)
+        # dza~[n][i] = sum_j dC[i][j] zb~[n][j] / BT ;  dzb~[n][j] = sum_i za~[n][i] dC[i][j] / BT
+        ops.gemm(zb2, dC, dza, B * T, D, D, a_kc=True, b_kc=True, lda=D, ldb=D, ldc=D, alpha=1.0 / (B * T))
+        ops.gemm(za2, dC, dzb, B * T, D, D, a_kc=True, b_kc=False, lda=D, ldb=D, ldc=D, alpha=1.0 / (B * T))
+        ga = ops.lfd_std_bwd(dza.view(B, T * D), za, isa).view(B, T, D)
+        gb = ops.lfd_std_bwd(dzb.view(B, T * D), zb, isb).view(B, T, D)
+        return ga, gb, None, None

@@ -1,0 +1,260 @@
+"""Thin torch-tensor wrappers over libfddm_hip (one function per C entry point, plus shape helpers).
+
+Every wrapper launches on torch's current HIP stream and checks the hipError_t. Tensors must be
+contiguous where the kernel assumes it; shapes are validated here before any launch so a kernel
+never sees operands that disagree with its grid.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ._lib import call
+
+F32, BF16 = 0, 1
+EPI_STORE, EPI_GELU, EPI_ACC, EPI_GELU_ONLY, EPI_DGELU = 0, 1, 2, 3, 4
+
+
+def code(t: torch.Tensor) -> int:
+    if t.dtype == torch.float32:
+        return F32
+    if t.dtype == torch.bfloat16:
+        return BF16
+    raise TypeError(f"unsupported dtype {t.dtype}")
+
+
+def tdtype(c: int):
+    return torch.float32 if c == F32 else torch.bfloat16
+
+
+def ptr(t):
+    return 0 if t is None else t.data_ptr()
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _chk(cond, msg):
+    if not cond:
+        raise ValueError(msg)
+
+
+# ------------------------------------------------------------------------------------------ GEMM
+def gemm(A, B, C, M, N, K, *, a_kc=True, b_kc=True, lda, ldb, ldc, epi=EPI_STORE, bias=None, alpha=1.0,
+         C2=None, Mi=0, sAb=0, drop_p=0.0, seed=0, rng_stream=0):
+    """C[m][n] = alpha * sum_k A(m,k) B(n,k) (+bias, epilogue). Compute dtype = B.dtype."""
+    _chk(B.dtype in (torch.float32, torch.bfloat16), "B dtype")
+    if M == 0 or N == 0:
+        return C
+    call("fddm_gemm", code(B), code(A), int(a_kc), int(b_kc), epi, code(C), ptr(A), lda, Mi, sAb, ptr(B), ldb,
+         ptr(C), ldc, ptr(C2), ptr(bias), float(alpha), M, N, K, seed, rng_stream, float(drop_p), stream())
+    return C
+
+
+def linear(x2d, w, bias=None, out_dtype=None, out=None, epi=EPI_STORE, C2=None, drop_p=0.0, seed=0, rng_stream=0):
+    """y[M,N] = x[M,K] @ w[N,K]^T + bias.  x, w: compute dtype (x may be f32 when w is bf16)."""
+    M, K = x2d.shape
+    N = w.shape[0]
+    _chk(w.shape[1] == K and x2d.stride(1) == 1 and w.is_contiguous(), "linear shapes")
+    if out is None:
+        out = torch.empty(M, N, device=x2d.device, dtype=out_dtype or w.dtype)
+    return gemm(x2d, w, out, M, N, K, lda=x2d.stride(0), ldb=K, ldc=out.stride(0), epi=epi, bias=bias, C2=C2,
+                drop_p=drop_p, seed=seed, rng_stream=rng_stream)
+
+
+def linear_dx(dy2d, w, out=None, accumulate=False, out_dtype=torch.float32, epi=None, C2=None, drop_p=0.0, seed=0,
+              rng_stream=0):
+    """dx[M,K] = dy[M,N] @ w[N,K]  (w M/N-contiguous operand). accumulate -> out (f32) += ."""
+    M, N = dy2d.shape
+    K = w.shape[1]
+    _chk(w.shape[0] == N and w.is_contiguous() and dy2d.stride(1) == 1, "linear_dx shapes")
+    if out is None:
+        out = torch.empty(M, K, device=dy2d.device, dtype=out_dtype)
+    e = EPI_ACC if accumulate else (EPI_STORE if epi is None else epi)
+    return gemm(dy2d, w, out, M, K, N, a_kc=True, b_kc=False, lda=dy2d.stride(0), ldb=K, ldc=out.stride(0), epi=e,
+                C2=C2, drop_p=drop_p, seed=seed, rng_stream=rng_stream)
+
+
+def linear_dw(dy2d, x2d, out=None, accumulate=False):
+    """dW[N,K] = dy[M,N]^T @ x[M,K]  (both M/N-contiguous operands, K-reduction over tokens)."""
+    M, N = dy2d.shape
+    K = x2d.shape[1]
+    _chk(x2d.shape[0] == M and dy2d.stride(1) == 1 and x2d.stride(1) == 1, "linear_dw shapes")
+    if out is None:
+        out = torch.empty(N, K, device=dy2d.device, dtype=torch.float32)
+    return gemm(dy2d, x2d, out, N, K, M, a_kc=False, b_kc=False, lda=dy2d.stride(0), ldb=x2d.stride(0),
+                ldc=out.stride(0), epi=EPI_ACC if accumulate else EPI_STORE)
+
+
+def colsum(X2d, out=None, accumulate=False):
+    M, N = X2d.shape
+    if out is None:
+        out = torch.zeros(N, device=X2d.device, dtype=torch.float32)
+    elif not accumulate:
+        out.zero_()
+    call("fddm_colsum", code(X2d), ptr(X2d), ptr(out), M, N, X2d.stride(0), stream())
+    return out
+
+
+def conv1d_gemm(x, W, out, *, lda, sAb, Tin, Cg, cstride, cpad, Bn, Tout, N, K, groups=1, bias=None, gelu=False):
+    call("fddm_conv1d_gemm", code(W), EPI_GELU_ONLY if gelu else EPI_STORE, ptr(x), lda, sAb, Tin, Cg, cstride,
+         cpad, ptr(W), ptr(out), out.shape[-1], ptr(bias), Bn, Tout, N, K, groups, stream())
+    return out
+
+
+def conv0_gn_gelu(wave, w, gamma, beta, out_dtype, C, K, S, eps=1e-5):
+    B, nsamp = wave.shape
+    T0 = (nsamp - K) // S + 1
+    sums = torch.zeros(2, B, C, device=wave.device, dtype=torch.float64)
+    out = torch.empty(B, T0, C, device=wave.device, dtype=out_dtype)
+    call("fddm_conv0_gn_gelu", code(out), ptr(wave), ptr(w), ptr(gamma), ptr(beta), ptr(sums[0]), ptr(sums[1]),
+         ptr(out), B, nsamp, T0, C, K, S, float(eps), stream())
+    return out
+
+
+def wavlm_gate(x2d, W, bias, cst, B, S, H):
+    E = x2d.shape[1]
+    gate = torch.empty(B * H, S, device=x2d.device, dtype=torch.float32)
+    call("fddm_wavlm_gate", code(x2d), ptr(x2d), ptr(W), ptr(bias), ptr(cst), ptr(gate), B, S, H, E, stream())
+    return gate
+
+
+# ------------------------------------------------------------------------------------- attention
+def attn_fwd(q, k, v, out, lse, B, H, Lq, Lk, *, key_keep=None, gate=None, table=None, drop_p=0.0, seed=0,
+             rng_stream=0, scale=None):
+    """q: [B*Lq, >=H*64] row stride q.stride(0); k/v: [B*Lk, ...]; out [B*Lq, H*64]; lse [B*H, Lq]."""
+    _chk(q.stride(-1) == 1 and k.stride(-1) == 1 and v.stride(-1) == 1, "attention inputs need unit inner stride")
+    _chk(q.dtype == k.dtype == v.dtype == out.dtype, "attention dtype mismatch")
+    sc = 1.0 / math.sqrt(64) if scale is None else scale
+    call("fddm_attn_fwd", code(q), ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out),
+         out.stride(0), ptr(lse), ptr(key_keep), ptr(gate), ptr(table), B, H, Lq, Lk, float(sc), float(drop_p), seed,
+         rng_stream, stream())
+    return out
+
+
+def attn_bwd(q, k, v, o, do, lse, dq, dk, dv, B, H, Lq, Lk, *, key_keep=None, drop_p=0.0, seed=0, rng_stream=0):
+    delta = torch.empty(B * H, Lq, device=q.device, dtype=torch.float32)
+    call("fddm_attn_bwd", code(q), ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(o),
+         o.stride(0), ptr(do), do.stride(0), ptr(lse), ptr(dq), dq.stride(0), ptr(dk), dk.stride(0), ptr(dv),
+         dv.stride(0), ptr(delta), ptr(key_keep), B, H, Lq, Lk, float(1.0 / 8.0), float(drop_p), seed, rng_stream,
+         stream())
+
+
+# ----------------------------------------------------------------------------------- layernorm
+def ln_fwd(x, y, gamma, beta, *, out_f32=None, out_t=None, save_s=None, mean=None, rstd=None, film=None,
+           rows_per_batch=0, eps=1e-5, drop_p=0.0, seed=0, rng_stream=0):
+    N, d = x.shape
+    fs, fh = film if film is not None else (None, None)
+    out_code = code(out_t) if out_t is not None else code(x if y is None else y)
+    ycode = code(y) if y is not None else code(x)
+    call("fddm_ln_fwd", code(x), ycode, out_code, ptr(x), ptr(y), ptr(gamma), ptr(beta), ptr(fs), ptr(fh),
+         ptr(out_f32), ptr(out_t), ptr(save_s), ptr(mean), ptr(rstd), N, d, rows_per_batch, float(eps), float(drop_p),
+         seed, rng_stream, stream())
+
+
+def ln_bwd(dout, s, mean, rstd, gamma, beta, *, dres=None, dy_t=None, dgamma=None, dbeta=None, film_scale=None,
+           dfilm=None, rows_per_batch=0, drop_p=0.0, seed=0, rng_stream=0):
+    N, d = dout.shape
+    dfs, dfh = dfilm if dfilm is not None else (None, None)
+    call("fddm_ln_bwd", code(dy_t) if dy_t is not None else F32, ptr(dout), ptr(s), ptr(mean), ptr(rstd), ptr(gamma),
+         ptr(beta), ptr(film_scale), ptr(dres), ptr(dy_t), ptr(dgamma), ptr(dbeta), ptr(dfs), ptr(dfh), N, d,
+         rows_per_batch, float(drop_p), seed, rng_stream, stream())
+
+
+# -------------------------------------------------------------------------------- small kernels
+def rope_fwd(x, cs, sn, out, L):
+    N, d = x.shape
+    call("fddm_rope_fwd", code(out), ptr(x), ptr(cs), ptr(sn), ptr(out), N, L, d, stream())
+    return out
+
+
+def rope_bwd(dy, cs, sn, dx, L):
+    N, d = dy.shape
+    call("fddm_rope_bwd", ptr(dy), ptr(cs), ptr(sn), ptr(dx), N, L, d, stream())
+
+
+def embed_fwd(tok, E, tbias, out, out_t, L):
+    N = tok.numel()
+    d = E.shape[1]
+    call("fddm_embed_fwd", code(out_t) if out_t is not None else F32, ptr(tok), ptr(E), ptr(tbias), ptr(out),
+         ptr(out_t), N, L, d, stream())
+
+
+def embed_bwd(tok, dx, dE, dtb, L, pad_id):
+    N, d = dx.shape
+    call("fddm_embed_bwd", ptr(tok), ptr(dx), ptr(dE), ptr(dtb), N, L, d, pad_id, stream())
+
+
+def cast(x, dtype, out=None):
+    if out is None:
+        out = torch.empty(x.shape, device=x.device, dtype=dtype)
+    call("fddm_cast", code(x), code(out), ptr(x), ptr(out), x.numel(), stream())
+    return out
+
+
+def sample_q(x0, t, thr, K, seed, rng_stream=1):
+    B, L = x0.shape
+    xt = torch.empty_like(x0)
+    call("fddm_sample_q", ptr(x0), ptr(t), ptr(thr), ptr(xt), B, L, K, seed, rng_stream, stream())
+    return xt
+
+
+def kl_fwd(logits2d, xt, x0, t, betas, L):
+    N, V = logits2d.shape
+    kl = torch.empty(N, device=logits2d.device, dtype=torch.float32)
+    call("fddm_kl_fwd", ptr(logits2d), ptr(xt), ptr(x0), ptr(t), ptr(betas), ptr(kl), N, L, V, stream())
+    return kl
+
+
+def kl_bwd(logits2d, xt, x0, t, betas, w, gscale, L, out_dtype=torch.float32):
+    N, V = logits2d.shape
+    dz = torch.empty(N, V, device=logits2d.device, dtype=out_dtype)
+    call("fddm_kl_bwd", ptr(logits2d), ptr(xt), ptr(x0), ptr(t), ptr(betas), ptr(w), ptr(gscale), ptr(dz),
+         code(dz), N, L, V, stream())
+    return dz
+
+
+def softmax_rows(x2d, out_dtype):
+    N, V = x2d.shape
+    y = torch.empty(N, V, device=x2d.device, dtype=out_dtype)
+    call("fddm_softmax_rows", ptr(x2d), ptr(y), code(y), N, V, stream())
+    return y
+
+
+def softmax_bwd_rows(y, dy, dz=None, accumulate=False):
+    N, V = y.shape
+    if dz is None:
+        dz = torch.empty(N, V, device=y.device, dtype=torch.float32)
+    call("fddm_softmax_bwd_rows", ptr(y), ptr(dy), ptr(dz), code(y), N, V, int(accumulate), stream())
+    return dz
+
+
+def lfd_std_fwd(z2d, out_dtype, eps=1e-5):
+    B, C = z2d.shape
+    zt = torch.empty(B, C, device=z2d.device, dtype=out_dtype)
+    inv_std = torch.empty(C, device=z2d.device, dtype=torch.float32)
+    call("fddm_lfd_std_fwd", code(zt), ptr(z2d), ptr(zt), ptr(inv_std), B, C, float(eps), stream())
+    return zt, inv_std
+
+
+def lfd_std_bwd(dzt, zt, inv_std):
+    B, C = dzt.shape
+    dz = torch.empty(B, C, device=dzt.device, dtype=torch.float32)
+    call("fddm_lfd_std_bwd", code(zt), ptr(dzt), ptr(zt), ptr(inv_std), ptr(dz), B, C, stream())
+    return dz
+
+
+def lfd_loss(Cm, lam):
+    D = Cm.shape[0]
+    loss = torch.empty((), device=Cm.device, dtype=torch.float32)
+    call("fddm_lfd_loss", ptr(Cm), ptr(loss), D, float(lam), stream())
+    return loss
+
+
+def lfd_dloss(Cm, gscale, lam, out_dtype):
+    D = Cm.shape[0]
+    dC = torch.empty(D, D, device=Cm.device, dtype=out_dtype)
+    call("fddm_lfd_dloss", code(dC), ptr(Cm), ptr(gscale), ptr(dC), D, float(lam), stream())
+    return dC

@@ -1,0 +1,162 @@
+"""Runtime state shared by the modules: compute precision, cached low-precision weight copies,
+dropout seeds, and small per-shape tables (RoPE cos/sin, WavLM relative-position bias).
+
+Precision modes (SURVEY §7 "Two precision modes"):
+  * "bf16" (default on GPU): MFMA bf16 with fp32 accumulation; residual stream, LayerNorm, softmax,
+    KL and L_fd statistics in fp32; fp32 master weights + AdamW.
+  * "fp32": every kernel in exact fp32 (f32-input MFMA) — the parity mode checked against the oracle.
+"""
+from __future__ import annotations
+
+import contextlib
+import itertools
+import math
+import os
+
+import torch
+
+from . import ops
+
+_precision = os.environ.get("FDDM_PRECISION", "bf16")
+
+
+def precision() -> str:
+    return _precision
+
+
+def set_precision(p: str) -> None:
+    global _precision
+    if p not in ("bf16", "fp32"):
+        raise ValueError(p)
+    _precision = p
+
+
+@contextlib.contextmanager
+def use_precision(p: str):
+    old = _precision
+    set_precision(p)
+    try:
+        yield
+    finally:
+        set_precision(old)
+
+
+def compute_dtype():
+    return torch.bfloat16 if _precision == "bf16" else torch.float32
+
+
+# --------------------------------------------------------------------------------- weight cache
+class _Entry:
+    __slots__ = ("version", "tensor", "ptr")
+
+
+_wcache: dict = {}
+
+
+def wt(p: torch.Tensor, dtype=None, transform=None, key=None) -> torch.Tensor:
+    """Return `p` in the compute dtype (cached; refreshed when p changes in place).
+
+    `transform(p) -> tensor` builds a derived layout (e.g. conv weights permuted for the implicit GEMM);
+    it is keyed by `key`. fp32 + no transform returns p itself.
+    """
+    dtype = dtype or compute_dtype()
+    if transform is None and dtype == p.dtype and p.is_contiguous():
+        return p.detach()
+    k = (id(p), dtype, key)
+    e = _wcache.get(k)
+    if e is not None and e.version == p._version and e.ptr == p.data_ptr():
+        return e.tensor
+    with torch.no_grad():
+        src = transform(p.detach()) if transform is not None else p.detach()
+        src = src.contiguous()
+        out = src if src.dtype == dtype else ops.cast(src, dtype)
+    e = _Entry()
+    e.version, e.tensor, e.ptr = p._version, out, p.data_ptr()
+    _wcache[k] = e
+    return out
+
+
+def wt_refresh_from(p: torch.Tensor, bf16_copy: torch.Tensor) -> None:
+    """Record a bf16 copy written by the fused optimizer as current for `p`."""
+    e = _Entry()
+    e.version, e.tensor, e.ptr = p._version, bf16_copy, p.data_ptr()
+    _wcache[(id(p), torch.bfloat16, None)] = e
+
+
+def wt_bf16_buffer(p: torch.Tensor) -> torch.Tensor:
+    """The cached bf16 copy buffer of p (allocating it), for the optimizer to write in place."""
+    k = (id(p), torch.bfloat16, None)
+    e = _wcache.get(k)
+    if e is None or e.tensor.shape != p.shape:
+        return wt(p, torch.bfloat16)
+    return e.tensor
+
+
+def clear_cache():
+    _wcache.clear()
+    _tables.clear()
+
+
+# ---------------------------------------------------------------------------------------- seeds
+_seed_counter = itertools.count(1)
+_base_seed = None
+
+
+def next_seed() -> int:
+    """A fresh dropout seed per forward call (deterministic given torch.initial_seed())."""
+    global _base_seed
+    if _base_seed is None:
+        _base_seed = int(torch.initial_seed()) & 0xFFFFFFFF
+    return (_base_seed * 1000003 + next(_seed_counter)) & 0x7FFFFFFFFFFFFFFF
+
+
+def reseed(seed: int) -> None:
+    global _base_seed, _seed_counter
+    _base_seed = int(seed) & 0xFFFFFFFF
+    _seed_counter = itertools.count(1)
+
+
+# --------------------------------------------------------------------------------------- tables
+_tables: dict = {}
+
+
+def rope_tables(L: int, inv_freq: torch.Tensor, device):
+    """cos/sin [L, d] exactly as RoPEEmbedding.forward (models/denoise_decoder.py:35-40), computed on
+    the host once per (L, d) and kept resident."""
+    k = ("rope", L, inv_freq.numel(), float(inv_freq[-1]) if inv_freq.numel() else 0.0, str(device))
+    t = _tables.get(k)
+    if t is None:
+        f = inv_freq.detach().float().cpu()
+        pos = torch.arange(L, dtype=f.dtype)
+        fr = torch.outer(pos, f)
+        emb = torch.cat((fr, fr), dim=-1)
+        t = (emb.cos().contiguous().to(device), emb.sin().contiguous().to(device))
+        _tables[k] = t
+    return t
+
+
+def rel_bucket(rel: torch.Tensor, num_buckets: int, max_distance: int) -> torch.Tensor:
+    """Relative-position buckets, HF modeling_wavlm.py:253-271 (integer-exact host computation)."""
+    nb = num_buckets // 2
+    buckets = (rel > 0).to(torch.long) * nb
+    rel = torch.abs(rel)
+    max_exact = nb // 2
+    is_small = rel < max_exact
+    large = torch.log(rel.float() / max_exact)
+    large = large / math.log(max_distance / max_exact)
+    large = large * (nb - max_exact)
+    large = (max_exact + large).to(torch.long)
+    large = torch.min(large, torch.full_like(large, nb - 1))
+    return buckets + torch.where(is_small, rel, large)
+
+
+def relbias_table(S: int, embed: torch.Tensor, num_buckets: int, max_distance: int):
+    """[H, 2S-1] fp32: table[h][r] = rel_attn_embed[bucket(r - (S-1))][h]  (r = key - query + S - 1)."""
+    k = ("rel", S, id(embed), embed._version, num_buckets, max_distance)
+    t = _tables.get(k)
+    if t is None:
+        rel = torch.arange(-(S - 1), S)
+        b = rel_bucket(rel, num_buckets, max_distance).to(embed.device)
+        t = embed.detach().float()[b].t().contiguous()
+        _tables[k] = t
+    return t

@@ -1,0 +1,227 @@
+"""Frozen WavLM encoder (forward only) on libfddm_hip.
+
+Parameter tree and state_dict names are those of transformers' WavLMModel (post-LN "group"
+geometry, HF modeling_wavlm.py:37-1088), so HF checkpoints of that family load with
+load_state_dict. The forward is a fixed kernel sequence per utterance batch:
+  conv0+GroupNorm+GELU -> 6 x implicit-GEMM conv+GELU -> LN -> Linear -> grouped positional
+  implicit-GEMM conv+GELU -> +x -> LN -> 12 x [gate, QKV GEMM, rel-bias flash attention, out GEMM,
+  +x LN, FF GEMM(GELU), FF GEMM, +x LN]
+All activations are channels-last [B, T, C] in the compute dtype.
+"""
+from __future__ import annotations
+
+import json
+import os
+from types import SimpleNamespace
+
+import torch
+import torch.nn as nn
+
+from fddm_hip import ops
+from fddm_hip import runtime as rt
+
+WAVLM_BASE = dict(hidden_size=768, num_hidden_layers=12, num_attention_heads=12, intermediate_size=3072,
+                  conv_dim=(512,) * 7, conv_kernel=(10, 3, 3, 3, 3, 2, 2), conv_stride=(5, 2, 2, 2, 2, 2, 2),
+                  conv_bias=False, num_conv_pos_embeddings=128, num_conv_pos_embedding_groups=16, num_buckets=320,
+                  max_bucket_distance=800, layer_norm_eps=1e-5, feat_extract_norm="group", do_stable_layer_norm=False,
+                  mask_time_prob=0.05, hidden_act="gelu", feat_extract_activation="gelu")
+
+
+def wavlm_config(**over) -> SimpleNamespace:
+    cfg = dict(WAVLM_BASE)
+    cfg.update({k: v for k, v in over.items() if k in WAVLM_BASE or k in ("mask_feature_prob",)})
+    return SimpleNamespace(**cfg)
+
+
+class _Sub(nn.Module):
+    pass
+
+
+class WavLMModel(nn.Module):
+    def __init__(self, config: SimpleNamespace):
+        super().__init__()
+        c = config
+        if c.feat_extract_norm != "group" or c.do_stable_layer_norm or c.conv_bias:
+            raise NotImplementedError("only the post-LN 'group' WavLM geometry (WavLM-base family) is built")
+        if c.hidden_size // c.num_attention_heads != 64:
+            raise NotImplementedError("head_dim must be 64")
+        self.config = c
+        fe = _Sub()
+        fe.conv_layers = nn.ModuleList()
+        cin = 1
+        for i, (co, k, s) in enumerate(zip(c.conv_dim, c.conv_kernel, c.conv_stride)):
+            layer = _Sub()
+            layer.conv = nn.Conv1d(cin, co, kernel_size=k, stride=s, bias=False)
+            if i == 0:
+                layer.layer_norm = nn.GroupNorm(co, co, affine=True)
+            fe.conv_layers.append(layer)
+            cin = co
+        self.feature_extractor = fe
+        fp = _Sub()
+        fp.layer_norm = nn.LayerNorm(c.conv_dim[-1], eps=c.layer_norm_eps)
+        fp.projection = nn.Linear(c.conv_dim[-1], c.hidden_size)
+        self.feature_projection = fp
+        if c.mask_time_prob > 0.0:
+            self.masked_spec_embed = nn.Parameter(torch.zeros(c.hidden_size).uniform_())
+        enc = _Sub()
+        pce = _Sub()
+        conv = nn.Conv1d(c.hidden_size, c.hidden_size, kernel_size=c.num_conv_pos_embeddings,
+                         padding=c.num_conv_pos_embeddings // 2, groups=c.num_conv_pos_embedding_groups)
+        pce.conv = nn.utils.parametrizations.weight_norm(conv, name="weight", dim=2)
+        enc.pos_conv_embed = pce
+        enc.layer_norm = nn.LayerNorm(c.hidden_size, eps=c.layer_norm_eps)
+        enc.layers = nn.ModuleList()
+        E, H = c.hidden_size, c.num_attention_heads
+        for i in range(c.num_hidden_layers):
+            L = _Sub()
+            a = _Sub()
+            a.k_proj, a.v_proj, a.q_proj, a.out_proj = (nn.Linear(E, E) for _ in range(4))
+            a.gru_rel_pos_const = nn.Parameter(torch.ones(1, H, 1, 1))
+            a.gru_rel_pos_linear = nn.Linear(E // H, 8)
+            if i == 0:
+                a.rel_attn_embed = nn.Embedding(c.num_buckets, H)
+            L.attention = a
+            L.layer_norm = nn.LayerNorm(E, eps=c.layer_norm_eps)
+            ff = _Sub()
+            ff.intermediate_dense = nn.Linear(E, c.intermediate_size)
+            ff.output_dense = nn.Linear(c.intermediate_size, E)
+            L.feed_forward = ff
+            L.final_layer_norm = nn.LayerNorm(E, eps=c.layer_norm_eps)
+            enc.layers.append(L)
+        self.encoder = enc
+        self._prep_key = None
+        self._prep = None
+
+    # ------------------------------------------------------------------ prepared (cast/permuted) weights
+    def _prepared(self, cd):
+        key = (cd,) + tuple((p.data_ptr(), p._version) for p in self.parameters())
+        if self._prep_key == key:
+            return self._prep
+        c = self.config
+        P = {}
+        with torch.no_grad():
+            def T(x):
+                x = x.detach().contiguous()
+                return x if x.dtype == cd else ops.cast(x.float().contiguous(), cd)
+
+            cl = self.feature_extractor.conv_layers
+            P["w0"] = cl[0].conv.weight.detach().float().reshape(c.conv_dim[0], -1).contiguous()
+            P["gn"] = (cl[0].layer_norm.weight.detach().float().contiguous(), cl[0].layer_norm.bias.detach().float().contiguous())
+            P["conv"] = [T(cl[i].conv.weight.permute(0, 2, 1)) for i in range(1, len(cl))]
+            fp = self.feature_projection
+            P["fp_ln"] = (fp.layer_norm.weight.detach().float(), fp.layer_norm.bias.detach().float())
+            P["fp"] = (T(fp.projection.weight), fp.projection.bias.detach().float())
+            pc = self.encoder.pos_conv_embed.conv
+            w = pc.weight.detach()                                   # weight-norm applied [E, E/G, k]
+            G = c.num_conv_pos_embedding_groups
+            E = c.hidden_size
+            Cg = E // G
+            P["pos"] = (T(w.view(G, Cg, Cg, -1).permute(0, 1, 3, 2)), pc.bias.detach().float().contiguous())
+            P["enc_ln"] = (self.encoder.layer_norm.weight.detach().float(), self.encoder.layer_norm.bias.detach().float())
+            layers = []
+            for L in self.encoder.layers:
+                a = L.attention
+                layers.append(dict(
+                    qkv=T(torch.cat([a.q_proj.weight, a.k_proj.weight, a.v_proj.weight], 0)),
+                    bqkv=torch.cat([a.q_proj.bias, a.k_proj.bias, a.v_proj.bias], 0).detach().float().contiguous(),
+                    o=(T(a.out_proj.weight), a.out_proj.bias.detach().float()),
+                    gru=(a.gru_rel_pos_linear.weight.detach().float().contiguous(),
+                         a.gru_rel_pos_linear.bias.detach().float().contiguous(),
+                         a.gru_rel_pos_const.detach().float().reshape(-1).contiguous()),
+                    ln1=(L.layer_norm.weight.detach().float(), L.layer_norm.bias.detach().float()),
+                    f1=(T(L.feed_forward.intermediate_dense.weight), L.feed_forward.intermediate_dense.bias.detach().float()),
+                    f2=(T(L.feed_forward.output_dense.weight), L.feed_forward.output_dense.bias.detach().float()),
+                    ln2=(L.final_layer_norm.weight.detach().float(), L.final_layer_norm.bias.detach().float()),
+                ))
+            P["layers"] = layers
+        self._prep_key, self._prep = key, P
+        return P
+
+    def frames(self, nsamp: int) -> int:
+        T = nsamp
+        for k, s in zip(self.config.conv_kernel, self.config.conv_stride):
+            T = (T - k) // s + 1
+        return T
+
+    @torch.no_grad()
+    def forward_hidden(self, wave: torch.Tensor) -> torch.Tensor:
+        """last_hidden_state [B, S, E] in the compute dtype (eval mode, attention_mask=None)."""
+        c = self.config
+        cd = rt.compute_dtype()
+        P = self._prepared(cd)
+        wave = wave.float().contiguous()
+        B, nsamp = wave.shape
+        # conv feature extractor (HF:747-782)
+        h = ops.conv0_gn_gelu(wave, P["w0"], P["gn"][0], P["gn"][1], cd, c.conv_dim[0], c.conv_kernel[0],
+                              c.conv_stride[0])
+        T = h.shape[1]
+        cin = c.conv_dim[0]
+        for i in range(1, len(c.conv_dim)):
+            k, s, co = c.conv_kernel[i], c.conv_stride[i], c.conv_dim[i]
+            Tout = (T - k) // s + 1
+            out = torch.empty(B, Tout, co, device=wave.device, dtype=cd)
+            ops.conv1d_gemm(h, P["conv"][i - 1], out, lda=cin, sAb=T * cin, Tin=T, Cg=cin, cstride=s, cpad=0, Bn=B,
+                            Tout=Tout, N=co, K=k * cin, gelu=True)
+            h, T, cin = out, Tout, co
+        S, E, H = T, c.hidden_size, c.num_attention_heads
+        eps = c.layer_norm_eps
+        # feature projection (HF:93-105)
+        h2 = h.view(B * S, cin)
+        hn = torch.empty_like(h2)
+        ops.ln_fwd(h2, None, P["fp_ln"][0], P["fp_ln"][1], out_t=hn, eps=eps)
+        x = ops.linear(hn, P["fp"][0], P["fp"][1], out_dtype=cd)
+        # positional conv embedding + LN (HF:37-90, 399-407)
+        G = c.num_conv_pos_embedding_groups
+        Cg = E // G
+        kp = c.num_conv_pos_embeddings
+        pos = torch.empty(B * S, E, device=wave.device, dtype=cd)
+        ops.conv1d_gemm(x, P["pos"][0], pos, lda=E, sAb=S * E, Tin=S, Cg=Cg, cstride=1, cpad=kp // 2, Bn=B, Tout=S,
+                        N=Cg, K=kp * Cg, groups=G, bias=P["pos"][1], gelu=True)
+        xn = torch.empty_like(x)
+        ops.ln_fwd(x, pos, P["enc_ln"][0], P["enc_ln"][1], out_t=xn, eps=eps)
+        x = xn
+        table = rt.relbias_table(S, self.encoder.layers[0].attention.rel_attn_embed.weight, c.num_buckets,
+                                 c.max_bucket_distance)
+        for Lp in P["layers"]:
+            gate = ops.wavlm_gate(x, Lp["gru"][0], Lp["gru"][1], Lp["gru"][2], B, S, H)
+            qkv = ops.linear(x, Lp["qkv"], Lp["bqkv"], out_dtype=cd)
+            o = torch.empty(B * S, E, device=wave.device, dtype=cd)
+            ops.attn_fwd(qkv, qkv[:, E:], qkv[:, 2 * E:], o, None, B, H, S, S, gate=gate, table=table)
+            y = ops.linear(o, Lp["o"][0], Lp["o"][1], out_dtype=cd)
+            x1 = torch.empty_like(x)
+            ops.ln_fwd(x, y, Lp["ln1"][0], Lp["ln1"][1], out_t=x1, eps=eps)
+            hh = ops.linear(x1, Lp["f1"][0], Lp["f1"][1], out_dtype=cd, epi=ops.EPI_GELU_ONLY)
+            y = ops.linear(hh, Lp["f2"][0], Lp["f2"][1], out_dtype=cd)
+            x = torch.empty_like(x1)
+            ops.ln_fwd(x1, y, Lp["ln2"][0], Lp["ln2"][1], out_t=x, eps=eps)
+        return x.view(B, S, E)
+
+    def forward(self, input_values, attention_mask=None, output_hidden_states=False, **kw):
+        if attention_mask is not None:
+            raise NotImplementedError("attention_mask is never passed on the train step (lengths=None)")
+        return SimpleNamespace(last_hidden_state=self.forward_hidden(input_values))
+
+    # ------------------------------------------------------------------ loading
+    @classmethod
+    def from_pretrained(cls, name_or_path, geometry: dict | None = None):
+        """Local directory with config.json (+ model.safetensors / pytorch_model.bin) -> loaded weights.
+        Anything else (e.g. a hub name; there is no network) -> WavLM-base geometry, random init."""
+        if isinstance(name_or_path, dict):
+            return cls(wavlm_config(**name_or_path))
+        path = str(name_or_path)
+        if os.path.isdir(path) and os.path.exists(os.path.join(path, "config.json")):
+            cfg = json.load(open(os.path.join(path, "config.json")))
+            m = cls(wavlm_config(**cfg))
+            sd = None
+            st_path = os.path.join(path, "model.safetensors")
+            bin_path = os.path.join(path, "pytorch_model.bin")
+            if os.path.exists(st_path):
+                from safetensors.torch import load_file
+                sd = load_file(st_path)
+            elif os.path.exists(bin_path):
+                sd = torch.load(bin_path, map_location="cpu", weights_only=True)
+            if sd is not None:
+                sd = {k[len("wavlm."):] if k.startswith("wavlm.") else k: v for k, v in sd.items()}
+                m.load_state_dict(sd, strict=False)
+            return m
+        return cls(wavlm_config(**(geometry or {})))

@@ -1,0 +1,242 @@
+"""FDDM-ASR training entry point on MI355X (drop-in for the reference's train.py).
+
+Keeps the reference surface: `python train.py --config configs/fddm_zhTW_base.yaml [--device]`, the
+`Config` dataclass (exactly the 8 top-level YAML keys), `SchedulerAdapter` (sample_q / kl_term / w_t)
+and `train_one_epoch(...)` with the same arguments and return value, and the checkpoint layout
+(`decoder`, `s_proj`, `t_embed`, `t_proj`, `epoch`, `step`, `config`).
+
+The step itself (train.py:340-443 of the reference) runs on libfddm_hip: fused q_sample draw, fused
+categorical KL, fused decoder blocks, fused L_fd, fused clip+AdamW; optional data-parallel gradient
+all-reduce over RCCL (fddm_hip.dist) when torch.distributed is initialised.
+"""
+from __future__ import annotations
+
+import argparse
+import logging
+import os
+import random
+from dataclasses import dataclass
+from datetime import datetime
+
+import torch
+import yaml
+
+from fddm.sched.diffusion_scheduler import DiscreteDiffusionScheduler
+from fddm_hip import dist as fdist
+from fddm_hip import functions as FN
+from fddm_hip import runtime as rt
+from fddm_hip.optim import FusedAdamW
+from losses.fddm_losses import lfd_loss
+from models.acoustic_encoder import AcousticEncoder
+from models.denoise_decoder import DenoisingTransformerDecoder
+from models.projection import SpeechProjector, TextEmbedding, TextProjector
+
+try:
+    from tqdm import tqdm
+except Exception:  # pragma: no cover
+    tqdm = None
+
+
+@dataclass
+class Config:
+    """YAML schema of configs/fddm_zhTW_base.yaml (reference train.py:164-173)."""
+    seed: int
+    data: dict
+    model: dict
+    diffusion: dict
+    inference: dict
+    optim: dict
+    lfd: dict
+    log: dict
+
+
+class SchedulerAdapter:
+    """train.py:176-273 of the reference. Dispatches to the fused kernels when the scheduler offers
+    them (same hasattr style as the reference's w_t)."""
+
+    def __init__(self, scheduler):
+        self.sch = scheduler
+
+    def sample_q(self, x0: torch.Tensor, t: torch.Tensor) -> torch.Tensor:
+        if hasattr(self.sch, "sample_xt"):
+            return self.sch.sample_xt(x0, t, rt.next_seed())
+        B, L = x0.shape
+        onehot = torch.zeros(B, L, self.sch.K, device=x0.device)
+        onehot.scatter_(-1, x0.unsqueeze(-1), 1.0)
+        p = self.sch.q_sample(onehot, t)
+        return torch.multinomial(p.view(-1, self.sch.K), 1).view(B, L)
+
+    def kl_term(self, xt, x0, logits_x0, t, x_mask=None) -> torch.Tensor:
+        if not hasattr(self.sch, "betas"):
+            raise ValueError("scheduler must provide betas [T] to build the posterior")
+        B, L, V = logits_x0.shape
+        eps = 1e-8
+        if x_mask is not None:
+            valid = x_mask.float()
+            w = (valid / (valid.sum(dim=1, keepdim=True) + eps) / B).reshape(-1).contiguous()
+        else:
+            w = torch.full((B * L,), 1.0 / (L * B), device=logits_x0.device)
+        betas = self.sch.betas.to(logits_x0.device).float().contiguous()
+        return FN.KLFn.apply(logits_x0.float(), xt, x0, t, w, betas)
+
+    def w_t(self, t: torch.Tensor) -> torch.Tensor:
+        if hasattr(self.sch, "alpha_bar"):
+            return self.sch.alpha_bar.to(t.device)[t - 1]
+        if hasattr(self.sch, "w_prefix"):
+            return self.sch.w_prefix.to(t.device)[t - 1]
+        if hasattr(self.sch, "betas"):
+            cp = torch.cumprod(1.0 - self.sch.betas.to(t.device), 0)
+            return cp[t - 1]
+        return torch.ones_like(t, dtype=torch.float32)
+
+
+def align_speech(z_speech: torch.Tensor, L: int) -> torch.Tensor:
+    """train.py:382-387: truncate, or repeat the last frame."""
+    S = z_speech.size(1)
+    if S >= L:
+        return z_speech[:, :L, :]
+    return torch.cat([z_speech, z_speech[:, -1:, :].repeat(1, L - S, 1)], dim=1)
+
+
+def train_one_epoch(encoder, decoder, s_proj, t_embed, t_proj, scheduler, loader, optimizer, device, cfg,
+                    global_step, scaler=None, epoch=1, print_epoch_summary=True, draw_t=None):
+    """reference train.py:293-449. `draw_t(B)` (optional) supplies t on the device; default
+    torch.randint(1, T+1) like the reference. Loss values stay on the device; the progress line is
+    refreshed every log.log_every steps so the step loop does not wait on the GPU."""
+    encoder.eval()
+    decoder.train()
+    s_proj.train()
+    t_embed.train()
+    t_proj.train()
+    pad_id = cfg.data["pad_id"]
+    T_total = cfg.diffusion["T"]
+    log_every = max(1, int(cfg.log.get("log_every", 50)))
+    n_step_fd = cfg.lfd["n_step_fd"]
+    tau = cfg.lfd.get("tau", 1.0)
+    lambda_off = cfg.lfd["lambda_offdiag"]
+    trainable = list(decoder.parameters()) + list(s_proj.parameters()) + list(t_embed.parameters()) + \
+        list(t_proj.parameters())
+    pbar = loader
+    if tqdm is not None and print_epoch_summary:
+        pbar = tqdm(loader, desc=f"Epoch {epoch} [train]", leave=False)
+    loss_sum = torch.zeros((), device=device)
+    nsteps = 0
+    for batch in pbar:
+        wave, x0 = batch
+        wave = wave.to(device, non_blocking=True)
+        x0 = x0.to(device, non_blocking=True)
+        B, L = x0.shape
+        c, c_mask, _ = encoder(wave)
+        t = draw_t(B) if draw_t is not None else torch.randint(1, T_total + 1, (B,), device=device)
+        xt = scheduler.sample_q(x0, t)
+        x_mask = x0 != pad_id
+        logits = decoder(xt, t, c, x_mask=x_mask, c_mask=c_mask)
+        loss_diff = scheduler.kl_term(xt, x0, logits, t, x_mask)
+        loss = loss_diff
+        loss_fd = None
+        if global_step % n_step_fd == 0:
+            z_text = t_proj(t_embed(logits))
+            z_speech = align_speech(s_proj(c), L)
+            w_t = scheduler.w_t(t).mean()
+            loss_fd = lfd_loss(z_speech, z_text, lambda_offdiag=lambda_off)
+            loss = loss + tau * w_t * loss_fd
+        optimizer.zero_grad(set_to_none=True)
+        if scaler is not None:
+            scaler.scale(loss).backward()
+            scaler.unscale_(optimizer)
+            fdist.allreduce_grads(trainable)
+            torch.nn.utils.clip_grad_norm_([p for p in trainable if p.grad is not None], max_norm=5.0)
+            scaler.step(optimizer)
+            scaler.update()
+        else:
+            loss.backward()
+            fdist.allreduce_grads(trainable)
+            if hasattr(optimizer, "clip_and_step"):
+                optimizer.clip_and_step(max_norm=5.0)
+            else:
+                torch.nn.utils.clip_grad_norm_([p for p in trainable if p.grad is not None], max_norm=5.0)
+                optimizer.step()
+        loss_sum += loss.detach()
+        nsteps += 1
+        if tqdm is not None and print_epoch_summary and (global_step % log_every == 0):
+            post = {"step": global_step, "loss": f"{float(loss):.3f}", "diff": f"{float(loss_diff):.3f}"}
+            if loss_fd is not None:
+                post["lfd"] = f"{float(loss_fd):.3f}"
+            pbar.set_postfix(post)
+        global_step += 1
+    avg = float(loss_sum) / max(1, nsteps)
+    if print_epoch_summary:
+        logging.info(f"[Summary] Epoch {epoch} Avg Train Loss: {avg:.4f}")
+    return global_step, avg
+
+
+def setup_logging():
+    os.makedirs("logs", exist_ok=True)
+    ts = datetime.now().strftime("%Y%m%d_%H%M%S")
+    logger = logging.getLogger()
+    logger.setLevel(logging.INFO)
+    logger.handlers.clear()
+    fmt = logging.Formatter("%(asctime)s - %(levelname)s - %(message)s")
+    for h in (logging.FileHandler(os.path.join("logs", f"train_{ts}.log"), encoding="utf-8"), logging.StreamHandler()):
+        h.setFormatter(fmt)
+        logger.addHandler(h)
+
+
+def build_models(cfg: Config, device):
+    d_model = cfg.model["d_model"]
+    vocab = cfg.data["vocab_size"]
+    pad_id = cfg.data["pad_id"]
+    encoder = AcousticEncoder(**cfg.model["encoder"], d_model=d_model).to(device)
+    decoder = DenoisingTransformerDecoder(vocab_size=vocab, d_model=d_model, nhead=cfg.model["nhead"],
+                                          num_layers=cfg.model["num_layers"], dim_ff=cfg.model["dim_ff"],
+                                          dropout=cfg.model["dropout"], max_len=1024, pad_id=pad_id).to(device)
+    d_proj = cfg.model["projector"]["d_proj"]
+    s_proj = SpeechProjector(d_in=d_model, d_proj=d_proj).to(device)
+    t_embed = TextEmbedding(vocab=vocab, d_out=d_proj, mode="logits").to(device)
+    t_proj = TextProjector(d_in=d_proj, d_proj=d_proj).to(device)
+    sched = SchedulerAdapter(DiscreteDiffusionScheduler(K=vocab, T=cfg.diffusion["T"], device=device,
+                                                        beta_max=cfg.diffusion["beta_max"]))
+    return encoder, decoder, s_proj, t_embed, t_proj, sched
+
+
+def main():
+    ap = argparse.ArgumentParser(description="FDDM-ASR Training Script (MI355X)")
+    ap.add_argument("--config", type=str, required=True)
+    ap.add_argument("--device", type=str, default="cuda" if torch.cuda.is_available() else "cpu")
+    args = ap.parse_args()
+    setup_logging()
+    with open(args.config, "r", encoding="utf-8") as f:
+        raw = yaml.safe_load(f)
+    cfg = Config(**raw)
+    random.seed(cfg.seed)
+    torch.manual_seed(cfg.seed)
+    rt.reseed(cfg.seed)
+    rt.set_precision(cfg.optim.get("precision", "bf16"))
+    device = torch.device(args.device)
+    if device.type != "cuda":
+        raise RuntimeError("the MI355X build runs on a HIP device only (no CPU fallback)")
+    encoder, decoder, s_proj, t_embed, t_proj, sched = build_models(cfg, device)
+    params = list(decoder.parameters()) + list(s_proj.parameters()) + list(t_embed.parameters()) + \
+        list(t_proj.parameters())
+    optim = FusedAdamW(params, lr=cfg.optim["lr"], weight_decay=cfg.optim["weight_decay"])
+
+    from data_io import CVZhTWDataset  # real-data input path (librosa / sentencepiece)
+    train_json = cfg.data.get("train_json", "data/processed/train.json")
+    tok_path = cfg.data.get("tokenizer_model_path", "data/tokenizer/zh-TW_A/spm_zhTW_A.model")
+    train_set = CVZhTWDataset(train_json, tok_path, cfg.data.get("max_len", 128), cfg.data["pad_id"],
+                              cfg.data.get("bos_id"), cfg.data.get("eos_id"))
+    loader = torch.utils.data.DataLoader(train_set, batch_size=cfg.optim["batch_size"], shuffle=True, drop_last=True)
+    os.makedirs(cfg.log["ckpt_dir"], exist_ok=True)
+    global_step = 1
+    for epoch in range(1, cfg.optim["num_epochs"] + 1):
+        logging.info(f"Epoch {epoch}")
+        global_step, train_loss = train_one_epoch(encoder, decoder, s_proj, t_embed, t_proj, sched, loader, optim,
+                                                  device, cfg, global_step, None, epoch)
+        logging.info(f"[Epoch {epoch} Summary] train_loss={train_loss:.4f}")
+        ckpt = {"decoder": decoder.state_dict(), "s_proj": s_proj.state_dict(), "t_embed": t_embed.state_dict(),
+                "t_proj": t_proj.state_dict(), "step": global_step, "epoch": epoch, "config": raw}
+        torch.save(ckpt, os.path.join(cfg.log["ckpt_dir"], f"ep{epoch:03d}.pt"))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,125 @@
+/* libfddm_hip — C-ABI of the MI355X (gfx950) kernels behind the FDDM-ASR train step.
+ *
+ * The reference (TeemoCaption/FDDM-asr) has no FFI layer: its hot path is the Python module API
+ * consumed by train.py. Each entry point below replaces the implicit torch op site(s)
+ * cited next to it; the Python package fddm-asr_amd/ (models/*, losses/*, fddm/sched/*, train.py)
+ * keeps the reference's module API and calls these through ctypes (fddm_hip/_lib.py).
+ *
+ * Conventions
+ *  - All pointers are device pointers owned by the caller (torch tensors); the library allocates
+ *    nothing and keeps no global state. Every call is asynchronous on `stream` (a hipStream_t).
+ *  - dtype codes: 0 = f32, 1 = bf16. "T" below means the selected compute/storage dtype.
+ *  - Return value: hipError_t as int (0 = success); fddm_error_string() describes it.
+ *  - Randomness: counter-based (seed, stream, element index) splitmix64 — see oracle/fddm_oracle.py.
+ */
+#ifndef FDDM_HIP_H
+#define FDDM_HIP_H
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+int fddm_abi_version(void);
+const char* fddm_error_string(int code);
+
+/* ---- GEMM (MFMA). C[m][n] = alpha * sum_k A(m,k) B(n,k) + bias[n], fused epilogue `epi`:
+ *      0 store (out_dtype), 1 GELU (C = pre-activation, C2 = dropout(gelu)), 2 accumulate into f32 C,
+ *      4 dGELU (C = acc * gelu'(C2) * dropout mask).  a_kc/b_kc: operand K-contiguous (1) or
+ *      M/N-contiguous (0).  A rows batched: A + (m/Mi)*sAb + (m%Mi)*lda (Mi <= 0: unbatched).
+ *      Replaces every nn.Linear / F.linear forward and backward on the path:
+ *      models/denoise_decoder.py:98-100,129-145,229,238  models/projection.py:14-55
+ *      models/acoustic_encoder.py:55  HF modeling_wavlm.py:93-105,125-128,274-295 */
+int fddm_gemm(int dtype, int a_dtype, int a_kc, int b_kc, int epi, int out_dtype, const void* A, long lda, long Mi,
+              long sAb, const void* B, long ldb, void* C, long ldc, void* C2, const float* bias, float alpha, long M,
+              long N, long K, unsigned long long seed, unsigned long long stream, float drop_p, void* hip_stream);
+
+/* ---- implicit-GEMM Conv1d on channels-last input (epi 0 store / 3 GELU), `groups` along gridDim.z.
+ *      HF modeling_wavlm.py:675-693 (conv layers 1..6), 37-90 (positional grouped conv). */
+int fddm_conv1d_gemm(int dtype, int epi, const void* x, long lda, long sAb, long Tin, long Cg, long cstride,
+                     long cpad, const void* W, void* out, long ldc, const float* bias, long Bn, long Tout, long N,
+                     long K, int groups, void* hip_stream);
+
+/* ---- conv layer 0 + GroupNorm + GELU. HF modeling_wavlm.py:723-744. sum/sq: zeroed [B][C] f64 scratch. */
+int fddm_conv0_gn_gelu(int out_dtype, const float* x, const float* w, const float* gamma, const float* beta,
+                       double* sum, double* sq, void* out, long B, long nsamp, long T0, int C, int K, int S, float eps,
+                       void* hip_stream);
+
+/* ---- WavLM gated rel-pos gate [B*H][S]. HF modeling_wavlm.py:166-180. */
+int fddm_wavlm_gate(int dtype, const void* x, const float* W, const float* bias, const float* cst, float* gate, long B,
+                    long S, int H, long E, void* hip_stream);
+
+/* ---- attention (head_dim 64). Element (b,pos,h,d) at base + (b*L+pos)*stride + h*64 + d.
+ *      nn.MultiheadAttention (models/denoise_decoder.py:129-130,164,169-174) with key_padding_mask
+ *      (key_keep[b][k] != 0 keeps) and attention-prob dropout; WavLM relative-bias attention
+ *      (HF modeling_wavlm.py:152-200) via gate [B*H][Lq] and table [H][2*Lk-1]. lse: [B*H][Lq]. */
+int fddm_attn_fwd(int dtype, const void* Q, long sq, const void* K, long sk, const void* V, long sv, void* O, long so,
+                  float* lse, const unsigned char* key_keep, const float* gate, const float* table, int B, int H,
+                  int Lq, int Lk, float scale, float drop_p, unsigned long long seed, unsigned long long stream,
+                  void* hip_stream);
+int fddm_attn_bwd(int dtype, const void* Q, long sq, const void* K, long sk, const void* V, long sv, const void* O,
+                  long so, const void* dO, long sdo, const float* lse, void* dQ, long sdq, void* dK, long sdk,
+                  void* dV, long sdv, float* delta_ws, const unsigned char* key_keep, int B, int H, int Lq, int Lk,
+                  float scale, float drop_p, unsigned long long seed, unsigned long long stream, void* hip_stream);
+
+/* ---- residual + dropout + LayerNorm (+FiLM). models/denoise_decoder.py:87-89,165-191;
+ *      HF modeling_wavlm.py:102,313-317,405. */
+int fddm_ln_fwd(int x_dtype, int y_dtype, int out_dtype, const void* x, const void* y, const float* gamma,
+                const float* beta, const float* film_scale, const float* film_shift, float* out_f32, void* out_t,
+                float* save_s, float* mean, float* rstd, long N, long d, long rows_per_batch, float eps, float drop_p,
+                unsigned long long seed, unsigned long long stream, void* hip_stream);
+int fddm_ln_bwd(int dy_dtype, const float* dout, const float* s, const float* mean, const float* rstd,
+                const float* gamma, const float* beta, const float* film_scale, float* dres, void* dy_t,
+                float* dgamma, float* dbeta, float* dfilm_scale, float* dfilm_shift, long N, long d,
+                long rows_per_batch, float drop_p, unsigned long long seed, unsigned long long stream,
+                void* hip_stream);
+
+/* ---- RoPE on the block input (models/denoise_decoder.py:42-53,157-159). cs/sn: [L][d]. */
+int fddm_rope_fwd(int out_dtype, const float* x, const float* cs, const float* sn, void* out, long N, long L, long d,
+                  void* hip_stream);
+int fddm_rope_bwd(const float* dy, const float* cs, const float* sn, float* dx, long N, long L, long d,
+                  void* hip_stream);
+
+/* ---- token embedding + time bias (models/denoise_decoder.py:214,254,272-274). */
+int fddm_embed_fwd(int out_dtype, const long* tok, const float* E, const float* tbias, float* out, void* out_t, long N,
+                   long L, long d, void* hip_stream);
+int fddm_embed_bwd(const long* tok, const float* dx, float* dE, float* dtb, long N, long L, long d, long pad_id,
+                   void* hip_stream);
+
+/* ---- helpers: column sums (bias grads), dtype casts */
+int fddm_colsum(int dtype, const void* X, float* out, long M, long N, long ldx, void* hip_stream);
+int fddm_cast(int src_dtype, int dst_dtype, const void* x, void* y, long n, void* hip_stream);
+
+/* ---- discrete diffusion: q_sample draw (train.py:180-188; diffusion_scheduler.py:31-50) and the
+ *      categorical KL + exact gradient (train.py:190-255). thr: [T] uint32 keep thresholds. */
+int fddm_sample_q(const long* x0, const long* t, const unsigned* thr, long* xt, long B, long L, long K,
+                  unsigned long long seed, unsigned long long stream, void* hip_stream);
+int fddm_kl_fwd(const float* logits, const long* xt, const long* x0, const long* t, const float* betas, float* kl_tok,
+                long N, long L, long V, void* hip_stream);
+int fddm_kl_bwd(const float* logits, const long* xt, const long* x0, const long* t, const float* betas,
+                const float* w, const float* gscale, void* dz, int dz_dtype, long N, long L, long V,
+                void* hip_stream);
+
+/* ---- TextEmbedding softmax (models/projection.py:41-47) */
+int fddm_softmax_rows(const float* x, void* y, int out_dtype, long N, long V, void* hip_stream);
+int fddm_softmax_bwd_rows(const void* y, const void* dy, float* dz, int dtype, long N, long V, int accumulate,
+                          void* hip_stream);
+
+/* ---- L_fd (losses/fddm_losses.py:18-58): batch-dim standardisation and the Barlow-Twins loss */
+int fddm_lfd_std_fwd(int out_dtype, const float* z, void* zt, float* inv_std, long B, long C, float eps,
+                     void* hip_stream);
+int fddm_lfd_std_bwd(int zt_dtype, const float* dzt, const void* zt, const float* inv_std, float* dz, long B, long C,
+                     void* hip_stream);
+int fddm_lfd_loss(const float* Cm, float* loss, long D, float lam, void* hip_stream);
+int fddm_lfd_dloss(int out_dtype, const float* Cm, const float* gscale, void* dC, long D, float lam, void* hip_stream);
+
+/* ---- clip_grad_norm_ + AdamW (train.py:411-423), multi-tensor over a chunk table */
+int fddm_grad_sumsq(const long* chunk_tensor, const long* chunk_start, const long* numel, const float* const* g,
+                    long nchunks, float* total, void* hip_stream);
+int fddm_adamw(const long* chunk_tensor, const long* chunk_start, const long* numel, float* const* p,
+               const float* const* g, float* const* m, float* const* v, unsigned short* const* pbf,
+               const float* step_size, const float* bc2_sqrt, long nchunks, const float* total, float max_norm,
+               float lr_wd, float b1, float b2, float eps, void* hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

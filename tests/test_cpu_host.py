@@ -1,0 +1,97 @@
+"""CPU tests of the host side: the C-ABI library loads and exports every declared symbol, the module
+API keeps the reference's signatures and state_dict keys, and host-side integer logic (sampler
+thresholds, rel-pos buckets, dropout streams) agrees with the oracle. No kernel is launched here."""
+import inspect
+
+import numpy as np
+import torch
+
+from helpers import SMALL_WAVLM, _dec_sd, wavlm_sd
+from oracle import fddm_oracle as O
+
+
+def test_library_exports_every_declared_symbol():
+    from fddm_hip import _lib
+    L = _lib.lib()
+    names = _lib.declared_symbols()
+    assert len(names) >= 25
+    for n in names:
+        assert hasattr(L, n), n
+    assert L.fddm_abi_version() == 1
+    assert b"no error" in L.fddm_error_string(0).lower()
+
+
+def test_decoder_state_dict_keys_match_reference():
+    from models.denoise_decoder import DenoisingTransformerDecoder
+    dec = DenoisingTransformerDecoder(vocab_size=1000, d_model=128, nhead=2, num_layers=2, dim_ff=256, dropout=0.0)
+    keys = set(dec.state_dict().keys())
+    ref_keys = set(_dec_sd(1000, 128, 2, 2, 256).keys()) | {"pos_emb.inv_freq"}
+    assert keys == ref_keys
+    sig = inspect.signature(DenoisingTransformerDecoder.__init__)
+    assert list(sig.parameters)[1:] == ["vocab_size", "d_model", "nhead", "num_layers", "dim_ff", "dropout", "max_len",
+                                        "pad_id", "pos_emb_type", "use_film", "rope_base"]
+    assert list(inspect.signature(DenoisingTransformerDecoder.forward).parameters)[1:] == \
+        ["xt", "t", "cond", "x_mask", "c_mask"]
+
+
+def test_encoder_state_dict_keys_match_hf_wavlm():
+    from models.acoustic_encoder import AcousticEncoder
+    enc = AcousticEncoder(wavlm_name=dict(SMALL_WAVLM), d_model=64)
+    ours = set(enc.state_dict().keys())
+    ref = set(wavlm_sd(O.wavlm_geometry(**SMALL_WAVLM), 64).keys())
+    assert ref <= ours
+    assert ours - ref == {"backbone.masked_spec_embed"}
+    # same names as transformers' WavLMModel (third-party reference of the encoder arithmetic)
+    from transformers import WavLMConfig, WavLMModel
+    hf = WavLMModel(WavLMConfig(**SMALL_WAVLM))
+    assert {"backbone." + k for k in hf.state_dict().keys()} == ours - {"proj.weight", "proj.bias"}
+
+
+def test_scheduler_tables_and_thresholds_match_oracle():
+    from fddm.sched.diffusion_scheduler import DiscreteDiffusionScheduler
+    s = DiscreteDiffusionScheduler(K=8000, T=200, device=torch.device("cpu"))
+    b, ab = O.sched_tables(200)
+    assert torch.equal(s.betas, b) and torch.equal(s.alpha_bar, ab)
+    thr = s.sample_thresholds().numpy().view(np.uint32).astype(np.uint64)
+    assert np.array_equal(thr, O.sample_thresholds(8000, ab))
+
+
+def test_relbias_buckets_match_oracle():
+    from fddm_hip import runtime as rt
+    rel = torch.arange(-998, 999)
+    assert torch.equal(rt.rel_bucket(rel, 320, 800), O.rel_position_bucket(rel, 320, 800))
+
+
+def test_projection_and_loss_api():
+    from losses.fddm_losses import lfd_loss
+    from models.projection import SpeechProjector, TextEmbedding, TextProjector
+    assert set(SpeechProjector(512, 256).state_dict()) == {"proj.net.0.weight", "proj.net.0.bias"}
+    assert set(TextEmbedding(8000, 256).state_dict()) == {"proj.weight"}
+    assert set(TextProjector(256, 256).state_dict()) == {"proj.net.0.weight", "proj.net.0.bias"}
+    assert list(inspect.signature(lfd_loss).parameters) == ["z_a", "z_b", "lambda_offdiag", "eps"]
+
+
+def test_train_surface():
+    import train
+    assert [f for f in train.Config.__dataclass_fields__] == ["seed", "data", "model", "diffusion", "inference",
+                                                               "optim", "lfd", "log"]
+    params = list(inspect.signature(train.train_one_epoch).parameters)
+    assert params[:13] == ["encoder", "decoder", "s_proj", "t_embed", "t_proj", "scheduler", "loader", "optimizer",
+                           "device", "cfg", "global_step", "scaler", "epoch"]
+    for m in ("sample_q", "kl_term", "w_t"):
+        assert hasattr(train.SchedulerAdapter, m)
+
+
+def test_align_speech_matches_oracle():
+    import train
+    z = torch.randn(2, 5, 3)
+    for L in (3, 5, 8):
+        assert torch.equal(train.align_speech(z, L), O.align_speech(z, L))
+
+
+def test_dropout_stream_contract():
+    # independent streams and the 16-bit threshold rate
+    k1 = O.dropout_keep(1, 1, 200000, 0.1)
+    k2 = O.dropout_keep(1, 2, 200000, 0.1)
+    assert abs(k1.float().mean().item() - 0.9) < 0.005
+    assert (k1 != k2).float().mean().item() > 0.1

@@ -1,0 +1,352 @@
+"""GPU parity tests of each libfddm_hip kernel against the CPU oracle / float64 references.
+
+Tolerances: fp32 kernels (exact f32 MFMA) within 1e-4 relative of the max reference magnitude
+(the north-star bar for fp32 logits/loss); bf16 kernels within 2e-2 relative; integer outputs
+(sampled token ids, dropout masks) bit-exact.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from helpers import close
+from oracle import fddm_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+dev = torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    import fddm_hip  # noqa: F401  (loads libfddm_hip.so, raises if absent)
+    from fddm_hip import ops
+    assert torch.cuda.is_available()
+    return ops
+
+
+def ops():
+    from fddm_hip import ops as o
+    return o
+
+
+TOL = {torch.float32: 1e-4, torch.bfloat16: 2e-2}
+
+
+def g(seed):
+    return torch.Generator().manual_seed(seed)
+
+
+# ------------------------------------------------------------------------------------------ GEMM
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("a_kc,b_kc", [(1, 1), (1, 0), (0, 0), (0, 1)])
+@pytest.mark.parametrize("M,N,K", [(200, 136, 96), (128, 128, 256), (8, 264, 520)])
+def test_gemm_layouts(dtype, a_kc, b_kc, M, N, K):
+    o = ops()
+    A = torch.randn(M, K, generator=g(1))
+    Bm = torch.randn(N, K, generator=g(2))
+    bias = torch.randn(N, generator=g(3))
+    ref = A.double() @ Bm.double().T + bias.double()
+    Ad = (A if a_kc else A.T.contiguous()).to(dev, dtype)
+    Bd = (Bm if b_kc else Bm.T.contiguous()).to(dev, dtype)
+    C = torch.zeros(M, N, device=dev, dtype=torch.float32)
+    o.gemm(Ad, Bd, C, M, N, K, a_kc=bool(a_kc), b_kc=bool(b_kc), lda=K if a_kc else M, ldb=K if b_kc else N, ldc=N,
+           bias=bias.to(dev))
+    torch.cuda.synchronize()
+    if dtype == torch.bfloat16:
+        ref = A.bfloat16().double() @ Bm.bfloat16().double().T + bias.double()
+    close(C, ref, rtol=1e-5 if dtype == torch.float32 else 1e-3, what="gemm")
+
+
+def test_gemm_epilogues_and_mixed_a():
+    o = ops()
+    M, N, K = 192, 160, 128
+    A = torch.randn(M, K, generator=g(4))
+    W = torch.randn(N, K, generator=g(5)) / math.sqrt(K)
+    b = torch.randn(N, generator=g(6))
+    Ad, Wd, bd = A.to(dev).bfloat16(), W.to(dev).bfloat16(), b.to(dev)
+    pre = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    act = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    o.linear(Ad, Wd, bd, out=pre, epi=o.EPI_GELU, C2=act, drop_p=0.1, seed=7, rng_stream=3)
+    ref = A.bfloat16().double() @ W.bfloat16().double().T + b.double()
+    keep = O.dropout_keep(7, 3, M * N, 0.1).view(M, N)
+    close(pre.float(), ref, rtol=1e-2, what="gelu pre")
+    close(act.float(), F.gelu(ref) * keep / 0.9, rtol=2e-2, what="gelu act+dropout")
+    # mixed: A stored f32, bf16 compute; accumulate epilogue
+    C = torch.ones(M, N, device=dev)
+    o.gemm(A.to(dev), Wd, C, M, N, K, lda=K, ldb=K, ldc=N, epi=o.EPI_ACC)
+    close(C, 1 + A.bfloat16().double() @ W.bfloat16().double().T, rtol=1e-2, what="mixed acc")
+    # dGELU epilogue
+    dy = torch.randn(M, K, generator=g(8))
+    dh = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    Wt = torch.randn(K, N, generator=g(9))  # [N_out=K][in=N] weight -> dx = dy @ Wt
+    o.linear_dx(dy.to(dev).bfloat16(), Wt.to(dev).bfloat16(), out=dh, epi=o.EPI_DGELU, C2=pre, drop_p=0.1, seed=7,
+                rng_stream=3)
+    x = pre.float().cpu().double()
+    cdf = 0.5 * (1 + torch.erf(x / math.sqrt(2)))
+    gg = cdf + x * torch.exp(-0.5 * x * x) / math.sqrt(2 * math.pi)
+    refd = (dy.bfloat16().double() @ Wt.bfloat16().double()) * gg * keep / 0.9
+    close(dh.float(), refd, rtol=2e-2, what="dgelu")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_conv1d_gemm_matches_conv(dtype):
+    o = ops()
+    B, Cin, Tin, Cout, k, s = 2, 64, 101, 64, 3, 2
+    x = torch.randn(B, Cin, Tin, generator=g(10))
+    w = torch.randn(Cout, Cin, k, generator=g(11)) / math.sqrt(Cin * k)
+    ref = F.conv1d(x.double(), w.double(), stride=s)            # [B, Cout, Tout]
+    Tout = ref.shape[-1]
+    xd = x.transpose(1, 2).contiguous().to(dev, dtype)
+    Wp = w.permute(0, 2, 1).contiguous().to(dev, dtype)
+    out = torch.empty(B, Tout, Cout, device=dev, dtype=dtype)
+    o.conv1d_gemm(xd, Wp, out, lda=Cin, sAb=Tin * Cin, Tin=Tin, Cg=Cin, cstride=s, cpad=0, Bn=B, Tout=Tout, N=Cout,
+                  K=k * Cin, gelu=True)
+    close(out.float().transpose(1, 2), F.gelu(ref), rtol=TOL[dtype], what="conv")
+    # grouped, padded (positional conv geometry scaled down)
+    E, G, kp, S = 64, 4, 16, 37
+    Cg = E // G
+    x = torch.randn(B, E, S, generator=g(12))
+    w = torch.randn(E, Cg, kp, generator=g(13)) / math.sqrt(Cg * kp)
+    bb = torch.randn(E, generator=g(14))
+    ref = F.conv1d(x.double(), w.double(), bb.double(), padding=kp // 2, groups=G)[:, :, :-1]
+    Wp = w.view(G, Cg, Cg, kp).permute(0, 1, 3, 2).contiguous().to(dev, dtype)
+    out = torch.empty(B * S, E, device=dev, dtype=dtype)
+    o.conv1d_gemm(x.transpose(1, 2).contiguous().to(dev, dtype), Wp, out, lda=E, sAb=S * E, Tin=S, Cg=Cg, cstride=1,
+                  cpad=kp // 2, Bn=B, Tout=S, N=Cg, K=kp * Cg, groups=G, bias=bb.to(dev), gelu=True)
+    close(out.float().view(B, S, E).transpose(1, 2), F.gelu(ref), rtol=TOL[dtype], what="grouped conv")
+
+
+# ------------------------------------------------------------------------------------- attention
+def _attn_ref(q, k, v, keep, p_drop, seed, stream, gate=None, table=None):
+    """q [B,H,Lq,64] ... float64 reference with the oracle's dropout mask."""
+    B, H, Lq, _ = q.shape
+    Lk = k.shape[2]
+    s = (q @ k.transpose(-1, -2)) / 8.0
+    if table is not None:
+        rel = torch.arange(Lk)[None, :] - torch.arange(Lq)[:, None] + Lk - 1
+        s = s + gate[..., None] * table[:, rel][None]
+    if keep is not None:
+        s = s.masked_fill(~keep[:, None, None, :], float("-inf"))
+    pr = torch.softmax(s, -1)
+    if p_drop > 0:
+        m = O.dropout_keep(seed, stream, B * H * Lq * Lk, p_drop).view(B, H, Lq, Lk).double()
+        pr = pr * m / (1 - p_drop)
+    return pr @ v
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("Lq,Lk,masked,p", [(70, 70, True, 0.0), (64, 130, False, 0.1), (33, 49, True, 0.1)])
+def test_attention_fwd_bwd(dtype, Lq, Lk, masked, p):
+    o = ops()
+    B, H = 2, 3
+    D = H * 64
+    q = torch.randn(B, Lq, D, generator=g(20))
+    k = torch.randn(B, Lk, D, generator=g(21))
+    v = torch.randn(B, Lk, D, generator=g(22))
+    do = torch.randn(B, Lq, D, generator=g(23))
+    keep = None
+    if masked:
+        keep = torch.ones(B, Lk, dtype=torch.bool)
+        keep[1, Lk - 9:] = False
+    to = lambda x: x.to(dev, dtype).reshape(-1, D).contiguous()  # noqa: E731
+    qd, kd, vd, dod = to(q), to(k), to(v), to(do)
+    od = torch.empty(B * Lq, D, device=dev, dtype=dtype)
+    lse = torch.empty(B * H, Lq, device=dev)
+    kk = keep.to(dev).to(torch.uint8) if keep is not None else None
+    o.attn_fwd(qd, kd, vd, od, lse, B, H, Lq, Lk, key_keep=kk, drop_p=p, seed=5, rng_stream=9)
+    dq = torch.empty_like(qd)
+    dk = torch.empty_like(kd)
+    dv = torch.empty_like(vd)
+    o.attn_bwd(qd, kd, vd, od, dod, lse, dq, dk, dv, B, H, Lq, Lk, key_keep=kk, drop_p=p, seed=5, rng_stream=9)
+    torch.cuda.synchronize()
+    hv = lambda x: x.to(dtype).double().view(B, -1, H, 64).transpose(1, 2)  # noqa: E731
+    qr, kr, vr = (hv(x).requires_grad_(True) for x in (q, k, v))
+    ref = _attn_ref(qr, kr, vr, keep, p, 5, 9)
+    ref.backward(hv(do))
+    back = lambda t: t.transpose(1, 2).reshape(B * t.shape[2], D)  # noqa: E731
+    tol = TOL[dtype]
+    close(od.float(), back(ref.detach()), rtol=tol, what="attn out")
+    close(dq.float(), back(qr.grad), rtol=3 * tol, what="dq")
+    close(dk.float(), back(kr.grad), rtol=3 * tol, what="dk")
+    close(dv.float(), back(vr.grad), rtol=3 * tol, what="dv")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_attention_relbias(dtype):
+    o = ops()
+    B, H, S = 2, 2, 75
+    D = H * 64
+    q = torch.randn(B, S, D, generator=g(30))
+    k = torch.randn(B, S, D, generator=g(31))
+    v = torch.randn(B, S, D, generator=g(32))
+    gate = torch.rand(B, H, S, generator=g(33)) + 1.0
+    table = torch.randn(H, 2 * S - 1, generator=g(34))
+    to = lambda x: x.to(dev, dtype).reshape(-1, D).contiguous()  # noqa: E731
+    od = torch.empty(B * S, D, device=dev, dtype=dtype)
+    o.attn_fwd(to(q), to(k), to(v), od, None, B, H, S, S, gate=gate.reshape(B * H, S).to(dev).contiguous(),
+               table=table.to(dev))
+    hv = lambda x: x.to(dtype).double().view(B, -1, H, 64).transpose(1, 2)  # noqa: E731
+    ref = _attn_ref(hv(q), hv(k), hv(v), None, 0.0, 0, 0, gate=gate.double(), table=table.double())
+    close(od.float(), ref.transpose(1, 2).reshape(B * S, D), rtol=TOL[dtype], what="relbias attn")
+
+
+# ----------------------------------------------------------------------------- LN / RoPE / embed
+@pytest.mark.parametrize("film", [False, True])
+def test_layernorm_fwd_bwd(film):
+    o = ops()
+    B, L, d = 3, 20, 192
+    N = B * L
+    x = torch.randn(N, d, generator=g(40))
+    y = torch.randn(N, d, generator=g(41))
+    gm = 1 + 0.1 * torch.randn(d, generator=g(42))
+    bt = 0.1 * torch.randn(d, generator=g(43))
+    fs = 0.2 * torch.randn(B, d, generator=g(44))
+    fh = 0.2 * torch.randn(B, d, generator=g(45))
+    dout = torch.randn(N, d, generator=g(46))
+    p = 0.1
+    keep = O.dropout_keep(3, 2, N * d, p).view(N, d).double()
+    xr, yr, gr, br, fsr, fhr = (t.double().requires_grad_(True) for t in (x, y, gm, bt, fs, fh))
+    s = xr + yr * keep / (1 - p)
+    out = F.layer_norm(s, (d,), gr, br, 1e-5)
+    if film:
+        out = (out.view(B, L, d) * (1 + fsr[:, None]) + fhr[:, None]).view(N, d)
+    out.backward(dout.double())
+    X = lambda t: t.to(dev).contiguous()  # noqa: E731
+    of = torch.empty(N, d, device=dev)
+    sv = torch.empty(N, d, device=dev)
+    mean = torch.empty(N, device=dev)
+    rstd = torch.empty(N, device=dev)
+    o.ln_fwd(X(x), X(y), X(gm), X(bt), out_f32=of, save_s=sv, mean=mean, rstd=rstd,
+             film=(X(fs), X(fh)) if film else None, rows_per_batch=L, drop_p=p, seed=3, rng_stream=2)
+    dres = torch.empty(N, d, device=dev)
+    dy = torch.empty(N, d, device=dev)
+    dg, db = torch.zeros(d, device=dev), torch.zeros(d, device=dev)
+    dfs, dfh = torch.zeros(B, d, device=dev), torch.zeros(B, d, device=dev)
+    o.ln_bwd(X(dout), sv, mean, rstd, X(gm), X(bt), dres=dres, dy_t=dy, dgamma=dg, dbeta=db,
+             film_scale=X(fs) if film else None, dfilm=(dfs, dfh) if film else None, rows_per_batch=L, drop_p=p,
+             seed=3, rng_stream=2)
+    close(of, out.detach(), rtol=1e-5, what="ln out")
+    close(dres, xr.grad, rtol=1e-4, what="ln dx")
+    close(dy, yr.grad, rtol=1e-4, what="ln dy")
+    close(dg, gr.grad, rtol=1e-4, what="dgamma")
+    close(db, br.grad, rtol=1e-4, what="dbeta")
+    if film:
+        close(dfs, fsr.grad, rtol=1e-4, what="dfilm scale")
+        close(dfh, fhr.grad, rtol=1e-4, what="dfilm shift")
+
+
+def test_rope_and_embedding():
+    o = ops()
+    B, L, d, V = 2, 9, 128, 50
+    inv = O.rope_inv_freq(d)
+    cos, sin = O.rope_cos_sin(L, inv)
+    x = torch.randn(B * L, d, generator=g(50))
+    out = torch.empty(B * L, d, device=dev)
+    o.rope_fwd(x.to(dev), cos.to(dev), sin.to(dev), out, L)
+    xr = x.view(B, L, d).double().requires_grad_(True)
+    ref = O.rope_apply(xr, cos.double(), sin.double())
+    close(out.view(B, L, d), ref.detach(), rtol=1e-6, what="rope")
+    dy = torch.randn(B, L, d, generator=g(51)).double()
+    ref.backward(dy)
+    dx = torch.zeros(B * L, d, device=dev)
+    o.rope_bwd(dy.float().view(-1, d).to(dev), cos.to(dev), sin.to(dev), dx, L)
+    close(dx.view(B, L, d), xr.grad, rtol=1e-5, what="rope bwd")
+    tok = torch.randint(0, V, (B, L), generator=g(52))
+    tok[1, -3:] = 0
+    E = torch.randn(V, d, generator=g(53))
+    tb = torch.randn(B, d, generator=g(54))
+    xo = torch.empty(B * L, d, device=dev)
+    o.embed_fwd(tok.to(dev), E.to(dev), tb.to(dev), xo, None, L)
+    close(xo.view(B, L, d), E[tok] + tb[:, None], rtol=1e-6, what="embed")
+    dxe = torch.randn(B * L, d, generator=g(55))
+    dE = torch.zeros(V, d, device=dev)
+    dtb = torch.zeros(B, d, device=dev)
+    o.embed_bwd(tok.to(dev).reshape(-1), dxe.to(dev), dE, dtb, L, 0)
+    refE = torch.zeros(V, d).index_add_(0, tok.reshape(-1), dxe)
+    refE[0] = 0
+    close(dE, refE, rtol=1e-5, what="dE")
+    close(dtb, dxe.view(B, L, d).sum(1), rtol=1e-5, what="dtbias")
+
+
+# ---------------------------------------------------------------------------- diffusion kernels
+def test_sampler_bit_exact_and_kl():
+    o = ops()
+    from fddm.sched.diffusion_scheduler import DiscreteDiffusionScheduler
+    K, Tn, B, L = 8000, 200, 16, 256
+    sch = DiscreteDiffusionScheduler(K=K, T=Tn, device=dev)
+    x0 = torch.randint(1, K, (B, L), generator=g(60))
+    t = torch.randint(1, Tn + 1, (B,), generator=g(61))
+    t[0], t[1] = 1, 2
+    xt = sch.sample_xt(x0.to(dev), t.to(dev), seed=1234)
+    _, ab = O.sched_tables(Tn)
+    ref = O.sample_xt(x0, t, K, ab, seed=1234, stream=1)
+    assert torch.equal(xt.cpu(), ref), "sampled indices must be bit-exact"
+    # fused KL forward/backward vs closed form oracle (and fixture-pinned formula)
+    from helpers import load, T
+    gk = load("kl")
+    logits, xtk, x0k, tk, xm, betas = (T(gk[n]) for n in ("logits", "xt", "x0", "t", "x_mask", "betas"))
+    Bk, Lk, Vk = logits.shape
+    valid = xm.float()
+    w = (valid / (valid.sum(1, keepdim=True) + 1e-8) / Bk).reshape(-1)
+    kl_tok = o.kl_fwd(logits.view(-1, Vk).to(dev), xtk.reshape(-1).to(dev), x0k.reshape(-1).to(dev), tk.to(dev),
+                      betas.to(dev), Lk)
+    loss = (kl_tok.cpu() * w).sum()
+    close(loss, gk["kl"], rtol=1e-5, what="kl loss")
+    gs = torch.full((1,), 2.0, device=dev)
+    dz = o.kl_bwd(logits.view(-1, Vk).to(dev), xtk.reshape(-1).to(dev), x0k.reshape(-1).to(dev), tk.to(dev),
+                  betas.to(dev), w.to(dev), gs, Lk)
+    close(dz.view(Bk, Lk, Vk), 2 * T(gk["dlogits"]), rtol=1e-4, atol=1e-10, what="kl grad")
+
+
+def test_lfd_kernels_match_reference():
+    from helpers import load, T
+    from fddm_hip import runtime as rt
+    from losses.fddm_losses import lfd_loss
+    gl = load("lfd")
+    with rt.use_precision("fp32"):
+        za = T(gl["za"]).to(dev).requires_grad_(True)
+        zb = T(gl["zb"]).to(dev).requires_grad_(True)
+        loss = lfd_loss(za, zb, 5e-3)
+        loss.backward()
+    close(loss, gl["loss"], rtol=1e-5, what="lfd")
+    close(za.grad, gl["dza"], rtol=1e-4, what="dza")
+    close(zb.grad, gl["dzb"], rtol=1e-4, what="dzb")
+
+
+def test_fused_adamw_matches_oracle():
+    from fddm_hip.optim import FusedAdamW
+    from fddm_hip import runtime as rt
+    torch.manual_seed(0)
+    shapes = [(300, 70), (70,), (1000,)]
+    ps = [torch.randn(*s) for s in shapes]
+    with rt.use_precision("fp32"):
+        dps = [torch.nn.Parameter(p.clone().to(dev)) for p in ps]
+        opt = FusedAdamW(dps, lr=2e-4, weight_decay=0.01)
+        ref = {str(i): p.clone() for i, p in enumerate(ps)}
+        ro = O.OracleAdamW()
+        for step in range(3):
+            grads = [10 * torch.randn(*s) for s in shapes]
+            skip = step == 1
+            for i, (p, gr) in enumerate(zip(dps, grads)):
+                p.grad = None if (skip and i == 2) else gr.to(dev)
+            opt.clip_and_step(max_norm=5.0)
+            gd = {str(i): (None if (skip and i == 2) else grads[i].clone()) for i in range(3)}
+            O.clip_grads(gd, 5.0)
+            ro.step(ref, gd)
+    for i, p in enumerate(dps):
+        close(p, ref[str(i)], rtol=1e-5, atol=1e-7, what=f"adamw p{i}")
+
+
+def test_softmax_rows_and_bwd():
+    o = ops()
+    x = 3 * torch.randn(37, 1000, generator=g(70))
+    y = o.softmax_rows(x.to(dev), torch.float32)
+    close(y, torch.softmax(x.double(), -1), rtol=1e-5, what="softmax")
+    dy = torch.randn(37, 1000, generator=g(71))
+    dz = o.softmax_bwd_rows(y, dy.to(dev))
+    yr = torch.softmax(x.double(), -1)
+    ref = yr * (dy.double() - (yr * dy.double()).sum(-1, keepdim=True))
+    close(dz, ref, rtol=1e-5, what="softmax bwd")

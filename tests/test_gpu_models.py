@@ -1,0 +1,191 @@
+"""Module-level GPU parity: the drop-in modules (fddm-asr_amd/) against the reference's golden
+fixtures and the CPU oracle, in the exact-fp32 parity mode (1e-4 relative), plus bf16-mode sanity.
+"""
+import numpy as np
+import pytest
+import torch
+
+from helpers import SMALL_WAVLM, T, _dec_sd, _step_params, close, load, wavlm_sd
+from oracle import fddm_oracle as O
+
+pytestmark = pytest.mark.gpu
+dev = torch.device("cuda:0")
+
+
+def _rt():
+    from fddm_hip import runtime as rt
+    return rt
+
+
+def make_decoder(V, d, H, NL, FF, dropout=0.0):
+    from models.denoise_decoder import DenoisingTransformerDecoder
+    dec = DenoisingTransformerDecoder(vocab_size=V, d_model=d, nhead=H, num_layers=NL, dim_ff=FF, dropout=dropout,
+                                      max_len=1024, pad_id=0)
+    sd = dec.state_dict()
+    for n, v in _dec_sd(V, d, H, NL, FF).items():
+        sd[n] = v
+    dec.load_state_dict(sd)
+    return dec.to(dev)
+
+
+def test_decoder_fp32_matches_reference_fixture():
+    g = load("decoder")
+    rt = _rt()
+    with rt.use_precision("fp32"):
+        dec = make_decoder(1000, 128, 2, 2, 256)
+        dec.train()
+        cond = T(g["cond"]).to(dev)
+        logits = dec(T(g["xt"]).to(dev), T(g["t"]).to(dev), cond, x_mask=T(g["x_mask"]).to(dev))
+        close(logits, g["logits"], rtol=1e-4, what="decoder logits")
+        (logits * T(g["R"]).to(dev)).sum().backward()
+        for n, p in dec.named_parameters():
+            if "g." + n in g:
+                close(p.grad, g["g." + n], rtol=1e-4, atol=1e-6, what="grad " + n)
+            close((p.grad.double() ** 2).sum(), g["g_sq." + n], rtol=2e-4, what="grad sq " + n)
+        with torch.no_grad():
+            l2 = dec(T(g["xt"]).to(dev), T(g["t"]).to(dev), cond)
+        close(l2, g["logits_defmask"], rtol=1e-4, what="decoder default mask")
+
+
+@pytest.mark.parametrize("prec,tol", [("fp32", 1e-4), ("bf16", 3e-2)])
+def test_decoder_dropout_matches_oracle(prec, tol, monkeypatch):
+    """Dropout 0.1 everywhere: masks follow the shared RNG contract, so GPU == oracle."""
+    rt = _rt()
+    V, d, H, NL, FF, B, L, S = 304, 128, 2, 2, 256, 2, 24, 30
+    gen = torch.Generator().manual_seed(3)
+    xt = torch.randint(1, V, (B, L), generator=gen)
+    xt[1, 20:] = 0
+    t = torch.tensor([5, 150])
+    cond = torch.randn(B, S, d, generator=gen)
+    R = torch.randn(B, L, V, generator=gen)
+    monkeypatch.setattr(rt, "next_seed", lambda: 777)
+    with rt.use_precision(prec):
+        dec = make_decoder(V, d, H, NL, FF, dropout=0.1)
+        dec.train()
+        logits = dec(xt.to(dev), t.to(dev), cond.to(dev))
+        (logits * R.to(dev)).sum().backward()
+    sd = {n: p.detach().cpu().clone().requires_grad_(True) for n, p in dec.named_parameters()}
+    ref = O.decoder_forward(sd, xt, t, cond, None, H=H, num_layers=NL, dropout=0.1, seed=777)
+    (ref * R).sum().backward()
+    close(logits, ref.detach(), rtol=tol, what=f"{prec} logits")
+    for n in ("blocks.0.self_attn.in_proj_weight", "blocks.1.ff.0.weight", "head.weight", "tok_emb.weight",
+              "blocks.0.norm2.weight", "blocks.1.film_layer.scale_proj.weight", "time_proj.weight"):
+        p = dict(dec.named_parameters())[n]
+        close(p.grad, sd[n].grad, rtol=(3 * tol), atol=1e-6, what=f"{prec} grad {n}")
+
+
+def _encoder(geom, d_model):
+    from models.acoustic_encoder import AcousticEncoder
+    over = {k: v for k, v in geom.items()}
+    enc = AcousticEncoder(wavlm_name=over, d_model=d_model)
+    sd = enc.state_dict()
+    for n, v in wavlm_sd(O.wavlm_geometry(**geom), d_model).items():
+        assert n in sd, n
+        sd[n] = v
+    enc.load_state_dict(sd)
+    return enc.to(dev).eval()
+
+
+def test_wavlm_small_fp32_matches_reference():
+    g = load("wavlm")
+    rt = _rt()
+    with rt.use_precision("fp32"):
+        enc = _encoder(SMALL_WAVLM, 64)
+        feats, m, pooled = enc(T(g["small_wave"]).to(dev))
+    assert m is None and pooled is None
+    close(feats, g["small_feats"], rtol=1e-4, what="small wavlm feats")
+
+
+@pytest.mark.parametrize("prec,tol", [("fp32", 1e-4), ("bf16", 5e-2)])
+def test_wavlm_base_matches_reference(prec, tol):
+    g = load("wavlm")
+    rt = _rt()
+    with rt.use_precision(prec):
+        enc = _encoder({}, 512)
+        feats, _, _ = enc(T(g["base_wave"]).to(dev))
+    close(feats.float(), g["base_feats"], rtol=tol, what=f"{prec} base wavlm feats")
+
+
+def test_wavlm_base_10s_batch_matches_oracle_bf16():
+    """C2 geometry (10 s -> S=499) on 2 utterances: bf16 kernels vs fp32 oracle."""
+    rt = _rt()
+    gen = torch.Generator().manual_seed(9)
+    wave = 0.1 * torch.randn(2, 160000, generator=gen)
+    with rt.use_precision("bf16"):
+        enc = _encoder({}, 512)
+        feats, _, _ = enc(wave.to(dev))
+    assert feats.shape == (2, 499, 512)
+    sd = wavlm_sd(O.wavlm_geometry(), 512)
+    ref = O.acoustic_encoder(sd, wave, O.wavlm_geometry(), 512)
+    close(feats.float(), ref, rtol=5e-2, what="10 s bf16 encoder")
+
+
+@pytest.mark.parametrize("tag,geom,V,d,H,NL,FF,Tn", [
+    ("step_c1", {}, 8000, 128, 2, 2, 2048, 10),
+    ("step_repeat", SMALL_WAVLM, 500, 128, 2, 1, 256, 20),
+])
+def test_train_step_fp32_matches_reference(tag, geom, V, d, H, NL, FF, Tn, monkeypatch):
+    """Four teacher-forced steps of train_one_epoch (incl. one L_fd step) vs the reference fixture."""
+    import train as T_
+    from fddm.sched.diffusion_scheduler import DiscreteDiffusionScheduler
+    from fddm_hip.optim import FusedAdamW
+    from models.projection import SpeechProjector, TextEmbedding, TextProjector
+    g = load(tag)
+    rt = _rt()
+    with rt.use_precision("fp32"):
+        enc = _encoder(geom, d)
+        dec = make_decoder(V, d, H, NL, FF)
+        sp, te, tp = SpeechProjector(d, 256), TextEmbedding(V, 256), TextProjector(256, 256)
+        params = _step_params(V, d, NL, FF, H)
+        for pre, m in (("s_proj.", sp), ("t_embed.", te), ("t_proj.", tp)):
+            m.load_state_dict({n: params[pre + n] for n, _ in m.named_parameters()})
+            m.to(dev)
+        xts = [T(x).to(dev) for x in g["xts"]]
+        ts = iter([T(x).to(dev) for x in g["ts"]])
+        rec = {"kl": [], "lfd": []}
+
+        class TF(T_.SchedulerAdapter):
+            i = 0
+
+            def sample_q(self, x0, t):
+                v = xts[TF.i]
+                TF.i += 1
+                return v
+
+            def kl_term(self, *a, **k):
+                v = super().kl_term(*a, **k)
+                rec["kl"].append(v)
+                return v
+
+        orig = T_.lfd_loss
+
+        def rl(*a, **k):
+            v = orig(*a, **k)
+            rec["lfd"].append(v)
+            return v
+
+        monkeypatch.setattr(T_, "lfd_loss", rl)
+        trainable = list(dec.parameters()) + list(sp.parameters()) + list(te.parameters()) + list(tp.parameters())
+        opt = FusedAdamW(trainable, lr=2e-4, weight_decay=0.01)
+        cfg = T_.Config(seed=1, data={"pad_id": 0}, model={}, diffusion={"T": Tn}, inference={}, optim={},
+                        lfd={"n_step_fd": 4, "tau": 1.0, "lambda_offdiag": 5e-3}, log={"log_every": 1000})
+        sch = TF(DiscreteDiffusionScheduler(K=V, T=Tn, device=dev))
+        loader = [(T(w), T(x)) for w, x in zip(g["waves"], g["x0s"])]
+        init = {("decoder." + n): p.detach().cpu().clone() for n, p in dec.named_parameters()}
+        init.update({k: v.clone() for k, v in params.items() if not k.startswith("decoder.")})
+        T_.train_one_epoch(enc, dec, sp, te, tp, sch, loader, opt, dev, cfg, 1, None, 1, False,
+                           draw_t=lambda B: next(ts))
+    close(torch.stack([v.detach().cpu() for v in rec["kl"]]), g["kl"], rtol=1e-4, what="per-step KL")
+    close(torch.stack([v.detach().cpu() for v in rec["lfd"]]), g["lfd"], rtol=1e-4, what="L_fd")
+    final = {("decoder." + n): p.detach().cpu() for n, p in dec.named_parameters()}
+    for pre, m in (("s_proj.", sp), ("t_embed.", te), ("t_proj.", tp)):
+        final.update({pre + n: p.detach().cpu() for n, p in m.named_parameters()})
+    noise_only = ("s_proj.proj.net.0.bias", "t_proj.proj.net.0.bias")
+    for n, p in final.items():
+        if n in noise_only:
+            continue
+        dp = p.double() - init[n].double()
+        close((dp ** 2).sum(), g["dp_sq." + n], rtol=5e-3, atol=1e-12, what="update " + n)
+        if "p." + n in g and "in_proj_bias" not in n:
+            err = (p.double() - T(g["p." + n]).double()).abs()
+            assert (err > 4e-6).float().mean().item() < 0.02, n
