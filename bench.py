@@ -1,0 +1,215 @@
+"""Benchmark: FDDM-ASR train-step utterances/sec on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1], "fddm_zhTW_base.yaml single MI355X"): WavLM-base encoder (random
+init; pretrained weights are not available offline) + 6-layer d_model=512 / 8-head / ff 2048 decoder,
+vocab 8000, T=200, dropout 0.1, n_step_fd=4, batch 32 x 10 s synthetic 16 kHz audio per GPU,
+seq_len 256 random token targets (per-utterance length U{128..256}, pad tail). One step = the full
+reference train step (train.py:340-443): encoder forward, q_sample, decoder fwd/bwd, KL, L_fd every 4th
+step, clip + AdamW. Inputs are resident in HBM before the timed region.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  N>1: launched by torch.distributed.run, one rank per GPU (RCCL); per-GPU batch fixed ("weak").
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "fddm-asr_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+GFLOP_PER_UTT = 193.87          # SURVEY §8(d), C2 (torch.utils.flop_counter on the reference)
+BF16_PEAK_TFLOPS = 2500.0       # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+F32_PEAK_TFLOPS = 157.3
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--warmup", type=int, default=4)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--seconds", type=float, default=10.0)
+    ap.add_argument("--seq-len", type=int, default=256)
+    ap.add_argument("--layers", type=int, default=6)
+    ap.add_argument("--d-model", type=int, default=512)
+    ap.add_argument("--heads", type=int, default=8)
+    ap.add_argument("--precision", default="bf16")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=2)
+    return ap.parse_args()
+
+
+def build(args, device):
+    import train as T_
+    from fddm_hip import runtime as rt
+    from fddm_hip.optim import FusedAdamW
+    cfg = T_.Config(seed=1337, data={"pad_id": 0, "vocab_size": 8000},
+                    model={"d_model": args.d_model, "nhead": args.heads, "num_layers": args.layers, "dim_ff": 2048,
+                           "dropout": 0.1, "encoder": {"wavlm_name": {}, "freeze": True, "proj": "linear",
+                                                       "pooling": "none"}, "projector": {"d_proj": 256}},
+                    diffusion={"T": 200, "beta_max": 0.2}, inference={}, optim={"lr": 2e-4, "weight_decay": 0.01},
+                    lfd={"n_step_fd": 4, "tau": 1.0, "lambda_offdiag": 5e-3}, log={"log_every": 10 ** 9})
+    rt.set_precision(args.precision)
+    models = T_.build_models(cfg, device)
+    enc, dec, sp, te, tp, sch = models
+    params = list(dec.parameters()) + list(sp.parameters()) + list(te.parameters()) + list(tp.parameters())
+    opt = FusedAdamW(params, lr=2e-4, weight_decay=0.01)
+    return T_, cfg, models, opt
+
+
+def synthetic_batches(args, device, n, seed):
+    g = torch.Generator(device=device).manual_seed(seed)
+    out = []
+    B, L, V = args.batch, args.seq_len, 8000
+    ns = int(16000 * args.seconds)
+    for _ in range(n):
+        wave = 0.1 * torch.randn(B, ns, device=device, generator=g)
+        x0 = torch.randint(1, V, (B, L), device=device, generator=g)
+        lens = torch.randint(L // 2, L + 1, (B,), device=device, generator=g)
+        x0 = torch.where(torch.arange(L, device=device)[None] < lens[:, None], x0, torch.zeros_like(x0))
+        out.append((wave, x0))
+    return out
+
+
+def measure_dominant(ops_mod, device, args):
+    """HIP-event timing of the dominant kernel (the implicit-GEMM conv of WavLM conv layer 1, the
+    largest MFMA launch of the step) on the bench stream, at the step's exact shape."""
+    from fddm_hip import ops
+    B = args.batch
+    T0 = (int(16000 * args.seconds) - 10) // 5 + 1
+    C = 512
+    T1 = (T0 - 3) // 2 + 1
+    x = torch.randn(B, T0, C, device=device, dtype=torch.bfloat16)
+    W = torch.randn(C, 3 * C, device=device, dtype=torch.bfloat16) / 40
+    out = torch.empty(B, T1, C, device=device, dtype=torch.bfloat16)
+    s = torch.cuda.current_stream()
+
+    def run():
+        ops.conv1d_gemm(x, W, out, lda=C, sAb=T0 * C, Tin=T0, Cg=C, cstride=2, cpad=0, Bn=B, Tout=T1, N=C, K=3 * C,
+                        gelu=True)
+    for _ in range(3):
+        run()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    R = 20
+    e0.record(s)
+    for _ in range(R):
+        run()
+    e1.record(s)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / R
+    flops = 2.0 * B * T1 * C * 3 * C
+    return ms, flops
+
+
+def cpu_baseline(args, models):
+    """The CPU oracle (plain torch fp32 restatement of the reference step) timed on the host cores on a
+    bounded sample: 2 utterances of the same geometry, `cpu_steps` steps (kind "port")."""
+    from oracle import fddm_oracle as O
+    ncores = min(16, len(os.sched_getaffinity(0)))
+    torch.set_num_threads(ncores)
+    enc, dec, sp, te, tp, sch = models
+    enc_sd = {k: v.detach().float().cpu() for k, v in enc.state_dict().items()}
+    w = enc.backbone.encoder.pos_conv_embed.conv.weight.detach().float().cpu()
+    geom = O.wavlm_geometry()
+    params = {("decoder." + k): v.detach().float().cpu().clone() for k, v in dec.named_parameters()}
+    for pre, m in (("s_proj.", sp), ("t_embed.", te), ("t_proj.", tp)):
+        params.update({pre + k: v.detach().float().cpu().clone() for k, v in m.named_parameters()})
+    betas, ab = O.sched_tables(200)
+    opt = O.OracleAdamW()
+    cfg = dict(d_model=args.d_model, nhead=args.heads, num_layers=args.layers, pad_id=0, n_step_fd=4, tau=1.0,
+               lambda_offdiag=5e-3)
+    g = torch.Generator().manual_seed(0)
+    Bc, L = 2, args.seq_len
+    ns = int(16000 * args.seconds)
+    del w
+    t0 = time.perf_counter()
+    for i in range(args.cpu_steps):
+        wave = 0.1 * torch.randn(Bc, ns, generator=g)
+        x0 = torch.randint(1, 8000, (Bc, L), generator=g)
+        t = torch.randint(1, 201, (Bc,), generator=g)
+        xt = O.sample_xt(x0, t, 8000, ab, seed=i)
+        O.oracle_train_step(params, enc_sd, geom, wave, x0, t, xt, cfg, opt, i + 4, betas, ab)
+    dt = time.perf_counter() - t0
+    return {"value": round(Bc * args.cpu_steps / dt, 4), "unit": "utterances/s", "cores": ncores, "kind": "port",
+            "sample": f"oracle train step (CPU fp32 restatement), {args.cpu_steps} steps x {Bc} utt x "
+                      f"{args.seconds:g} s, C2 geometry, incl. one L_fd step; {dt:.1f} s wall"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.manual_seed(1337 + rank)
+    T_, cfg, models, opt = build(args, device)
+    from fddm_hip import runtime as rt
+    rt.reseed(1337 + rank)
+    enc, dec, sp, te, tp, sch = models
+    batches = synthetic_batches(args, device, 4, 1000 + rank)
+    loader_w = [batches[i % 4] for i in range(args.warmup)]
+    loader_t = [batches[i % 4] for i in range(args.steps)]
+    gs = 1
+    gs, _ = T_.train_one_epoch(enc, dec, sp, te, tp, sch, loader_w, opt, device, cfg, gs, None, 0, False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    gs, avg_loss = T_.train_one_epoch(enc, dec, sp, te, tp, sch, loader_t, opt, device, cfg, gs, None, 1, False)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        tt = torch.tensor([el], device=device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    utt = args.batch * args.steps * world
+    value = utt / el
+    ms_step = 1000.0 * el / args.steps
+    if rank == 0:
+        from fddm_hip import ops
+        kms, kflops = measure_dominant(ops, device, args)
+        peak = BF16_PEAK_TFLOPS if args.precision == "bf16" else F32_PEAK_TFLOPS
+        achieved = kflops / (kms * 1e-3) / 1e12
+        step_tflops = value / world * GFLOP_PER_UTT / 1e3
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(args, models)
+        out = {
+            "metric": "train-step utterances/sec (10 s @16 kHz, seq_len 256) at 1/2/4/8 MI355X",
+            "value": round(value, 2), "unit": "utterances/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": args.precision, "data": "synthetic (random-init WavLM-base, random audio/tokens)",
+            "config": {"workload": "fddm_zhTW_base C2: WavLM-base + 6L d512 H8 ff2048 decoder, V=8000, T=200, "
+                                   "dropout 0.1, n_step_fd=4",
+                       "global_batch": args.batch * world, "seq_len": args.seq_len, "audio_seconds": args.seconds,
+                       "parallelism": f"dp{world}"},
+            "roofline": {"bound": "mfma", "kernel": "gemm_kernel<bf16,conv,GELU> (WavLM conv layer 1 implicit GEMM)",
+                         "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
+                         "frac": round(achieved / peak, 4), "traffic": None, "avg_ms": round(kms, 4),
+                         "flops_per_launch": kflops},
+            "step_mfma_frac": round(step_tflops / peak, 4),
+            "step_tflops": round(step_tflops, 1),
+            "avg_loss": round(avg_loss, 4),
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
