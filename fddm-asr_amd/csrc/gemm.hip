@@ -22,6 +22,8 @@
 // Register-staged prefetch of step k+1 is issued before the MFMAs of step k (one barrier per step).
 // A may be stored in f32 while the MFMA runs in bf16 (TA=float, T=bf16): converted while staging.
 #include "common.h"
+#include <algorithm>
+#include <cstdlib>
 
 namespace fddm {
 
@@ -138,6 +140,24 @@ struct Operand {
 #pragma unroll
     for (int i = 0; i < 4; ++i) *(uint4*)(s + lds_off[i]) = r[i];
   }
+  // MC operand: the 4 chunks of a thread share the same 8 (bf16) / 4 (f32) consecutive m's
+  __device__ __forceinline__ void accum_rows(float (&cs)[8]) const {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint4 u = r[i];
+      if constexpr (sizeof(T) == 2) {
+        const unsigned w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          cs[2 * j] += __uint_as_float(w[j] << 16);
+          cs[2 * j + 1] += __uint_as_float(w[j] & 0xffff0000u);
+        }
+      } else {
+        cs[0] += __uint_as_float(u.x); cs[1] += __uint_as_float(u.y);
+        cs[2] += __uint_as_float(u.z); cs[3] += __uint_as_float(u.w);
+      }
+    }
+  }
   // fragment for the 16-row tile starting at rb, sub-step sub (0/1)
   __device__ __forceinline__ static uint4 frag(const unsigned char* s, int rb, int sub, int lane) {
     const int g = lane >> 4, i = lane & 15;
@@ -178,6 +198,8 @@ struct GemmArgs {
   uint64_t seed, stream; unsigned thr16; float drop_scale;
   ConvGeo geo;
   long sAz, sBz, sCz, sbiasz;  // per-blockIdx.z offsets (grouped conv)
+  long ksplit;                 // K elements per split-K slice (plain GEMM)
+  float* colsum;               // optional: colsum[m] += sum_k A(m,k) (MC A operand) — fused bias gradient
 };
 
 template <typename T, typename TA, bool AKC, bool BKC, int EPI, typename OT, bool CONV>
@@ -188,13 +210,24 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g) {
   const int wr = wid >> 1, wc = wid & 1;
   const long m0 = (long)blockIdx.y * GBM, n0 = (long)blockIdx.x * GBN;
 
+  // blockIdx.z: group index (implicit conv) or split-K slice (plain GEMM, f32 atomic epilogue)
   const long z = blockIdx.z;
   Operand<T, TA, AKC, CONV> opa;
   Operand<T, T, BKC> opb;
-  opa.init((const TA*)g.A + z * g.sAz, g.lda, g.Mi, g.sAb, m0, g.M, g.K, g.geo);
-  opb.init((const T*)g.B + z * g.sBz, g.ldb, 1L << 62, 0, n0, g.N, g.K);
-  OT* Cz = (OT*)g.C + z * g.sCz;
-  const float* biasz = g.bias ? g.bias + z * g.sbiasz : nullptr;
+  long kbeg = 0, klen = g.K;
+  long zg = CONV ? z : 0;
+  if (!CONV && gridDim.z > 1) {
+    kbeg = z * g.ksplit;
+    klen = min(g.ksplit, g.K - kbeg);
+  }
+  const TA* Abase = (const TA*)g.A + zg * g.sAz + (AKC ? kbeg : kbeg * g.lda);
+  const T* Bbase = (const T*)g.B + zg * g.sBz + (BKC ? kbeg : kbeg * g.ldb);
+  opa.init(Abase, g.lda, g.Mi, g.sAb, m0, g.M, klen, g.geo);
+  opb.init(Bbase, g.ldb, 1L << 62, 0, n0, g.N, klen);
+  OT* Cz = (OT*)g.C + zg * g.sCz;
+  const float* biasz = g.bias ? g.bias + zg * g.sbiasz : nullptr;
+  if (!CONV && z > 0) biasz = nullptr;
+  const bool atomic_out = !CONV && gridDim.z > 1;
 
   f32x4_t acc[4][4];
 #pragma unroll
@@ -202,9 +235,13 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  const long nk = (g.K + KSTEP - 1) / KSTEP;
+  const long nk = (klen + KSTEP - 1) / KSTEP;
+  // fused bias gradient: only the first N-tile column of blocks sums its A rows (MC A, bf16/f32 A)
+  const bool do_cs = !AKC && (sizeof(TA) == sizeof(T)) && g.colsum != nullptr && blockIdx.x == 0;
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   opa.gload(0);
   opb.gload(0);
+  if constexpr (!AKC && sizeof(TA) == sizeof(T)) if (do_cs) opa.accum_rows(cs);
   opa.lstore(smem);
   opb.lstore(smem + GTILE_BYTES);
   __syncthreads();
@@ -230,10 +267,29 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g) {
     }
     if (kt + 1 < nk) {
       unsigned char* na = smem + (buf ^ 1) * 2 * GTILE_BYTES;
+      if constexpr (!AKC && sizeof(TA) == sizeof(T)) if (do_cs) opa.accum_rows(cs);
       opa.lstore(na);
       opb.lstore(na + GTILE_BYTES);
     }
     __syncthreads();
+  }
+  if constexpr (!AKC && sizeof(TA) == sizeof(T)) {
+    if (do_cs) {
+      // reduce the 256/CPR threads that share each m in LDS (the K loop has retired every LDS read),
+      // then one atomic per (block, m)
+      constexpr int ECH = Mma<T>::ECH, CPR = 128 / ECH;
+      float* red = (float*)smem;  // [256][ECH]
+#pragma unroll
+      for (int j = 0; j < ECH; ++j) red[tid * ECH + j] = cs[j];
+      __syncthreads();
+      if (tid < 128) {
+        const int mc = tid / ECH, j = tid % ECH;
+        float sacc = 0.f;
+        for (int q = mc; q < 256; q += CPR) sacc += red[q * ECH + j];
+        const long m = m0 + tid;
+        if (m < g.M) atomicAdd(g.colsum + m, sacc);
+      }
+    }
   }
 
   // epilogue: acc[i][j][e] -> row m0 + wr*64 + i*16 + 4*fg + e, col n0 + wc*64 + j*16 + fr
@@ -265,11 +321,195 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g) {
           st<OT>(Cz + m * g.ldc + n, dv);
         } else {
           float* c = (float*)Cz + m * g.ldc + n;
-          *c += v;
+          if (atomic_out) atomicAdd(c, v);
+          else *c += v;
         }
       }
     }
   }
+}
+
+
+// =====================================================================================================
+// "big" bf16 NT GEMM for the large forward shapes (WavLM conv layers 1..6, encoder/decoder projections
+// with >= 256 output tiles): 256x128 tile, 512 threads = 8 waves (4 x 2, 64x64 each), BK = 64,
+// operands staged by LDS-DMA (global_load_lds_dwordx4, no VGPR round trip) into a 3-deep LDS ring
+// (3 x 48 KB), two K-steps in flight behind a counted vmcnt, one raw s_barrier per K-step,
+// XCD-aware tile order (tiles that share an A panel run on one XCD and hit its L2).
+// Preconditions (checked on the host): K % 64 == 0, no padded conv taps, 16-B aligned rows.
+// =====================================================================================================
+constexpr int BBM = 256, BBN = 128, BSTAGES = 3;
+constexpr int BA_BYTES = BBM * 128, BB_BYTES = BBN * 128, BSTAGE_BYTES = BA_BYTES + BB_BYTES;
+
+typedef __attribute__((address_space(1))) const void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+
+// LDS fragment read issued as inline asm: hipcc's waitcnt pass would otherwise make every ds_read wait for
+// ALL outstanding LDS-DMA (vmcnt(0)), serialising the ring. The caller waits lgkmcnt itself.
+__device__ __forceinline__ u32x4_t ds_read128(const unsigned char* p) {
+  const unsigned a = (unsigned)(size_t)(lptr_t)(void*)p;
+  u32x4_t v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a) : "memory");
+  return v;
+}
+
+template <int EPI, typename OT, bool CONV>
+__global__ void __launch_bounds__(512) gemm_big_kernel(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform (LDS-DMA base in M0)
+  const int wr = wid >> 1, wc = wid & 1;
+  // XCD-aware bijective remap of the linear block id (blocks b, b+8, ... share an XCD)
+  const long nN = (g.N + BBN - 1) / BBN, nM = (g.M + BBM - 1) / BBM;
+  const long nwg = nN * nM;
+  const long orig = blockIdx.x;
+  const long q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+  const long t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+  const long m0 = (t / nN) * BBM, n0 = (t % nN) * BBN;
+
+  const bf16_t* A = (const bf16_t*)g.A;
+  const bf16_t* B = (const bf16_t*)g.B;
+  // LDS-DMA issue geometry: one wave instruction fills 1 KB = 8 rows x 128 B of an image; lane l lands at
+  // byte 16*l, i.e. row (l >> 3), physical chunk (l & 7) which must hold logical chunk (l&7) ^ ((row>>1)&7).
+  // A: 256 rows = 32 pieces -> 4 per wave; B: 128 rows = 16 pieces -> 2 per wave.
+  const bf16_t* asrc[4];
+  const bf16_t* bsrc[2];
+  long atpos[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (wid * 4 + i) * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ ((row >> 1) & 7);
+    long m = m0 + row;
+    if (m >= g.M) m = g.M - 1;
+    if (CONV) {
+      asrc[i] = A + (m / g.Mi) * g.sAb + c * 8;
+      atpos[i] = (m % g.Mi) * g.geo.cstride;
+    } else {
+      asrc[i] = A + m * g.lda + c * 8;
+      atpos[i] = 0;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (wid * 2 + i) * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ ((row >> 1) & 7);
+    long n = n0 + row;
+    if (n >= g.N) n = g.N - 1;
+    bsrc[i] = B + n * g.ldb + c * 8;
+  }
+  // issue cursor (wave-uniform scalars): next K-step's element offset, conv (tap, channel) split
+  int ik_tap = 0, ik_c = 0;
+  long ik_k0 = 0;
+  auto issue = [&](int stage) {
+    unsigned char* sa = smem + stage * BSTAGE_BYTES;
+    unsigned char* sb = sa + BA_BYTES;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      // implicit conv: the 64-wide K-step never crosses a tap (Cg % 64 == 0, host check)
+      const bf16_t* src = CONV ? asrc[i] + (atpos[i] + ik_tap) * g.lda + ik_c : asrc[i] + ik_k0;
+      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(sa + (wid * 4 + i) * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((gptr_t)(bsrc[i] + ik_k0), (lptr_t)(sb + (wid * 2 + i) * 1024), 16, 0, 0);
+    ik_k0 += 64;
+    if (CONV) {
+      ik_c += 64;
+      if (ik_c == (int)g.geo.Cg) {
+        ik_c = 0;
+        ++ik_tap;
+      }
+    }
+  };
+
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (int)(g.K / 64);
+  issue(0);
+  if (nk > 1) issue(1);
+  int cur = 0, nxt = 2;  // ring slots of K-step kt and kt + 2
+  for (int kt = 0; kt < nk; ++kt) {
+    // stage kt landed for this thread's DMAs (the next stage may stay in flight), then every wave's
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + 2 < nk) issue(nxt);
+    const unsigned char* sa = smem + cur * BSTAGE_BYTES;
+    cur = cur == BSTAGES - 1 ? 0 : cur + 1;
+    nxt = nxt == BSTAGES - 1 ? 0 : nxt + 1;
+    const unsigned char* sb = sa + BA_BYTES;
+    const int fr = lane & 15, fg = lane >> 4;
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      u32x4_t af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = ds_read128(sa + swz_kc(wr * 64 + i * 16 + fr, sub * 4 + fg));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = ds_read128(sb + swz_kc(wc * 64 + j * 16 + fr, sub * 4 + fg));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[i]),
+                                                              __builtin_bit_cast(bf16x8_t, bfr[j]), acc[i][j], 0, 0, 0);
+    }
+  }
+
+  const int fr = lane & 15, fg = lane >> 4;
+  float bvs[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const long n = n0 + wc * 64 + j * 16 + fr;
+    bvs[j] = (g.bias && n < g.N) ? g.bias[n] : 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const long n = n0 + wc * 64 + j * 16 + fr;
+    if (n >= g.N) continue;
+    const float bv = bvs[j];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const long m = m0 + wr * 64 + i * 16 + 4 * fg + e;
+        if (m >= g.M) continue;
+        const float v = acc[i][j][e] * g.alpha + bv;
+        OT* c = (OT*)g.C + m * g.ldc + n;
+        if constexpr (EPI == EPI_STORE) {
+          st<OT>(c, v);
+        } else if constexpr (EPI == EPI_GELU) {
+          st<OT>(c, v);
+          float a = gelu_f(v);
+          if (g.thr16) a = drop_keep(g.seed, g.stream, (uint64_t)(m * g.N + n), g.thr16) ? a * g.drop_scale : 0.f;
+          st<OT>((OT*)g.C2 + m * g.ldc + n, a);
+        } else if constexpr (EPI == EPI_GELU_ONLY) {
+          st<OT>(c, gelu_f(v));
+        }
+      }
+    }
+  }
+}
+
+template <int EPI, typename OT, bool CONV>
+static int launch_big(const GemmArgs& g, hipStream_t s) {
+  const long tiles = ((g.N + BBN - 1) / BBN) * ((g.M + BBM - 1) / BBM);
+  hipLaunchKernelGGL((gemm_big_kernel<EPI, OT, CONV>), dim3((unsigned)tiles), dim3(512), BSTAGES * BSTAGE_BYTES, s, g);
+  return (int)hipGetLastError();
+}
+
+static bool big_ok(const GemmArgs& g, bool conv) {
+  if (g.K % 64) return false;
+  const long tiles = ((g.N + BBN - 1) / BBN) * ((g.M + BBM - 1) / BBM);
+  if (tiles < 240) return false;
+  if (conv && (g.geo.cpad != 0 || g.geo.Cg % 64)) return false;
+  return true;
 }
 
 template <typename T, typename TA, bool AKC, bool BKC, int EPI, typename OT, bool CONV = false>
@@ -297,11 +537,11 @@ static int dispatch_epi(int epi, int out_dtype, const GemmArgs& g, hipStream_t s
 }
 
 template <typename T, typename TA>
-static int dispatch_layout(int a_kc, int b_kc, int epi, int out_dtype, const GemmArgs& g, hipStream_t s) {
-  if (a_kc && b_kc) return dispatch_epi<T, TA, true, true>(epi, out_dtype, g, s, 1);
-  if (a_kc && !b_kc) return dispatch_epi<T, TA, true, false>(epi, out_dtype, g, s, 1);
-  if (!a_kc && !b_kc) return dispatch_epi<T, TA, false, false>(epi, out_dtype, g, s, 1);
-  return dispatch_epi<T, TA, false, true>(epi, out_dtype, g, s, 1);
+static int dispatch_layout(int a_kc, int b_kc, int epi, int out_dtype, const GemmArgs& g, hipStream_t s, int nz) {
+  if (a_kc && b_kc) return dispatch_epi<T, TA, true, true>(epi, out_dtype, g, s, nz);
+  if (a_kc && !b_kc) return dispatch_epi<T, TA, true, false>(epi, out_dtype, g, s, nz);
+  if (!a_kc && !b_kc) return dispatch_epi<T, TA, false, false>(epi, out_dtype, g, s, nz);
+  return dispatch_epi<T, TA, false, true>(epi, out_dtype, g, s, nz);
 }
 
 }  // namespace fddm
@@ -311,7 +551,7 @@ using namespace fddm;
 FDDM_API int fddm_gemm(int dtype, int a_dtype, int a_kc, int b_kc, int epi, int out_dtype, const void* A, long lda,
                        long Mi, long sAb, const void* B, long ldb, void* C, long ldc, void* C2, const float* bias,
                        float alpha, long M, long N, long K, unsigned long long seed, unsigned long long stream,
-                       float drop_p, void* hip_stream) {
+                       float drop_p, float* colsum, void* hip_stream) {
   if (M <= 0 || N <= 0) return 0;
   const int ech = dtype == FDDM_BF16 ? 8 : 4;
   // layout preconditions (16-B chunks never straddle a row end or the tile edge)
@@ -320,17 +560,50 @@ FDDM_API int fddm_gemm(int dtype, int a_dtype, int a_kc, int b_kc, int epi, int 
   if (((uintptr_t)A & 15) || ((uintptr_t)B & 15)) return (int)hipErrorInvalidValue;
   if (!a_kc && Mi > 0 && Mi != M) return (int)hipErrorInvalidValue;
   if (Mi <= 0) Mi = 1L << 62;
-  GemmArgs g{A, lda, Mi, sAb, B, ldb, C, ldc, C2, bias, alpha, M, N, K, seed, stream, 0u, 1.f, ConvGeo{1, 0, 0, 0}, 0, 0, 0, 0};
+  GemmArgs g{A, lda, Mi, sAb, B, ldb, C, ldc, C2, bias, alpha, M, N, K, seed, stream, 0u, 1.f, ConvGeo{1, 0, 0, 0}, 0, 0, 0, 0, K, nullptr};
+  if (colsum) {
+    if (a_kc || a_dtype != dtype) return (int)hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(colsum, 0, M * sizeof(float), (hipStream_t)hip_stream);
+    if (e != hipSuccess) return (int)e;
+    g.colsum = colsum;
+  }
   if ((epi == EPI_GELU || epi == EPI_DGELU) && drop_p > 0.f) {
     g.thr16 = (unsigned)llrintf(drop_p * 65536.f);
     g.drop_scale = 1.f / (1.f - drop_p);
   }
   hipStream_t s = (hipStream_t)hip_stream;
+  // split-K when the output has too few 128x128 tiles to fill 256 CUs (weight gradients, small N):
+  // f32 output only, atomically accumulated; STORE becomes memset + accumulate.
+  int nz = 1;
+  const long tiles = ((M + GBM - 1) / GBM) * ((N + GBN - 1) / GBN);
+  const int kstep = dtype == FDDM_BF16 ? 64 : 32;
+  if (out_dtype == FDDM_F32 && (epi == EPI_STORE || epi == EPI_ACC_F32) && tiles < 512 && K >= 8 * kstep && Mi >= M) {
+    long want = (1024 + tiles - 1) / tiles;
+    long maxs = K / (4 * kstep);
+    nz = (int)std::max(1L, std::min(want, std::min(maxs, 64L)));
+    if (nz > 1) {
+      long ks = (K + nz - 1) / nz;
+      ks = (ks + kstep - 1) / kstep * kstep;
+      nz = (int)((K + ks - 1) / ks);
+      g.ksplit = ks;
+      if (epi == EPI_STORE) {
+        hipError_t e = hipMemset2DAsync(C, ldc * sizeof(float), 0, N * sizeof(float), M, s);
+        if (e != hipSuccess) return (int)e;
+        epi = EPI_ACC_F32;
+      }
+    }
+  }
+  if (dtype == FDDM_BF16 && a_dtype == FDDM_BF16 && a_kc && b_kc && nz == 1 && Mi >= M && !colsum &&
+      out_dtype == FDDM_BF16 && big_ok(g, false) && !getenv("FDDM_NO_BIG_GEMM")) {
+    if (epi == EPI_STORE) return launch_big<EPI_STORE, bf16_t, false>(g, s);
+    if (epi == EPI_GELU) return launch_big<EPI_GELU, bf16_t, false>(g, s);
+    if (epi == EPI_GELU_ONLY) return launch_big<EPI_GELU_ONLY, bf16_t, false>(g, s);
+  }
   if (dtype == FDDM_BF16) {
-    if (a_dtype == FDDM_BF16) return dispatch_layout<bf16_t, bf16_t>(a_kc, b_kc, epi, out_dtype, g, s);
-    if (a_dtype == FDDM_F32) return dispatch_layout<bf16_t, float>(a_kc, b_kc, epi, out_dtype, g, s);
+    if (a_dtype == FDDM_BF16) return dispatch_layout<bf16_t, bf16_t>(a_kc, b_kc, epi, out_dtype, g, s, nz);
+    if (a_dtype == FDDM_F32) return dispatch_layout<bf16_t, float>(a_kc, b_kc, epi, out_dtype, g, s, nz);
   } else if (dtype == FDDM_F32 && a_dtype == FDDM_F32) {
-    return dispatch_layout<float, float>(a_kc, b_kc, epi, out_dtype, g, s);
+    return dispatch_layout<float, float>(a_kc, b_kc, epi, out_dtype, g, s, nz);
   }
   return (int)hipErrorInvalidValue;
 }
@@ -348,8 +621,12 @@ FDDM_API int fddm_conv1d_gemm(int dtype, int epi, const void* x, long lda, long 
   if (K % ech || Cg % ech || lda % ech || sAb % ech || ((uintptr_t)x & 15) || ((uintptr_t)W & 15))
     return (int)hipErrorInvalidValue;
   GemmArgs g{x, lda, Tout, sAb, W, K, out, ldc, nullptr, bias, 1.f, Bn * Tout, N, K, 0, 0, 0u, 1.f,
-             ConvGeo{Cg, cstride, cpad, Tin}, Cg, N * K, N, N};
+             ConvGeo{Cg, cstride, cpad, Tin}, Cg, N * K, N, N, K, nullptr};
   hipStream_t s = (hipStream_t)hip_stream;
+  if (dtype == FDDM_BF16 && groups == 1 && big_ok(g, true) && !getenv("FDDM_NO_BIG_GEMM")) {
+    if (epi == EPI_GELU_ONLY) return launch_big<EPI_GELU_ONLY, bf16_t, true>(g, s);
+    return launch_big<EPI_STORE, bf16_t, true>(g, s);
+  }
   if (dtype == FDDM_BF16) {
     if (epi == EPI_GELU_ONLY) return launch<bf16_t, bf16_t, true, true, EPI_GELU_ONLY, bf16_t, true>(g, s, groups);
     return launch<bf16_t, bf16_t, true, true, EPI_STORE, bf16_t, true>(g, s, groups);

@@ -1,5 +1,6 @@
 // HBM-bound helper kernels of the train step: RoPE, token embedding, column sums, casts.
 #include "common.h"
+#include <algorithm>
 
 namespace fddm {
 
@@ -75,16 +76,42 @@ __global__ void embed_bwd_kernel(const long* __restrict__ tok, const float* __re
   }
 }
 
-// out[n] (+)= sum_m X[m][n]   (bias gradients); caller zeroes `out` when accumulate=0 is not used
+// out[n] += sum_m X[m][n]   (bias gradients): thread = 8 consecutive columns x a 64-row slab, one
+// vector load per row, then 8 atomics (caller zeroes `out`)
 template <typename T>
-__global__ void colsum_kernel(const T* __restrict__ X, float* __restrict__ out, long M, long N, long ldx, long rows_per_block) {
-  const long n = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= N) return;
-  const long m0 = (long)blockIdx.y * rows_per_block;
+__global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ X, float* __restrict__ out, long M, long N,
+                                                     long ldx, long rows_per_block) {
+  const long ncg = (N + 7) / 8;
+  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long cg = tid % ncg, rc = tid / ncg;
+  const long n0 = cg * 8;
+  const long m0 = rc * rows_per_block;
+  if (m0 >= M) return;
   const long m1 = min(M, m0 + rows_per_block);
-  float acc = 0.f;
-  for (long m = m0; m < m1; ++m) acc += ld<T>(X + m * ldx + n);
-  atomicAdd(out + n, acc);
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (n0 + 8 <= N && ((ldx * sizeof(T)) % 16 == 0) && ((((uintptr_t)X) & 15) == 0)) {
+#pragma unroll 4
+    for (long m = m0; m < m1; ++m) {
+      const T* p = X + m * ldx + n0;
+      if constexpr (sizeof(T) == 2) {
+        const uint4 u = *(const uint4*)p;
+        const unsigned w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          acc[2 * i] += __uint_as_float(w[i] << 16);
+          acc[2 * i + 1] += __uint_as_float(w[i] & 0xffff0000u);
+        }
+      } else {
+        const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+        acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
+        acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
+      }
+    }
+  } else {
+    for (long m = m0; m < m1; ++m)
+      for (int i = 0; i < 8 && n0 + i < N; ++i) acc[i] += ld<T>(X + m * ldx + n0 + i);
+  }
+  for (int i = 0; i < 8 && n0 + i < N; ++i) atomicAdd(out + n0 + i, acc[i]);
 }
 
 __global__ void cast_f32_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, long n) {
@@ -150,8 +177,11 @@ FDDM_API int fddm_embed_bwd(const long* tok, const float* dx, float* dE, float* 
 
 FDDM_API int fddm_colsum(int dtype, const void* X, float* out, long M, long N, long ldx, void* hs) {
   if (M <= 0 || N <= 0) return 0;
-  const long rpb = 64;
-  dim3 grid((unsigned)((N + 255) / 256), (unsigned)((M + rpb - 1) / rpb));
+  const long ncg = (N + 7) / 8;
+  long chunks = std::max(1L, std::min((M + 7) / 8, (65536 + ncg - 1) / ncg));
+  const long rpb = (M + chunks - 1) / chunks;
+  chunks = (M + rpb - 1) / rpb;
+  dim3 grid((unsigned)((ncg * chunks + 255) / 256));
   if (dtype == FDDM_BF16)
     hipLaunchKernelGGL((colsum_kernel<bf16_t>), grid, dim3(256), 0, (hipStream_t)hs, (const bf16_t*)X, out, M, N, ldx, rpb);
   else

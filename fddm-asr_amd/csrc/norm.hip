@@ -22,53 +22,100 @@ struct LnFwdArgs {
   uint64_t seed, stream; unsigned thr16; float drop_scale;
 };
 
+// 8 consecutive elements per lane per chunk (16-B bf16 / 32-B f32 accesses); d % 8 == 0
+template <typename T>
+__device__ __forceinline__ void ld8(const T* p, float (&v)[8]) {
+  if constexpr (sizeof(T) == 2) {
+    const uint4 u = *(const uint4*)p;
+    const unsigned w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(w[i] << 16);
+      v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+  } else {
+    const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+}
+template <typename T>
+__device__ __forceinline__ void st8(T* p, const float (&v)[8]) {
+  if constexpr (sizeof(T) == 2) {
+    uint4 u;
+    u.x = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
+    u.y = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
+    u.z = (unsigned)f2bf(v[4]) | ((unsigned)f2bf(v[5]) << 16);
+    u.w = (unsigned)f2bf(v[6]) | ((unsigned)f2bf(v[7]) << 16);
+    *(uint4*)p = u;
+  } else {
+    *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
+    *(float4*)(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  }
+}
+
+constexpr int LN_MAXCH = 2;  // chunks of 8 per lane: d <= 1024
+
 template <typename XT, typename YT, typename OT>
 __global__ void __launch_bounds__(256) ln_fwd_kernel(LnFwdArgs a) {
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= a.N) return;
-  const long d = a.d;
+  const long d = a.d, nch = d / 8;
   const XT* x = (const XT*)a.x + row * d;
   const YT* y = a.y ? (const YT*)a.y + row * d : nullptr;
-  float v[LN_MAXPL];
+  float v[LN_MAXCH][8];
   float sum = 0.f;
 #pragma unroll
-  for (int i = 0; i < LN_MAXPL; ++i) {
-    const long c = lane + 64L * i;
-    float t = 0.f;
-    if (c < d) {
-      t = ld<XT>(x + c);
+  for (int i = 0; i < LN_MAXCH; ++i) {
+    const long ch = lane + 64L * i;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[i][e] = 0.f;
+    if (ch < nch) {
+      ld8<XT>(x + ch * 8, v[i]);
       if (y) {
-        float yv = ld<YT>(y + c);
-        if (a.thr16) yv = drop_keep(a.seed, a.stream, (uint64_t)(row * d + c), a.thr16) ? yv * a.drop_scale : 0.f;
-        t += yv;
+        float yv[8];
+        ld8<YT>(y + ch * 8, yv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float t = yv[e];
+          if (a.thr16) t = drop_keep(a.seed, a.stream, (uint64_t)(row * d + ch * 8 + e), a.thr16) ? t * a.drop_scale : 0.f;
+          v[i][e] += t;
+        }
       }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sum += v[i][e];
     }
-    v[i] = t;
-    sum += t;
   }
   const float mean = wave_sum(sum) / (float)d;
   float sq = 0.f;
 #pragma unroll
-  for (int i = 0; i < LN_MAXPL; ++i) {
-    const long c = lane + 64L * i;
-    if (c < d) {
-      const float t = v[i] - mean;
-      sq += t * t;
+  for (int i = 0; i < LN_MAXCH; ++i) {
+    const long ch = lane + 64L * i;
+    if (ch < nch) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float t = v[i][e] - mean;
+        sq += t * t;
+      }
     }
   }
   const float var = wave_sum(sq) / (float)d;
   const float rstd = 1.f / sqrtf(var + a.eps);
   const long b = row / a.rows_per_batch;
 #pragma unroll
-  for (int i = 0; i < LN_MAXPL; ++i) {
-    const long c = lane + 64L * i;
-    if (c < d) {
-      if (a.save_s) a.save_s[row * d + c] = v[i];
-      float o = (v[i] - mean) * rstd * a.gamma[c] + a.beta[c];
-      if (a.fsc) o = o * (1.f + a.fsc[b * d + c]) + a.fsh[b * d + c];
-      if (a.out_f32) a.out_f32[row * d + c] = o;
-      if (a.out_t) st<OT>((OT*)a.out_t + row * d + c, o);
+  for (int i = 0; i < LN_MAXCH; ++i) {
+    const long ch = lane + 64L * i;
+    if (ch < nch) {
+      const long c0 = ch * 8;
+      if (a.save_s) st8<float>(a.save_s + row * d + c0, v[i]);
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        o[e] = (v[i][e] - mean) * rstd * a.gamma[c0 + e] + a.beta[c0 + e];
+        if (a.fsc) o[e] = o[e] * (1.f + a.fsc[b * d + c0 + e]) + a.fsh[b * d + c0 + e];
+      }
+      if (a.out_f32) st8<float>(a.out_f32 + row * d + c0, o);
+      if (a.out_t) st8<OT>((OT*)a.out_t + row * d + c0, o);
     }
   }
   if (lane == 0) {
@@ -85,86 +132,87 @@ struct LnBwdArgs {
   uint64_t seed, stream; unsigned thr16; float drop_scale;
 };
 
-constexpr int LN_BWD_ROWS = 8;  // rows per wave
-
+// pass 1: one wave per row: ds (residual gradient) and the dropout-masked dy for the GEMM
 template <typename OT>
 __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
   const int lane = threadIdx.x & 63;
-  const long row0 = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * LN_BWD_ROWS;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= a.N) return;
   const long d = a.d;
-  float dg[LN_MAXPL], db[LN_MAXPL], dsc[LN_MAXPL], dsh[LN_MAXPL];
-#pragma unroll
-  for (int i = 0; i < LN_MAXPL; ++i) dg[i] = db[i] = dsc[i] = dsh[i] = 0.f;
-  long cur_b = -1;
-  auto flush_film = [&]() {
-    if (cur_b < 0 || !a.fsc) return;
-#pragma unroll
-    for (int i = 0; i < LN_MAXPL; ++i) {
-      const long c = lane + 64L * i;
-      if (c < d) {
-        atomicAdd(a.dfsc + cur_b * d + c, dsc[i]);
-        atomicAdd(a.dfsh + cur_b * d + c, dsh[i]);
-      }
-      dsc[i] = dsh[i] = 0.f;
-    }
-  };
-  for (int r = 0; r < LN_BWD_ROWS; ++r) {
-    const long row = row0 + r;
-    if (row >= a.N) break;
-    const long b = row / a.rows_per_batch;
-    if (b != cur_b) {
-      flush_film();
-      cur_b = b;
-    }
-    const float mean = a.mean[row], rstd = a.rstd[row];
-    float xh[LN_MAXPL], dxh[LN_MAXPL];
-    float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-    for (int i = 0; i < LN_MAXPL; ++i) {
-      const long c = lane + 64L * i;
-      xh[i] = dxh[i] = 0.f;
-      if (c < d) {
-        const float x = (a.s[row * d + c] - mean) * rstd;
-        float go = a.dout[row * d + c];
-        if (a.fsc) {
-          const float lo = x * a.gamma[c] + a.beta[c];
-          dsc[i] += go * lo;
-          dsh[i] += go;
-          go *= 1.f + a.fsc[b * d + c];
-        }
-        dg[i] += go * x;
-        db[i] += go;
-        const float gx = go * a.gamma[c];
-        xh[i] = x;
-        dxh[i] = gx;
-        s1 += gx;
-        s2 += gx * x;
-      }
-    }
-    s1 = wave_sum(s1) / (float)d;
-    s2 = wave_sum(s2) / (float)d;
-#pragma unroll
-    for (int i = 0; i < LN_MAXPL; ++i) {
-      const long c = lane + 64L * i;
-      if (c < d) {
-        const float ds = rstd * (dxh[i] - s1 - xh[i] * s2);
-        if (a.dres) a.dres[row * d + c] = ds;
-        if (a.dy_t) {
-          float dy = ds;
-          if (a.thr16) dy = drop_keep(a.seed, a.stream, (uint64_t)(row * d + c), a.thr16) ? dy * a.drop_scale : 0.f;
-          st<OT>((OT*)a.dy_t + row * d + c, dy);
-        }
-      }
-    }
-  }
-  flush_film();
+  const long b = row / a.rows_per_batch;
+  const float mean = a.mean[row], rstd = a.rstd[row];
+  float xh[LN_MAXPL], dxh[LN_MAXPL];
+  float s1 = 0.f, s2 = 0.f;
 #pragma unroll
   for (int i = 0; i < LN_MAXPL; ++i) {
     const long c = lane + 64L * i;
-    if (c < d && a.dgamma) {
-      atomicAdd(a.dgamma + c, dg[i]);
-      atomicAdd(a.dbeta + c, db[i]);
+    xh[i] = dxh[i] = 0.f;
+    if (c < d) {
+      const float x = (a.s[row * d + c] - mean) * rstd;
+      float go = a.dout[row * d + c];
+      if (a.fsc) go *= 1.f + a.fsc[b * d + c];
+      const float gx = go * a.gamma[c];
+      xh[i] = x;
+      dxh[i] = gx;
+      s1 += gx;
+      s2 += gx * x;
     }
+  }
+  s1 = wave_sum(s1) / (float)d;
+  s2 = wave_sum(s2) / (float)d;
+#pragma unroll
+  for (int i = 0; i < LN_MAXPL; ++i) {
+    const long c = lane + 64L * i;
+    if (c < d) {
+      const float ds = rstd * (dxh[i] - s1 - xh[i] * s2);
+      if (a.dres) a.dres[row * d + c] = ds;
+      if (a.dy_t) {
+        float dy = ds;
+        if (a.thr16) dy = drop_keep(a.seed, a.stream, (uint64_t)(row * d + c), a.thr16) ? dy * a.drop_scale : 0.f;
+        st<OT>((OT*)a.dy_t + row * d + c, dy);
+      }
+    }
+  }
+}
+
+// pass 2: parameter gradients as column reductions over row slabs (no per-row atomics):
+//   dgamma[c] += sum dout'*xhat, dbeta[c] += sum dout', dfilm_scale[b][c] += sum dout*lnout,
+//   dfilm_shift[b][c] += sum dout   (dout' = dout * (1 + film_scale[b]))
+constexpr int LNP_ROWS = 64;
+__global__ void __launch_bounds__(256) ln_bwd_params_kernel(LnBwdArgs a) {
+  const long d = a.d;
+  const long c = (long)blockIdx.x * 256 + threadIdx.x;
+  if (c >= d) return;
+  const long r0 = (long)blockIdx.y * LNP_ROWS;
+  const long r1 = min(a.N, r0 + LNP_ROWS);
+  const float gm = a.gamma[c], bt = a.beta[c];
+  float dg = 0.f, db = 0.f, dsc = 0.f, dsh = 0.f;
+  long cur_b = r0 / a.rows_per_batch;
+  for (long r = r0; r < r1; ++r) {
+    const long b = r / a.rows_per_batch;
+    if (a.fsc && b != cur_b) {
+      atomicAdd(a.dfsc + cur_b * d + c, dsc);
+      atomicAdd(a.dfsh + cur_b * d + c, dsh);
+      dsc = dsh = 0.f;
+      cur_b = b;
+    }
+    const float x = (a.s[r * d + c] - a.mean[r]) * a.rstd[r];
+    float go = a.dout[r * d + c];
+    if (a.fsc) {
+      dsc += go * (x * gm + bt);
+      dsh += go;
+      go *= 1.f + a.fsc[b * d + c];
+    }
+    dg += go * x;
+    db += go;
+  }
+  if (a.dgamma) {
+    atomicAdd(a.dgamma + c, dg);
+    atomicAdd(a.dbeta + c, db);
+  }
+  if (a.fsc) {
+    atomicAdd(a.dfsc + cur_b * d + c, dsc);
+    atomicAdd(a.dfsh + cur_b * d + c, dsh);
   }
 }
 
@@ -178,7 +226,7 @@ FDDM_API int fddm_ln_fwd(int x_dtype, int y_dtype, int out_dtype, const void* x,
                          void* out_t, float* save_s, float* mean, float* rstd, long N, long d, long rows_per_batch,
                          float eps, float drop_p, unsigned long long seed, unsigned long long stream, void* hs) {
   if (N <= 0) return 0;
-  if (d > 64 * LN_MAXPL) return (int)hipErrorInvalidValue;
+  if (d > 64 * 8 * LN_MAXCH || d % 8) return (int)hipErrorInvalidValue;
   LnFwdArgs a{x, y, gamma, beta, film_scale, film_shift, out_f32, out_t, save_s, mean, rstd, N, d,
               rows_per_batch > 0 ? rows_per_batch : N, eps, seed, stream, 0u, 1.f};
   if (drop_p > 0.f) {
@@ -213,12 +261,15 @@ FDDM_API int fddm_ln_bwd(int dy_dtype, const float* dout, const float* s, const 
     a.thr16 = (unsigned)llrintf(drop_p * 65536.f);
     a.drop_scale = 1.f / (1.f - drop_p);
   }
-  const long waves = (N + LN_BWD_ROWS - 1) / LN_BWD_ROWS;
-  dim3 grid((unsigned)((waves + 3) / 4));
+  dim3 grid((unsigned)((N + 3) / 4));
   hipStream_t st_ = (hipStream_t)hs;
   if (dy_dtype == FDDM_BF16)
     hipLaunchKernelGGL((ln_bwd_kernel<bf16_t>), grid, dim3(256), 0, st_, a);
   else
     hipLaunchKernelGGL((ln_bwd_kernel<float>), grid, dim3(256), 0, st_, a);
+  if (dgamma || dfilm_scale) {
+    dim3 pg((unsigned)((d + 255) / 256), (unsigned)((N + LNP_ROWS - 1) / LNP_ROWS));
+    hipLaunchKernelGGL(ln_bwd_params_kernel, pg, dim3(256), 0, st_, a);
+  }
   return (int)hipGetLastError();
 }

@@ -10,10 +10,99 @@
 
 namespace fddm {
 
-constexpr int C0_FRAMES = 64;  // frames per block
+constexpr int C0_FRAMES = 64;         // frames per apply block
+constexpr int C0_MAXK = 16;
 
-__global__ void __launch_bounds__(256) conv0_stats_kernel(const float* __restrict__ x, const float* __restrict__ w,
-                                                          double* __restrict__ sum, double* __restrict__ sq, long nsamp,
+// GroupNorm statistics without materialising y: per utterance the K sums S1[k] = sum_t x[S t + k] and
+// the K x K Gram G[k][k'] = sum_t x[S t + k] x[S t + k'] (fp64) give, per channel c,
+//   sum_t y = w_c . S1      sum_t y^2 = w_c^T G w_c.
+// ws layout per utterance: [K] S1 then [K*K] G, fp64, zeroed by the caller.
+constexpr int C0_GRAM_FRAMES = 4096;
+template <int K>
+__global__ void __launch_bounds__(256) conv0_gram_kernel(const float* __restrict__ x, double* __restrict__ ws, long nsamp,
+                                                         long T0, int S) {
+  const long b = blockIdx.y;
+  const long f0 = (long)blockIdx.x * C0_GRAM_FRAMES;
+  const long f1 = min(T0, f0 + C0_GRAM_FRAMES);
+  double s1[K], g[K * (K + 1) / 2];
+#pragma unroll
+  for (int k = 0; k < K; ++k) s1[k] = 0.0;
+#pragma unroll
+  for (int k = 0; k < K * (K + 1) / 2; ++k) g[k] = 0.0;
+  for (long f = f0 + threadIdx.x; f < f1; f += 256) {
+    float xv[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) xv[k] = x[b * nsamp + f * S + k];
+    int q = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      s1[k] += (double)xv[k];
+#pragma unroll
+      for (int j = k; j < K; ++j) g[q++] += (double)xv[k] * (double)xv[j];
+    }
+  }
+  // reduce over the block in LDS, one atomic per value
+  __shared__ double red[K + K * (K + 1) / 2][4];
+  const int w = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    double v = s1[k];
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if ((threadIdx.x & 63) == 0) red[k][w] = v;
+  }
+#pragma unroll
+  for (int q = 0; q < K * (K + 1) / 2; ++q) {
+    double v = g[q];
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if ((threadIdx.x & 63) == 0) red[K + q][w] = v;
+  }
+  __syncthreads();
+  double* out = ws + b * (K + K * K);
+  if (threadIdx.x < K) {
+    const int k = threadIdx.x;
+    atomicAdd(out + k, red[k][0] + red[k][1] + red[k][2] + red[k][3]);
+  }
+  if (threadIdx.x < K * (K + 1) / 2) {
+    int q = threadIdx.x, k = 0;
+    while (q >= K - k) { q -= K - k; ++k; }
+    const int j = k + q;
+    const int qi = threadIdx.x;
+    const double t = red[K + qi][0] + red[K + qi][1] + red[K + qi][2] + red[K + qi][3];
+    atomicAdd(out + K + k * K + j, t);
+    if (j != k) atomicAdd(out + K + j * K + k, t);
+  }
+}
+
+// per (b, c): mean/var from (S1, G) -> fused GroupNorm affine  sc = gamma*rstd, sh = beta - mean*sc
+__global__ void conv0_gn_affine_kernel(const double* __restrict__ ws, const float* __restrict__ w,
+                                       const float* __restrict__ gamma, const float* __restrict__ beta,
+                                       float* __restrict__ scsh, long B, long T0, int C, int K, float eps) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= B * C) return;
+  const long b = e / C;
+  const int c = (int)(e % C);
+  const double* s1 = ws + b * (K + K * K);
+  const double* G = s1 + K;
+  double m = 0.0, q = 0.0;
+  for (int k = 0; k < K; ++k) {
+    const double wk = w[c * K + k];
+    m += wk * s1[k];
+    double r = 0.0;
+    for (int j = 0; j < K; ++j) r += G[k * K + j] * (double)w[c * K + j];
+    q += wk * r;
+  }
+  m /= (double)T0;
+  const double var = fmax(q / (double)T0 - m * m, 0.0);
+  const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float sc = rstd * gamma[c];
+  scsh[2 * e] = sc;
+  scsh[2 * e + 1] = beta[c] - (float)m * sc;
+}
+
+// recompute y, normalise, GELU; thread owns channel pair (2c, 2c+1) -> 4-B stores, 1 KB per wave row
+template <typename OT>
+__global__ void __launch_bounds__(256) conv0_apply_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                          const float* __restrict__ scsh, OT* __restrict__ out, long nsamp,
                                                           long T0, int C, int K, int S) {
   extern __shared__ float xs[];
   const long b = blockIdx.y;
@@ -22,91 +111,95 @@ __global__ void __launch_bounds__(256) conv0_stats_kernel(const float* __restric
   const int span = (nf - 1) * S + K;
   for (int i = threadIdx.x; i < span; i += 256) xs[i] = x[b * nsamp + t0 * S + i];
   __syncthreads();
-  for (int c = threadIdx.x; c < C; c += 256) {
-    float wk[16];
-    for (int k = 0; k < K; ++k) wk[k] = w[c * K + k];
-    float s = 0.f, s2 = 0.f;
-    for (int f = 0; f < nf; ++f) {
-      float y = 0.f;
-      for (int k = 0; k < K; ++k) y += wk[k] * xs[f * S + k];
-      s += y;
-      s2 += y * y;
+  for (int c = 2 * threadIdx.x; c < C; c += 512) {
+    float wk[2][C0_MAXK], sc[2], sh[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+#pragma unroll
+      for (int k = 0; k < C0_MAXK; ++k) wk[j][k] = k < K ? w[(c + j) * K + k] : 0.f;
+      sc[j] = scsh[2 * (b * C + c + j)];
+      sh[j] = scsh[2 * (b * C + c + j) + 1];
     }
-    atomicAdd(sum + b * C + c, (double)s);
-    atomicAdd(sq + b * C + c, (double)s2);
-  }
-}
-
-template <typename OT>
-__global__ void __launch_bounds__(256) conv0_apply_kernel(const float* __restrict__ x, const float* __restrict__ w,
-                                                          const double* __restrict__ sum, const double* __restrict__ sq,
-                                                          const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                          OT* __restrict__ out, long nsamp, long T0, int C, int K, int S,
-                                                          float eps) {
-  extern __shared__ float xs[];
-  const long b = blockIdx.y;
-  const long t0 = (long)blockIdx.x * C0_FRAMES;
-  const int nf = (int)min((long)C0_FRAMES, T0 - t0);
-  const int span = (nf - 1) * S + K;
-  for (int i = threadIdx.x; i < span; i += 256) xs[i] = x[b * nsamp + t0 * S + i];
-  __syncthreads();
-  for (int c = threadIdx.x; c < C; c += 256) {
-    float wk[16];
-    for (int k = 0; k < K; ++k) wk[k] = w[c * K + k];
-    const double mean = sum[b * C + c] / (double)T0;
-    const double var = fmax(sq[b * C + c] / (double)T0 - mean * mean, 0.0);
-    const float rstd = (float)(1.0 / sqrt(var + (double)eps));
-    const float sc = rstd * gamma[c];
-    const float sh = beta[c] - (float)mean * sc;
     for (int f = 0; f < nf; ++f) {
-      float y = 0.f;
-      for (int k = 0; k < K; ++k) y += wk[k] * xs[f * S + k];
-      st<OT>(out + (b * T0 + t0 + f) * C + c, gelu_f(y * sc + sh));
+      float y0 = 0.f, y1 = 0.f;
+#pragma unroll
+      for (int k = 0; k < C0_MAXK; ++k)
+        if (k < K) {
+          const float xv = xs[f * S + k];
+          y0 += wk[0][k] * xv;
+          y1 += wk[1][k] * xv;
+        }
+      OT* o = out + (b * T0 + t0 + f) * C + c;
+      const float g0 = gelu_f(y0 * sc[0] + sh[0]), g1 = gelu_f(y1 * sc[1] + sh[1]);
+      if constexpr (sizeof(OT) == 2) {
+        *(unsigned*)o = (unsigned)f2bf(g0) | ((unsigned)f2bf(g1) << 16);
+      } else {
+        o[0] = g0;
+        o[1] = g1;
+      }
     }
   }
 }
 
+// one thread per (token, head): 64-element slice in 16-B loads, W (8 x 64) broadcast from LDS
 template <typename T>
-__global__ void wavlm_gate_kernel(const T* __restrict__ x, const float* __restrict__ W, const float* __restrict__ bias,
-                                  const float* __restrict__ cst, float* __restrict__ gate, long B, long S, int H, long E) {
-  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;  // over B*S*H
-  if (e >= B * S * H) return;
-  const int h = (int)(e % H);
-  const long bs = e / H;
-  const long b = bs / S, s = bs % S;
+__global__ void __launch_bounds__(256) wavlm_gate_kernel(const T* __restrict__ x, const float* __restrict__ W,
+                                                         const float* __restrict__ bias, const float* __restrict__ cst,
+                                                         float* __restrict__ gate, long B, long S, int H, long E) {
+  __shared__ float ws[8 * 64];
   const int dh = (int)(E / H);
-  const T* xr = x + bs * E + (long)h * dh;
+  for (int i = threadIdx.x; i < 8 * dh; i += 256) ws[i] = W[i];
+  __syncthreads();
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;  // e = tok * H + h
+  if (e >= B * S * H) return;
+  const long tok = e / H;
+  const int h = (int)(e % H);
+  const long b = tok / S, s = tok % S;
+  const T* xr = x + tok * E + (long)h * dh;
   float r[8];
+#pragma unroll
   for (int o = 0; o < 8; ++o) r[o] = bias[o];
-  for (int d = 0; d < dh; ++d) {
-    const float xv = ld<T>(xr + d);
-    for (int o = 0; o < 8; ++o) r[o] += W[o * dh + d] * xv;
+  constexpr int EPC = 16 / sizeof(T);
+  for (int d0 = 0; d0 < dh; d0 += EPC) {
+    const uint4 u = *(const uint4*)(xr + d0);
+    const T* v = (const T*)&u;
+#pragma unroll
+    for (int j = 0; j < EPC; ++j) {
+      const float xv = ld<T>(v + j);
+#pragma unroll
+      for (int o = 0; o < 8; ++o) r[o] += ws[o * dh + d0 + j] * xv;
+    }
   }
-  const float a = 1.f / (1.f + __expf(-(r[0] + r[1] + r[2] + r[3])));
-  const float g = 1.f / (1.f + __expf(-(r[4] + r[5] + r[6] + r[7])));
-  gate[(b * H + h) * S + s] = a * (g * cst[h] - 1.f) + 2.f;
+  const float ga = 1.f / (1.f + __expf(-(r[0] + r[1] + r[2] + r[3])));
+  const float gb = 1.f / (1.f + __expf(-(r[4] + r[5] + r[6] + r[7])));
+  gate[(b * H + h) * S + s] = ga * (gb * cst[h] - 1.f) + 2.f;
 }
 
 }  // namespace fddm
 
 using namespace fddm;
 
-// sum/sq: [B][C] doubles, zeroed by the caller
+// ws: zeroed f64 scratch of B*(K + K*K) + B*C (the GroupNorm affine is stored after the Gram block)
 FDDM_API int fddm_conv0_gn_gelu(int out_dtype, const float* x, const float* w, const float* gamma, const float* beta,
-                                double* sum, double* sq, void* out, long B, long nsamp, long T0, int C, int K, int S,
-                                float eps, void* hs) {
+                                double* ws, void* out, long B, long nsamp, long T0, int C, int K, int S, float eps,
+                                void* hs) {
   if (B <= 0 || T0 <= 0) return 0;
-  if (K > 16) return (int)hipErrorInvalidValue;
+  if (K > C0_MAXK || C % 2) return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)hs;
+  dim3 gg((unsigned)((T0 + C0_GRAM_FRAMES - 1) / C0_GRAM_FRAMES), (unsigned)B);
+  if (K != 10) return (int)hipErrorInvalidValue;  // WavLM conv layer 0 (kernel 10, stride 5)
+  hipLaunchKernelGGL(conv0_gram_kernel<10>, gg, dim3(256), 0, s, x, ws, nsamp, T0, S);
+  float* scsh = (float*)(ws + B * (K + K * K));
+  hipLaunchKernelGGL(conv0_gn_affine_kernel, dim3((unsigned)((B * C + 255) / 256)), dim3(256), 0, s, ws, w, gamma, beta,
+                     scsh, B, T0, C, K, eps);
   dim3 grid((unsigned)((T0 + C0_FRAMES - 1) / C0_FRAMES), (unsigned)B);
   const size_t lds = ((C0_FRAMES - 1) * S + K) * sizeof(float);
-  hipStream_t s = (hipStream_t)hs;
-  hipLaunchKernelGGL(conv0_stats_kernel, grid, dim3(256), lds, s, x, w, sum, sq, nsamp, T0, C, K, S);
   if (out_dtype == FDDM_BF16)
-    hipLaunchKernelGGL((conv0_apply_kernel<bf16_t>), grid, dim3(256), lds, s, x, w, sum, sq, gamma, beta, (bf16_t*)out,
-                       nsamp, T0, C, K, S, eps);
+    hipLaunchKernelGGL((conv0_apply_kernel<bf16_t>), grid, dim3(256), lds, s, x, w, scsh, (bf16_t*)out, nsamp, T0, C,
+                       K, S);
   else
-    hipLaunchKernelGGL((conv0_apply_kernel<float>), grid, dim3(256), lds, s, x, w, sum, sq, gamma, beta, (float*)out,
-                       nsamp, T0, C, K, S, eps);
+    hipLaunchKernelGGL((conv0_apply_kernel<float>), grid, dim3(256), lds, s, x, w, scsh, (float*)out, nsamp, T0, C, K,
+                       S);
   return (int)hipGetLastError();
 }
 
@@ -115,6 +208,7 @@ FDDM_API int fddm_wavlm_gate(int dtype, const void* x, const float* W, const flo
                              long B, long S, int H, long E, void* hs) {
   const long n = B * S * H;
   if (n <= 0) return 0;
+  if (E / H > 64 || (E / H) % 8) return (int)hipErrorInvalidValue;
   dim3 g((unsigned)((n + 255) / 256));
   if (dtype == FDDM_BF16)
     hipLaunchKernelGGL((wavlm_gate_kernel<bf16_t>), g, dim3(256), 0, (hipStream_t)hs, (const bf16_t*)x, W, bias, cst, gate,

@@ -39,10 +39,12 @@ class LinearFn(torch.autograd.Function):
         dx = dW = db = None
         if ctx.needs_input_grad[0]:
             dx = ops.linear_dx(dyt, rt.wt(weight)).view(ctx.shp)
-        if ctx.needs_input_grad[1]:
-            dW = ops.linear_dw(dyt, x2)
         if bias is not None and ctx.needs_input_grad[2]:
-            db = ops.colsum(dy2)
+            db = torch.empty(weight.shape[0], device=dy.device, dtype=F32)
+        if ctx.needs_input_grad[1]:
+            dW = ops.linear_dw(dyt, x2, db=db)
+        elif db is not None:
+            ops.colsum(dy2, out=db)
         return dx, dW, db
 
 
@@ -174,13 +176,13 @@ class DecoderBlockFn(torch.autograd.Function):
         ops.ln_bwd(dx3, s3, m3, r3, n3w, n3b, dres=dx2, dy_t=dy3, dgamma=g["n3w"], dbeta=g["n3b"], drop_p=p,
                    seed=seed, rng_stream=st + 6)
         # FF
-        g["f3w"] = ops.linear_dw(dy3, hact)
-        g["f3b"] = ops.colsum(dy3)
+        g["f3b"] = torch.empty(d, device=dev, dtype=F32)
+        g["f3w"] = ops.linear_dw(dy3, hact, db=g["f3b"])
         FF = f0_w.shape[0]
         dh = torch.empty(N, FF, device=dev, dtype=cd)
         ops.linear_dx(dy3, W["f3"], out=dh, epi=ops.EPI_DGELU, C2=hpre, drop_p=p, seed=seed, rng_stream=st + 5)
-        g["f0w"] = ops.linear_dw(dh, x2T)
-        g["f0b"] = ops.colsum(dh)
+        g["f0b"] = torch.empty(FF, device=dev, dtype=F32)
+        g["f0w"] = ops.linear_dw(dh, x2T, db=g["f0b"])
         ops.linear_dx(dh, W["f0"], out=dx2, accumulate=True)
         # LN2 + FiLM
         dx1 = torch.empty(N, d, device=dev, dtype=F32)
@@ -192,19 +194,17 @@ class DecoderBlockFn(torch.autograd.Function):
         ops.ln_bwd(dx2, s2, m2, r2, n2w, n2b, dres=dx1, dy_t=dyc, dgamma=g["n2w"], dbeta=g["n2b"], film_scale=fsc,
                    dfilm=(dfs, dfh), rows_per_batch=L, drop_p=p, seed=seed, rng_stream=st + 4)
         # cross out-proj + attention
-        g["cow"] = ops.linear_dw(dyc, oc)
-        g["cob"] = ops.colsum(dyc)
+        g["cob"] = torch.empty(d, device=dev, dtype=F32)
+        g["cow"] = ops.linear_dw(dyc, oc, db=g["cob"])
         doc = ops.linear_dx(dyc, W["co"], out_dtype=cd)
         dqc = torch.empty(N, d, device=dev, dtype=cd)
         dkvc = torch.empty(B * S, 2 * d, device=dev, dtype=cd)
         ops.attn_bwd(qc, kvc, kvc[:, d:], oc, doc, lsec, dqc, dkvc, dkvc[:, d:], B, H, L, S, drop_p=p, seed=seed,
                      rng_stream=st + 3)
         gca_w = torch.empty(3 * d, d, device=dev, dtype=F32)
-        ops.linear_dw(dqc, x1T, out=gca_w[:d])
-        ops.linear_dw(dkvc, cT, out=gca_w[d:])
         gca_b = torch.empty(3 * d, device=dev, dtype=F32)
-        ops.colsum(dqc, out=gca_b[:d])
-        ops.colsum(dkvc, out=gca_b[d:])
+        ops.linear_dw(dqc, x1T, out=gca_w[:d], db=gca_b[:d])
+        ops.linear_dw(dkvc, cT, out=gca_w[d:], db=gca_b[d:])
         ops.linear_dx(dqc, W["ca"][:d], out=dx1, accumulate=True)
         # LN1
         dx = torch.empty(N, d, device=dev, dtype=F32)
@@ -214,19 +214,17 @@ class DecoderBlockFn(torch.autograd.Function):
         ops.ln_bwd(dx1, s1, m1, r1, n1w, n1b, dres=dx, dy_t=dy, dgamma=g["n1w"], dbeta=g["n1b"], drop_p=p, seed=seed,
                    rng_stream=st + 2)
         # self out-proj + attention
-        g["sow"] = ops.linear_dw(dy, o)
-        g["sob"] = ops.colsum(dy)
+        g["sob"] = torch.empty(d, device=dev, dtype=F32)
+        g["sow"] = ops.linear_dw(dy, o, db=g["sob"])
         do = ops.linear_dx(dy, W["so"], out_dtype=cd)
         dqk = torch.empty(N, 2 * d, device=dev, dtype=cd)
         dv = torch.empty(N, d, device=dev, dtype=cd)
         ops.attn_bwd(qk, qk[:, d:], v, o, do, lse, dqk, dqk[:, d:], dv, B, H, L, L, key_keep=key_keep, drop_p=p,
                      seed=seed, rng_stream=st + 1)
         gsa_w = torch.empty(3 * d, d, device=dev, dtype=F32)
-        ops.linear_dw(dqk, xr, out=gsa_w[: 2 * d])
-        ops.linear_dw(dv, xT, out=gsa_w[2 * d:])
         gsa_b = torch.empty(3 * d, device=dev, dtype=F32)
-        ops.colsum(dqk, out=gsa_b[: 2 * d])
-        ops.colsum(dv, out=gsa_b[2 * d:])
+        ops.linear_dw(dqk, xr, out=gsa_w[: 2 * d], db=gsa_b[: 2 * d])
+        ops.linear_dw(dv, xT, out=gsa_w[2 * d:], db=gsa_b[2 * d:])
         ops.linear_dx(dv, W["sa"][2 * d:], out=dx, accumulate=True)
         dxr = ops.linear_dx(dqk, W["sa"][: 2 * d])
         ops.rope_bwd(dxr, cos, sin, dx, L)
@@ -252,8 +250,8 @@ class HeadFn(torch.autograd.Function):
         dl = dlogits.contiguous()
         w = rt.wt(weight)
         dx = ops.linear_dx(dl, w)                 # A = dlogits (f32, converted while staging)
-        dW = ops.linear_dw(dl, xT)
-        db = ops.colsum(dl)
+        db = torch.empty(weight.shape[0], device=dl.device, dtype=F32)
+        dW = ops.linear_dw(dl, xT, db=db)
         return dx, None, dW, db
 
 

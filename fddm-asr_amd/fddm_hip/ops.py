@@ -43,13 +43,14 @@ def _chk(cond, msg):
 
 # ------------------------------------------------------------------------------------------ GEMM
 def gemm(A, B, C, M, N, K, *, a_kc=True, b_kc=True, lda, ldb, ldc, epi=EPI_STORE, bias=None, alpha=1.0,
-         C2=None, Mi=0, sAb=0, drop_p=0.0, seed=0, rng_stream=0):
+         C2=None, Mi=0, sAb=0, drop_p=0.0, seed=0, rng_stream=0, colsum=None):
     """C[m][n] = alpha * sum_k A(m,k) B(n,k) (+bias, epilogue). Compute dtype = B.dtype."""
     _chk(B.dtype in (torch.float32, torch.bfloat16), "B dtype")
     if M == 0 or N == 0:
         return C
     call("fddm_gemm", code(B), code(A), int(a_kc), int(b_kc), epi, code(C), ptr(A), lda, Mi, sAb, ptr(B), ldb,
-         ptr(C), ldc, ptr(C2), ptr(bias), float(alpha), M, N, K, seed, rng_stream, float(drop_p), stream())
+         ptr(C), ldc, ptr(C2), ptr(bias), float(alpha), M, N, K, seed, rng_stream, float(drop_p), ptr(colsum),
+         stream())
     return C
 
 
@@ -77,15 +78,21 @@ def linear_dx(dy2d, w, out=None, accumulate=False, out_dtype=torch.float32, epi=
                 C2=C2, drop_p=drop_p, seed=seed, rng_stream=rng_stream)
 
 
-def linear_dw(dy2d, x2d, out=None, accumulate=False):
-    """dW[N,K] = dy[M,N]^T @ x[M,K]  (both M/N-contiguous operands, K-reduction over tokens)."""
+def linear_dw(dy2d, x2d, out=None, accumulate=False, db=None):
+    """dW[N,K] = dy[M,N]^T @ x[M,K]  (both M/N-contiguous operands, K-reduction over tokens);
+    db (optional, f32 [N]) receives sum_m dy[m] — the bias gradient, fused into the same launch."""
     M, N = dy2d.shape
     K = x2d.shape[1]
     _chk(x2d.shape[0] == M and dy2d.stride(1) == 1 and x2d.stride(1) == 1, "linear_dw shapes")
     if out is None:
         out = torch.empty(N, K, device=dy2d.device, dtype=torch.float32)
+    if db is not None and dy2d.dtype != x2d.dtype:
+        gemm(dy2d, x2d, out, N, K, M, a_kc=False, b_kc=False, lda=dy2d.stride(0), ldb=x2d.stride(0),
+             ldc=out.stride(0), epi=EPI_ACC if accumulate else EPI_STORE)
+        colsum(dy2d, out=db)
+        return out
     return gemm(dy2d, x2d, out, N, K, M, a_kc=False, b_kc=False, lda=dy2d.stride(0), ldb=x2d.stride(0),
-                ldc=out.stride(0), epi=EPI_ACC if accumulate else EPI_STORE)
+                ldc=out.stride(0), epi=EPI_ACC if accumulate else EPI_STORE, colsum=db)
 
 
 def colsum(X2d, out=None, accumulate=False):
@@ -107,10 +114,10 @@ def conv1d_gemm(x, W, out, *, lda, sAb, Tin, Cg, cstride, cpad, Bn, Tout, N, K, 
 def conv0_gn_gelu(wave, w, gamma, beta, out_dtype, C, K, S, eps=1e-5):
     B, nsamp = wave.shape
     T0 = (nsamp - K) // S + 1
-    sums = torch.zeros(2, B, C, device=wave.device, dtype=torch.float64)
+    ws = torch.zeros(B * (K + K * K) + B * C, device=wave.device, dtype=torch.float64)
     out = torch.empty(B, T0, C, device=wave.device, dtype=out_dtype)
-    call("fddm_conv0_gn_gelu", code(out), ptr(wave), ptr(w), ptr(gamma), ptr(beta), ptr(sums[0]), ptr(sums[1]),
-         ptr(out), B, nsamp, T0, C, K, S, float(eps), stream())
+    call("fddm_conv0_gn_gelu", code(out), ptr(wave), ptr(w), ptr(gamma), ptr(beta), ptr(ws), ptr(out), B, nsamp, T0,
+         C, K, S, float(eps), stream())
     return out
 
 

@@ -25,12 +25,15 @@ const char* fddm_error_string(int code);
  *      0 store (out_dtype), 1 GELU (C = pre-activation, C2 = dropout(gelu)), 2 accumulate into f32 C,
  *      4 dGELU (C = acc * gelu'(C2) * dropout mask).  a_kc/b_kc: operand K-contiguous (1) or
  *      M/N-contiguous (0).  A rows batched: A + (m/Mi)*sAb + (m%Mi)*lda (Mi <= 0: unbatched).
+ *      colsum (optional, M/N-contiguous A only): colsum[m] = sum_k A(m,k) — the fused bias gradient of
+ *      a weight-gradient GEMM dW = dY^T X (colsum = sum over tokens of dY).
  *      Replaces every nn.Linear / F.linear forward and backward on the path:
  *      models/denoise_decoder.py:98-100,129-145,229,238  models/projection.py:14-55
  *      models/acoustic_encoder.py:55  HF modeling_wavlm.py:93-105,125-128,274-295 */
 int fddm_gemm(int dtype, int a_dtype, int a_kc, int b_kc, int epi, int out_dtype, const void* A, long lda, long Mi,
               long sAb, const void* B, long ldb, void* C, long ldc, void* C2, const float* bias, float alpha, long M,
-              long N, long K, unsigned long long seed, unsigned long long stream, float drop_p, void* hip_stream);
+              long N, long K, unsigned long long seed, unsigned long long stream, float drop_p, float* colsum,
+              void* hip_stream);
 
 /* ---- implicit-GEMM Conv1d on channels-last input (epi 0 store / 3 GELU), `groups` along gridDim.z.
  *      HF modeling_wavlm.py:675-693 (conv layers 1..6), 37-90 (positional grouped conv). */
@@ -38,9 +41,10 @@ int fddm_conv1d_gemm(int dtype, int epi, const void* x, long lda, long sAb, long
                      long cpad, const void* W, void* out, long ldc, const float* bias, long Bn, long Tout, long N,
                      long K, int groups, void* hip_stream);
 
-/* ---- conv layer 0 + GroupNorm + GELU. HF modeling_wavlm.py:723-744. sum/sq: zeroed [B][C] f64 scratch. */
+/* ---- conv layer 0 + GroupNorm + GELU. HF modeling_wavlm.py:723-744. ws: zeroed f64 scratch of
+ *      B*(K + K*K) + B*C doubles (per-utterance Gram statistics, then the GroupNorm affine). */
 int fddm_conv0_gn_gelu(int out_dtype, const float* x, const float* w, const float* gamma, const float* beta,
-                       double* sum, double* sq, void* out, long B, long nsamp, long T0, int C, int K, int S, float eps,
+                       double* ws, void* out, long B, long nsamp, long T0, int C, int K, int S, float eps,
                        void* hip_stream);
 
 /* ---- WavLM gated rel-pos gate [B*H][S]. HF modeling_wavlm.py:166-180. */

@@ -92,6 +92,72 @@ def test_gemm_epilogues_and_mixed_a():
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,N,K", [(200, 136, 96), (512, 256, 8192), (24, 512, 300)])
+def test_weight_grad_gemm_with_fused_bias_grad(dtype, M, N, K):
+    """dW = dy^T x (split-K when the output has few tiles) and db = colsum(dy) in the same launch."""
+    o = ops()
+    dy = torch.randn(K, M, generator=g(15))
+    x = torch.randn(K, N, generator=g(16))
+    dW = torch.empty(M, N, device=dev)
+    db = torch.empty(M, device=dev)
+    o.linear_dw(dy.to(dev, dtype), x.to(dev, dtype), out=dW, db=db)
+    ref = dy.to(dtype).double().T @ x.to(dtype).double()
+    close(dW, ref, rtol=1e-5 if dtype == torch.float32 else 1e-3, what="dW")
+    close(db, dy.to(dtype).double().sum(0), rtol=1e-5 if dtype == torch.float32 else 1e-3, what="db")
+
+
+@pytest.mark.parametrize("M,N,K,epi", [(8192, 2048, 512, 0), (15968, 768, 3072, 1), (8200, 2056, 768, 3)])
+def test_big_gemm_matches_torch(M, N, K, epi, monkeypatch):
+    """256x128 LDS-DMA GEMM (taken for >= 240 tiles) vs torch fp32 on the same bf16 operands,
+    and vs the 128x128 path (FDDM_NO_BIG_GEMM) — ragged M/N edges included."""
+    o = ops()
+    gen = torch.Generator(device=dev).manual_seed(3)
+    A = torch.randn(M, K, device=dev, generator=gen).bfloat16()
+    W = (torch.randn(N, K, device=dev, generator=gen) / math.sqrt(K)).bfloat16()
+    b = torch.randn(N, device=dev, generator=gen)
+    ref = A.float() @ W.float().T + b
+    out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    act = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    o.gemm(A, W, out, M, N, K, lda=K, ldb=K, ldc=N, bias=b, epi=epi, C2=act if epi == 1 else None)
+    chk = (act if epi == 1 else out).float()
+    want = F.gelu(ref) if epi in (1, 3) else ref
+    err = (chk - want).abs().max().item()
+    assert err <= 2e-2 * want.abs().max().item(), err
+    monkeypatch.setenv("FDDM_NO_BIG_GEMM", "1")
+    out2 = torch.empty_like(out)
+    act2 = torch.empty_like(act)
+    o.gemm(A, W, out2, M, N, K, lda=K, ldb=K, ldc=N, bias=b, epi=epi, C2=act2 if epi == 1 else None)
+    chk2 = (act2 if epi == 1 else out2).float()
+    assert (chk - chk2).abs().max().item() <= 1e-2 * want.abs().max().item()
+
+
+def test_big_conv_gemm_matches_torch(monkeypatch):
+    o = ops()
+    B, Cin, Tin, Cout, k, s = 8, 512, 4001, 512, 3, 2
+    gen = torch.Generator(device=dev).manual_seed(4)
+    x = torch.randn(B, Tin, Cin, device=dev, generator=gen).bfloat16()
+    w = (torch.randn(Cout, Cin, k, device=dev, generator=gen) / math.sqrt(Cin * k)).bfloat16()
+    ref = F.gelu(F.conv1d(x.float().transpose(1, 2), w.float(), stride=s)).transpose(1, 2)
+    Tout = ref.shape[1]
+    Wp = w.permute(0, 2, 1).contiguous()
+    out = torch.empty(B, Tout, Cout, device=dev, dtype=torch.bfloat16)
+    o.conv1d_gemm(x, Wp, out, lda=Cin, sAb=Tin * Cin, Tin=Tin, Cg=Cin, cstride=s, cpad=0, Bn=B, Tout=Tout, N=Cout,
+                  K=k * Cin, gelu=True)
+    err = (out.float() - ref).abs().max().item()
+    assert err <= 2e-2 * ref.abs().max().item(), err
+
+
+def test_gelu_fast_erf_accuracy():
+    o = ops()
+    x = torch.linspace(-8, 8, 4096).view(32, 128)
+    W = torch.eye(128)
+    pre = torch.empty(32, 128, device=dev)
+    act = torch.empty(32, 128, device=dev)
+    o.linear(x.to(dev), W.to(dev), None, out=pre, epi=o.EPI_GELU, C2=act)
+    close(act, F.gelu(x.double()), rtol=0, atol=2e-6, what="gelu")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_conv1d_gemm_matches_conv(dtype):
     o = ops()
     B, Cin, Tin, Cout, k, s = 2, 64, 101, 64, 3, 2

@@ -1,0 +1,80 @@
+"""Micro-benchmark of the libfddm_hip GEMM at the train step's shapes (HIP-event timing, bf16)."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "fddm-asr_amd"))
+import torch  # noqa: E402
+
+from fddm_hip import ops  # noqa: E402
+
+dev = torch.device("cuda:0")
+bf = torch.bfloat16
+
+
+def timeit(fn, iters=20):
+    for _ in range(3):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def report(name, flops, ms):
+    print(f"{name:48s} {ms*1e3:9.1f} us  {flops/ms/1e9:8.1f} TF/s", flush=True)
+
+
+def main():
+    only = sys.argv[1] if len(sys.argv) > 1 else ""
+    B, T0, C = 32, 31999, 512
+    T1 = (T0 - 3) // 2 + 1
+    if not only or only == "conv":
+        x = torch.randn(B, T0, C, device=dev, dtype=bf)
+        W = torch.randn(C, 3 * C, device=dev, dtype=bf) / 40
+        out = torch.empty(B, T1, C, device=dev, dtype=bf)
+        f = lambda: ops.conv1d_gemm(x, W, out, lda=C, sAb=T0 * C, Tin=T0, Cg=C, cstride=2, cpad=0, Bn=B, Tout=T1,  # noqa
+                                    N=C, K=3 * C, gelu=True)
+        report("conv1 implicit GEMM 511968x512x1536", 2 * B * T1 * C * 3 * C, timeit(f))
+    shapes = [("enc FF1 15968x3072x768 GELU", 15968, 3072, 768, ops.EPI_GELU_ONLY),
+              ("enc QKV 15968x2304x768", 15968, 2304, 768, ops.EPI_STORE),
+              ("enc FF2 15968x768x3072", 15968, 768, 3072, ops.EPI_STORE),
+              ("dec FF1 8192x2048x512", 8192, 2048, 512, ops.EPI_STORE),
+              ("dec out 8192x512x512", 8192, 512, 512, ops.EPI_STORE),
+              ("dec head 8192x8000x512 f32out", 8192, 8000, 512, -1)]
+    for name, M, N, K, epi in shapes:
+        if only and only != "fwd":
+            break
+        A = torch.randn(M, K, device=dev, dtype=bf)
+        Wt = torch.randn(N, K, device=dev, dtype=bf) / 30
+        o = torch.empty(M, N, device=dev, dtype=torch.float32 if epi < 0 else bf)
+        e = ops.EPI_STORE if epi < 0 else epi
+        f = lambda: ops.gemm(A, Wt, o, M, N, K, lda=K, ldb=K, ldc=N, epi=e)  # noqa: E731
+        report(name, 2 * M * N * K, timeit(f))
+    dws = [("dW dec FF1 2048x512 (K=8192)", 2048, 512, 8192), ("dW dec out 512x512 (K=8192)", 512, 512, 8192),
+           ("dW head 8000x512 (K=8192)", 8000, 512, 8192), ("dW cross kv 1024x512 (K=15968)", 1024, 512, 15968)]
+    for name, M, N, K in dws:
+        if only and only != "dw":
+            break
+        dy = torch.randn(K, M, device=dev, dtype=bf)
+        x = torch.randn(K, N, device=dev, dtype=bf)
+        o = torch.empty(M, N, device=dev)
+        db = torch.empty(M, device=dev)
+        f = lambda: ops.linear_dw(dy, x, out=o, db=db)  # noqa: E731
+        report(name, 2 * M * N * K, timeit(f))
+    dxs = [("dX dec FF1 8192x512 (K=2048)", 8192, 512, 2048), ("dX head 8192x512 (K=8000, f32 A)", 8192, 512, 8000)]
+    for name, M, N, K in dxs:
+        if only and only != "dx":
+            break
+        dy = torch.randn(M, K, device=dev, dtype=torch.float32 if "f32" in name else bf)
+        w = torch.randn(K, N, device=dev, dtype=bf)
+        o = torch.empty(M, N, device=dev)
+        f = lambda: ops.linear_dx(dy, w, out=o)  # noqa: E731
+        report(name, 2 * M * N * K, timeit(f))
+
+
+if __name__ == "__main__":
+    main()
