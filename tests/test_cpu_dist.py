@@ -1,0 +1,55 @@
+"""world_size-2 gloo test of the DP gradient exchange (fddm_hip.dist.allreduce_grads):
+ranks hold different gradients; after the exchange every rank holds the mean, bucketing (forced tiny
+here so several buckets flush) keeps tensor boundaries, and params whose grad is None (projectors on
+non-L_fd steps, reference train.py:400-410) stay None. CPU only."""
+import os
+import socket
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from fddm_hip import dist as fdist
+        shapes = [(3, 5), (7,), (2, 2, 2), (11, 3), (1,)]
+        params = [torch.nn.Parameter(torch.zeros(s)) for s in shapes]
+        for i, p in enumerate(params):
+            if i == 3:
+                continue  # grad None on every rank
+            g = torch.Generator().manual_seed(100 * rank + i)
+            p.grad = torch.randn(p.shape, generator=g)
+        fdist.allreduce_grads(params, bucket_bytes=64)
+        q.put((rank, [None if p.grad is None else p.grad.clone() for p in params]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_allreduce_grads_gloo_world2():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    shapes = [(3, 5), (7,), (2, 2, 2), (11, 3), (1,)]
+    for i, s in enumerate(shapes):
+        if i == 3:
+            assert got[0][i] is None and got[1][i] is None
+            continue
+        exp = sum(torch.randn(s, generator=torch.Generator().manual_seed(100 * r + i)) for r in range(world)) / world
+        for r in range(world):
+            torch.testing.assert_close(got[r][i], exp, rtol=1e-6, atol=1e-6)
