@@ -548,6 +548,12 @@ static int dispatch_layout(int a_kc, int b_kc, int epi, int out_dtype, const Gem
 
 using namespace fddm;
 
+// FDDM_NO_BIG_GEMM=1 routes every GEMM through the 128x128 kernel (read once per process)
+static bool big_enabled() {
+  static const bool on = getenv("FDDM_NO_BIG_GEMM") == nullptr;
+  return on;
+}
+
 FDDM_API int fddm_gemm(int dtype, int a_dtype, int a_kc, int b_kc, int epi, int out_dtype, const void* A, long lda,
                        long Mi, long sAb, const void* B, long ldb, void* C, long ldc, void* C2, const float* bias,
                        float alpha, long M, long N, long K, unsigned long long seed, unsigned long long stream,
@@ -563,8 +569,10 @@ FDDM_API int fddm_gemm(int dtype, int a_dtype, int a_kc, int b_kc, int epi, int 
   GemmArgs g{A, lda, Mi, sAb, B, ldb, C, ldc, C2, bias, alpha, M, N, K, seed, stream, 0u, 1.f, ConvGeo{1, 0, 0, 0}, 0, 0, 0, 0, K, nullptr};
   if (colsum) {
     if (a_kc || a_dtype != dtype) return (int)hipErrorInvalidValue;
-    hipError_t e = hipMemsetAsync(colsum, 0, M * sizeof(float), (hipStream_t)hip_stream);
-    if (e != hipSuccess) return (int)e;
+    if (epi != EPI_ACC_F32) {  // colsum follows C: overwritten by STORE, accumulated by ACC
+      hipError_t e = hipMemsetAsync(colsum, 0, M * sizeof(float), (hipStream_t)hip_stream);
+      if (e != hipSuccess) return (int)e;
+    }
     g.colsum = colsum;
   }
   if ((epi == EPI_GELU || epi == EPI_DGELU) && drop_p > 0.f) {
@@ -594,7 +602,7 @@ FDDM_API int fddm_gemm(int dtype, int a_dtype, int a_kc, int b_kc, int epi, int 
     }
   }
   if (dtype == FDDM_BF16 && a_dtype == FDDM_BF16 && a_kc && b_kc && nz == 1 && Mi >= M && !colsum &&
-      out_dtype == FDDM_BF16 && big_ok(g, false) && !getenv("FDDM_NO_BIG_GEMM")) {
+      out_dtype == FDDM_BF16 && big_ok(g, false) && big_enabled()) {
     if (epi == EPI_STORE) return launch_big<EPI_STORE, bf16_t, false>(g, s);
     if (epi == EPI_GELU) return launch_big<EPI_GELU, bf16_t, false>(g, s);
     if (epi == EPI_GELU_ONLY) return launch_big<EPI_GELU_ONLY, bf16_t, false>(g, s);
@@ -623,7 +631,7 @@ FDDM_API int fddm_conv1d_gemm(int dtype, int epi, const void* x, long lda, long 
   GemmArgs g{x, lda, Tout, sAb, W, K, out, ldc, nullptr, bias, 1.f, Bn * Tout, N, K, 0, 0, 0u, 1.f,
              ConvGeo{Cg, cstride, cpad, Tin}, Cg, N * K, N, N, K, nullptr};
   hipStream_t s = (hipStream_t)hip_stream;
-  if (dtype == FDDM_BF16 && groups == 1 && big_ok(g, true) && !getenv("FDDM_NO_BIG_GEMM")) {
+  if (dtype == FDDM_BF16 && groups == 1 && big_ok(g, true) && big_enabled()) {
     if (epi == EPI_GELU_ONLY) return launch_big<EPI_GELU_ONLY, bf16_t, true>(g, s);
     return launch_big<EPI_STORE, bf16_t, true>(g, s);
   }

@@ -20,6 +20,19 @@ def allreduce_grads(params, bucket_bytes: int = BUCKET_BYTES) -> None:
     W = world()
     if W <= 1:
         return
+    params = list(params)
+    arena = next((a for a in (getattr(p, "_fddm_arena", None) for p in params) if a is not None), None)
+    if arena is not None and all(p.grad is not None and p.grad.data_ptr() == v.data_ptr()
+                                 for p, v in zip(arena.params, arena.views)):
+        # the arena is already flat: all-reduce it in place in bucket-sized slices
+        flat = arena.flat
+        step = max(1, bucket_bytes // 4)
+        for s0 in range(0, flat.numel(), step):
+            sl = flat[s0:s0 + step]
+            dist.all_reduce(sl, op=dist.ReduceOp.SUM)
+            sl.mul_(1.0 / W)
+        inside = set(id(p) for p in arena.params)
+        params = [p for p in params if id(p) not in inside]
     grads = [p.grad for p in params if p.grad is not None]
     bucket, size = [], 0
 

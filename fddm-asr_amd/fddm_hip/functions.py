@@ -17,6 +17,19 @@ def _t(x):
     return x if x.dtype == cd else ops.cast(x.contiguous(), cd)
 
 
+def _gdst(p, zero=False):
+    """(destination, in_arena) for p's gradient: its GradArena view, accumulated in place by the kernels
+    (the Function then returns None for p), or a fresh fp32 tensor returned to autograd."""
+    s = rt.grad_slot(p)
+    if s is not None:
+        return s, True
+    return (torch.zeros if zero else torch.empty)(p.shape, device=p.device, dtype=F32), False
+
+
+def _ret(t, in_arena):
+    return None if in_arena else t
+
+
 # ------------------------------------------------------------------------------- generic Linear
 class LinearFn(torch.autograd.Function):
     """y = x W^T + b (f32 out) — SpeechProjector / TextProjector / encoder proj (models/projection.py)."""
@@ -37,15 +50,21 @@ class LinearFn(torch.autograd.Function):
         dy2 = dy.reshape(-1, weight.shape[0]).contiguous()
         dyt = _t(dy2)
         dx = dW = db = None
+        aw = ab = False
         if ctx.needs_input_grad[0]:
             dx = ops.linear_dx(dyt, rt.wt(weight)).view(ctx.shp)
         if bias is not None and ctx.needs_input_grad[2]:
-            db = torch.empty(weight.shape[0], device=dy.device, dtype=F32)
+            db, ab = _gdst(bias)
         if ctx.needs_input_grad[1]:
-            dW = ops.linear_dw(dyt, x2, db=db)
+            dW, aw = _gdst(weight)
+            if db is not None and ab != aw:      # bias and weight disagree on accumulation: separate sum
+                ops.linear_dw(dyt, x2, out=dW, accumulate=aw)
+                ops.colsum(dy2, out=db, accumulate=ab)
+            else:
+                ops.linear_dw(dyt, x2, out=dW, accumulate=aw, db=db)
         elif db is not None:
-            ops.colsum(dy2, out=db)
-        return dx, dW, db
+            ops.colsum(dy2, out=db, accumulate=ab)
+        return dx, _ret(dW, aw), _ret(db, ab)
 
 
 def linear(x, weight, bias=None):
@@ -65,6 +84,7 @@ class EmbedFn(torch.autograd.Function):
         xT = torch.empty(B * L, d, device=E.device, dtype=cd)
         ops.embed_fwd(xt.contiguous(), E.detach(), tbias.detach().contiguous(), x, xT, L)
         ctx.save_for_backward(xt)
+        ctx.E = (E,)
         ctx.pad_id, ctx.L, ctx.V = pad_id, L, E.shape[0]
         ctx.mark_non_differentiable(xT)
         return x, xT
@@ -74,10 +94,11 @@ class EmbedFn(torch.autograd.Function):
         (xt,) = ctx.saved_tensors
         d = dx.shape[1]
         B = xt.shape[0]
-        dE = torch.zeros(ctx.V, d, device=dx.device, dtype=F32)
+        E, = ctx.E
+        dE, aE = _gdst(E, zero=True)
         dtb = torch.zeros(B, d, device=dx.device, dtype=F32)
         ops.embed_bwd(xt.contiguous(), dx.contiguous(), dE, dtb, ctx.L, ctx.pad_id)
-        return None, dE, dtb, None
+        return None, _ret(dE, aE), dtb, None
 
 
 # -------------------------------------------------------------------------------- decoder block
@@ -166,70 +187,59 @@ class DecoderBlockFn(torch.autograd.Function):
         cd = rt.compute_dtype()
         W = {k: rt.wt(v_) for k, v_ in (("sa", sa_w), ("so", so_w), ("ca", ca_w), ("co", co_w), ("f0", f0_w),
                                          ("f3", f3_w))}
-        g = {}
+        # gradient destinations: arena views (accumulated in place) or fresh tensors
+        G = [_gdst(p_, zero=(i >= 12)) for i, p_ in enumerate(params)]  # LN params are atomically summed
+        (gsa_w, asa), (gsa_b, _), (gso_w, aso), (gso_b, _), (gca_w, aca), (gca_b, _), (gco_w, aco), (gco_b, _), \
+            (gf0_w, af0), (gf0_b, _), (gf3_w, af3), (gf3_b, _), (gn1w, _), (gn1b, _), (gn2w, _), (gn2b, _), \
+            (gn3w, _), (gn3b, _) = G
         dx3 = dx3.contiguous()
         # LN3
         dx2 = torch.empty(N, d, device=dev, dtype=F32)
         dy3 = torch.empty(N, d, device=dev, dtype=cd)
-        g["n3w"] = torch.zeros(d, device=dev, dtype=F32)
-        g["n3b"] = torch.zeros(d, device=dev, dtype=F32)
-        ops.ln_bwd(dx3, s3, m3, r3, n3w, n3b, dres=dx2, dy_t=dy3, dgamma=g["n3w"], dbeta=g["n3b"], drop_p=p,
+        ops.ln_bwd(dx3, s3, m3, r3, n3w, n3b, dres=dx2, dy_t=dy3, dgamma=gn3w, dbeta=gn3b, drop_p=p,
                    seed=seed, rng_stream=st + 6)
         # FF
-        g["f3b"] = torch.empty(d, device=dev, dtype=F32)
-        g["f3w"] = ops.linear_dw(dy3, hact, db=g["f3b"])
+        ops.linear_dw(dy3, hact, out=gf3_w, accumulate=af3, db=gf3_b)
         FF = f0_w.shape[0]
         dh = torch.empty(N, FF, device=dev, dtype=cd)
         ops.linear_dx(dy3, W["f3"], out=dh, epi=ops.EPI_DGELU, C2=hpre, drop_p=p, seed=seed, rng_stream=st + 5)
-        g["f0b"] = torch.empty(FF, device=dev, dtype=F32)
-        g["f0w"] = ops.linear_dw(dh, x2T, db=g["f0b"])
+        ops.linear_dw(dh, x2T, out=gf0_w, accumulate=af0, db=gf0_b)
         ops.linear_dx(dh, W["f0"], out=dx2, accumulate=True)
         # LN2 + FiLM
         dx1 = torch.empty(N, d, device=dev, dtype=F32)
         dyc = torch.empty(N, d, device=dev, dtype=cd)
-        g["n2w"] = torch.zeros(d, device=dev, dtype=F32)
-        g["n2b"] = torch.zeros(d, device=dev, dtype=F32)
         dfs = torch.zeros(B, d, device=dev, dtype=F32)
         dfh = torch.zeros(B, d, device=dev, dtype=F32)
-        ops.ln_bwd(dx2, s2, m2, r2, n2w, n2b, dres=dx1, dy_t=dyc, dgamma=g["n2w"], dbeta=g["n2b"], film_scale=fsc,
+        ops.ln_bwd(dx2, s2, m2, r2, n2w, n2b, dres=dx1, dy_t=dyc, dgamma=gn2w, dbeta=gn2b, film_scale=fsc,
                    dfilm=(dfs, dfh), rows_per_batch=L, drop_p=p, seed=seed, rng_stream=st + 4)
         # cross out-proj + attention
-        g["cob"] = torch.empty(d, device=dev, dtype=F32)
-        g["cow"] = ops.linear_dw(dyc, oc, db=g["cob"])
+        ops.linear_dw(dyc, oc, out=gco_w, accumulate=aco, db=gco_b)
         doc = ops.linear_dx(dyc, W["co"], out_dtype=cd)
         dqc = torch.empty(N, d, device=dev, dtype=cd)
         dkvc = torch.empty(B * S, 2 * d, device=dev, dtype=cd)
         ops.attn_bwd(qc, kvc, kvc[:, d:], oc, doc, lsec, dqc, dkvc, dkvc[:, d:], B, H, L, S, drop_p=p, seed=seed,
                      rng_stream=st + 3)
-        gca_w = torch.empty(3 * d, d, device=dev, dtype=F32)
-        gca_b = torch.empty(3 * d, device=dev, dtype=F32)
-        ops.linear_dw(dqc, x1T, out=gca_w[:d], db=gca_b[:d])
-        ops.linear_dw(dkvc, cT, out=gca_w[d:], db=gca_b[d:])
+        ops.linear_dw(dqc, x1T, out=gca_w[:d], accumulate=aca, db=gca_b[:d])
+        ops.linear_dw(dkvc, cT, out=gca_w[d:], accumulate=aca, db=gca_b[d:])
         ops.linear_dx(dqc, W["ca"][:d], out=dx1, accumulate=True)
         # LN1
         dx = torch.empty(N, d, device=dev, dtype=F32)
         dy = torch.empty(N, d, device=dev, dtype=cd)
-        g["n1w"] = torch.zeros(d, device=dev, dtype=F32)
-        g["n1b"] = torch.zeros(d, device=dev, dtype=F32)
-        ops.ln_bwd(dx1, s1, m1, r1, n1w, n1b, dres=dx, dy_t=dy, dgamma=g["n1w"], dbeta=g["n1b"], drop_p=p, seed=seed,
+        ops.ln_bwd(dx1, s1, m1, r1, n1w, n1b, dres=dx, dy_t=dy, dgamma=gn1w, dbeta=gn1b, drop_p=p, seed=seed,
                    rng_stream=st + 2)
         # self out-proj + attention
-        g["sob"] = torch.empty(d, device=dev, dtype=F32)
-        g["sow"] = ops.linear_dw(dy, o, db=g["sob"])
+        ops.linear_dw(dy, o, out=gso_w, accumulate=aso, db=gso_b)
         do = ops.linear_dx(dy, W["so"], out_dtype=cd)
         dqk = torch.empty(N, 2 * d, device=dev, dtype=cd)
         dv = torch.empty(N, d, device=dev, dtype=cd)
         ops.attn_bwd(qk, qk[:, d:], v, o, do, lse, dqk, dqk[:, d:], dv, B, H, L, L, key_keep=key_keep, drop_p=p,
                      seed=seed, rng_stream=st + 1)
-        gsa_w = torch.empty(3 * d, d, device=dev, dtype=F32)
-        gsa_b = torch.empty(3 * d, device=dev, dtype=F32)
-        ops.linear_dw(dqk, xr, out=gsa_w[: 2 * d], db=gsa_b[: 2 * d])
-        ops.linear_dw(dv, xT, out=gsa_w[2 * d:], db=gsa_b[2 * d:])
+        ops.linear_dw(dqk, xr, out=gsa_w[: 2 * d], accumulate=asa, db=gsa_b[: 2 * d])
+        ops.linear_dw(dv, xT, out=gsa_w[2 * d:], accumulate=asa, db=gsa_b[2 * d:])
         ops.linear_dx(dv, W["sa"][2 * d:], out=dx, accumulate=True)
         dxr = ops.linear_dx(dqk, W["sa"][: 2 * d])
         ops.rope_bwd(dxr, cos, sin, dx, L)
-        grads = (gsa_w, gsa_b, g["sow"], g["sob"], gca_w, gca_b, g["cow"], g["cob"], g["f0w"], g["f0b"], g["f3w"],
-                 g["f3b"], g["n1w"], g["n1b"], g["n2w"], g["n2b"], g["n3w"], g["n3b"])
+        grads = tuple(_ret(t_, a_) for t_, a_ in G)
         return (dx, None, None, None, dfs, dfh, None) + grads
 
 
@@ -242,6 +252,7 @@ class HeadFn(torch.autograd.Function):
         w = rt.wt(weight)
         logits = ops.linear(xT, w, bias, out_dtype=F32)
         ctx.save_for_backward(xT, weight)
+        ctx.bias = (bias,)
         return logits
 
     @staticmethod
@@ -250,9 +261,12 @@ class HeadFn(torch.autograd.Function):
         dl = dlogits.contiguous()
         w = rt.wt(weight)
         dx = ops.linear_dx(dl, w)                 # A = dlogits (f32, converted while staging)
-        db = torch.empty(weight.shape[0], device=dl.device, dtype=F32)
-        dW = ops.linear_dw(dl, xT, db=db)
-        return dx, None, dW, db
+        dW, aw = _gdst(weight)
+        db, ab = _gdst(ctx.bias[0])
+        if aw != ab:
+            raise RuntimeError("head weight and bias must share the grad arena")
+        ops.linear_dw(dl, xT, out=dW, accumulate=aw, db=db)
+        return dx, None, _ret(dW, aw), _ret(db, ab)
 
 
 # -------------------------------------------------------------------------------------- KL term

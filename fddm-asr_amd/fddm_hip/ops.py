@@ -80,7 +80,8 @@ def linear_dx(dy2d, w, out=None, accumulate=False, out_dtype=torch.float32, epi=
 
 def linear_dw(dy2d, x2d, out=None, accumulate=False, db=None):
     """dW[N,K] = dy[M,N]^T @ x[M,K]  (both M/N-contiguous operands, K-reduction over tokens);
-    db (optional, f32 [N]) receives sum_m dy[m] — the bias gradient, fused into the same launch."""
+    db (optional, f32 [N]) receives sum_m dy[m] — the bias gradient, fused into the same launch.
+    accumulate: out += and db += (grad-arena slots); otherwise both are overwritten."""
     M, N = dy2d.shape
     K = x2d.shape[1]
     _chk(x2d.shape[0] == M and dy2d.stride(1) == 1 and x2d.stride(1) == 1, "linear_dw shapes")
@@ -89,7 +90,7 @@ def linear_dw(dy2d, x2d, out=None, accumulate=False, db=None):
     if db is not None and dy2d.dtype != x2d.dtype:
         gemm(dy2d, x2d, out, N, K, M, a_kc=False, b_kc=False, lda=dy2d.stride(0), ldb=x2d.stride(0),
              ldc=out.stride(0), epi=EPI_ACC if accumulate else EPI_STORE)
-        colsum(dy2d, out=db)
+        colsum(dy2d, out=db, accumulate=accumulate)
         return out
     return gemm(dy2d, x2d, out, N, K, M, a_kc=False, b_kc=False, lda=dy2d.stride(0), ldb=x2d.stride(0),
                 ldc=out.stride(0), epi=EPI_ACC if accumulate else EPI_STORE, colsum=db)

@@ -21,6 +21,26 @@ class FusedAdamW(torch.optim.Optimizer):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
         self._tables = {}
         self.last_total_sq = None
+        self.arena = None
+
+    def use_grad_arena(self, params):
+        """Back the grads of `params` (parameters that get a gradient every step) by one flat buffer
+        (runtime.GradArena); zero_grad() then zeroes it with a single fill instead of dropping grads."""
+        self.arena = rt.GradArena(params)
+        return self.arena
+
+    def zero_grad(self, set_to_none: bool = True):
+        if self.arena is None:
+            return super().zero_grad(set_to_none)
+        inside = set(id(p) for p in self.arena.params)
+        for group in self.param_groups:
+            for p in group["params"]:
+                if id(p) not in inside and p.grad is not None:
+                    if set_to_none:
+                        p.grad = None
+                    else:
+                        p.grad.zero_()
+        self.arena.zero_()
 
     def _table(self, group, plist):
         dev = plist[0].device

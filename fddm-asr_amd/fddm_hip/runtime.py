@@ -160,3 +160,51 @@ def relbias_table(S: int, embed: torch.Tensor, num_buckets: int, max_distance: i
         t = embed.detach().float()[b].t().contiguous()
         _tables[k] = t
     return t
+
+
+# ---------------------------------------------------------------------------------- grad arena
+class GradArena:
+    """One flat fp32 buffer backing the .grad of parameters that receive a gradient on every step
+    (the decoder). Kernels accumulate weight gradients straight into these views (the autograd
+    Function returns None for them), one fill zeroes all of them, the fused AdamW walks them in
+    place and the DP all-reduce moves the flat buffer without packing. Each slot starts on a 256-B
+    boundary. Parameters outside the arena keep torch's None-until-touched semantics (the L_fd
+    projectors, whose None grads on non-L_fd steps make AdamW skip them, reference train.py:400-423)."""
+
+    ALIGN = 64
+
+    def __init__(self, params):
+        self.params = [p for p in params if p.requires_grad]
+        if not self.params:
+            raise ValueError("empty grad arena")
+        offs, n = [], 0
+        for p in self.params:
+            offs.append(n)
+            n += (p.numel() + self.ALIGN - 1) // self.ALIGN * self.ALIGN
+        dev = self.params[0].device
+        self.flat = torch.zeros(n, device=dev, dtype=torch.float32)
+        self.views = []
+        for p, o in zip(self.params, offs):
+            v = self.flat[o:o + p.numel()].view_as(p)
+            self.views.append(v)
+            p._fddm_arena = self
+        self.attach()
+
+    def attach(self):
+        """(re)bind every param's .grad to its arena view (after a set_to_none zero_grad)."""
+        for p, v in zip(self.params, self.views):
+            if p.grad is None or p.grad.data_ptr() != v.data_ptr():
+                p.grad = v
+
+    def zero_(self):
+        self.attach()
+        self.flat.zero_()
+
+
+def grad_slot(p: torch.Tensor):
+    """The arena view a kernel should accumulate p's gradient into, or None (autograd returns it)."""
+    a = getattr(p, "_fddm_arena", None)
+    g = p.grad
+    if a is None or g is None or g.dtype != torch.float32:
+        return None
+    return g

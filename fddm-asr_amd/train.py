@@ -116,6 +116,12 @@ def train_one_epoch(encoder, decoder, s_proj, t_embed, t_proj, scheduler, loader
     lambda_off = cfg.lfd["lambda_offdiag"]
     trainable = list(decoder.parameters()) + list(s_proj.parameters()) + list(t_embed.parameters()) + \
         list(t_proj.parameters())
+    if getattr(optimizer, "arena", 1) is None:
+        # decoder grads live in one flat buffer the kernels accumulate into (fddm_hip.runtime.GradArena)
+        opt_ids = set(id(p) for g in optimizer.param_groups for p in g["params"])
+        dparams = [p for p in decoder.parameters() if p.requires_grad]
+        if all(id(p) in opt_ids for p in dparams):
+            optimizer.use_grad_arena(dparams)
     pbar = loader
     if tqdm is not None and print_epoch_summary:
         pbar = tqdm(loader, desc=f"Epoch {epoch} [train]", leave=False)

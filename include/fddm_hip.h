@@ -26,7 +26,8 @@ const char* fddm_error_string(int code);
  *      4 dGELU (C = acc * gelu'(C2) * dropout mask).  a_kc/b_kc: operand K-contiguous (1) or
  *      M/N-contiguous (0).  A rows batched: A + (m/Mi)*sAb + (m%Mi)*lda (Mi <= 0: unbatched).
  *      colsum (optional, M/N-contiguous A only): colsum[m] = sum_k A(m,k) — the fused bias gradient of
- *      a weight-gradient GEMM dW = dY^T X (colsum = sum over tokens of dY).
+ *      a weight-gradient GEMM dW = dY^T X (colsum = sum over tokens of dY); like C it is overwritten
+ *      for EPI_STORE and accumulated (+=) for EPI_ACC.
  *      Replaces every nn.Linear / F.linear forward and backward on the path:
  *      models/denoise_decoder.py:98-100,129-145,229,238  models/projection.py:14-55
  *      models/acoustic_encoder.py:55  HF modeling_wavlm.py:93-105,125-128,274-295 */
