@@ -79,8 +79,10 @@ class DiscreteDiffusionScheduler:
         return post / post.sum(-1, keepdim=True).clamp_min(self.eps)
 
     def multi_step_coeffs(self, t: torch.Tensor, delta: int):
-        """(a_cum, b_cum) of M_{t:t-delta+1} and (a_tgt, b_tgt) of M_{t-delta}, fp32 recurrence
-        a <- a_s a, b <- a_s b + b_s (a + K b) for s = t .. t-delta+1 (diffusion_scheduler.py:124-164)."""
+        """(a_cum, b_cum) of M_{t:t-delta+1} and (a_tgt, b_tgt) of M_{t-delta}, fp32 recurrence over
+        s = t .. t-delta+1 as the reference executes it (diffusion_scheduler.py:146-167):
+        a' = a_s a, b' = a_s b + b_s (a' + K b). Note a' (not a) in the b update: the reference reads
+        `a_old` as a 0-d view of a_cumulative, which the preceding in-place store has already updated."""
         B = t.shape[0]
         a = torch.ones(B, device=self.device)
         b = torch.zeros(B, device=self.device)
@@ -89,7 +91,8 @@ class DiscreteDiffusionScheduler:
             valid = (s >= 1) & (s <= self.T)
             bs = self.betas[(s - 1).clamp(0, self.T - 1)]
             a_s, b_s = 1.0 - bs, bs / self.K
-            na, nb = a_s * a, a_s * b + b_s * (a + self.K * b)
+            na = a_s * a
+            nb = a_s * b + b_s * (na + self.K * b)
             a, b = torch.where(valid, na, a), torch.where(valid, nb, b)
         tt = (t - delta).clamp(min=0)
         btg = self.betas[(tt - 1).clamp(0, self.T - 1)]

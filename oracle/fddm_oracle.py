@@ -459,3 +459,95 @@ def oracle_train_step(params: Dict[str, torch.Tensor], enc_sd, enc_geom, wave, x
     optim.step(params, grads)
     return dict(kl=float(kl.detach()), lfd=None if lfd_v is None else float(lfd_v.detach()), loss=float(loss.detach()), c=c,
                 logits=logits.detach())
+
+
+# ------------------------------------------------------------------------------------------------
+# Jumpy sampler: sampler/jumpy_sampler.py:167-293 + q_posterior_multi_step
+# fddm/sched/diffusion_scheduler.py:106-208.
+# ------------------------------------------------------------------------------------------------
+def jump_coeffs(betas: np.ndarray, K: int, T: int, t: int, delta: int):
+    """(a_cum, b_cum, a_tg, b_tg) for one batch element, in the reference's fp32 scalar arithmetic:
+    M_{t:t-Δ+1} ≈ a_cum I + b_cum 11ᵀ over s = t..t-Δ+1 (diffusion_scheduler.py:146-167) exactly as
+    executed: a' = a_s·a, then b' = a_s·b + b_s(a' + K b) — `a_old` (:160) is a 0-d view of
+    a_cumulative, so the store at :163 is visible to the b update at :164 (pinned by the jumpy
+    fixture). M_{t-Δ} = a_tg I + b_tg 11ᵀ, identity at t-Δ = 0 (:170-185)."""
+    f = np.float32
+    betas = np.asarray(betas, dtype=np.float32)
+    a, b = f(1.0), f(0.0)
+    for s in range(t, t - delta, -1):
+        if 1 <= s <= T:
+            bs = betas[s - 1]
+            a_s = f(1.0) - bs
+            b_s = bs / f(K)
+            a = a_s * a
+            b = a_s * b + b_s * (a + f(K) * b)
+    tg = t - delta
+    if tg > 0 and tg <= T:
+        a_tg, b_tg = f(1.0) - betas[tg - 1], betas[tg - 1] / f(K)
+    else:
+        a_tg, b_tg = f(1.0), f(0.0)
+    return a, b, a_tg, b_tg
+
+
+def jump_argmax(logits: torch.Tensor, xt: torch.Tensor, t: torch.Tensor, delta: int, betas, K: int, T: int):
+    """argmax_k q(x_{t-Δ}=k | x_t, x̂0=softmax(logits)) (diffusion_scheduler.py:187-206 + argmax,
+    jumpy_sampler.py:212-215) in closed form. With x_t one-hot, the unnormalised posterior is
+    (a_cum[k=x_t] + b_cum)(a_tg x̂_k + b_tg Σx̂): every k ≠ x_t shares the factor b_cum, so the winner
+    is x_t or o = first argmax_{k≠x_t} x̂_k. Returns (next indices, margin) where margin is the
+    relative score gap (near-ties, |margin| ~ fp32 eps, may round either way in the reference)."""
+    B, L, V = logits.shape
+    delta = min(int(delta), int(t.min()))
+    z = logits.double()
+    p = torch.softmax(z, -1)
+    out = torch.empty(B, L, dtype=torch.long)
+    margin = torch.empty(B, L, dtype=torch.float64)
+    for bi in range(B):
+        a, b, a_tg, b_tg = (float(v) for v in jump_coeffs(betas, K, T, int(t[bi]), delta))
+        for li in range(L):
+            x = int(xt[bi, li])
+            row = p[bi, li].clone()
+            px = float(row[x])
+            row[x] = -1.0
+            o = int(torch.argmax(row))
+            so = b * (a_tg * float(row[o]) + b_tg)
+            sx = (a + b) * (a_tg * px + b_tg)
+            if sx > so or (sx == so and x < o):
+                out[bi, li] = x
+            else:
+                out[bi, li] = o
+            margin[bi, li] = (sx - so) / max(sx, so)
+    return out, margin
+
+
+def alpha_bar_at_t_train(alpha_bar, t_infer: int, T_infer: int, T_train: int):
+    """jumpy_sampler.py:217-233 (fast mode): nearest training step of t_infer; ᾱ₀ = 1. Indexes the
+    0-based alpha_bar[T] with a 1..T_train step exactly as the reference does (IndexError at T_train)."""
+    if t_infer <= 0:
+        return np.float32(1.0)
+    tf = max(1.0, min(float(T_train), float(t_infer) / float(max(1, T_infer)) * float(T_train)))
+    return np.float32(np.asarray(alpha_bar, dtype=np.float32)[int(round(tf))])
+
+
+def jumpy_sample(logits_fn, xT: torch.Tensor, T_infer: int, r: int, betas, alpha_bar, K: int, T_train: int,
+                 mode: str = "exact"):
+    """DiffusionJumpySampler.sample with greedy decoding (jumpy_sampler.py:235-293): from x_T jump by
+    Δ = min(r, t) until t = 0; returns the per-jump x_{t-Δ} and x̂0 argmaxes and the final
+    x0 = argmax p_x0_last. `logits_fn(x, t_vec)` is the decoder forward."""
+    B, L = xT.shape
+    x, t = xT.clone(), T_infer
+    xs, x0hats, logits = [], [], None
+    while t > 0:
+        delta = min(r, t)
+        tv = torch.full((B,), t, dtype=torch.long)
+        logits = logits_fn(x, tv)
+        if mode == "exact":
+            nx, _ = jump_argmax(logits, x, tv, delta, betas, K, T_train)
+        else:
+            ab = float(alpha_bar_at_t_train(alpha_bar, max(0, t - delta), T_infer, T_train))
+            p = torch.softmax(logits.double(), -1)
+            nx = (ab * p + (1.0 - ab) / K).argmax(-1)
+        xs.append(nx)
+        x0hats.append(logits.argmax(-1))
+        x = nx
+        t -= delta
+    return torch.stack(xs), torch.stack(x0hats), logits.argmax(-1)

@@ -316,8 +316,81 @@ def gen_step(tag, geometry, B, L, V, d, H, NL, FF, T, nsteps, seconds=1):
     save(tag, **out)
 
 
+# ---------------------------------------------------------------- jumpy sampler (C5)
+def jumpy_case_inputs(i, B, L, K):
+    """Seeded inputs of posterior case i (regenerated by tests/test_oracle_golden.py; numpy PCG64 is
+    platform-independent), so the fixture stores only the outputs."""
+    r = rng(300 + i)
+    logits = torch.from_numpy(3.0 * r.standard_normal((B, L, K), dtype=np.float32))
+    xt = torch.from_numpy(r.integers(0, K, size=(B, L))).long()
+    # make x_t a serious contender on some rows
+    boost = torch.from_numpy(r.uniform(-10.0, 6.0, size=(B, L)).astype(np.float32))
+    logits.scatter_add_(-1, xt[..., None], boost[..., None])
+    return logits, xt
+
+
+def gen_jumpy():
+    from fddm.sched.diffusion_scheduler import DiscreteDiffusionScheduler
+    from models.denoise_decoder import DenoisingTransformerDecoder
+    import sampler.jumpy_sampler as js
+
+    out = {}
+    r = rng(21)
+    # A. exact multi-step posterior argmax for given logits (q_posterior_multi_step + argmax)
+    K, T = 2000, 200
+    sch = DiscreteDiffusionScheduler(K=K, T=T, device=torch.device("cpu"), beta_max=0.2)
+    cases = [([20, 20, 20, 20], 5), ([5, 5, 5, 5], 5), ([1, 1, 1, 1], 1), ([200, 150, 90, 7], 5),
+             ([10, 12, 3, 40], 2), ([2, 30, 100, 199], 1)]
+    B, L = 4, 48
+    for i, (ts, delta) in enumerate(cases):
+        t = torch.tensor(ts)
+        logits, xt = jumpy_case_inputs(i, B, L, K)
+        p = torch.softmax(logits, -1)
+        oh = torch.zeros(B, L, K)
+        oh.scatter_(-1, xt[..., None], 1.0)
+        post = sch.q_posterior_multi_step(oh, p, t, delta)
+        out[f"c{i}_t"] = t
+        out[f"c{i}_delta"] = np.int64(delta)
+        out[f"c{i}_xt"] = xt
+        out[f"c{i}_next"] = post.argmax(-1)
+        out[f"c{i}_post_max"] = post.max(-1).values
+    # B. full sampler run (exact, greedy) with a small decoder, x_T drawn from torch.manual_seed(5)
+    V, d, H, NL, FF = 1000, 128, 2, 2, 256
+    Bs, S, Ls = 3, 20, 16
+    dec = DenoisingTransformerDecoder(vocab_size=V, d_model=d, nhead=H, num_layers=NL, dim_ff=FF, dropout=0.1,
+                                      max_len=1024, pad_id=0)
+    load_pcg(dec, prefix="dec.", pad_row=("tok_emb.weight", 0))
+    dec.eval()
+    cond = torch.from_numpy(r.standard_normal((Bs, S, d), dtype=np.float32))
+    sch2 = DiscreteDiffusionScheduler(K=V, T=200, device=torch.device("cpu"), beta_max=0.2)
+    for mode in ("exact", "fast"):
+        smp = js.DiffusionJumpySampler(sch2, dec, K=V, T_train=200, T_infer=20, r=5, greedy=True,
+                                       posterior_mode="map", sampling_mode=mode, device=torch.device("cpu"))
+        seq = []
+        orig = smp._jump_once
+
+        def rec(x, t_scalar, delta, cond_c, seq_len, _orig=orig, _seq=seq):
+            nx, p = _orig(x, t_scalar=t_scalar, delta=delta, cond_c=cond_c, seq_len=seq_len)
+            _seq.append((x.clone(), t_scalar, delta, nx.clone(), p.argmax(-1)))
+            return nx, p
+
+        smp._jump_once = rec
+        torch.manual_seed(5)
+        with torch.no_grad():
+            x0, plast = smp.sample(cond, seq_len=Ls)
+        out[f"run_{mode}_xT"] = seq[0][0]
+        out[f"run_{mode}_ts"] = np.array([s_[1] for s_ in seq])
+        out[f"run_{mode}_deltas"] = np.array([s_[2] for s_ in seq])
+        out[f"run_{mode}_xs"] = torch.stack([s_[3] for s_ in seq])
+        out[f"run_{mode}_x0hat"] = torch.stack([s_[4] for s_ in seq])
+        out[f"run_{mode}_x0"] = x0
+        out[f"run_{mode}_plast_max"] = plast.max(-1).values
+    out["run_cond"] = cond
+    save("jumpy", **out)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["sched", "kl", "rope", "lfd", "decoder", "wavlm", "step_c1", "step_repeat"]
+    which = sys.argv[1:] or ["sched", "kl", "rope", "lfd", "decoder", "wavlm", "step_c1", "step_repeat", "jumpy"]
     if "sched" in which:
         gen_sched()
     if "kl" in which:
@@ -333,6 +406,8 @@ if __name__ == "__main__":
     if "step_c1" in which:
         # C1: WavLM-base, 2-layer d=128 decoder (H=2 -> head_dim 64), 4 x (1 s, 32 tokens), T=10, V=8000
         gen_step("step_c1", {}, B=4, L=32, V=8000, d=128, H=2, NL=2, FF=2048, T=10, nsteps=4)
+    if "jumpy" in which:
+        gen_jumpy()
     if "step_repeat" in which:
         # S (49) < L (64): exercises the repeat-last-frame alignment branch (train.py:385-387)
         gen_step("step_repeat", SMALL_WAVLM, B=3, L=64, V=500, d=128, H=2, NL=1, FF=256, T=20, nsteps=4)

@@ -114,3 +114,14 @@ def _step_params(V, d, NL, FF, H):
     return params
 
 
+
+
+def jumpy_case_inputs(i, B, L, K):
+    """Seeded inputs of jumpy posterior case i — the same numpy-PCG64 draws as
+    tests/golden/make_golden.py:jumpy_case_inputs (the fixture stores only the outputs)."""
+    r = np.random.Generator(np.random.PCG64(300 + i))
+    logits = torch.from_numpy(3.0 * r.standard_normal((B, L, K), dtype=np.float32))
+    xt = torch.from_numpy(r.integers(0, K, size=(B, L))).long()
+    boost = torch.from_numpy(r.uniform(-10.0, 6.0, size=(B, L)).astype(np.float32))
+    logits.scatter_add_(-1, xt[..., None], boost[..., None])
+    return logits, xt
