@@ -266,3 +266,21 @@ def lfd_dloss(Cm, gscale, lam, out_dtype):
     dC = torch.empty(D, D, device=Cm.device, dtype=out_dtype)
     call("fddm_lfd_dloss", code(dC), ptr(Cm), ptr(gscale), ptr(dC), D, float(lam), stream())
     return dC
+
+
+JUMP_FAST, JUMP_SAMPLE = 1, 2
+
+
+def jump(logits2d, xt, coef, L, mode=0, temperature=1.0, seed=0, rng_stream=0, x_next=None, x0hat=None):
+    """One jumpy-sampler step over logits [N, V] (f32): returns (x_next [N], x0hat [N]) int64."""
+    N, V = logits2d.shape
+    _chk(logits2d.dtype == torch.float32 and logits2d.stride(1) == 1, "jump: f32 rows with unit stride")
+    _chk(xt.numel() == N and xt.dtype == torch.int64 and coef.dtype == torch.float32, "jump: xt/coef")
+    _chk(coef.numel() >= 4 * ((N + L - 1) // L), "jump: coef holds 4 floats per batch element")
+    if x_next is None:
+        x_next = torch.empty(N, device=logits2d.device, dtype=torch.int64)
+    if x0hat is None:
+        x0hat = torch.empty(N, device=logits2d.device, dtype=torch.int64)
+    call("fddm_jump", ptr(logits2d), logits2d.stride(0), ptr(xt), ptr(coef), ptr(x_next), ptr(x0hat), N, L, V, mode,
+         float(temperature), seed, rng_stream, stream())
+    return x_next, x0hat

@@ -124,6 +124,15 @@ int fddm_adamw(const long* chunk_tensor, const long* chunk_start, const long* nu
                const float* step_size, const float* bc2_sqrt, long nchunks, const float* total, float max_norm,
                float lr_wd, float b1, float b2, float eps, void* hip_stream);
 
+/* ---- jumpy sampler denoise step (sampler/jumpy_sampler.py:167-215 + q_posterior_multi_step,
+ *      fddm/sched/diffusion_scheduler.py:106-208): x_next = argmax (or a tempered draw) of the
+ *      multi-step posterior q(x_{t-Δ} | x_t, softmax(logits)); x0hat = argmax logits.
+ *      coef: per batch element {a_cum, b_cum, a_tg, b_tg} (exact) or {abar, 0, 0, 0} (fast).
+ *      mode: bit0 fast (ᾱ/uniform mix, jumpy_sampler.py:138-151), bit1 sample (Categorical). */
+int fddm_jump(const float* logits, long ldz, const long* xt, const float* coef, long* x_next, long* x0hat, long N,
+              long L, long V, int mode, float temperature, unsigned long long seed, unsigned long long stream,
+              void* hip_stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -95,3 +95,27 @@ def test_dropout_stream_contract():
     k2 = O.dropout_keep(1, 2, 200000, 0.1)
     assert abs(k1.float().mean().item() - 0.9) < 0.005
     assert (k1 != k2).float().mean().item() > 0.1
+
+
+def test_jumpy_sampler_api_and_plan():
+    """DiffusionJumpySampler keeps the reference signature (jumpy_sampler.py:106-119, 238-243); the jump
+    plan and the exact-mode coefficients (host fp32) equal the oracle's restatement bit for bit."""
+    from fddm.sched.diffusion_scheduler import DiscreteDiffusionScheduler
+    from sampler.jumpy_sampler import DiffusionJumpySampler
+    sig = list(inspect.signature(DiffusionJumpySampler.__init__).parameters)[1:]
+    assert sig == ["scheduler", "decoder", "K", "T_train", "T_infer", "r", "greedy", "posterior_mode", "sampling_mode",
+                   "temperature", "device"]
+    assert list(inspect.signature(DiffusionJumpySampler.sample).parameters)[1:4] == ["cond_c", "seq_len", "init"]
+    cpu = torch.device("cpu")
+    sch = DiscreteDiffusionScheduler(K=8000, T=200, device=cpu)
+    b, _ = O.sched_tables(200)
+    for T_inf, r in ((20, 5), (20, 3), (7, 7)):
+        smp = DiffusionJumpySampler(sch, None, K=8000, T_train=200, T_infer=T_inf, r=r, device=cpu)
+        plan = smp._plan(2)
+        ts = [p[0] for p in plan]
+        assert ts == list(range(T_inf, 0, -r)) and sum(p[1] for p in plan) == T_inf
+        for t, d, coef in plan:
+            ref = np.array(O.jump_coeffs(b.numpy(), 8000, 200, t, d), dtype=np.float32)
+            assert np.array_equal(coef[0].numpy(), ref) and np.array_equal(coef[1].numpy(), ref)
+    fast = DiffusionJumpySampler(sch, None, K=8000, T_train=200, T_infer=20, r=5, sampling_mode="fast", device=cpu)
+    assert float(fast._plan(1)[0][2][0, 0]) == float(sch.alpha_bar[150])
