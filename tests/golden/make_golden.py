@@ -389,8 +389,45 @@ def gen_jumpy():
     save("jumpy", **out)
 
 
+# ---------------------------------------------------------------- CER / WER evaluation
+def gen_cer():
+    from models.evaluate import _ids_to_text_one, calculate_cer, calculate_wer
+
+    r = rng(31)
+    pool = list("我這可以交流道台有一沒中在大個們公路臺捷運新高什麼自己你是的人就問題還雄但他知政府現也") + [" "] * 6
+    refs, hyps = [], []
+    for i in range(60):
+        n = int(r.integers(0, 40)) if i % 10 else 0
+        ref = "".join(r.choice(pool, size=n))
+        hyp = list(ref)
+        for _ in range(int(r.integers(0, 8))):          # random edits
+            op = int(r.integers(0, 3))
+            pos = int(r.integers(0, len(hyp) + 1))
+            if op == 0 and hyp and pos < len(hyp):
+                hyp[pos] = str(r.choice(pool))
+            elif op == 1:
+                hyp.insert(pos, str(r.choice(pool)))
+            elif hyp and pos < len(hyp):
+                del hyp[pos]
+        hyp = "".join(hyp) if i % 13 else ""
+        refs.append(ref)
+        hyps.append(hyp)
+    cer = [calculate_cer(a, b) for a, b in zip(refs, hyps)]
+    wer = [calculate_wer(a, b) for a, b in zip(refs, hyps)]
+
+    class Rec:  # records the ids _ids_to_text_one hands to the tokenizer
+        def DecodeIds(self, ids):
+            return ",".join(str(i) for i in ids)
+
+    ids = torch.from_numpy(r.integers(0, 12, size=(40, 24))).long()
+    clean = [_ids_to_text_one(ids[i], Rec(), pad_id=0, bos_id=1 if i % 2 else None, eos_id=2 if i % 3 else None)
+             for i in range(40)]
+    save("cer", refs=np.array(refs), hyps=np.array(hyps), cer=np.array(cer), wer=np.array(wer), ids=ids,
+         clean=np.array(clean))
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["sched", "kl", "rope", "lfd", "decoder", "wavlm", "step_c1", "step_repeat", "jumpy"]
+    which = sys.argv[1:] or ["sched", "kl", "rope", "lfd", "decoder", "wavlm", "step_c1", "step_repeat", "jumpy", "cer"]
     if "sched" in which:
         gen_sched()
     if "kl" in which:
@@ -408,6 +445,8 @@ if __name__ == "__main__":
         gen_step("step_c1", {}, B=4, L=32, V=8000, d=128, H=2, NL=2, FF=2048, T=10, nsteps=4)
     if "jumpy" in which:
         gen_jumpy()
+    if "cer" in which:
+        gen_cer()
     if "step_repeat" in which:
         # S (49) < L (64): exercises the repeat-last-frame alignment branch (train.py:385-387)
         gen_step("step_repeat", SMALL_WAVLM, B=3, L=64, V=500, d=128, H=2, NL=1, FF=256, T=20, nsteps=4)
