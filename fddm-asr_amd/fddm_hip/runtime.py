@@ -9,7 +9,6 @@ Precision modes (SURVEY §7 "Two precision modes"):
 from __future__ import annotations
 
 import contextlib
-import itertools
 import math
 import os
 
@@ -98,22 +97,35 @@ def clear_cache():
 
 
 # ---------------------------------------------------------------------------------------- seeds
-_seed_counter = itertools.count(1)
+_seed_counter = 0
 _base_seed = None
 
 
 def next_seed() -> int:
     """A fresh dropout seed per forward call (deterministic given torch.initial_seed())."""
-    global _base_seed
+    global _base_seed, _seed_counter
     if _base_seed is None:
         _base_seed = int(torch.initial_seed()) & 0xFFFFFFFF
-    return (_base_seed * 1000003 + next(_seed_counter)) & 0x7FFFFFFFFFFFFFFF
+    _seed_counter += 1
+    return (_base_seed * 1000003 + _seed_counter) & 0x7FFFFFFFFFFFFFFF
 
 
 def reseed(seed: int) -> None:
     global _base_seed, _seed_counter
     _base_seed = int(seed) & 0xFFFFFFFF
-    _seed_counter = itertools.count(1)
+    _seed_counter = 0
+
+
+def seed_state() -> list:
+    """[base seed, counter] — saved in checkpoints so a resumed run continues the same streams."""
+    return [-1 if _base_seed is None else int(_base_seed), int(_seed_counter)]
+
+
+def set_seed_state(state) -> None:
+    global _base_seed, _seed_counter
+    b, c = int(state[0]), int(state[1])
+    _base_seed = None if b < 0 else b
+    _seed_counter = c
 
 
 # --------------------------------------------------------------------------------------- tables

@@ -205,10 +205,54 @@ def build_models(cfg: Config, device):
     return encoder, decoder, s_proj, t_embed, t_proj, sched
 
 
+def _tokenizer(cfg, tok_path):
+    """SentencePiece when its .model is present (reference train.py:596-598), else the offline
+    vocab.json decoder (models.evaluate.VocabTokenizer)."""
+    if tok_path and os.path.exists(tok_path):
+        try:
+            import sentencepiece as spm
+            tok = spm.SentencePieceProcessor()
+            tok.load(tok_path)
+            return tok
+        except Exception:
+            pass
+    from models.evaluate import VocabTokenizer
+    vj = cfg.data.get("vocab_json") or os.path.join(os.path.dirname(tok_path or "."), "vocab.json")
+    return VocabTokenizer(vj)
+
+
+def save_checkpoint(path, decoder, s_proj, t_embed, t_proj, step, epoch, raw, optimizer=None, **extra):
+    """Reference checkpoint layout (train.py:622-664): decoder / s_proj / t_embed / t_proj state_dicts,
+    step, epoch, config. Additive keys for resuming: optimizer (torch AdamW layout), rng seed state."""
+    ckpt = {"decoder": decoder.state_dict(), "s_proj": s_proj.state_dict(), "t_embed": t_embed.state_dict(),
+            "t_proj": t_proj.state_dict(), "step": step, "epoch": epoch, "config": raw}
+    ckpt.update(extra)
+    if optimizer is not None:
+        ckpt["optimizer"] = optimizer.state_dict()
+        ckpt["fddm_seed"] = rt.seed_state()
+    torch.save(ckpt, path)
+
+
+def load_checkpoint(path, decoder, s_proj, t_embed, t_proj, optimizer=None, map_location="cpu"):
+    """Loads a reference or MI355X checkpoint (weights only, no pickled code); returns (step, epoch)."""
+    ck = torch.load(path, map_location=map_location, weights_only=True)
+    decoder.load_state_dict(ck["decoder"])
+    s_proj.load_state_dict(ck["s_proj"])
+    t_embed.load_state_dict(ck["t_embed"])
+    t_proj.load_state_dict(ck["t_proj"])
+    if optimizer is not None and "optimizer" in ck:
+        optimizer.load_state_dict(ck["optimizer"])
+    if "fddm_seed" in ck:
+        rt.set_seed_state(ck["fddm_seed"])
+    rt.clear_cache()
+    return int(ck.get("step", 1)), int(ck.get("epoch", 0))
+
+
 def main():
     ap = argparse.ArgumentParser(description="FDDM-ASR Training Script (MI355X)")
     ap.add_argument("--config", type=str, required=True)
     ap.add_argument("--device", type=str, default="cuda" if torch.cuda.is_available() else "cpu")
+    ap.add_argument("--resume", type=str, default=None, help="checkpoint to resume from (additive option)")
     args = ap.parse_args()
     setup_logging()
     with open(args.config, "r", encoding="utf-8") as f:
@@ -221,6 +265,15 @@ def main():
     device = torch.device(args.device)
     if device.type != "cuda":
         raise RuntimeError("the MI355X build runs on a HIP device only (no CPU fallback)")
+    distributed = int(os.environ.get("WORLD_SIZE", "1")) > 1
+    if distributed:
+        import torch.distributed as tdist
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        device = torch.device("cuda", local)
+        torch.cuda.set_device(device)
+        tdist.init_process_group("nccl", device_id=device)
+        rt.reseed(cfg.seed + tdist.get_rank())
+    rank0 = not distributed or int(os.environ.get("RANK", "0")) == 0
     encoder, decoder, s_proj, t_embed, t_proj, sched = build_models(cfg, device)
     params = list(decoder.parameters()) + list(s_proj.parameters()) + list(t_embed.parameters()) + \
         list(t_proj.parameters())
@@ -228,20 +281,58 @@ def main():
 
     from data_io import CVZhTWDataset  # real-data input path (librosa / sentencepiece)
     train_json = cfg.data.get("train_json", "data/processed/train.json")
+    val_json = cfg.data.get("val_json", "data/processed/val.json")
+    test_json = cfg.data.get("test_json", "data/processed/test.json")
     tok_path = cfg.data.get("tokenizer_model_path", "data/tokenizer/zh-TW_A/spm_zhTW_A.model")
-    train_set = CVZhTWDataset(train_json, tok_path, cfg.data.get("max_len", 128), cfg.data["pad_id"],
-                              cfg.data.get("bos_id"), cfg.data.get("eos_id"))
-    loader = torch.utils.data.DataLoader(train_set, batch_size=cfg.optim["batch_size"], shuffle=True, drop_last=True)
+
+    def _loader(path, shuffle):
+        ds = CVZhTWDataset(path, tok_path, cfg.data.get("max_len", 128), cfg.data["pad_id"], cfg.data.get("bos_id"),
+                           cfg.data.get("eos_id"))
+        sampler = None
+        if distributed and shuffle:
+            sampler = torch.utils.data.distributed.DistributedSampler(ds, shuffle=True, drop_last=True)
+        return torch.utils.data.DataLoader(ds, batch_size=cfg.optim["batch_size"], shuffle=shuffle and sampler is None,
+                                           sampler=sampler, drop_last=shuffle)
+
+    train_loader = _loader(train_json, True)
+    val_loader = _loader(val_json, False) if os.path.exists(val_json) else None
+    test_loader = _loader(test_json, False) if os.path.exists(test_json) else None
+    tokenizer = _tokenizer(cfg, tok_path) if (val_loader or test_loader) else None
     os.makedirs(cfg.log["ckpt_dir"], exist_ok=True)
-    global_step = 1
-    for epoch in range(1, cfg.optim["num_epochs"] + 1):
+    global_step, start_epoch = 1, 1
+    if args.resume:
+        global_step, last_epoch = load_checkpoint(args.resume, decoder, s_proj, t_embed, t_proj, optim, device)
+        start_epoch = last_epoch + 1
+    from models.evaluate import evaluate_cer_with_jumpy_sampling, evaluate_validation_loss
+    best_val_cer, best_epoch = float("inf"), 0
+    for epoch in range(start_epoch, cfg.optim["num_epochs"] + 1):
         logging.info(f"Epoch {epoch}")
-        global_step, train_loss = train_one_epoch(encoder, decoder, s_proj, t_embed, t_proj, sched, loader, optim,
-                                                  device, cfg, global_step, None, epoch)
-        logging.info(f"[Epoch {epoch} Summary] train_loss={train_loss:.4f}")
-        ckpt = {"decoder": decoder.state_dict(), "s_proj": s_proj.state_dict(), "t_embed": t_embed.state_dict(),
-                "t_proj": t_proj.state_dict(), "step": global_step, "epoch": epoch, "config": raw}
-        torch.save(ckpt, os.path.join(cfg.log["ckpt_dir"], f"ep{epoch:03d}.pt"))
+        if hasattr(train_loader.sampler, "set_epoch"):
+            train_loader.sampler.set_epoch(epoch)
+        global_step, train_loss = train_one_epoch(encoder, decoder, s_proj, t_embed, t_proj, sched, train_loader,
+                                                  optim, device, cfg, global_step, None, epoch)
+        msg = f"[Epoch {epoch} Summary] train_loss={train_loss:.4f}"
+        if rank0 and val_loader is not None:
+            val_cer = evaluate_cer_with_jumpy_sampling(encoder, decoder, sched, val_loader, device, cfg, tokenizer)
+            val_loss = evaluate_validation_loss(encoder, decoder, s_proj, t_embed, t_proj, sched, val_loader, device,
+                                                cfg)
+            msg += f" | val_loss={val_loss:.4f} | val_cer={val_cer:.4f}"
+            if val_cer < best_val_cer:
+                best_val_cer, best_epoch = val_cer, epoch
+                save_checkpoint(os.path.join(cfg.log["ckpt_dir"], "best_model.pt"), decoder, s_proj, t_embed, t_proj,
+                                global_step, epoch, raw, best_val_cer=best_val_cer)
+        if rank0 and test_loader is not None:
+            test_cer = evaluate_cer_with_jumpy_sampling(encoder, decoder, sched, test_loader, device, cfg, tokenizer)
+            msg += f" | test_cer={test_cer:.4f}"
+        logging.info(msg)
+        if rank0:
+            save_checkpoint(os.path.join(cfg.log["ckpt_dir"], f"ep{epoch:03d}.pt"), decoder, s_proj, t_embed, t_proj,
+                            global_step, epoch, raw, optimizer=optim)
+    if rank0:
+        logging.info(f"Best validation CER: {best_val_cer:.4f} (Epoch {best_epoch})")
+    if distributed:
+        import torch.distributed as tdist
+        tdist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -119,3 +119,41 @@ def test_jumpy_sampler_api_and_plan():
             assert np.array_equal(coef[0].numpy(), ref) and np.array_equal(coef[1].numpy(), ref)
     fast = DiffusionJumpySampler(sch, None, K=8000, T_train=200, T_infer=20, r=5, sampling_mode="fast", device=cpu)
     assert float(fast._plan(1)[0][2][0, 0]) == float(sch.alpha_bar[150])
+
+
+def test_checkpoint_layout_and_resume_roundtrip(tmp_path):
+    """save/load_checkpoint keep the reference's checkpoint keys (train.py:652-664) and restore weights,
+    optimizer state and the dropout seed stream (torch.load weights_only)."""
+    import train as T_
+    from fddm_hip import runtime as rt
+    from fddm_hip.optim import FusedAdamW
+    from models.denoise_decoder import DenoisingTransformerDecoder
+    from models.projection import SpeechProjector, TextEmbedding, TextProjector
+
+    def build(seed):
+        torch.manual_seed(seed)
+        mods = (DenoisingTransformerDecoder(vocab_size=304, d_model=128, nhead=2, num_layers=1, dim_ff=256),
+                SpeechProjector(128, 64), TextEmbedding(304, 64), TextProjector(64, 64))
+        ps = [p for m in mods for p in m.parameters()]
+        return mods, FusedAdamW(ps, lr=1e-3)
+
+    (dec, sp, te, tp), opt = build(1)
+    st = opt.state[next(iter(dec.parameters()))]
+    st["step"], st["exp_avg"], st["exp_avg_sq"] = 3, torch.ones(1), torch.full((1,), 2.0)
+    rt.reseed(77)
+    rt.next_seed()
+    path = str(tmp_path / "ep001.pt")
+    T_.save_checkpoint(path, dec, sp, te, tp, step=42, epoch=1, raw={"seed": 1}, optimizer=opt)
+    ck = torch.load(path, weights_only=True)
+    assert {"decoder", "s_proj", "t_embed", "t_proj", "step", "epoch", "config"} <= set(ck)
+    expect_next = rt.next_seed()
+    (dec2, sp2, te2, tp2), opt2 = build(2)
+    rt.reseed(5)
+    step, epoch = T_.load_checkpoint(path, dec2, sp2, te2, tp2, opt2)
+    assert (step, epoch) == (42, 1)
+    for a, b in ((dec, dec2), (sp, sp2), (te, te2), (tp, tp2)):
+        for (n, x), (_, y) in zip(a.state_dict().items(), b.state_dict().items()):
+            assert torch.equal(x, y), n
+    st2 = opt2.state[next(iter(dec2.parameters()))]
+    assert st2["step"] == 3 and float(st2["exp_avg_sq"][0]) == 2.0
+    assert rt.next_seed() == expect_next
