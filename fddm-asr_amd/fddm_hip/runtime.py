@@ -220,3 +220,34 @@ def grad_slot(p: torch.Tensor):
     if a is None or g is None or g.dtype != torch.float32:
         return None
     return g
+
+
+# ------------------------------------------------------------------------------ launch probes
+_probes: dict | None = None
+
+
+@contextlib.contextmanager
+def probe(name: str):
+    """HIP events around one launch site on the current stream, recorded only while
+    `probing([...names])` is active (bench.py times its dominant kernel inside the timed steps)."""
+    if _probes is None or name not in _probes:
+        yield
+        return
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    yield
+    e1.record(s)
+    _probes[name].append((e0, e1))
+
+
+@contextlib.contextmanager
+def probing(names):
+    """Collect probe events for `names`; yields the dict name -> list of (start, end) events."""
+    global _probes
+    old = _probes
+    _probes = {n: [] for n in names}
+    try:
+        yield _probes
+    finally:
+        _probes = old

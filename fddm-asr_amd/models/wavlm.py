@@ -160,8 +160,9 @@ class WavLMModel(nn.Module):
             k, s, co = c.conv_kernel[i], c.conv_stride[i], c.conv_dim[i]
             Tout = (T - k) // s + 1
             out = torch.empty(B, Tout, co, device=wave.device, dtype=cd)
-            ops.conv1d_gemm(h, P["conv"][i - 1], out, lda=cin, sAb=T * cin, Tin=T, Cg=cin, cstride=s, cpad=0, Bn=B,
-                            Tout=Tout, N=co, K=k * cin, gelu=True)
+            with rt.probe(f"wavlm.conv{i}"):
+                ops.conv1d_gemm(h, P["conv"][i - 1], out, lda=cin, sAb=T * cin, Tin=T, Cg=cin, cstride=s, cpad=0,
+                                Bn=B, Tout=Tout, N=co, K=k * cin, gelu=True)
             h, T, cin = out, Tout, co
         S, E, H = T, c.hidden_size, c.num_attention_heads
         eps = c.layer_norm_eps
