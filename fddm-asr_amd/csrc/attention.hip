@@ -236,6 +236,183 @@ __global__ void __launch_bounds__(256) fwd_kernel(AttnArgs a) {
   if (a.lse && g == 0) a.lse[(long)bh * a.Lq + q] = (l > 0.f) ? m + __logf(l) : NAN;
 }
 
+// ------------------------------------------------------------------------------------ fwd (bf16)
+// 128 queries per workgroup: each wave owns two 16-query groups, so every K fragment (LDS row read) and
+// every V^T fragment (tr read) feeds two MFMAs. K/V tiles are double-buffered in LDS; the next tile's
+// global loads are issued before this tile's MFMAs and written after them (one barrier per tile).
+// The WavLM bias slice for the tile (191 table entries: key - q spans [k0-q0-127, k0+63-q0]) is staged
+// with the tile instead of gathered from global memory per score.
+__global__ void __launch_bounds__(256) fwd2_kernel(AttnArgs a) {
+  constexpr int RB = 128;
+  __shared__ __attribute__((aligned(16))) unsigned char kbuf[2][64 * RB];
+  __shared__ __attribute__((aligned(16))) unsigned char vbuf[2][64 * RB];
+  __shared__ float tbuf[2][192];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, i = lane & 15;
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int qbase = blockIdx.x * 128;
+  const bf16_t* Qb = (const bf16_t*)a.Q + (long)b * a.Lq * a.sq + h * DH;
+  const bf16_t* Kb = (const bf16_t*)a.K + (long)b * a.Lk * a.sk + h * DH;
+  const bf16_t* Vb = (const bf16_t*)a.V + (long)b * a.Lk * a.sv + h * DH;
+  const float* tabh = a.table ? a.table + (long)h * (2 * a.Lk - 1) : nullptr;
+  int q[2];
+  bool qv[2];
+  uint4 qf[2][2];
+  float gate[2];
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq) {
+    q[gq] = qbase + w * 32 + gq * 16 + i;
+    qv[gq] = q[gq] < a.Lq;
+    row_frags<bf16_t>(qf[gq], Qb, a.sq, qv[gq] ? q[gq] : 0, qv[gq], lane);
+    gate[gq] = (a.gate && qv[gq]) ? a.gate[(long)bh * a.Lq + q[gq]] : 0.f;
+  }
+  // tile loader: 512 16-B chunks of K and of V per tile, 2 each per thread
+  uint4 kr[2], vr[2];
+  float tv = 0.f;
+  auto load = [&](int k0) {
+    const int nv = min(64, a.Lk - k0);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int idx = tid + 256 * u, r = idx >> 3, c = idx & 7;
+      kr[u] = vr[u] = make_uint4(0, 0, 0, 0);
+      if (r < nv) {
+        kr[u] = *(const uint4*)(Kb + (long)(k0 + r) * a.sk + c * 8);
+        vr[u] = *(const uint4*)(Vb + (long)(k0 + r) * a.sv + c * 8);
+      }
+    }
+    if (tabh && tid < 191) {
+      const long ti = (long)k0 - qbase - 127 + (a.Lk - 1) + tid;
+      tv = (ti >= 0 && ti < 2L * a.Lk - 1) ? tabh[ti] : 0.f;
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int idx = tid + 256 * u, r = idx >> 3, c = idx & 7;
+      *(uint4*)(kbuf[buf] + kc_off(RB, r, c)) = kr[u];
+      *(uint4*)(vbuf[buf] + r * 128 + (((2 * c) ^ hatt(r)) << 3)) = vr[u];
+    }
+    if (tabh && tid < 191) tbuf[buf][tid] = tv;
+  };
+
+  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
+  f32x4_t o[2][4];
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq)
+#pragma unroll
+    for (int d = 0; d < 4; ++d) o[gq][d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  load(0);
+  store(0);
+  __syncthreads();
+  const int ntiles = (a.Lk + 63) / 64;
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1, k0 = t * 64;
+    if (t + 1 < ntiles) load(k0 + 64);
+    const unsigned char* kimg = kbuf[cur];
+    const unsigned char* vimg = vbuf[cur];
+    f32x4_t s[2][4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      s[0][kb] = s[1][kb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub) {
+        const uint4 af = *(const uint4*)(kimg + kc_off(RB, kb * 16 + i, sub * 4 + g));
+        mma<bf16_t>(s[0][kb], af, qf[0][sub]);
+        mma<bf16_t>(s[1][kb], af, qf[1][sub]);
+      }
+    }
+    float p[2][4][4];
+#pragma unroll
+    for (int gq = 0; gq < 2; ++gq) {
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int kl = kb * 16 + 4 * g + j, key = k0 + kl;
+          float x = s[gq][kb][j] * a.scale;
+          if (tabh) x += gate[gq] * tbuf[cur][kl - (q[gq] - qbase) + 127];
+          if (!key_ok(a, b, key)) x = -INFINITY;
+          p[gq][kb][j] = x;
+          tmax = fmaxf(tmax, x);
+        }
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const float mn = fmaxf(m[gq], tmax);
+      const float alpha = (mn == -INFINITY) ? 1.f : __expf(m[gq] - mn);
+      float ls = 0.f;
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float e = (mn == -INFINITY) ? 0.f : __expf(p[gq][kb][j] - mn);
+          ls += e;
+          if (a.thr16) {
+            const int key = k0 + kb * 16 + 4 * g + j;
+            const uint64_t idx = ((uint64_t)bh * a.Lq + q[gq]) * a.Lk + key;
+            e = drop_keep(a.seed, a.stream, idx, a.thr16) ? e * a.drop_scale : 0.f;
+          }
+          p[gq][kb][j] = e;
+        }
+      l[gq] = l[gq] * alpha + ls;
+      m[gq] = mn;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) o[gq][d] *= alpha;
+    }
+    // O^T += V^T P^T for both query groups (one tr-read A fragment, two MFMAs)
+    {
+      const int qq = i >> 2, pp = i & 3;
+      typedef __attribute__((address_space(3))) s16x4_t* lp;
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        uint4 bq[2];
+#pragma unroll
+        for (int gq = 0; gq < 2; ++gq) {
+          bq[gq].x = pk(p[gq][2 * ss][0], p[gq][2 * ss][1]);
+          bq[gq].y = pk(p[gq][2 * ss][2], p[gq][2 * ss][3]);
+          bq[gq].z = pk(p[gq][2 * ss + 1][0], p[gq][2 * ss + 1][1]);
+          bq[gq].w = pk(p[gq][2 * ss + 1][2], p[gq][2 * ss + 1][3]);
+        }
+        const int k1 = 32 * ss + 4 * g + qq, k2 = k1 + 16;
+#pragma unroll
+        for (int db = 0; db < 4; ++db) {
+          const int u = db * 4 + pp;
+          const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(vimg + k1 * 128 + ((u ^ hatt(k1)) << 3)));
+          const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(vimg + k2 * 128 + ((u ^ hatt(k2)) << 3)));
+          uint4 af;
+          af.x = (unsigned)(unsigned short)lo[0] | ((unsigned)(unsigned short)lo[1] << 16);
+          af.y = (unsigned)(unsigned short)lo[2] | ((unsigned)(unsigned short)lo[3] << 16);
+          af.z = (unsigned)(unsigned short)hi[0] | ((unsigned)(unsigned short)hi[1] << 16);
+          af.w = (unsigned)(unsigned short)hi[2] | ((unsigned)(unsigned short)hi[3] << 16);
+          mma<bf16_t>(o[0][db], af, bq[0]);
+          mma<bf16_t>(o[1][db], af, bq[1]);
+        }
+      }
+    }
+    if (t + 1 < ntiles) {
+      store(cur ^ 1);
+      __syncthreads();
+    }
+  }
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq) {
+    float lt = l[gq];
+    lt += __shfl_xor(lt, 16, 64);
+    lt += __shfl_xor(lt, 32, 64);
+    if (!qv[gq]) continue;
+    const float inv = (lt > 0.f) ? 1.f / lt : NAN;  // fully masked row -> NaN like softmax(all -inf)
+    bf16_t* Ob = (bf16_t*)a.Out + ((long)b * a.Lq + q[gq]) * a.so + h * DH;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      uint2 u2;
+      u2.x = pk(o[gq][d][0] * inv, o[gq][d][1] * inv);
+      u2.y = pk(o[gq][d][2] * inv, o[gq][d][3] * inv);
+      *(uint2*)(Ob + d * 16 + 4 * g) = u2;
+    }
+    if (a.lse && g == 0) a.lse[(long)bh * a.Lq + q[gq]] = (lt > 0.f) ? m[gq] + __logf(lt) : NAN;
+  }
+}
+
 // ------------------------------------------------------------------------------------------- dQ
 // query-owned: recompute S^T, dP^T = V dO^T; dS = P (dP - delta); dQ^T = K^T dS^T
 template <typename T>
@@ -395,6 +572,13 @@ template <typename T>
 static int run(int which, AttnArgs& a, hipStream_t s) {
   constexpr int RB = Cfg<T>::RB;
   if (which == 0) {
+    if constexpr (sizeof(T) == 2) {
+      if (!getenv("FDDM_ATTN_V1")) {
+        dim3 grid((a.Lq + 127) / 128, a.B * a.H);
+        hipLaunchKernelGGL(fwd2_kernel, grid, dim3(256), 0, s, a);
+        return (int)hipGetLastError();
+      }
+    }
     dim3 grid((a.Lq + 63) / 64, a.B * a.H);
     hipLaunchKernelGGL(fwd_kernel<T>, grid, dim3(256), 128 * RB, s, a);
   } else if (which == 1) {
