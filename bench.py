@@ -81,6 +81,20 @@ def synthetic_batches(args, device, n, seed):
     return out
 
 
+def pmc_traffic(args):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary
+    (profiles/*_pmc_conv1.json, written by tools/pmc_traffic.py for this workload), else None."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_conv1.json")), reverse=True):
+        try:
+            d = json.load(open(path))
+        except Exception:
+            continue
+        if d.get("batch") == args.batch and d.get("traffic_bytes"):
+            return float(d["traffic_bytes"]), os.path.basename(path)
+    return None, None
+
+
 def dominant_flops(args):
     """Algorithmic FLOPs of one launch of the dominant kernel: WavLM conv layer 1 as an implicit GEMM
     (M = B*T1 output frames, N = 512 channels, K = 3 taps * 512), the largest MFMA launch of the step."""
@@ -162,6 +176,7 @@ def main():
         ev = probes["wavlm.conv1"]
         kms = sum(a.elapsed_time(b) for a, b in ev) / max(1, len(ev))
         kflops = dominant_flops(args)
+        traffic, traffic_src = pmc_traffic(args)
         peak = BF16_PEAK_TFLOPS if args.precision == "bf16" else F32_PEAK_TFLOPS
         achieved = kflops / (kms * 1e-3) / 1e12
         step_tflops = value / world * GFLOP_PER_UTT / 1e3
@@ -179,7 +194,8 @@ def main():
                        "parallelism": f"dp{world}"},
             "roofline": {"bound": "mfma", "kernel": "WavLM conv layer 1 implicit GEMM (gemm_big_kernel, GELU)",
                          "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
-                         "frac": round(achieved / peak, 4), "traffic": None, "avg_ms": round(kms, 4),
+                         "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_unit": "B/launch",
+                         "traffic_source": traffic_src, "avg_ms": round(kms, 4),
                          "launches_timed": len(ev), "flops_per_launch": kflops},
             "step_mfma_frac": round(step_tflops / peak, 4),
             "step_tflops": round(step_tflops, 1),

@@ -1,0 +1,64 @@
+"""Micro-benchmark of libfddm_hip attention at the train step's shapes (HIP-event timing, bf16).
+Forward v2 vs v1 (FDDM_ATTN_V1 is read per launch) and the backward pair."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "fddm-asr_amd"))
+import torch  # noqa: E402
+
+from fddm_hip import ops  # noqa: E402
+
+dev = torch.device("cuda:0")
+bf = torch.bfloat16
+
+
+def timeit(fn, iters=20):
+    for _ in range(3):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def main():
+    cases = [("WavLM self S=499 B32 H12 (relbias)", 32, 12, 499, 499, True, 0.0, False),
+             ("decoder self L=256 B32 H8 (kpm, drop .1)", 32, 8, 256, 256, False, 0.1, True),
+             ("decoder self L=256 B32 H8 (no drop)", 32, 8, 256, 256, False, 0.0, True),
+             ("decoder cross 256x499 B32 H8 (drop .1)", 32, 8, 256, 499, False, 0.1, False)]
+    for name, B, H, Lq, Lk, rel, p, kpm in cases:
+        q = torch.randn(B * Lq, H * 64, device=dev, dtype=bf)
+        k = torch.randn(B * Lk, H * 64, device=dev, dtype=bf)
+        v = torch.randn(B * Lk, H * 64, device=dev, dtype=bf)
+        o = torch.empty(B * Lq, H * 64, device=dev, dtype=bf)
+        lse = torch.empty(B * H, Lq, device=dev)
+        gate = torch.rand(B * H, Lq, device=dev) if rel else None
+        table = torch.randn(H, 2 * Lk - 1, device=dev) if rel else None
+        keep = None
+        if kpm:
+            keep = torch.ones(B, Lk, dtype=torch.uint8, device=dev)
+            keep[:, Lk * 3 // 4:] = 0
+        f = lambda: ops.attn_fwd(q, k, v, o, lse, B, H, Lq, Lk, key_keep=keep, gate=gate, table=table,  # noqa
+                                 drop_p=p, seed=1, rng_stream=1)
+        fl = 4.0 * B * H * Lq * Lk * 64
+        t2 = timeit(f)
+        os.environ["FDDM_ATTN_V1"] = "1"
+        t1 = timeit(f)
+        del os.environ["FDDM_ATTN_V1"]
+        print(f"fwd {name:44s} v2 {t2*1e3:8.1f} us {fl/t2/1e9:7.1f} TF/s | v1 {t1*1e3:8.1f} us {fl/t1/1e9:7.1f} TF/s",
+              flush=True)
+        if not rel:
+            do = torch.randn_like(o)
+            dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+            g = lambda: ops.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, B, H, Lq, Lk, key_keep=keep, drop_p=p,  # noqa
+                                     seed=1, rng_stream=1)
+            tb = timeit(g)
+            print(f"bwd {name:44s}    {tb*1e3:8.1f} us {2.5*fl/tb/1e9:7.1f} TF/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,50 @@
+"""HBM traffic per launch of the bench's dominant kernel from two rocprofv3 PMC passes
+(FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950; MI355X_MICROARCH.md 'rocprofv3 PMC slots').
+
+FETCH_SIZE is in KB and, on gfx950, reports half the bytes of wide coalesced streaming reads
+(MI355X_MICROARCH.md § HBM): traffic = 2 * FETCH_SIZE + WRITE_SIZE (KB -> bytes).
+The dominant launch (WavLM conv layer 1) shares its kernel symbol with conv layers 2-6; it is the
+dispatch of that symbol with the largest grid.
+
+  python tools/pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> <kernel substring> <out.json>
+"""
+import csv
+import json
+import sys
+from collections import defaultdict
+
+
+def load(path, counter):
+    rows = defaultdict(dict)
+    for r in csv.DictReader(open(path)):
+        if r.get("Counter_Name") != counter:
+            continue
+        did = r.get("Dispatch_Id") or r.get("Correlation_Id")
+        rows[did]["name"] = r.get("Kernel_Name", "")
+        rows[did]["grid"] = int(float(r.get("Grid_Size", 0) or 0))
+        rows[did][counter] = rows[did].get(counter, 0.0) + float(r["Counter_Value"])
+    return rows
+
+
+def pick(rows, sub, counter):
+    sel = [v for v in rows.values() if sub in v["name"] and counter in v]
+    if not sel:
+        return None, 0, 0
+    gmax = max(v["grid"] for v in sel)
+    vals = [v[counter] for v in sel if v["grid"] == gmax]
+    return sum(vals) / len(vals), len(vals), gmax
+
+
+def main():
+    fpath, wpath, sub, out = sys.argv[1:5]
+    f, nf, g1 = pick(load(fpath, "FETCH_SIZE"), sub, "FETCH_SIZE")
+    w, nw, g2 = pick(load(wpath, "WRITE_SIZE"), sub, "WRITE_SIZE")
+    res = {"kernel_substring": sub, "grid": g1, "launches": [nf, nw], "fetch_size_kb": f, "write_size_kb": w}
+    if f is not None and w is not None:
+        res["traffic_bytes"] = (2.0 * f + w) * 1024.0
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
