@@ -101,18 +101,24 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(LnFwdArgs a) {
   }
   const float var = wave_sum(sq) / (float)d;
   const float rstd = 1.f / sqrtf(var + a.eps);
-  const long b = row / a.rows_per_batch;
+  const long b = a.fsc ? row / a.rows_per_batch : 0;
 #pragma unroll
   for (int i = 0; i < LN_MAXCH; ++i) {
     const long ch = lane + 64L * i;
     if (ch < nch) {
       const long c0 = ch * 8;
       if (a.save_s) st8<float>(a.save_s + row * d + c0, v[i]);
-      float o[8];
+      float o[8], gm[8], bt[8];
+      ld8<float>(a.gamma + c0, gm);
+      ld8<float>(a.beta + c0, bt);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        o[e] = (v[i][e] - mean) * rstd * a.gamma[c0 + e] + a.beta[c0 + e];
-        if (a.fsc) o[e] = o[e] * (1.f + a.fsc[b * d + c0 + e]) + a.fsh[b * d + c0 + e];
+      for (int e = 0; e < 8; ++e) o[e] = (v[i][e] - mean) * rstd * gm[e] + bt[e];
+      if (a.fsc) {
+        float fs[8], fh[8];
+        ld8<float>(a.fsc + b * d + c0, fs);
+        ld8<float>(a.fsh + b * d + c0, fh);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = o[e] * (1.f + fs[e]) + fh[e];
       }
       if (a.out_f32) st8<float>(a.out_f32 + row * d + c0, o);
       if (a.out_t) st8<OT>((OT*)a.out_t + row * d + c0, o);
@@ -227,6 +233,9 @@ FDDM_API int fddm_ln_fwd(int x_dtype, int y_dtype, int out_dtype, const void* x,
                          float eps, float drop_p, unsigned long long seed, unsigned long long stream, void* hs) {
   if (N <= 0) return 0;
   if (d > 64 * 8 * LN_MAXCH || d % 8) return (int)hipErrorInvalidValue;
+  if ((((uintptr_t)gamma | (uintptr_t)beta | (uintptr_t)film_scale | (uintptr_t)film_shift | (uintptr_t)x |
+        (uintptr_t)y) & 15))
+    return (int)hipErrorInvalidValue;  // 16-B vector accesses
   LnFwdArgs a{x, y, gamma, beta, film_scale, film_shift, out_f32, out_t, save_s, mean, rstd, N, d,
               rows_per_batch > 0 ? rows_per_batch : N, eps, seed, stream, 0u, 1.f};
   if (drop_p > 0.f) {

@@ -6,7 +6,7 @@ FETCH_SIZE is in KB and, on gfx950, reports half the bytes of wide coalesced str
 The dominant launch (WavLM conv layer 1) shares its kernel symbol with conv layers 2-6; it is the
 dispatch of that symbol with the largest grid.
 
-  python tools/pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> <kernel substring> <out.json>
+  python tools/pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> <kernel substring> <out.json> <batch>
 """
 import csv
 import json
@@ -39,7 +39,7 @@ def main():
     fpath, wpath, sub, out = sys.argv[1:5]
     f, nf, g1 = pick(load(fpath, "FETCH_SIZE"), sub, "FETCH_SIZE")
     w, nw, g2 = pick(load(wpath, "WRITE_SIZE"), sub, "WRITE_SIZE")
-    res = {"kernel_substring": sub, "grid": g1, "launches": [nf, nw], "fetch_size_kb": f, "write_size_kb": w}
+    res = {"batch": int(sys.argv[5]) if len(sys.argv) > 5 else None, "kernel_substring": sub, "grid": g1, "launches": [nf, nw], "fetch_size_kb": f, "write_size_kb": w}
     if f is not None and w is not None:
         res["traffic_bytes"] = (2.0 * f + w) * 1024.0
     json.dump(res, open(out, "w"), indent=1)
