@@ -53,7 +53,7 @@ __device__ __forceinline__ bool drop_keep(uint64_t seed, uint64_t stream, uint64
 // erff's branchy rational approximations; exact GELU (torch approximate='none') to ~1e-7.
 __device__ __forceinline__ float erf_fast(float x) {
   const float ax = fabsf(x);
-  const float t = __frcp_rn(1.0f + 0.3275911f * ax);
+  const float t = __builtin_amdgcn_rcpf(1.0f + 0.3275911f * ax);  // v_rcp_f32 (1 ulp)
   float p = 1.061405429f;
   p = fmaf(p, t, -1.453152027f);
   p = fmaf(p, t, 1.421413741f);

@@ -99,11 +99,30 @@ __global__ void conv0_gn_affine_kernel(const double* __restrict__ ws, const floa
   scsh[2 * e + 1] = beta[c] - (float)m * sc;
 }
 
-// recompute y, normalise, GELU; thread owns channel pair (2c, 2c+1) -> 4-B stores, 1 KB per wave row
-template <typename OT>
+// recompute y, normalise, GELU; thread owns channel pair (2c, 2c+1) -> 4-B stores, 1 KB per wave row.
+// VALU-bound (10 FMAs + affine + GELU per output): the channel pair is carried as a float2 so the
+// FMAs, the affine and the GELU polynomial issue as packed v_pk_* f32 instructions.
+typedef float f2_t __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f2_t gelu2(f2_t x) {
+  const f2_t z = x * 0.70710678118654752f;
+  const f2_t az = {fabsf(z.x), fabsf(z.y)};
+  const f2_t den = az * 0.3275911f + 1.0f;
+  const f2_t t = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+  f2_t p = t * 1.061405429f - 1.453152027f;
+  p = p * t + 1.421413741f;
+  p = p * t - 0.284496736f;
+  p = p * t + 0.254829592f;
+  const f2_t e = {__expf(-az.x * az.x), __expf(-az.y * az.y)};
+  const f2_t r = 1.0f - p * t * e;
+  const f2_t erfz = {copysignf(r.x, z.x), copysignf(r.y, z.y)};
+  return 0.5f * x * (1.0f + erfz);
+}
+
+template <typename OT, int K>
 __global__ void __launch_bounds__(256) conv0_apply_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                           const float* __restrict__ scsh, OT* __restrict__ out, long nsamp,
-                                                          long T0, int C, int K, int S) {
+                                                          long T0, int C, int S) {
   extern __shared__ float xs[];
   const long b = blockIdx.y;
   const long t0 = (long)blockIdx.x * C0_FRAMES;
@@ -112,30 +131,22 @@ __global__ void __launch_bounds__(256) conv0_apply_kernel(const float* __restric
   for (int i = threadIdx.x; i < span; i += 256) xs[i] = x[b * nsamp + t0 * S + i];
   __syncthreads();
   for (int c = 2 * threadIdx.x; c < C; c += 512) {
-    float wk[2][C0_MAXK], sc[2], sh[2];
+    f2_t wk[K];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-#pragma unroll
-      for (int k = 0; k < C0_MAXK; ++k) wk[j][k] = k < K ? w[(c + j) * K + k] : 0.f;
-      sc[j] = scsh[2 * (b * C + c + j)];
-      sh[j] = scsh[2 * (b * C + c + j) + 1];
-    }
+    for (int k = 0; k < K; ++k) wk[k] = f2_t{w[c * K + k], w[(c + 1) * K + k]};
+    const f2_t sc = {scsh[2 * (b * C + c)], scsh[2 * (b * C + c + 1)]};
+    const f2_t sh = {scsh[2 * (b * C + c) + 1], scsh[2 * (b * C + c + 1) + 1]};
+    OT* o = out + (b * T0 + t0) * C + c;
     for (int f = 0; f < nf; ++f) {
-      float y0 = 0.f, y1 = 0.f;
+      f2_t y = {0.f, 0.f};
 #pragma unroll
-      for (int k = 0; k < C0_MAXK; ++k)
-        if (k < K) {
-          const float xv = xs[f * S + k];
-          y0 += wk[0][k] * xv;
-          y1 += wk[1][k] * xv;
-        }
-      OT* o = out + (b * T0 + t0 + f) * C + c;
-      const float g0 = gelu_f(y0 * sc[0] + sh[0]), g1 = gelu_f(y1 * sc[1] + sh[1]);
+      for (int k = 0; k < K; ++k) y += wk[k] * xs[f * S + k];
+      const f2_t gv = gelu2(y * sc + sh);
       if constexpr (sizeof(OT) == 2) {
-        *(unsigned*)o = (unsigned)f2bf(g0) | ((unsigned)f2bf(g1) << 16);
+        *(unsigned*)(o + (long)f * C) = (unsigned)f2bf(gv.x) | ((unsigned)f2bf(gv.y) << 16);
       } else {
-        o[0] = g0;
-        o[1] = g1;
+        o[(long)f * C] = gv.x;
+        o[(long)f * C + 1] = gv.y;
       }
     }
   }
@@ -195,10 +206,10 @@ FDDM_API int fddm_conv0_gn_gelu(int out_dtype, const float* x, const float* w, c
   dim3 grid((unsigned)((T0 + C0_FRAMES - 1) / C0_FRAMES), (unsigned)B);
   const size_t lds = ((C0_FRAMES - 1) * S + K) * sizeof(float);
   if (out_dtype == FDDM_BF16)
-    hipLaunchKernelGGL((conv0_apply_kernel<bf16_t>), grid, dim3(256), lds, s, x, w, scsh, (bf16_t*)out, nsamp, T0, C,
-                       K, S);
+    hipLaunchKernelGGL((conv0_apply_kernel<bf16_t, 10>), grid, dim3(256), lds, s, x, w, scsh, (bf16_t*)out, nsamp, T0,
+                       C, S);
   else
-    hipLaunchKernelGGL((conv0_apply_kernel<float>), grid, dim3(256), lds, s, x, w, scsh, (float*)out, nsamp, T0, C, K,
+    hipLaunchKernelGGL((conv0_apply_kernel<float, 10>), grid, dim3(256), lds, s, x, w, scsh, (float*)out, nsamp, T0, C,
                        S);
   return (int)hipGetLastError();
 }
