@@ -135,7 +135,7 @@ _tables: dict = {}
 def rope_tables(L: int, inv_freq: torch.Tensor, device):
     """cos/sin [L, d] exactly as RoPEEmbedding.forward (models/denoise_decoder.py:35-40), computed on
     the host once per (L, d) and kept resident."""
-    k = ("rope", L, inv_freq.numel(), float(inv_freq[-1]) if inv_freq.numel() else 0.0, str(device))
+    k = ("rope", L, id(inv_freq), inv_freq._version, inv_freq.numel(), str(device))  # no device read (graph capture)
     t = _tables.get(k)
     if t is None:
         f = inv_freq.detach().float().cpu()
