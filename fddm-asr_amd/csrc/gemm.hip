@@ -553,6 +553,19 @@ static bool big_enabled() {
   static const bool on = getenv("FDDM_NO_BIG_GEMM") == nullptr;
   return on;
 }
+static long env_long(const char* name, long dflt) {
+  const char* v = getenv(name);
+  return v ? atol(v) : dflt;
+}
+// split-K tuning (FDDM_SPLITK_TARGET workgroups, FDDM_SPLITK_MINK minimum K per split; read once)
+static long splitk_target() {
+  static const long v = env_long("FDDM_SPLITK_TARGET", 512);
+  return v;
+}
+static long splitk_mink() {
+  static const long v = env_long("FDDM_SPLITK_MINK", 1024);
+  return v;
+}
 
 FDDM_API int fddm_gemm(int dtype, int a_dtype, int a_kc, int b_kc, int epi, int out_dtype, const void* A, long lda,
                        long Mi, long sAb, const void* B, long ldb, void* C, long ldc, void* C2, const float* bias,
@@ -586,8 +599,10 @@ FDDM_API int fddm_gemm(int dtype, int a_dtype, int a_kc, int b_kc, int epi, int 
   const long tiles = ((M + GBM - 1) / GBM) * ((N + GBN - 1) / GBN);
   const int kstep = dtype == FDDM_BF16 ? 64 : 32;
   if (out_dtype == FDDM_F32 && (epi == EPI_STORE || epi == EPI_ACC_F32) && tiles < 512 && K >= 8 * kstep && Mi >= M) {
-    long want = (1024 + tiles - 1) / tiles;
-    long maxs = K / (4 * kstep);
+    // Split count: enough workgroups to cover the chip (splitk_target), but every split keeps at least
+    // splitk_mink of K — each extra split costs M*N*4 B of float atomics (~1.3 TB/s chip-wide).
+    long want = (splitk_target() + tiles - 1) / tiles;
+    long maxs = K / std::max((long)kstep, splitk_mink());
     nz = (int)std::max(1L, std::min(want, std::min(maxs, 64L)));
     if (nz > 1) {
       long ks = (K + nz - 1) / nz;
