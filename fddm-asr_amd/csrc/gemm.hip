@@ -202,6 +202,33 @@ struct GemmArgs {
   float* colsum;               // optional: colsum[m] += sum_k A(m,k) (MC A operand) — fused bias gradient
 };
 
+// 8 consecutive outputs as one 16-B (bf16) or two 16-B (f32) accesses
+__device__ __forceinline__ void st_vec8(bf16_t* p, const float (&v)[8]) {
+  uint4 u;
+  u.x = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
+  u.y = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
+  u.z = (unsigned)f2bf(v[4]) | ((unsigned)f2bf(v[5]) << 16);
+  u.w = (unsigned)f2bf(v[6]) | ((unsigned)f2bf(v[7]) << 16);
+  *(uint4*)p = u;
+}
+__device__ __forceinline__ void st_vec8(float* p, const float (&v)[8]) {
+  *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
+  *(float4*)(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+__device__ __forceinline__ void ld_vec8(const bf16_t* p, float (&v)[8]) {
+  const uint4 u = *(const uint4*)p;
+  const unsigned w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(w[i] << 16);
+    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ void ld_vec8(const float* p, float (&v)[8]) {
+  const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
 template <typename T, typename TA, bool AKC, bool BKC, int EPI, typename OT, bool CONV>
 __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -292,38 +319,99 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g) {
     }
   }
 
-  // epilogue: acc[i][j][e] -> row m0 + wr*64 + i*16 + 4*fg + e, col n0 + wc*64 + j*16 + fr
-  const int fr = lane & 15, fg = lane >> 4;
+  // epilogue, staged through LDS so that global accesses run along rows: each wave parks its 64x64 f32
+  // sub-tile (16 KB; column chunks XOR-swizzled by row group against bank conflicts), then
+  //  * f32 accumulate (split-K atomics / +=): lane = column, one 256-B contiguous row per instruction;
+  //  * other epilogues: 8 consecutive columns per lane (16-B bf16 / 2x16-B f32 accesses).
+  __syncthreads();  // K loop / colsum reduction have retired every LDS read
+  float* tile = (float*)smem + wid * 4096;
+  {
+    const int fr = lane & 15, fg = lane >> 4;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const long n = n0 + wc * 64 + j * 16 + fr;
-    if (n >= g.N) continue;
-    const float bv = biasz ? biasz[n] : 0.f;
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+      for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const long m = m0 + wr * 64 + i * 16 + 4 * fg + e;
-        if (m >= g.M) continue;
-        const float v = acc[i][j][e] * g.alpha + bv;
-        if constexpr (EPI == EPI_STORE) {
-          st<OT>(Cz + m * g.ldc + n, v);
-        } else if constexpr (EPI == EPI_GELU) {
-          st<OT>(Cz + m * g.ldc + n, v);  // pre-activation, saved for backward
-          float a = gelu_f(v);
-          if (g.thr16) a = drop_keep(g.seed, g.stream, (uint64_t)(m * g.N + n), g.thr16) ? a * g.drop_scale : 0.f;
-          st<OT>((OT*)g.C2 + m * g.ldc + n, a);
-        } else if constexpr (EPI == EPI_GELU_ONLY) {
-          st<OT>(Cz + m * g.ldc + n, gelu_f(v));
-        } else if constexpr (EPI == EPI_DGELU) {
-          float dv = v * gelu_grad(ld<OT>((const OT*)g.C2 + m * g.ldc + n));
-          if (g.thr16) dv = drop_keep(g.seed, g.stream, (uint64_t)(m * g.N + n), g.thr16) ? dv * g.drop_scale : 0.f;
-          st<OT>(Cz + m * g.ldc + n, dv);
-        } else {
-          float* c = (float*)Cz + m * g.ldc + n;
-          if (atomic_out) atomicAdd(c, v);
-          else *c += v;
+        for (int e = 0; e < 4; ++e) {
+          const int r = i * 16 + 4 * fg + e, c = j * 16 + fr;
+          tile[r * 64 + (c ^ (((r >> 2) & 3) << 4))] = acc[i][j][e];
         }
+  }
+  __syncthreads();
+  const long mw = m0 + wr * 64, nw = n0 + wc * 64;
+  if constexpr (EPI == EPI_ACC_F32) {
+    const long n = nw + lane;
+    const bool nok = n < g.N;
+    const float bv = (biasz && nok) ? biasz[n] : 0.f;
+    for (int r = 0; r < 64; ++r) {
+      const long m = mw + r;
+      if (m >= g.M) break;
+      const float v = tile[r * 64 + (lane ^ (((r >> 2) & 3) << 4))] * g.alpha + bv;
+      if (nok) {
+        float* c = (float*)Cz + m * g.ldc + n;
+        if (atomic_out) atomicAdd(c, v);
+        else *c += v;
+      }
+    }
+  } else {
+    const int cq = lane & 7, rq = lane >> 3;  // 8 columns per lane, 8 rows per pass
+    const long n = nw + cq * 8;
+    const bool vec = ((g.N & 7) == 0) && ((g.ldc & 7) == 0) && ((((uintptr_t)Cz) | ((uintptr_t)g.C2)) & 15) == 0;
+    float bv[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) bv[t] = (biasz && n + t < g.N) ? biasz[n + t] : 0.f;
+    for (int r0 = 0; r0 < 64; r0 += 8) {
+      const int r = r0 + rq;
+      const long m = mw + r;
+      if (m >= g.M || n >= g.N) continue;
+      const int sw = ((r >> 2) & 3) << 4;
+      const float4 lo = *(const float4*)(tile + r * 64 + ((cq * 8) ^ sw));
+      const float4 hi = *(const float4*)(tile + r * 64 + ((cq * 8 + 4) ^ sw));
+      float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+#pragma unroll
+      for (int t = 0; t < 8; ++t) v[t] = v[t] * g.alpha + bv[t];
+      OT* crow = Cz + m * g.ldc + n;
+      if constexpr (EPI == EPI_GELU) {
+        float a[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          a[t] = gelu_f(v[t]);
+          if (g.thr16)
+            a[t] = drop_keep(g.seed, g.stream, (uint64_t)(m * g.N + n + t), g.thr16) ? a[t] * g.drop_scale : 0.f;
+        }
+        OT* c2 = (OT*)g.C2 + m * g.ldc + n;
+        if (vec) {
+          st_vec8(crow, v);   // pre-activation, saved for backward
+          st_vec8(c2, a);
+        } else {
+          for (int t = 0; t < 8 && n + t < g.N; ++t) {
+            st<OT>(crow + t, v[t]);
+            st<OT>(c2 + t, a[t]);
+          }
+        }
+      } else if constexpr (EPI == EPI_DGELU) {
+        const OT* pre = (const OT*)g.C2 + m * g.ldc + n;
+        float pv[8];
+        if (vec) {
+          ld_vec8(pre, pv);
+        } else {
+          for (int t = 0; t < 8; ++t) pv[t] = (n + t < g.N) ? ld<OT>(pre + t) : 0.f;
+        }
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          v[t] *= gelu_grad(pv[t]);
+          if (g.thr16)
+            v[t] = drop_keep(g.seed, g.stream, (uint64_t)(m * g.N + n + t), g.thr16) ? v[t] * g.drop_scale : 0.f;
+        }
+        if (vec) st_vec8(crow, v);
+        else for (int t = 0; t < 8 && n + t < g.N; ++t) st<OT>(crow + t, v[t]);
+      } else {
+        if constexpr (EPI == EPI_GELU_ONLY) {
+#pragma unroll
+          for (int t = 0; t < 8; ++t) v[t] = gelu_f(v[t]);
+        }
+        if (vec) st_vec8(crow, v);
+        else for (int t = 0; t < 8 && n + t < g.N; ++t) st<OT>(crow + t, v[t]);
       }
     }
   }
@@ -563,7 +651,7 @@ static long splitk_target() {
   return v;
 }
 static long splitk_mink() {
-  static const long v = env_long("FDDM_SPLITK_MINK", 1024);
+  static const long v = env_long("FDDM_SPLITK_MINK", 512);
   return v;
 }
 
