@@ -85,7 +85,7 @@ __device__ __forceinline__ void rows_times_frag(f32x4_t (&acc)[4], const unsigne
   }
 }
 
-__device__ __forceinline__ unsigned pk(float a, float b) { return (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16); }
+__device__ __forceinline__ unsigned pk(float a, float b) { return pk_bf16(a, b); }
 
 // out[db] += sum_rows  A(MC image transposed: [col d][row]) x B(lane-owned values v[kb][j] at row kb*16+4g+j)
 template <typename T>
@@ -242,18 +242,22 @@ __global__ void __launch_bounds__(256) fwd_kernel(AttnArgs a) {
 // global loads are issued before this tile's MFMAs and written after them (one barrier per tile).
 // The WavLM bias slice for the tile (191 table entries: key - q spans [k0-q0-127, k0+63-q0]) is staged
 // with the tile instead of gathered from global memory per score.
+// Template flags: DROP (dropout on P), MASK (key-padding mask and/or a ragged last tile: a 0/-inf bias row
+// per tile in LDS), REL (WavLM gated relative-position bias).
+template <bool DROP, bool MASK, bool REL>
 __global__ void __launch_bounds__(256) fwd2_kernel(AttnArgs a) {
   constexpr int RB = 128;
   __shared__ __attribute__((aligned(16))) unsigned char kbuf[2][64 * RB];
   __shared__ __attribute__((aligned(16))) unsigned char vbuf[2][64 * RB];
   __shared__ float tbuf[2][192];
+  __shared__ __attribute__((aligned(16))) float mbuf[2][64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, i = lane & 15;
   const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
   const int qbase = blockIdx.x * 128;
   const bf16_t* Qb = (const bf16_t*)a.Q + (long)b * a.Lq * a.sq + h * DH;
   const bf16_t* Kb = (const bf16_t*)a.K + (long)b * a.Lk * a.sk + h * DH;
   const bf16_t* Vb = (const bf16_t*)a.V + (long)b * a.Lk * a.sv + h * DH;
-  const float* tabh = a.table ? a.table + (long)h * (2 * a.Lk - 1) : nullptr;
+  const float* tabh = REL ? a.table + (long)h * (2 * a.Lk - 1) : nullptr;
   int q[2];
   bool qv[2];
   uint4 qf[2][2];
@@ -267,7 +271,7 @@ __global__ void __launch_bounds__(256) fwd2_kernel(AttnArgs a) {
   }
   // tile loader: 512 16-B chunks of K and of V per tile, 2 each per thread
   uint4 kr[2], vr[2];
-  float tv = 0.f;
+  float tv = 0.f, mv = 0.f;
   auto load = [&](int k0) {
     const int nv = min(64, a.Lk - k0);
 #pragma unroll
@@ -279,9 +283,13 @@ __global__ void __launch_bounds__(256) fwd2_kernel(AttnArgs a) {
         vr[u] = *(const uint4*)(Vb + (long)(k0 + r) * a.sv + c * 8);
       }
     }
-    if (tabh && tid < 191) {
+    if (REL && tid < 191) {
       const long ti = (long)k0 - qbase - 127 + (a.Lk - 1) + tid;
       tv = (ti >= 0 && ti < 2L * a.Lk - 1) ? tabh[ti] : 0.f;
+    }
+    if (MASK && tid >= 192) {
+      const int key = k0 + tid - 192;
+      mv = key_ok(a, b, key) ? 0.f : -INFINITY;
     }
   };
   auto store = [&](int buf) {
@@ -291,9 +299,11 @@ __global__ void __launch_bounds__(256) fwd2_kernel(AttnArgs a) {
       *(uint4*)(kbuf[buf] + kc_off(RB, r, c)) = kr[u];
       *(uint4*)(vbuf[buf] + r * 128 + (((2 * c) ^ hatt(r)) << 3)) = vr[u];
     }
-    if (tabh && tid < 191) tbuf[buf][tid] = tv;
+    if (REL && tid < 191) tbuf[buf][tid] = tv;
+    if (MASK && tid >= 192) mbuf[buf][tid - 192] = mv;
   };
 
+  const float sl2 = a.scale * 1.4426950408889634f;  // running max m is kept in log2 units
   float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
   f32x4_t o[2][4];
 #pragma unroll
@@ -321,39 +331,63 @@ __global__ void __launch_bounds__(256) fwd2_kernel(AttnArgs a) {
         mma<bf16_t>(s[1][kb], af, qf[1][sub]);
       }
     }
+    // softmax in the exp2 domain: x = s*scale*log2e (+ gate*bias*log2e) (+ 0/-inf mask row)
+    float mrow[4][4];
+    if constexpr (MASK) {
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        const float4 mv4 = *(const float4*)(&mbuf[cur][kb * 16 + 4 * g]);
+        mrow[kb][0] = mv4.x; mrow[kb][1] = mv4.y; mrow[kb][2] = mv4.z; mrow[kb][3] = mv4.w;
+      }
+    }
     float p[2][4][4];
 #pragma unroll
     for (int gq = 0; gq < 2; ++gq) {
       float tmax = -INFINITY;
+      const float gl = gate[gq] * 1.4426950408889634f;
+      const int toff = 127 - (q[gq] - qbase);
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int kl = kb * 16 + 4 * g + j, key = k0 + kl;
-          float x = s[gq][kb][j] * a.scale;
-          if (tabh) x += gate[gq] * tbuf[cur][kl - (q[gq] - qbase) + 127];
-          if (!key_ok(a, b, key)) x = -INFINITY;
+          const int kl = kb * 16 + 4 * g + j;
+          float x = s[gq][kb][j] * sl2;
+          if constexpr (REL) x = fmaf(gl, tbuf[cur][kl + toff], x);
+          if constexpr (MASK) x += mrow[kb][j];
           p[gq][kb][j] = x;
           tmax = fmaxf(tmax, x);
         }
       tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
       const float mn = fmaxf(m[gq], tmax);
-      const float alpha = (mn == -INFINITY) ? 1.f : __expf(m[gq] - mn);
+      const float mref = (mn == -INFINITY) ? 0.f : mn;  // all-masked so far: exp2(-inf - 0) = 0
+      const float alpha = __builtin_amdgcn_exp2f(m[gq] - mref);
       float ls = 0.f;
 #pragma unroll
-      for (int kb = 0; kb < 4; ++kb)
+      for (int kb = 0; kb < 4; ++kb) {
+        unsigned keep = 0xF;
+        if constexpr (DROP) {
+          // elements e0..e0+3 (consecutive keys) span at most two 64-bit hash words
+          const uint64_t e0 = ((uint64_t)bh * a.Lq + q[gq]) * a.Lk + (k0 + kb * 16 + 4 * g);
+          const uint64_t h0 = mix64(a.seed, a.stream, e0 >> 2);
+          const uint64_t h1 = ((e0 & 3) == 0) ? h0 : mix64(a.seed, a.stream, (e0 >> 2) + 1);
+          keep = 0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const unsigned sl = (unsigned)((e0 & 3) + j);
+            const uint64_t hw = sl < 4 ? h0 : h1;
+            const unsigned u = (unsigned)(hw >> (16u * (sl & 3u))) & 0xFFFFu;
+            keep |= (u >= a.thr16 ? 1u : 0u) << j;
+          }
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          float e = (mn == -INFINITY) ? 0.f : __expf(p[gq][kb][j] - mn);
+          float e = __builtin_amdgcn_exp2f(p[gq][kb][j] - mref);
           ls += e;
-          if (a.thr16) {
-            const int key = k0 + kb * 16 + 4 * g + j;
-            const uint64_t idx = ((uint64_t)bh * a.Lq + q[gq]) * a.Lk + key;
-            e = drop_keep(a.seed, a.stream, idx, a.thr16) ? e * a.drop_scale : 0.f;
-          }
+          if constexpr (DROP) e = ((keep >> j) & 1u) ? e * a.drop_scale : 0.f;
           p[gq][kb][j] = e;
         }
+      }
       l[gq] = l[gq] * alpha + ls;
       m[gq] = mn;
 #pragma unroll
@@ -409,7 +443,7 @@ __global__ void __launch_bounds__(256) fwd2_kernel(AttnArgs a) {
       u2.y = pk(o[gq][d][2] * inv, o[gq][d][3] * inv);
       *(uint2*)(Ob + d * 16 + 4 * g) = u2;
     }
-    if (a.lse && g == 0) a.lse[(long)bh * a.Lq + q[gq]] = (lt > 0.f) ? m[gq] + __logf(lt) : NAN;
+    if (a.lse && g == 0) a.lse[(long)bh * a.Lq + q[gq]] = (lt > 0.f) ? (m[gq] + __log2f(lt)) * 0.69314718055994531f : NAN;
   }
 }
 
@@ -575,7 +609,17 @@ static int run(int which, AttnArgs& a, hipStream_t s) {
     if constexpr (sizeof(T) == 2) {
       if (!getenv("FDDM_ATTN_V1")) {
         dim3 grid((a.Lq + 127) / 128, a.B * a.H);
-        hipLaunchKernelGGL(fwd2_kernel, grid, dim3(256), 0, s, a);
+        const bool drop = a.thr16 != 0, mask = a.key_keep != nullptr || (a.Lk % 64) != 0;
+        const bool rel = a.table != nullptr && a.gate != nullptr;
+#define FWD2(D, M, R) hipLaunchKernelGGL((fwd2_kernel<D, M, R>), grid, dim3(256), 0, s, a)
+        if (rel) {
+          if (drop) { if (mask) FWD2(true, true, true); else FWD2(true, false, true); }
+          else { if (mask) FWD2(false, true, true); else FWD2(false, false, true); }
+        } else {
+          if (drop) { if (mask) FWD2(true, true, false); else FWD2(true, false, false); }
+          else { if (mask) FWD2(false, true, false); else FWD2(false, false, false); }
+        }
+#undef FWD2
         return (int)hipGetLastError();
       }
     }

@@ -57,7 +57,7 @@ template <> struct Mma<float> {
   }
 };
 
-__device__ __forceinline__ unsigned pack_bf2(float a, float b) { return (unsigned)f2bf(a) | ((unsigned)f2bf(b) << 16); }
+__device__ __forceinline__ unsigned pack_bf2(float a, float b) { return pk_bf16(a, b); }
 
 // load one 16-B chunk of compute type T (ECH elements) from storage type TS
 template <typename T, typename TS>
@@ -205,10 +205,10 @@ struct GemmArgs {
 // 8 consecutive outputs as one 16-B (bf16) or two 16-B (f32) accesses
 __device__ __forceinline__ void st_vec8(bf16_t* p, const float (&v)[8]) {
   uint4 u;
-  u.x = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
-  u.y = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
-  u.z = (unsigned)f2bf(v[4]) | ((unsigned)f2bf(v[5]) << 16);
-  u.w = (unsigned)f2bf(v[6]) | ((unsigned)f2bf(v[7]) << 16);
+  u.x = pk_bf16(v[0], v[1]);
+  u.y = pk_bf16(v[2], v[3]);
+  u.z = pk_bf16(v[4], v[5]);
+  u.w = pk_bf16(v[6], v[7]);
   *(uint4*)p = u;
 }
 __device__ __forceinline__ void st_vec8(float* p, const float (&v)[8]) {

@@ -42,10 +42,10 @@ template <typename T>
 __device__ __forceinline__ void st8(T* p, const float (&v)[8]) {
   if constexpr (sizeof(T) == 2) {
     uint4 u;
-    u.x = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
-    u.y = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
-    u.z = (unsigned)f2bf(v[4]) | ((unsigned)f2bf(v[5]) << 16);
-    u.w = (unsigned)f2bf(v[6]) | ((unsigned)f2bf(v[7]) << 16);
+    u.x = pk_bf16(v[0], v[1]);
+    u.y = pk_bf16(v[2], v[3]);
+    u.z = pk_bf16(v[4], v[5]);
+    u.w = pk_bf16(v[6], v[7]);
     *(uint4*)p = u;
   } else {
     *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);

@@ -143,7 +143,7 @@ __global__ void __launch_bounds__(256) conv0_apply_kernel(const float* __restric
       for (int k = 0; k < K; ++k) y += wk[k] * xs[f * S + k];
       const f2_t gv = gelu2(y * sc + sh);
       if constexpr (sizeof(OT) == 2) {
-        *(unsigned*)(o + (long)f * C) = (unsigned)f2bf(gv.x) | ((unsigned)f2bf(gv.y) << 16);
+        *(unsigned*)(o + (long)f * C) = pk_bf16(gv.x, gv.y);
       } else {
         o[(long)f * C] = gv.x;
         o[(long)f * C + 1] = gv.y;
