@@ -602,6 +602,328 @@ __global__ void __launch_bounds__(256) dkv_kernel(AttnArgs a) {
     }
 }
 
+// ------------------------------------------------------------------------------- bwd (bf16, v2)
+// Shared pieces of the 2-group backward kernels: out[gq][db] += A^T(MC image [k][d]) x v[gq] with one tr-read
+// A fragment feeding both groups.
+__device__ __forceinline__ void trans_times_vals2(f32x4_t (&out)[2][4], const unsigned char* img,
+                                                  const float (&v)[2][4][4], int lane) {
+  const int g = lane >> 4, i = lane & 15, qq = i >> 2, pp = i & 3;
+  typedef __attribute__((address_space(3))) s16x4_t* lp;
+#pragma unroll
+  for (int ss = 0; ss < 2; ++ss) {
+    uint4 bq[2];
+#pragma unroll
+    for (int gq = 0; gq < 2; ++gq) {
+      bq[gq].x = pk(v[gq][2 * ss][0], v[gq][2 * ss][1]);
+      bq[gq].y = pk(v[gq][2 * ss][2], v[gq][2 * ss][3]);
+      bq[gq].z = pk(v[gq][2 * ss + 1][0], v[gq][2 * ss + 1][1]);
+      bq[gq].w = pk(v[gq][2 * ss + 1][2], v[gq][2 * ss + 1][3]);
+    }
+    const int k1 = 32 * ss + 4 * g + qq, k2 = k1 + 16;
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      const int u = db * 4 + pp;
+      const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(img + k1 * 128 + ((u ^ hatt(k1)) << 3)));
+      const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(img + k2 * 128 + ((u ^ hatt(k2)) << 3)));
+      uint4 af;
+      af.x = (unsigned)(unsigned short)lo[0] | ((unsigned)(unsigned short)lo[1] << 16);
+      af.y = (unsigned)(unsigned short)lo[2] | ((unsigned)(unsigned short)lo[3] << 16);
+      af.z = (unsigned)(unsigned short)hi[0] | ((unsigned)(unsigned short)hi[1] << 16);
+      af.w = (unsigned)(unsigned short)hi[2] | ((unsigned)(unsigned short)hi[3] << 16);
+      mma<bf16_t>(out[0][db], af, bq[0]);
+      mma<bf16_t>(out[1][db], af, bq[1]);
+    }
+  }
+}
+
+// keep bits of 4 consecutive dropout elements e0..e0+3 (at most two hash words)
+__device__ __forceinline__ unsigned keep4(const AttnArgs& a, uint64_t e0) {
+  const uint64_t h0 = mix64(a.seed, a.stream, e0 >> 2);
+  const uint64_t h1 = ((e0 & 3) == 0) ? h0 : mix64(a.seed, a.stream, (e0 >> 2) + 1);
+  unsigned keep = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const unsigned sl = (unsigned)((e0 & 3) + j);
+    const uint64_t hw = sl < 4 ? h0 : h1;
+    keep |= (((unsigned)(hw >> (16u * (sl & 3u))) & 0xFFFFu) >= a.thr16 ? 1u : 0u) << j;
+  }
+  return keep;
+}
+
+// dQ, query-owned: 128 queries per workgroup (two 16-query groups per wave), K/V tiles double-buffered.
+// S^T = K Q^T and dP^T = V dO^T share the LDS row reads across both groups; dS = P (dP' - delta);
+// dQ^T += K^T dS^T from the K MC image. Writes delta = rowsum(dO*O) for the dK/dV kernel.
+template <bool DROP, bool MASK>
+__global__ void __launch_bounds__(256) dq2_kernel(AttnArgs a) {
+  constexpr int RB = 128;
+  __shared__ __attribute__((aligned(16))) unsigned char kc[2][64 * RB];
+  __shared__ __attribute__((aligned(16))) unsigned char kt[2][64 * RB];
+  __shared__ __attribute__((aligned(16))) unsigned char vc[2][64 * RB];
+  __shared__ __attribute__((aligned(16))) float mbuf[2][64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, i = lane & 15;
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int qbase = blockIdx.x * 128;
+  const bf16_t* Qb = (const bf16_t*)a.Q + (long)b * a.Lq * a.sq + h * DH;
+  const bf16_t* Ob = (const bf16_t*)a.O + (long)b * a.Lq * a.so + h * DH;
+  const bf16_t* dOb = (const bf16_t*)a.dO + (long)b * a.Lq * a.sdo + h * DH;
+  const bf16_t* Kb = (const bf16_t*)a.K + (long)b * a.Lk * a.sk + h * DH;
+  const bf16_t* Vb = (const bf16_t*)a.V + (long)b * a.Lk * a.sv + h * DH;
+  const float sl2 = a.scale * 1.4426950408889634f;
+  int q[2];
+  bool qv[2];
+  uint4 qf[2][2], dof[2][2];
+  float delta[2], lse2[2];
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq) {
+    q[gq] = qbase + w * 32 + gq * 16 + i;
+    qv[gq] = q[gq] < a.Lq;
+    const int qq = qv[gq] ? q[gq] : 0;
+    row_frags<bf16_t>(qf[gq], Qb, a.sq, qq, qv[gq], lane);
+    row_frags<bf16_t>(dof[gq], dOb, a.sdo, qq, qv[gq], lane);
+    uint4 of[2];
+    row_frags<bf16_t>(of, Ob, a.so, qq, qv[gq], lane);
+    float dl = 0.f;
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb) {
+      const bf16_t* x = (const bf16_t*)&dof[gq][sb];
+      const bf16_t* y = (const bf16_t*)&of[sb];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dl += bf2f(x[e]) * bf2f(y[e]);
+    }
+    dl += __shfl_xor(dl, 16, 64);
+    dl += __shfl_xor(dl, 32, 64);
+    delta[gq] = dl;
+    if (qv[gq] && g == 0) a.delta[(long)bh * a.Lq + q[gq]] = dl;
+    lse2[gq] = qv[gq] ? a.lse[(long)bh * a.Lq + q[gq]] * 1.4426950408889634f : 0.f;
+  }
+  uint4 kr[2], vr[2];
+  float mv = 1.f;
+  auto load = [&](int k0) {
+    const int nv = min(64, a.Lk - k0);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int idx = tid + 256 * u, r = idx >> 3, c = idx & 7;
+      kr[u] = vr[u] = make_uint4(0, 0, 0, 0);
+      if (r < nv) {
+        kr[u] = *(const uint4*)(Kb + (long)(k0 + r) * a.sk + c * 8);
+        vr[u] = *(const uint4*)(Vb + (long)(k0 + r) * a.sv + c * 8);
+      }
+    }
+    if (MASK && tid >= 192) mv = key_ok(a, b, k0 + tid - 192) ? 1.f : 0.f;
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int idx = tid + 256 * u, r = idx >> 3, c = idx & 7;
+      *(uint4*)(kc[buf] + kc_off(RB, r, c)) = kr[u];
+      *(uint4*)(kt[buf] + r * 128 + (((2 * c) ^ hatt(r)) << 3)) = kr[u];
+      *(uint4*)(vc[buf] + kc_off(RB, r, c)) = vr[u];
+    }
+    if (MASK && tid >= 192) mbuf[buf][tid - 192] = mv;
+  };
+  f32x4_t dq[2][4];
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq)
+#pragma unroll
+    for (int d = 0; d < 4; ++d) dq[gq][d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  load(0);
+  store(0);
+  __syncthreads();
+  const int ntiles = (a.Lk + 63) / 64;
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1, k0 = t * 64;
+    if (t + 1 < ntiles) load(k0 + 64);
+    f32x4_t s[2][4], dp[2][4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      s[0][kb] = s[1][kb] = dp[0][kb] = dp[1][kb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub) {
+        const uint4 ak = *(const uint4*)(kc[cur] + kc_off(RB, kb * 16 + i, sub * 4 + g));
+        const uint4 av = *(const uint4*)(vc[cur] + kc_off(RB, kb * 16 + i, sub * 4 + g));
+        mma<bf16_t>(s[0][kb], ak, qf[0][sub]);
+        mma<bf16_t>(s[1][kb], ak, qf[1][sub]);
+        mma<bf16_t>(dp[0][kb], av, dof[0][sub]);
+        mma<bf16_t>(dp[1][kb], av, dof[1][sub]);
+      }
+    }
+    float mrow[4][4];
+    if constexpr (MASK) {
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        const float4 m4 = *(const float4*)(&mbuf[cur][kb * 16 + 4 * g]);
+        mrow[kb][0] = m4.x; mrow[kb][1] = m4.y; mrow[kb][2] = m4.z; mrow[kb][3] = m4.w;
+      }
+    }
+    float ds[2][4][4];
+#pragma unroll
+    for (int gq = 0; gq < 2; ++gq)
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        unsigned keep = 0xF;
+        if constexpr (DROP) keep = keep4(a, ((uint64_t)bh * a.Lq + q[gq]) * a.Lk + (k0 + kb * 16 + 4 * g));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float pr = __builtin_amdgcn_exp2f(s[gq][kb][j] * sl2 - lse2[gq]);
+          if constexpr (MASK) pr = mrow[kb][j] != 0.f ? pr : 0.f;
+          float dpv = dp[gq][kb][j];
+          if constexpr (DROP) dpv = ((keep >> j) & 1u) ? dpv * a.drop_scale : 0.f;
+          ds[gq][kb][j] = pr * (dpv - delta[gq]);
+        }
+      }
+    trans_times_vals2(dq, kt[cur], ds, lane);
+    if (t + 1 < ntiles) {
+      store(cur ^ 1);
+      __syncthreads();
+    }
+  }
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq) {
+    if (!qv[gq]) continue;
+    bf16_t* dQb = (bf16_t*)a.dQ + ((long)b * a.Lq + q[gq]) * a.sdq + h * DH;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      uint2 u2;
+      u2.x = pk(dq[gq][d][0] * a.scale, dq[gq][d][1] * a.scale);
+      u2.y = pk(dq[gq][d][2] * a.scale, dq[gq][d][3] * a.scale);
+      *(uint2*)(dQb + d * 16 + 4 * g) = u2;
+    }
+  }
+}
+
+// dK, dV, key-owned: 128 keys per workgroup (two 16-key groups per wave), Q/dO tiles double-buffered
+// (row images for S, dP and transposed images for dV^T += dO^T P', dK^T += Q^T dS).
+template <bool DROP>
+__global__ void __launch_bounds__(256) dkv2_kernel(AttnArgs a) {
+  constexpr int RB = 128;
+  __shared__ __attribute__((aligned(16))) unsigned char qc[2][64 * RB];
+  __shared__ __attribute__((aligned(16))) unsigned char qt[2][64 * RB];
+  __shared__ __attribute__((aligned(16))) unsigned char oc[2][64 * RB];
+  __shared__ __attribute__((aligned(16))) unsigned char ot[2][64 * RB];
+  __shared__ float lse_s[2][64], del_s[2][64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, i = lane & 15;
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int kbase = blockIdx.x * 128;
+  const bf16_t* Qb = (const bf16_t*)a.Q + (long)b * a.Lq * a.sq + h * DH;
+  const bf16_t* dOb = (const bf16_t*)a.dO + (long)b * a.Lq * a.sdo + h * DH;
+  const bf16_t* Kb = (const bf16_t*)a.K + (long)b * a.Lk * a.sk + h * DH;
+  const bf16_t* Vb = (const bf16_t*)a.V + (long)b * a.Lk * a.sv + h * DH;
+  const float sl2 = a.scale * 1.4426950408889634f;
+  int key[2];
+  bool kvld[2], kok[2];
+  uint4 kf[2][2], vf[2][2];
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq) {
+    key[gq] = kbase + w * 32 + gq * 16 + i;
+    kvld[gq] = key[gq] < a.Lk;
+    kok[gq] = kvld[gq] && key_ok(a, b, key[gq]);
+    row_frags<bf16_t>(kf[gq], Kb, a.sk, kvld[gq] ? key[gq] : 0, kvld[gq], lane);
+    row_frags<bf16_t>(vf[gq], Vb, a.sv, kvld[gq] ? key[gq] : 0, kvld[gq], lane);
+  }
+  uint4 qr[2], orr[2];
+  float lv = 0.f;
+  auto load = [&](int q0) {
+    const int nv = min(64, a.Lq - q0);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int idx = tid + 256 * u, r = idx >> 3, c = idx & 7;
+      qr[u] = orr[u] = make_uint4(0, 0, 0, 0);
+      if (r < nv) {
+        qr[u] = *(const uint4*)(Qb + (long)(q0 + r) * a.sq + c * 8);
+        orr[u] = *(const uint4*)(dOb + (long)(q0 + r) * a.sdo + c * 8);
+      }
+    }
+    if (tid < 128) {
+      const int qq = q0 + (tid & 63);
+      lv = 0.f;
+      if (qq < a.Lq) lv = tid < 64 ? a.lse[(long)bh * a.Lq + qq] * 1.4426950408889634f : a.delta[(long)bh * a.Lq + qq];
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int idx = tid + 256 * u, r = idx >> 3, c = idx & 7;
+      *(uint4*)(qc[buf] + kc_off(RB, r, c)) = qr[u];
+      *(uint4*)(qt[buf] + r * 128 + (((2 * c) ^ hatt(r)) << 3)) = qr[u];
+      *(uint4*)(oc[buf] + kc_off(RB, r, c)) = orr[u];
+      *(uint4*)(ot[buf] + r * 128 + (((2 * c) ^ hatt(r)) << 3)) = orr[u];
+    }
+    if (tid < 64) lse_s[buf][tid] = lv;
+    else if (tid < 128) del_s[buf][tid - 64] = lv;
+  };
+  f32x4_t dk[2][4], dv[2][4];
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq)
+#pragma unroll
+    for (int d = 0; d < 4; ++d) dk[gq][d] = dv[gq][d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  load(0);
+  store(0);
+  __syncthreads();
+  const int ntiles = (a.Lq + 63) / 64;
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1, q0 = t * 64;
+    if (t + 1 < ntiles) load(q0 + 64);
+    f32x4_t s[2][4], dp[2][4];
+#pragma unroll
+    for (int qb = 0; qb < 4; ++qb) {
+      s[0][qb] = s[1][qb] = dp[0][qb] = dp[1][qb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub) {
+        const uint4 aq = *(const uint4*)(qc[cur] + kc_off(RB, qb * 16 + i, sub * 4 + g));
+        const uint4 ao = *(const uint4*)(oc[cur] + kc_off(RB, qb * 16 + i, sub * 4 + g));
+        mma<bf16_t>(s[0][qb], aq, kf[0][sub]);
+        mma<bf16_t>(s[1][qb], aq, kf[1][sub]);
+        mma<bf16_t>(dp[0][qb], ao, vf[0][sub]);
+        mma<bf16_t>(dp[1][qb], ao, vf[1][sub]);
+      }
+    }
+    float pd[2][4][4], ds[2][4][4];
+#pragma unroll
+    for (int qb = 0; qb < 4; ++qb) {
+      const float4 l4 = *(const float4*)(&lse_s[cur][qb * 16 + 4 * g]);
+      const float4 d4 = *(const float4*)(&del_s[cur][qb * 16 + 4 * g]);
+      const float lr[4] = {l4.x, l4.y, l4.z, l4.w}, dr[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+      for (int gq = 0; gq < 2; ++gq)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float pr = __builtin_amdgcn_exp2f(s[gq][qb][j] * sl2 - lr[j]);
+          pr = kok[gq] ? pr : 0.f;
+          float keep = 1.f;
+          if constexpr (DROP) {
+            const int qq = q0 + qb * 16 + 4 * g + j;
+            const uint64_t idx = ((uint64_t)bh * a.Lq + qq) * a.Lk + key[gq];
+            keep = drop_keep(a.seed, a.stream, idx, a.thr16) ? a.drop_scale : 0.f;
+          }
+          pd[gq][qb][j] = pr * keep;
+          ds[gq][qb][j] = pr * (dp[gq][qb][j] * keep - dr[j]);
+        }
+    }
+    trans_times_vals2(dv, ot[cur], pd, lane);
+    trans_times_vals2(dk, qt[cur], ds, lane);
+    if (t + 1 < ntiles) {
+      store(cur ^ 1);
+      __syncthreads();
+    }
+  }
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq) {
+    if (!kvld[gq]) continue;
+    bf16_t* dKb = (bf16_t*)a.dK + ((long)b * a.Lk + key[gq]) * a.sdk + h * DH;
+    bf16_t* dVb = (bf16_t*)a.dV + ((long)b * a.Lk + key[gq]) * a.sdv + h * DH;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      uint2 uk, uv;
+      uk.x = pk(dk[gq][d][0] * a.scale, dk[gq][d][1] * a.scale);
+      uk.y = pk(dk[gq][d][2] * a.scale, dk[gq][d][3] * a.scale);
+      uv.x = pk(dv[gq][d][0], dv[gq][d][1]);
+      uv.y = pk(dv[gq][d][2], dv[gq][d][3]);
+      *(uint2*)(dKb + d * 16 + 4 * g) = uk;
+      *(uint2*)(dVb + d * 16 + 4 * g) = uv;
+    }
+  }
+}
+
 template <typename T>
 static int run(int which, AttnArgs& a, hipStream_t s) {
   constexpr int RB = Cfg<T>::RB;
@@ -626,9 +948,28 @@ static int run(int which, AttnArgs& a, hipStream_t s) {
     dim3 grid((a.Lq + 63) / 64, a.B * a.H);
     hipLaunchKernelGGL(fwd_kernel<T>, grid, dim3(256), 128 * RB, s, a);
   } else if (which == 1) {
+    if constexpr (sizeof(T) == 2) {
+      if (!getenv("FDDM_ATTN_V1")) {
+        dim3 grid((a.Lq + 127) / 128, a.B * a.H);
+        const bool drop = a.thr16 != 0, mask = a.key_keep != nullptr || (a.Lk % 64) != 0;
+        if (drop) { if (mask) hipLaunchKernelGGL((dq2_kernel<true, true>), grid, dim3(256), 0, s, a);
+                    else hipLaunchKernelGGL((dq2_kernel<true, false>), grid, dim3(256), 0, s, a); }
+        else { if (mask) hipLaunchKernelGGL((dq2_kernel<false, true>), grid, dim3(256), 0, s, a);
+               else hipLaunchKernelGGL((dq2_kernel<false, false>), grid, dim3(256), 0, s, a); }
+        return (int)hipGetLastError();
+      }
+    }
     dim3 grid((a.Lq + 63) / 64, a.B * a.H);
     hipLaunchKernelGGL(dq_kernel<T>, grid, dim3(256), 192 * RB, s, a);
   } else {
+    if constexpr (sizeof(T) == 2) {
+      if (!getenv("FDDM_ATTN_V1")) {
+        dim3 grid((a.Lk + 127) / 128, a.B * a.H);
+        if (a.thr16) hipLaunchKernelGGL((dkv2_kernel<true>), grid, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((dkv2_kernel<false>), grid, dim3(256), 0, s, a);
+        return (int)hipGetLastError();
+      }
+    }
     dim3 grid((a.Lk + 63) / 64, a.B * a.H);
     hipLaunchKernelGGL(dkv_kernel<T>, grid, dim3(256), 256 * RB + 512, s, a);
   }
