@@ -140,6 +140,7 @@ struct AttnArgs {
   void *Out, *dQ, *dK, *dV;
   float* lse;
   float* delta;  // [B*H][Lq] workspace: rowsum(dO*O), written by dq_kernel
+  uint64_t* dbits;  // [B*H][Lq][ceil(Lk/64)] dropout keep bits: written by the forward, read by the backward
   long sq, sk, sv, so, sdo, sdq, sdk, sdv;
   const unsigned char* key_keep;  // [B][Lk] or null
   const float* gate;              // [B*H][Lq] or null (WavLM)
@@ -363,6 +364,7 @@ __global__ void __launch_bounds__(256) fwd2_kernel(AttnArgs a) {
       const float mref = (mn == -INFINITY) ? 0.f : mn;  // all-masked so far: exp2(-inf - 0) = 0
       const float alpha = __builtin_amdgcn_exp2f(m[gq] - mref);
       float ls = 0.f;
+      uint64_t bits = 0;
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb) {
         unsigned keep = 0xF;
@@ -379,6 +381,7 @@ __global__ void __launch_bounds__(256) fwd2_kernel(AttnArgs a) {
             const unsigned u = (unsigned)(hw >> (16u * (sl & 3u))) & 0xFFFFu;
             keep |= (u >= a.thr16 ? 1u : 0u) << j;
           }
+          bits |= (uint64_t)keep << (kb * 16 + 4 * g);
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -386,6 +389,16 @@ __global__ void __launch_bounds__(256) fwd2_kernel(AttnArgs a) {
           ls += e;
           if constexpr (DROP) e = ((keep >> j) & 1u) ? e * a.drop_scale : 0.f;
           p[gq][kb][j] = e;
+        }
+      }
+      if constexpr (DROP) {
+        if (a.dbits) {  // the 4 lanes of a query hold disjoint key nibbles: OR them into the tile's 64-bit word
+          unsigned lo = (unsigned)bits, hi = (unsigned)(bits >> 32);
+          lo |= __shfl_xor(lo, 16, 64);
+          hi |= __shfl_xor(hi, 16, 64);
+          lo |= __shfl_xor(lo, 32, 64);
+          hi |= __shfl_xor(hi, 32, 64);
+          if (g == 0 && qv[gq]) a.dbits[((long)bh * a.Lq + q[gq]) * ntiles + t] = ((uint64_t)hi << 32) | lo;
         }
       }
       l[gq] = l[gq] * alpha + ls;
@@ -755,13 +768,24 @@ __global__ void __launch_bounds__(256) dq2_kernel(AttnArgs a) {
         mrow[kb][0] = m4.x; mrow[kb][1] = m4.y; mrow[kb][2] = m4.z; mrow[kb][3] = m4.w;
       }
     }
+    uint64_t wbits[2] = {0, 0};
+    if constexpr (DROP) {
+      if (a.dbits) {
+#pragma unroll
+        for (int gq = 0; gq < 2; ++gq)
+          wbits[gq] = qv[gq] ? a.dbits[((long)bh * a.Lq + q[gq]) * ntiles + t] : 0;
+      }
+    }
     float ds[2][4][4];
 #pragma unroll
     for (int gq = 0; gq < 2; ++gq)
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb) {
         unsigned keep = 0xF;
-        if constexpr (DROP) keep = keep4(a, ((uint64_t)bh * a.Lq + q[gq]) * a.Lk + (k0 + kb * 16 + 4 * g));
+        if constexpr (DROP) {
+          if (a.dbits) keep = (unsigned)(wbits[gq] >> (kb * 16 + 4 * g)) & 0xFu;
+          else keep = keep4(a, ((uint64_t)bh * a.Lq + q[gq]) * a.Lk + (k0 + kb * 16 + 4 * g));
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           float pr = __builtin_amdgcn_exp2f(s[gq][kb][j] * sl2 - lse2[gq]);
@@ -801,9 +825,11 @@ __global__ void __launch_bounds__(256) dkv2_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) unsigned char oc[2][64 * RB];
   __shared__ __attribute__((aligned(16))) unsigned char ot[2][64 * RB];
   __shared__ float lse_s[2][64], del_s[2][64];
+  __shared__ __attribute__((aligned(16))) uint64_t wb_s[2][2][64];  // [buf][key tile of the block][query]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, i = lane & 15;
   const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
   const int kbase = blockIdx.x * 128;
+  const int ntk = (a.Lk + 63) / 64;
   const bf16_t* Qb = (const bf16_t*)a.Q + (long)b * a.Lq * a.sq + h * DH;
   const bf16_t* dOb = (const bf16_t*)a.dO + (long)b * a.Lq * a.sdo + h * DH;
   const bf16_t* Kb = (const bf16_t*)a.K + (long)b * a.Lk * a.sk + h * DH;
@@ -822,6 +848,7 @@ __global__ void __launch_bounds__(256) dkv2_kernel(AttnArgs a) {
   }
   uint4 qr[2], orr[2];
   float lv = 0.f;
+  uint64_t wv = 0;
   auto load = [&](int q0) {
     const int nv = min(64, a.Lq - q0);
 #pragma unroll
@@ -838,6 +865,10 @@ __global__ void __launch_bounds__(256) dkv2_kernel(AttnArgs a) {
       lv = 0.f;
       if (qq < a.Lq) lv = tid < 64 ? a.lse[(long)bh * a.Lq + qq] * 1.4426950408889634f : a.delta[(long)bh * a.Lq + qq];
     }
+    if (DROP && a.dbits && tid >= 128) {
+      const int qq = q0 + (tid & 63), kt = 2 * blockIdx.x + ((tid - 128) >> 6);
+      wv = (qq < a.Lq && kt < ntk) ? a.dbits[((long)bh * a.Lq + qq) * ntk + kt] : 0;
+    }
   };
   auto store = [&](int buf) {
 #pragma unroll
@@ -850,6 +881,7 @@ __global__ void __launch_bounds__(256) dkv2_kernel(AttnArgs a) {
     }
     if (tid < 64) lse_s[buf][tid] = lv;
     else if (tid < 128) del_s[buf][tid - 64] = lv;
+    if (DROP && a.dbits && tid >= 128) wb_s[buf][(tid - 128) >> 6][tid & 63] = wv;
   };
   f32x4_t dk[2][4], dv[2][4];
 #pragma unroll
@@ -878,11 +910,23 @@ __global__ void __launch_bounds__(256) dkv2_kernel(AttnArgs a) {
       }
     }
     float pd[2][4][4], ds[2][4][4];
+    const int kbit = (w * 32 + i) & 63;  // key bit within its tile (groups gq add 16)
 #pragma unroll
     for (int qb = 0; qb < 4; ++qb) {
       const float4 l4 = *(const float4*)(&lse_s[cur][qb * 16 + 4 * g]);
       const float4 d4 = *(const float4*)(&del_s[cur][qb * 16 + 4 * g]);
       const float lr[4] = {l4.x, l4.y, l4.z, l4.w}, dr[4] = {d4.x, d4.y, d4.z, d4.w};
+      uint64_t wq[4] = {0, 0, 0, 0};
+      if constexpr (DROP) {
+        if (a.dbits) {
+          const uint64_t* src = &wb_s[cur][w >> 1][qb * 16 + 4 * g];
+          const uint4 u0 = *(const uint4*)src, u1 = *(const uint4*)(src + 2);
+          wq[0] = ((uint64_t)u0.y << 32) | u0.x;
+          wq[1] = ((uint64_t)u0.w << 32) | u0.z;
+          wq[2] = ((uint64_t)u1.y << 32) | u1.x;
+          wq[3] = ((uint64_t)u1.w << 32) | u1.z;
+        }
+      }
 #pragma unroll
       for (int gq = 0; gq < 2; ++gq)
 #pragma unroll
@@ -891,9 +935,14 @@ __global__ void __launch_bounds__(256) dkv2_kernel(AttnArgs a) {
           pr = kok[gq] ? pr : 0.f;
           float keep = 1.f;
           if constexpr (DROP) {
-            const int qq = q0 + qb * 16 + 4 * g + j;
-            const uint64_t idx = ((uint64_t)bh * a.Lq + qq) * a.Lk + key[gq];
-            keep = drop_keep(a.seed, a.stream, idx, a.thr16) ? a.drop_scale : 0.f;
+            bool kp;
+            if (a.dbits) {
+              kp = (wq[j] >> (kbit + 16 * gq)) & 1u;
+            } else {
+              const int qq = q0 + qb * 16 + 4 * g + j;
+              kp = drop_keep(a.seed, a.stream, ((uint64_t)bh * a.Lq + qq) * a.Lk + key[gq], a.thr16);
+            }
+            keep = kp ? a.drop_scale : 0.f;
           }
           pd[gq][qb][j] = pr * keep;
           ds[gq][qb][j] = pr * (dp[gq][qb][j] * keep - dr[j]);
@@ -1007,8 +1056,9 @@ static int attn_dispatch(int which, int dtype, AttnArgs& a, float drop_p, void* 
 FDDM_API int fddm_attn_fwd(int dtype, const void* Q, long sq, const void* K, long sk, const void* V, long sv, void* O,
                            long so, float* lse, const unsigned char* key_keep, const float* gate, const float* table,
                            int B, int H, int Lq, int Lk, float scale, float drop_p, unsigned long long seed,
-                           unsigned long long stream, void* hs) {
+                           unsigned long long stream, unsigned long long* drop_bits, void* hs) {
   AttnArgs a{};
+  a.dbits = (uint64_t*)drop_bits;
   a.Q = Q; a.K = K; a.V = V; a.Out = O; a.lse = lse;
   a.sq = sq; a.sk = sk; a.sv = sv; a.so = so;
   a.key_keep = key_keep; a.gate = gate; a.table = table;
@@ -1021,8 +1071,9 @@ FDDM_API int fddm_attn_bwd(int dtype, const void* Q, long sq, const void* K, lon
                            const void* O, long so, const void* dO, long sdo, const float* lse, void* dQ, long sdq,
                            void* dK, long sdk, void* dV, long sdv, float* delta_ws, const unsigned char* key_keep,
                            int B, int H, int Lq, int Lk, float scale, float drop_p, unsigned long long seed,
-                           unsigned long long stream, void* hs) {
+                           unsigned long long stream, const unsigned long long* drop_bits, void* hs) {
   AttnArgs a{};
+  a.dbits = (uint64_t*)drop_bits;
   a.delta = delta_ws;
   a.Q = Q; a.K = K; a.V = V; a.O = O; a.dO = dO; a.lse = (float*)lse;
   a.dQ = dQ; a.dK = dK; a.dV = dV;

@@ -203,4 +203,4 @@ FDDM_API int fddm_cast(int src_dtype, int dst_dtype, const void* x, void* y, lon
 
 FDDM_API const char* fddm_error_string(int code) { return hipGetErrorString((hipError_t)code); }
 
-FDDM_API int fddm_abi_version() { return 1; }
+FDDM_API int fddm_abi_version() { return 2; }

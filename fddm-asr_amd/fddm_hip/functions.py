@@ -131,7 +131,9 @@ class DecoderBlockFn(torch.autograd.Function):
         v = ops.linear(xT, W["sa"][2 * d:], sa_b[2 * d:], out_dtype=cd)
         o = torch.empty(N, d, device=dev, dtype=cd)
         lse = torch.empty(B * H, L, device=dev, dtype=F32)
-        ops.attn_fwd(qk, qk[:, d:], v, o, lse, B, H, L, L, key_keep=key_keep, drop_p=p, seed=seed, rng_stream=st + 1)
+        bits_s = ops.drop_bits(B, H, L, L, dev) if p > 0 else None
+        ops.attn_fwd(qk, qk[:, d:], v, o, lse, B, H, L, L, key_keep=key_keep, drop_p=p, seed=seed, rng_stream=st + 1,
+                     dbits=bits_s)
         y = ops.linear(o, W["so"], so_b, out_dtype=cd)
         s1 = torch.empty(N, d, device=dev, dtype=F32)
         m1 = torch.empty(N, device=dev, dtype=F32)
@@ -145,7 +147,8 @@ class DecoderBlockFn(torch.autograd.Function):
         kvc = ops.linear(cT, W["ca"][d:], ca_b[d:], out_dtype=cd)
         oc = torch.empty(N, d, device=dev, dtype=cd)
         lsec = torch.empty(B * H, L, device=dev, dtype=F32)
-        ops.attn_fwd(qc, kvc, kvc[:, d:], oc, lsec, B, H, L, S, drop_p=p, seed=seed, rng_stream=st + 3)
+        bits_c = ops.drop_bits(B, H, L, S, dev) if p > 0 else None
+        ops.attn_fwd(qc, kvc, kvc[:, d:], oc, lsec, B, H, L, S, drop_p=p, seed=seed, rng_stream=st + 3, dbits=bits_c)
         yc = ops.linear(oc, W["co"], co_b, out_dtype=cd)
         s2 = torch.empty(N, d, device=dev, dtype=F32)
         m2 = torch.empty(N, device=dev, dtype=F32)
@@ -171,6 +174,7 @@ class DecoderBlockFn(torch.autograd.Function):
         ctx.save_for_backward(xT, xr, qk, v, o, lse, s1, m1, r1, x1T, qc, kvc, oc, lsec, s2, m2, r2, x2T, hpre, hact,
                               s3, m3, r3, cT, key_keep, fsc, *params)
         ctx.meta = meta
+        ctx.bits = (bits_s, bits_c)
         ctx.mark_non_differentiable(x3T)
         return x3, x3T
 
@@ -217,8 +221,9 @@ class DecoderBlockFn(torch.autograd.Function):
         doc = ops.linear_dx(dyc, W["co"], out_dtype=cd)
         dqc = torch.empty(N, d, device=dev, dtype=cd)
         dkvc = torch.empty(B * S, 2 * d, device=dev, dtype=cd)
+        bits_s, bits_c = ctx.bits
         ops.attn_bwd(qc, kvc, kvc[:, d:], oc, doc, lsec, dqc, dkvc, dkvc[:, d:], B, H, L, S, drop_p=p, seed=seed,
-                     rng_stream=st + 3)
+                     rng_stream=st + 3, dbits=bits_c)
         ops.linear_dw(dqc, x1T, out=gca_w[:d], accumulate=aca, db=gca_b[:d])
         ops.linear_dw(dkvc, cT, out=gca_w[d:], accumulate=aca, db=gca_b[d:])
         ops.linear_dx(dqc, W["ca"][:d], out=dx1, accumulate=True)
@@ -233,7 +238,7 @@ class DecoderBlockFn(torch.autograd.Function):
         dqk = torch.empty(N, 2 * d, device=dev, dtype=cd)
         dv = torch.empty(N, d, device=dev, dtype=cd)
         ops.attn_bwd(qk, qk[:, d:], v, o, do, lse, dqk, dqk[:, d:], dv, B, H, L, L, key_keep=key_keep, drop_p=p,
-                     seed=seed, rng_stream=st + 1)
+                     seed=seed, rng_stream=st + 1, dbits=bits_s)
         ops.linear_dw(dqk, xr, out=gsa_w[: 2 * d], accumulate=asa, db=gsa_b[: 2 * d])
         ops.linear_dw(dv, xT, out=gsa_w[2 * d:], accumulate=asa, db=gsa_b[2 * d:])
         ops.linear_dx(dv, W["sa"][2 * d:], out=dx, accumulate=True)

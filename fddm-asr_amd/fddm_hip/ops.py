@@ -130,24 +130,31 @@ def wavlm_gate(x2d, W, bias, cst, B, S, H):
 
 
 # ------------------------------------------------------------------------------------- attention
+def drop_bits(B, H, Lq, Lk, device):
+    """Buffer for the forward's dropout keep bits ([B*H][Lq][ceil(Lk/64)] u64), read by the backward."""
+    return torch.empty(B * H * Lq * ((Lk + 63) // 64), device=device, dtype=torch.int64)
+
+
 def attn_fwd(q, k, v, out, lse, B, H, Lq, Lk, *, key_keep=None, gate=None, table=None, drop_p=0.0, seed=0,
-             rng_stream=0, scale=None):
-    """q: [B*Lq, >=H*64] row stride q.stride(0); k/v: [B*Lk, ...]; out [B*Lq, H*64]; lse [B*H, Lq]."""
+             rng_stream=0, scale=None, dbits=None):
+    """q: [B*Lq, >=H*64] row stride q.stride(0); k/v: [B*Lk, ...]; out [B*Lq, H*64]; lse [B*H, Lq].
+    dbits (optional, drop_bits()): records the dropout keep bits for the backward."""
     _chk(q.stride(-1) == 1 and k.stride(-1) == 1 and v.stride(-1) == 1, "attention inputs need unit inner stride")
     _chk(q.dtype == k.dtype == v.dtype == out.dtype, "attention dtype mismatch")
     sc = 1.0 / math.sqrt(64) if scale is None else scale
     call("fddm_attn_fwd", code(q), ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out),
          out.stride(0), ptr(lse), ptr(key_keep), ptr(gate), ptr(table), B, H, Lq, Lk, float(sc), float(drop_p), seed,
-         rng_stream, stream())
+         rng_stream, ptr(dbits), stream())
     return out
 
 
-def attn_bwd(q, k, v, o, do, lse, dq, dk, dv, B, H, Lq, Lk, *, key_keep=None, drop_p=0.0, seed=0, rng_stream=0):
+def attn_bwd(q, k, v, o, do, lse, dq, dk, dv, B, H, Lq, Lk, *, key_keep=None, drop_p=0.0, seed=0, rng_stream=0,
+             dbits=None):
     delta = torch.empty(B * H, Lq, device=q.device, dtype=torch.float32)
     call("fddm_attn_bwd", code(q), ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(o),
          o.stride(0), ptr(do), do.stride(0), ptr(lse), ptr(dq), dq.stride(0), ptr(dk), dk.stride(0), ptr(dv),
          dv.stride(0), ptr(delta), ptr(key_keep), B, H, Lq, Lk, float(1.0 / 8.0), float(drop_p), seed, rng_stream,
-         stream())
+         ptr(dbits), stream())
 
 
 # ----------------------------------------------------------------------------------- layernorm

@@ -54,16 +54,19 @@ int fddm_wavlm_gate(int dtype, const void* x, const float* W, const float* bias,
 
 /* ---- attention (head_dim 64). Element (b,pos,h,d) at base + (b*L+pos)*stride + h*64 + d.
  *      nn.MultiheadAttention (models/denoise_decoder.py:129-130,164,169-174) with key_padding_mask
- *      (key_keep[b][k] != 0 keeps) and attention-prob dropout; WavLM relative-bias attention
+ *      (key_keep[b][k] != 0 keeps) and attention-prob dropout (drop_bits, optional: the forward records
+ *      the keep bits as [B*H][Lq][ceil(Lk/64)] u64 words, the backward reads them instead of rehashing);
+ *      WavLM relative-bias attention
  *      (HF modeling_wavlm.py:152-200) via gate [B*H][Lq] and table [H][2*Lk-1]. lse: [B*H][Lq]. */
 int fddm_attn_fwd(int dtype, const void* Q, long sq, const void* K, long sk, const void* V, long sv, void* O, long so,
                   float* lse, const unsigned char* key_keep, const float* gate, const float* table, int B, int H,
                   int Lq, int Lk, float scale, float drop_p, unsigned long long seed, unsigned long long stream,
-                  void* hip_stream);
+                  unsigned long long* drop_bits, void* hip_stream);
 int fddm_attn_bwd(int dtype, const void* Q, long sq, const void* K, long sk, const void* V, long sv, const void* O,
                   long so, const void* dO, long sdo, const float* lse, void* dQ, long sdq, void* dK, long sdk,
                   void* dV, long sdv, float* delta_ws, const unsigned char* key_keep, int B, int H, int Lq, int Lk,
-                  float scale, float drop_p, unsigned long long seed, unsigned long long stream, void* hip_stream);
+                  float scale, float drop_p, unsigned long long seed, unsigned long long stream,
+                  const unsigned long long* drop_bits, void* hip_stream);
 
 /* ---- residual + dropout + LayerNorm (+FiLM). models/denoise_decoder.py:87-89,165-191;
  *      HF modeling_wavlm.py:102,313-317,405. */

@@ -204,8 +204,11 @@ def _attn_ref(q, k, v, keep, p_drop, seed, stream, gate=None, table=None):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("Lq,Lk,masked,p", [(70, 70, True, 0.0), (64, 130, False, 0.1), (33, 49, True, 0.1)])
-def test_attention_fwd_bwd(dtype, Lq, Lk, masked, p):
+@pytest.mark.parametrize("Lq,Lk,masked,p,bits", [(70, 70, True, 0.0, False), (64, 130, False, 0.1, False),
+                                                 (33, 49, True, 0.1, False), (150, 200, True, 0.1, True),
+                                                 (64, 130, False, 0.1, True)])
+def test_attention_fwd_bwd(dtype, Lq, Lk, masked, p, bits):
+    """bits: the forward records the dropout keep bits and the backward reads them (bf16 path)."""
     o = ops()
     B, H = 2, 3
     D = H * 64
@@ -222,11 +225,13 @@ def test_attention_fwd_bwd(dtype, Lq, Lk, masked, p):
     od = torch.empty(B * Lq, D, device=dev, dtype=dtype)
     lse = torch.empty(B * H, Lq, device=dev)
     kk = keep.to(dev).to(torch.uint8) if keep is not None else None
-    o.attn_fwd(qd, kd, vd, od, lse, B, H, Lq, Lk, key_keep=kk, drop_p=p, seed=5, rng_stream=9)
+    db = o.drop_bits(B, H, Lq, Lk, dev) if bits else None
+    o.attn_fwd(qd, kd, vd, od, lse, B, H, Lq, Lk, key_keep=kk, drop_p=p, seed=5, rng_stream=9, dbits=db)
     dq = torch.empty_like(qd)
     dk = torch.empty_like(kd)
     dv = torch.empty_like(vd)
-    o.attn_bwd(qd, kd, vd, od, dod, lse, dq, dk, dv, B, H, Lq, Lk, key_keep=kk, drop_p=p, seed=5, rng_stream=9)
+    o.attn_bwd(qd, kd, vd, od, dod, lse, dq, dk, dv, B, H, Lq, Lk, key_keep=kk, drop_p=p, seed=5, rng_stream=9,
+               dbits=db)
     torch.cuda.synchronize()
     hv = lambda x: x.to(dtype).double().view(B, -1, H, 64).transpose(1, 2)  # noqa: E731
     qr, kr, vr = (hv(x).requires_grad_(True) for x in (q, k, v))
