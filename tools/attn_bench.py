@@ -42,8 +42,9 @@ def main():
         if kpm:
             keep = torch.ones(B, Lk, dtype=torch.uint8, device=dev)
             keep[:, Lk * 3 // 4:] = 0
+        db = ops.drop_bits(B, H, Lq, Lk, dev) if p > 0 else None
         f = lambda: ops.attn_fwd(q, k, v, o, lse, B, H, Lq, Lk, key_keep=keep, gate=gate, table=table,  # noqa
-                                 drop_p=p, seed=1, rng_stream=1)
+                                 drop_p=p, seed=1, rng_stream=1, dbits=db)
         fl = 4.0 * B * H * Lq * Lk * 64
         t2 = timeit(f)
         os.environ["FDDM_ATTN_V1"] = "1"
@@ -55,7 +56,7 @@ def main():
             do = torch.randn_like(o)
             dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
             g = lambda: ops.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, B, H, Lq, Lk, key_keep=keep, drop_p=p,  # noqa
-                                     seed=1, rng_stream=1)
+                                     seed=1, rng_stream=1, dbits=db)
             tb = timeit(g)
             print(f"bwd {name:44s}    {tb*1e3:8.1f} us {2.5*fl/tb/1e9:7.1f} TF/s", flush=True)
 
