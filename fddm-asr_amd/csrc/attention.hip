@@ -140,7 +140,7 @@ struct AttnArgs {
   void *Out, *dQ, *dK, *dV;
   float* lse;
   float* delta;  // [B*H][Lq] workspace: rowsum(dO*O), written by dq_kernel
-  uint64_t* dbits;  // [B*H][Lq][ceil(Lk/64)] dropout keep bits: written by the forward, read by the backward
+  uint64_t* dbits;  // [B*H][ceil(Lk/64)][Lq] dropout keep bits: written by the forward, read by the backward
   long sq, sk, sv, so, sdo, sdq, sdk, sdv;
   const unsigned char* key_keep;  // [B][Lk] or null
   const float* gate;              // [B*H][Lq] or null (WavLM)
@@ -398,7 +398,7 @@ __global__ void __launch_bounds__(256) fwd2_kernel(AttnArgs a) {
           hi |= __shfl_xor(hi, 16, 64);
           lo |= __shfl_xor(lo, 32, 64);
           hi |= __shfl_xor(hi, 32, 64);
-          if (g == 0 && qv[gq]) a.dbits[((long)bh * a.Lq + q[gq]) * ntiles + t] = ((uint64_t)hi << 32) | lo;
+          if (g == 0 && qv[gq]) a.dbits[((long)bh * ntiles + t) * a.Lq + q[gq]] = ((uint64_t)hi << 32) | lo;
         }
       }
       l[gq] = l[gq] * alpha + ls;
@@ -666,8 +666,10 @@ __device__ __forceinline__ unsigned keep4(const AttnArgs& a, uint64_t e0) {
 // dQ, query-owned: 128 queries per workgroup (two 16-query groups per wave), K/V tiles double-buffered.
 // S^T = K Q^T and dP^T = V dO^T share the LDS row reads across both groups; dS = P (dP' - delta);
 // dQ^T += K^T dS^T from the K MC image. Writes delta = rowsum(dO*O) for the dK/dV kernel.
-template <bool DROP, bool MASK>
-__global__ void __launch_bounds__(256) dq2_kernel(AttnArgs a) {
+// DM: 0 no dropout, 1 rehash the keep bits, 2 read the forward's recorded bits
+template <int DM, bool MASK>
+__global__ void __launch_bounds__(256, 2) dq2_kernel(AttnArgs a) {
+  constexpr bool DROP = DM != 0;
   constexpr int RB = 128;
   __shared__ __attribute__((aligned(16))) unsigned char kc[2][64 * RB];
   __shared__ __attribute__((aligned(16))) unsigned char kt[2][64 * RB];
@@ -769,12 +771,9 @@ __global__ void __launch_bounds__(256) dq2_kernel(AttnArgs a) {
       }
     }
     uint64_t wbits[2] = {0, 0};
-    if constexpr (DROP) {
-      if (a.dbits) {
+    if constexpr (DM == 2) {
 #pragma unroll
-        for (int gq = 0; gq < 2; ++gq)
-          wbits[gq] = qv[gq] ? a.dbits[((long)bh * a.Lq + q[gq]) * ntiles + t] : 0;
-      }
+      for (int gq = 0; gq < 2; ++gq) wbits[gq] = qv[gq] ? a.dbits[((long)bh * ntiles + t) * a.Lq + q[gq]] : 0;
     }
     float ds[2][4][4];
 #pragma unroll
@@ -782,10 +781,8 @@ __global__ void __launch_bounds__(256) dq2_kernel(AttnArgs a) {
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb) {
         unsigned keep = 0xF;
-        if constexpr (DROP) {
-          if (a.dbits) keep = (unsigned)(wbits[gq] >> (kb * 16 + 4 * g)) & 0xFu;
-          else keep = keep4(a, ((uint64_t)bh * a.Lq + q[gq]) * a.Lk + (k0 + kb * 16 + 4 * g));
-        }
+        if constexpr (DM == 2) keep = (unsigned)(wbits[gq] >> (kb * 16 + 4 * g)) & 0xFu;
+        if constexpr (DM == 1) keep = keep4(a, ((uint64_t)bh * a.Lq + q[gq]) * a.Lk + (k0 + kb * 16 + 4 * g));
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           float pr = __builtin_amdgcn_exp2f(s[gq][kb][j] * sl2 - lse2[gq]);
@@ -817,8 +814,9 @@ __global__ void __launch_bounds__(256) dq2_kernel(AttnArgs a) {
 
 // dK, dV, key-owned: 128 keys per workgroup (two 16-key groups per wave), Q/dO tiles double-buffered
 // (row images for S, dP and transposed images for dV^T += dO^T P', dK^T += Q^T dS).
-template <bool DROP>
-__global__ void __launch_bounds__(256) dkv2_kernel(AttnArgs a) {
+template <int DM>
+__global__ void __launch_bounds__(256, (DM == 1 ? 1 : 2)) dkv2_kernel(AttnArgs a) {
+  constexpr bool DROP = DM != 0;
   constexpr int RB = 128;
   __shared__ __attribute__((aligned(16))) unsigned char qc[2][64 * RB];
   __shared__ __attribute__((aligned(16))) unsigned char qt[2][64 * RB];
@@ -865,9 +863,9 @@ __global__ void __launch_bounds__(256) dkv2_kernel(AttnArgs a) {
       lv = 0.f;
       if (qq < a.Lq) lv = tid < 64 ? a.lse[(long)bh * a.Lq + qq] * 1.4426950408889634f : a.delta[(long)bh * a.Lq + qq];
     }
-    if (DROP && a.dbits && tid >= 128) {
+    if (DM == 2 && tid >= 128) {
       const int qq = q0 + (tid & 63), kt = 2 * blockIdx.x + ((tid - 128) >> 6);
-      wv = (qq < a.Lq && kt < ntk) ? a.dbits[((long)bh * a.Lq + qq) * ntk + kt] : 0;
+      wv = (qq < a.Lq && kt < ntk) ? a.dbits[((long)bh * ntk + kt) * a.Lq + qq] : 0;
     }
   };
   auto store = [&](int buf) {
@@ -881,7 +879,7 @@ __global__ void __launch_bounds__(256) dkv2_kernel(AttnArgs a) {
     }
     if (tid < 64) lse_s[buf][tid] = lv;
     else if (tid < 128) del_s[buf][tid - 64] = lv;
-    if (DROP && a.dbits && tid >= 128) wb_s[buf][(tid - 128) >> 6][tid & 63] = wv;
+    if (DM == 2 && tid >= 128) wb_s[buf][(tid - 128) >> 6][tid & 63] = wv;
   };
   f32x4_t dk[2][4], dv[2][4];
 #pragma unroll
@@ -917,8 +915,8 @@ __global__ void __launch_bounds__(256) dkv2_kernel(AttnArgs a) {
       const float4 d4 = *(const float4*)(&del_s[cur][qb * 16 + 4 * g]);
       const float lr[4] = {l4.x, l4.y, l4.z, l4.w}, dr[4] = {d4.x, d4.y, d4.z, d4.w};
       uint64_t wq[4] = {0, 0, 0, 0};
-      if constexpr (DROP) {
-        if (a.dbits) {
+      if constexpr (DM == 2) {
+        {
           const uint64_t* src = &wb_s[cur][w >> 1][qb * 16 + 4 * g];
           const uint4 u0 = *(const uint4*)src, u1 = *(const uint4*)(src + 2);
           wq[0] = ((uint64_t)u0.y << 32) | u0.x;
@@ -936,7 +934,7 @@ __global__ void __launch_bounds__(256) dkv2_kernel(AttnArgs a) {
           float keep = 1.f;
           if constexpr (DROP) {
             bool kp;
-            if (a.dbits) {
+            if constexpr (DM == 2) {
               kp = (wq[j] >> (kbit + 16 * gq)) & 1u;
             } else {
               const int qq = q0 + qb * 16 + 4 * g + j;
@@ -1001,10 +999,12 @@ static int run(int which, AttnArgs& a, hipStream_t s) {
       if (!getenv("FDDM_ATTN_V1")) {
         dim3 grid((a.Lq + 127) / 128, a.B * a.H);
         const bool drop = a.thr16 != 0, mask = a.key_keep != nullptr || (a.Lk % 64) != 0;
-        if (drop) { if (mask) hipLaunchKernelGGL((dq2_kernel<true, true>), grid, dim3(256), 0, s, a);
-                    else hipLaunchKernelGGL((dq2_kernel<true, false>), grid, dim3(256), 0, s, a); }
-        else { if (mask) hipLaunchKernelGGL((dq2_kernel<false, true>), grid, dim3(256), 0, s, a);
-               else hipLaunchKernelGGL((dq2_kernel<false, false>), grid, dim3(256), 0, s, a); }
+        const int dm = drop ? (a.dbits ? 2 : 1) : 0;
+#define DQ2(D, M) hipLaunchKernelGGL((dq2_kernel<D, M>), grid, dim3(256), 0, s, a)
+        if (dm == 2) { if (mask) DQ2(2, true); else DQ2(2, false); }
+        else if (dm == 1) { if (mask) DQ2(1, true); else DQ2(1, false); }
+        else { if (mask) DQ2(0, true); else DQ2(0, false); }
+#undef DQ2
         return (int)hipGetLastError();
       }
     }
@@ -1014,8 +1014,9 @@ static int run(int which, AttnArgs& a, hipStream_t s) {
     if constexpr (sizeof(T) == 2) {
       if (!getenv("FDDM_ATTN_V1")) {
         dim3 grid((a.Lk + 127) / 128, a.B * a.H);
-        if (a.thr16) hipLaunchKernelGGL((dkv2_kernel<true>), grid, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((dkv2_kernel<false>), grid, dim3(256), 0, s, a);
+        if (a.thr16 && a.dbits) hipLaunchKernelGGL((dkv2_kernel<2>), grid, dim3(256), 0, s, a);
+        else if (a.thr16) hipLaunchKernelGGL((dkv2_kernel<1>), grid, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((dkv2_kernel<0>), grid, dim3(256), 0, s, a);
         return (int)hipGetLastError();
       }
     }

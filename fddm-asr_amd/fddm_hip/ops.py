@@ -131,7 +131,7 @@ def wavlm_gate(x2d, W, bias, cst, B, S, H):
 
 # ------------------------------------------------------------------------------------- attention
 def drop_bits(B, H, Lq, Lk, device):
-    """Buffer for the forward's dropout keep bits ([B*H][Lq][ceil(Lk/64)] u64), read by the backward."""
+    """Buffer for the forward's dropout keep bits ([B*H][ceil(Lk/64)][Lq] u64), read by the backward."""
     return torch.empty(B * H * Lq * ((Lk + 63) // 64), device=device, dtype=torch.int64)
 
 

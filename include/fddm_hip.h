@@ -55,7 +55,7 @@ int fddm_wavlm_gate(int dtype, const void* x, const float* W, const float* bias,
 /* ---- attention (head_dim 64). Element (b,pos,h,d) at base + (b*L+pos)*stride + h*64 + d.
  *      nn.MultiheadAttention (models/denoise_decoder.py:129-130,164,169-174) with key_padding_mask
  *      (key_keep[b][k] != 0 keeps) and attention-prob dropout (drop_bits, optional: the forward records
- *      the keep bits as [B*H][Lq][ceil(Lk/64)] u64 words, the backward reads them instead of rehashing);
+ *      the keep bits as [B*H][ceil(Lk/64)][Lq] u64 words, the backward reads them instead of rehashing);
  *      WavLM relative-bias attention
  *      (HF modeling_wavlm.py:152-200) via gate [B*H][Lq] and table [H][2*Lk-1]. lse: [B*H][Lq]. */
 int fddm_attn_fwd(int dtype, const void* Q, long sq, const void* K, long sk, const void* V, long sv, void* O, long so,
