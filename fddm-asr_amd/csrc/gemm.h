@@ -1,0 +1,38 @@
+// Shared declarations of the MFMA GEMM kernels (gemm.hip: 128x128 general kernel; gemm256.hip: 256x256
+// 8-phase kernel for the large NT shapes).
+#pragma once
+#include "common.h"
+
+namespace fddm {
+
+enum { EPI_STORE = 0, EPI_GELU = 1, EPI_ACC_F32 = 2, EPI_GELU_ONLY = 3, EPI_DGELU = 4 };
+
+// implicit-conv addressing of a KC A operand: A(m,k) = A + (m/Mi)*sAb + (t*cstride - cpad + k/Cg)*lda + k%Cg,
+// t = m%Mi, zero outside 0 <= time < Tin (WavLM conv feature extractor and grouped positional conv)
+struct ConvGeo { long Cg, cstride, cpad, Tin; };
+
+struct GemmArgs {
+  const void* A; long lda, Mi, sAb;
+  const void* B; long ldb;
+  void* C; long ldc; void* C2;
+  const float* bias; float alpha;
+  long M, N, K;
+  uint64_t seed, stream; unsigned thr16; float drop_scale;
+  ConvGeo geo;
+  long sAz, sBz, sCz, sbiasz;  // per-blockIdx.z offsets (grouped conv)
+  long ksplit;                 // K elements per split-K slice (plain GEMM)
+  float* colsum;               // optional: colsum[m] += sum_k A(m,k) (MC A operand) — fused bias gradient
+};
+
+// KC LDS image: 16-B chunk c of 128-B row r at r*128 + ((c ^ ((r>>1)&7))<<4) — conflict-free ds_read_b128 of
+// MFMA fragments (16 rows x one chunk per lane group)
+__device__ __forceinline__ int swz_kc(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
+
+// 256x256 8-phase bf16 NT GEMM (gemm256.hip). Preconditions: bf16 A/B, both K-contiguous, K % 64 == 0,
+// 16-B aligned rows, N % 8 == 0, conv without padding taps and Cg % 64 == 0. epi: STORE, GELU, GELU_ONLY;
+// out_dtype: FDDM_BF16 or FDDM_F32 (STORE only). Returns hipError_t.
+int gemm256_launch(const GemmArgs& g, int epi, int out_dtype, bool conv, hipStream_t s);
+bool gemm256_ok(const GemmArgs& g, int epi, int out_dtype, bool conv);
+long gemm256_tiles(long M, long N);
+
+}  // namespace fddm

@@ -21,22 +21,16 @@
 //       f32: plain rows of 512 B, scalar reads.
 // Register-staged prefetch of step k+1 is issued before the MFMAs of step k (one barrier per step).
 // A may be stored in f32 while the MFMA runs in bf16 (TA=float, T=bf16): converted while staging.
-#include "common.h"
+#include "gemm.h"
 #include <algorithm>
 #include <cstdlib>
 
 namespace fddm {
 
-enum { EPI_STORE = 0, EPI_GELU = 1, EPI_ACC_F32 = 2, EPI_GELU_ONLY = 3, EPI_DGELU = 4 };
-
-// implicit-conv addressing of a KC A operand: A(m,k) = A + (m/Mi)*sAb + (t*cstride - cpad + k/Cg)*lda + k%Cg,
-// t = m%Mi, zero outside 0 <= time < Tin (WavLM conv feature extractor and grouped positional conv)
-struct ConvGeo { long Cg, cstride, cpad, Tin; };
 
 constexpr int GBM = 128, GBN = 128;
 constexpr int GTILE_BYTES = 16384;  // per operand per stage
 
-__device__ __forceinline__ int swz_kc(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
 __device__ __forceinline__ int hk(int k) { return ((k & 3) << 2) | (((k >> 3) & 1) << 4); }
 
 template <typename T> struct Mma;
@@ -189,18 +183,6 @@ struct Operand {
   }
 };
 
-struct GemmArgs {
-  const void* A; long lda, Mi, sAb;
-  const void* B; long ldb;
-  void* C; long ldc; void* C2;
-  const float* bias; float alpha;
-  long M, N, K;
-  uint64_t seed, stream; unsigned thr16; float drop_scale;
-  ConvGeo geo;
-  long sAz, sBz, sCz, sbiasz;  // per-blockIdx.z offsets (grouped conv)
-  long ksplit;                 // K elements per split-K slice (plain GEMM)
-  float* colsum;               // optional: colsum[m] += sum_k A(m,k) (MC A operand) — fused bias gradient
-};
 
 // 8 consecutive outputs as one 16-B (bf16) or two 16-B (f32) accesses
 __device__ __forceinline__ void st_vec8(bf16_t* p, const float (&v)[8]) {
@@ -636,10 +618,28 @@ static int dispatch_layout(int a_kc, int b_kc, int epi, int out_dtype, const Gem
 
 using namespace fddm;
 
-// FDDM_NO_BIG_GEMM=1 routes every GEMM through the 128x128 kernel (read once per process)
-static bool big_enabled() {
-  static const bool on = getenv("FDDM_NO_BIG_GEMM") == nullptr;
-  return on;
+// FDDM_GEMM_PATH (read per call, for A/B benchmarks): "small" routes every GEMM through the 128x128 kernel,
+// "big" disables the 256x256 kernel, unset = automatic choice;
+// "256" takes the 256x256 kernel wherever its preconditions hold
+static int gemm_path() {
+  const char* v = getenv("FDDM_GEMM_PATH");
+  if (!v) return 0;
+  if (v[0] == 's') return 2;
+  if (v[0] == 'b') return 1;
+  if (v[0] == '2') return 3;
+  return 0;
+}
+static bool big_enabled() { return gemm_path() != 2; }
+static bool g256_enabled() { return gemm_path() == 0 || gemm_path() == 3; }
+// 256x256 tiles pay off once they fill the chip: at least ~one tile per CU, and not much worse quantised than
+// 256x128 tiles (rounds of 256 workgroups)
+static bool prefer_256(long M, long N) {
+  if (gemm_path() == 3) return true;
+  const long t256 = gemm256_tiles(M, N);
+  if (t256 < 192) return false;
+  const long t128 = ((M + 255) / 256) * ((N + 127) / 128);
+  const double r256 = (double)((t256 + 255) / 256), r128 = (double)((t128 + 255) / 256);
+  return r256 <= 0.5 * r128 * 1.15;  // a 256x256 round does twice the work of a 256x128 round
 }
 static long env_long(const char* name, long dflt) {
   const char* v = getenv(name);
@@ -705,6 +705,9 @@ FDDM_API int fddm_gemm(int dtype, int a_dtype, int a_kc, int b_kc, int epi, int 
     }
   }
   if (dtype == FDDM_BF16 && a_dtype == FDDM_BF16 && a_kc && b_kc && nz == 1 && Mi >= M && !colsum &&
+      g256_enabled() && gemm256_ok(g, epi, out_dtype, false) && prefer_256(M, N))
+    return gemm256_launch(g, epi, out_dtype, false, s);
+  if (dtype == FDDM_BF16 && a_dtype == FDDM_BF16 && a_kc && b_kc && nz == 1 && Mi >= M && !colsum &&
       out_dtype == FDDM_BF16 && big_ok(g, false) && big_enabled()) {
     if (epi == EPI_STORE) return launch_big<EPI_STORE, bf16_t, false>(g, s);
     if (epi == EPI_GELU) return launch_big<EPI_GELU, bf16_t, false>(g, s);
@@ -734,6 +737,9 @@ FDDM_API int fddm_conv1d_gemm(int dtype, int epi, const void* x, long lda, long 
   GemmArgs g{x, lda, Tout, sAb, W, K, out, ldc, nullptr, bias, 1.f, Bn * Tout, N, K, 0, 0, 0u, 1.f,
              ConvGeo{Cg, cstride, cpad, Tin}, Cg, N * K, N, N, K, nullptr};
   hipStream_t s = (hipStream_t)hip_stream;
+  if (dtype == FDDM_BF16 && groups == 1 && g256_enabled() && gemm256_ok(g, epi, FDDM_BF16, true) &&
+      prefer_256(g.M, N))
+    return gemm256_launch(g, epi, FDDM_BF16, true, s);
   if (dtype == FDDM_BF16 && groups == 1 && big_ok(g, true) && big_enabled()) {
     if (epi == EPI_GELU_ONLY) return launch_big<EPI_GELU_ONLY, bf16_t, true>(g, s);
     return launch_big<EPI_STORE, bf16_t, true>(g, s);

@@ -106,24 +106,31 @@ def test_weight_grad_gemm_with_fused_bias_grad(dtype, M, N, K):
     close(db, dy.to(dtype).double().sum(0), rtol=1e-5 if dtype == torch.float32 else 1e-3, what="db")
 
 
-@pytest.mark.parametrize("M,N,K,epi", [(8192, 2048, 512, 0), (15968, 768, 3072, 1), (8200, 2056, 768, 3)])
-def test_big_gemm_matches_torch(M, N, K, epi, monkeypatch):
-    """256x128 LDS-DMA GEMM (taken for >= 240 tiles) vs torch fp32 on the same bf16 operands,
-    and vs the 128x128 path (FDDM_NO_BIG_GEMM) — ragged M/N edges included."""
+@pytest.mark.parametrize("path", ["256", "big"])
+@pytest.mark.parametrize("M,N,K,epi,odt", [(8192, 2048, 512, 0, "bf16"), (15968, 768, 3072, 1, "bf16"),
+                                           (8200, 2056, 768, 3, "bf16"), (8192, 8000, 512, 0, "f32"),
+                                           (300, 264, 64, 0, "bf16"), (1000, 3072, 192, 1, "bf16")])
+def test_big_gemm_matches_torch(M, N, K, epi, odt, path, monkeypatch):
+    """256x256 8-phase GEMM / 256x128 LDS-DMA GEMM (FDDM_GEMM_PATH) vs torch fp32 on the same bf16 operands,
+    and vs the 128x128 path — ragged M/N edges, f32 output, dropout-free GELU epilogues included."""
     o = ops()
     gen = torch.Generator(device=dev).manual_seed(3)
     A = torch.randn(M, K, device=dev, generator=gen).bfloat16()
     W = (torch.randn(N, K, device=dev, generator=gen) / math.sqrt(K)).bfloat16()
     b = torch.randn(N, device=dev, generator=gen)
     ref = A.float() @ W.float().T + b
-    out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-    act = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    odtype = torch.float32 if odt == "f32" else torch.bfloat16
+    out = torch.full((M, N), float("nan"), device=dev, dtype=odtype)
+    act = torch.full((M, N), float("nan"), device=dev, dtype=odtype)
+    monkeypatch.setenv("FDDM_GEMM_PATH", path)
     o.gemm(A, W, out, M, N, K, lda=K, ldb=K, ldc=N, bias=b, epi=epi, C2=act if epi == 1 else None)
     chk = (act if epi == 1 else out).float()
     want = F.gelu(ref) if epi in (1, 3) else ref
     err = (chk - want).abs().max().item()
     assert err <= 2e-2 * want.abs().max().item(), err
-    monkeypatch.setenv("FDDM_NO_BIG_GEMM", "1")
+    if epi == 1:
+        assert (out.float() - ref).abs().max().item() <= 2e-2 * ref.abs().max().item()
+    monkeypatch.setenv("FDDM_GEMM_PATH", "small")
     out2 = torch.empty_like(out)
     act2 = torch.empty_like(act)
     o.gemm(A, W, out2, M, N, K, lda=K, ldb=K, ldc=N, bias=b, epi=epi, C2=act2 if epi == 1 else None)
@@ -131,7 +138,27 @@ def test_big_gemm_matches_torch(M, N, K, epi, monkeypatch):
     assert (chk - chk2).abs().max().item() <= 1e-2 * want.abs().max().item()
 
 
-def test_big_conv_gemm_matches_torch(monkeypatch):
+def test_gemm256_dropout_gelu_matches_small_path(monkeypatch):
+    """EPI_GELU with dropout: the 256x256 epilogue draws the same keep mask (counter-based hash of m*N+n)."""
+    o = ops()
+    M, N, K, p = 1100, 2048, 512, 0.1
+    gen = torch.Generator(device=dev).manual_seed(5)
+    A = torch.randn(M, K, device=dev, generator=gen).bfloat16()
+    W = (torch.randn(N, K, device=dev, generator=gen) / math.sqrt(K)).bfloat16()
+    b = torch.randn(N, device=dev, generator=gen)
+    outs = []
+    for path in ("256", "small"):
+        monkeypatch.setenv("FDDM_GEMM_PATH", path)
+        pre = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        act = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        o.gemm(A, W, pre, M, N, K, lda=K, ldb=K, ldc=N, bias=b, epi=1, C2=act, drop_p=p, seed=7, rng_stream=3)
+        outs.append((pre.float(), act.float()))
+    assert torch.equal(outs[0][1] == 0, outs[1][1] == 0)
+    assert (outs[0][1] - outs[1][1]).abs().max().item() <= 2e-2 * outs[1][1].abs().max().item()
+
+
+@pytest.mark.parametrize("path", ["256", "big"])
+def test_big_conv_gemm_matches_torch(path, monkeypatch):
     o = ops()
     B, Cin, Tin, Cout, k, s = 8, 512, 4001, 512, 3, 2
     gen = torch.Generator(device=dev).manual_seed(4)
@@ -141,6 +168,7 @@ def test_big_conv_gemm_matches_torch(monkeypatch):
     Tout = ref.shape[1]
     Wp = w.permute(0, 2, 1).contiguous()
     out = torch.empty(B, Tout, Cout, device=dev, dtype=torch.bfloat16)
+    monkeypatch.setenv("FDDM_GEMM_PATH", path)
     o.conv1d_gemm(x, Wp, out, lda=Cin, sAb=Tin * Cin, Tin=Tin, Cg=Cin, cstride=s, cpad=0, Bn=B, Tout=Tout, N=Cout,
                   K=k * Cin, gelu=True)
     err = (out.float() - ref).abs().max().item()

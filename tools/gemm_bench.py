@@ -28,6 +28,20 @@ def report(name, flops, ms):
     print(f"{name:48s} {ms*1e3:9.1f} us  {flops/ms/1e9:8.1f} TF/s", flush=True)
 
 
+def report_paths(name, flops, fn, paths=("auto", "256", "big")):
+    """time fn under each FDDM_GEMM_PATH (read per launch by the library)"""
+    cells = []
+    for p in paths:
+        if p == "auto":
+            os.environ.pop("FDDM_GEMM_PATH", None)
+        else:
+            os.environ["FDDM_GEMM_PATH"] = p
+        ms = timeit(fn)
+        cells.append(f"{p}:{ms*1e3:8.1f} us {flops/ms/1e9:7.1f} TF/s")
+    os.environ.pop("FDDM_GEMM_PATH", None)
+    print(f"{name:40s} " + " | ".join(cells), flush=True)
+
+
 def main():
     only = sys.argv[1] if len(sys.argv) > 1 else ""
     B, T0, C = 32, 31999, 512
@@ -38,8 +52,9 @@ def main():
         out = torch.empty(B, T1, C, device=dev, dtype=bf)
         f = lambda: ops.conv1d_gemm(x, W, out, lda=C, sAb=T0 * C, Tin=T0, Cg=C, cstride=2, cpad=0, Bn=B, Tout=T1,  # noqa
                                     N=C, K=3 * C, gelu=True)
-        report("conv1 implicit GEMM 511968x512x1536", 2 * B * T1 * C * 3 * C, timeit(f))
-    shapes = [("enc FF1 15968x3072x768 GELU", 15968, 3072, 768, ops.EPI_GELU_ONLY),
+        report_paths("conv1 implicit GEMM 511968x512x1536", 2 * B * T1 * C * 3 * C, f)
+    shapes = [("square 8192^3", 8192, 8192, 8192, ops.EPI_STORE),
+              ("enc FF1 15968x3072x768 GELU", 15968, 3072, 768, ops.EPI_GELU_ONLY),
               ("enc QKV 15968x2304x768", 15968, 2304, 768, ops.EPI_STORE),
               ("enc FF2 15968x768x3072", 15968, 768, 3072, ops.EPI_STORE),
               ("dec FF1 8192x2048x512", 8192, 2048, 512, ops.EPI_STORE),
@@ -53,7 +68,7 @@ def main():
         o = torch.empty(M, N, device=dev, dtype=torch.float32 if epi < 0 else bf)
         e = ops.EPI_STORE if epi < 0 else epi
         f = lambda: ops.gemm(A, Wt, o, M, N, K, lda=K, ldb=K, ldc=N, epi=e)  # noqa: E731
-        report(name, 2 * M * N * K, timeit(f))
+        report_paths(name, 2 * M * N * K, f)
     dws = [("dW dec FF1 2048x512 (K=8192)", 2048, 512, 8192), ("dW dec out 512x512 (K=8192)", 512, 512, 8192),
            ("dW head 8000x512 (K=8192)", 8000, 512, 8192), ("dW cross kv 1024x512 (K=15968)", 1024, 512, 15968)]
     for name, M, N, K in dws:
