@@ -211,21 +211,21 @@ __device__ __forceinline__ void ld_vec8(const float* p, float (&v)[8]) {
   v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
 
+// one 128x128 output tile (bx, by) of K-slice / group bz out of nz
 template <typename T, typename TA, bool AKC, bool BKC, int EPI, typename OT, bool CONV>
-__global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+__device__ __forceinline__ void gemm_tile(const GemmArgs& g, unsigned char* smem, long bx, long by, long bz, long nzs) {
   constexpr int KSTEP = Mma<T>::KSTEP;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
-  const long m0 = (long)blockIdx.y * GBM, n0 = (long)blockIdx.x * GBN;
+  const long m0 = by * GBM, n0 = bx * GBN;
 
-  // blockIdx.z: group index (implicit conv) or split-K slice (plain GEMM, f32 atomic epilogue)
-  const long z = blockIdx.z;
+  // bz: group index (implicit conv) or split-K slice (plain GEMM, f32 atomic epilogue)
+  const long z = bz;
   Operand<T, TA, AKC, CONV> opa;
   Operand<T, T, BKC> opb;
   long kbeg = 0, klen = g.K;
   long zg = CONV ? z : 0;
-  if (!CONV && gridDim.z > 1) {
+  if (!CONV && nzs > 1) {
     kbeg = z * g.ksplit;
     klen = min(g.ksplit, g.K - kbeg);
   }
@@ -236,7 +236,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g) {
   OT* Cz = (OT*)g.C + zg * g.sCz;
   const float* biasz = g.bias ? g.bias + zg * g.sbiasz : nullptr;
   if (!CONV && z > 0) biasz = nullptr;
-  const bool atomic_out = !CONV && gridDim.z > 1;
+  const bool atomic_out = !CONV && nzs > 1;
 
   f32x4_t acc[4][4];
 #pragma unroll
@@ -246,7 +246,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g) {
 
   const long nk = (klen + KSTEP - 1) / KSTEP;
   // fused bias gradient: only the first N-tile column of blocks sums its A rows (MC A, bf16/f32 A)
-  const bool do_cs = !AKC && (sizeof(TA) == sizeof(T)) && g.colsum != nullptr && blockIdx.x == 0;
+  const bool do_cs = !AKC && (sizeof(TA) == sizeof(T)) && g.colsum != nullptr && bx == 0;
   float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   opa.gload(0);
   opb.gload(0);
@@ -399,6 +399,33 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g) {
   }
 }
 
+
+template <typename T, typename TA, bool AKC, bool BKC, int EPI, typename OT, bool CONV>
+__global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  gemm_tile<T, TA, AKC, BKC, EPI, OT, CONV>(g, smem, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.z);
+}
+
+// Grouped launch of independent GEMMs of one layout/epilogue (the weight gradients of a decoder block):
+// workgroups [start[p], start[p+1]) run problem p, tiles ordered (split, row, column).
+constexpr int GROUP_MAX = 12;
+struct GroupArgs {
+  int np;
+  int start[GROUP_MAX + 1];
+  int tn[GROUP_MAX], tm[GROUP_MAX], nz[GROUP_MAX];
+  GemmArgs g[GROUP_MAX];
+};
+
+template <typename T, typename TA, bool AKC, bool BKC, int EPI, typename OT>
+__global__ void __launch_bounds__(256) gemm_grouped_kernel(GroupArgs ga) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int b = blockIdx.x;
+  int p = 0;
+  while (p + 1 < ga.np && b >= ga.start[p + 1]) ++p;
+  const int local = b - ga.start[p], per = ga.tn[p] * ga.tm[p];
+  const int bz = local / per, rem = local - bz * per;
+  gemm_tile<T, TA, AKC, BKC, EPI, OT, false>(ga.g[p], smem, rem % ga.tn[p], rem / ga.tn[p], bz, ga.nz[p]);
+}
 
 // =====================================================================================================
 // "big" bf16 NT GEMM for the large forward shapes (WavLM conv layers 1..6, encoder/decoder projections
@@ -751,4 +778,43 @@ FDDM_API int fddm_conv1d_gemm(int dtype, int epi, const void* x, long lda, long 
     if (epi == EPI_GELU_ONLY) return launch<float, float, true, true, EPI_GELU_ONLY, float, true>(g, s, groups);
     return launch<float, float, true, true, EPI_STORE, float, true>(g, s, groups);
   }
+}
+
+// Grouped weight-gradient GEMMs dW_p[M_p][N_p] += dY_p^T X_p (dY_p stored [K_p][M_p], X_p stored [K_p][N_p], both
+// bf16 and M/N-contiguous), with the bias gradient db_p[m] += sum_k dY_p[k][m] fused (db_p may be null).
+// One launch for up to 12 problems; a problem's K is split so that every workgroup reduces about
+// `kchunk` tokens (f32 atomics between splits).
+FDDM_API int fddm_gemm_dw_grouped(int n, const void* const* dy, const long* ldy, const void* const* x, const long* ldx,
+                                  float* const* dw, const long* lddw, float* const* db, const long* M, const long* N,
+                                  const long* K, long kchunk, void* hip_stream) {
+  if (n <= 0) return 0;
+  if (n > GROUP_MAX) return (int)hipErrorInvalidValue;
+  GroupArgs ga{};
+  ga.np = n;
+  int total = 0;
+  for (int p = 0; p < n; ++p) {
+    if (M[p] <= 0 || N[p] <= 0 || K[p] <= 0) return (int)hipErrorInvalidValue;
+    if (M[p] % 8 || N[p] % 8 || ldy[p] % 8 || ldx[p] % 8) return (int)hipErrorInvalidValue;
+    if ((((uintptr_t)dy[p]) | ((uintptr_t)x[p])) & 15) return (int)hipErrorInvalidValue;
+    GemmArgs g{dy[p], ldy[p], 1L << 62, 0, x[p], ldx[p], dw[p], lddw[p], nullptr, nullptr, 1.f, M[p], N[p], K[p],
+               0, 0, 0u, 1.f, ConvGeo{1, 0, 0, 0}, 0, 0, 0, 0, K[p], db[p]};
+    long nz = kchunk > 0 ? (K[p] + kchunk / 2) / kchunk : 1;
+    if (nz < 1) nz = 1;
+    if (nz > 1) {
+      long ks = (K[p] + nz - 1) / nz;
+      ks = (ks + 63) / 64 * 64;
+      nz = (K[p] + ks - 1) / ks;
+      g.ksplit = ks;
+    }
+    ga.g[p] = g;
+    ga.tn[p] = (int)((N[p] + GBN - 1) / GBN);
+    ga.tm[p] = (int)((M[p] + GBM - 1) / GBM);
+    ga.nz[p] = (int)nz;
+    ga.start[p] = total;
+    total += ga.tn[p] * ga.tm[p] * (int)nz;
+  }
+  ga.start[n] = total;
+  hipLaunchKernelGGL((gemm_grouped_kernel<bf16_t, bf16_t, false, false, EPI_ACC_F32, float>), dim3(total), dim3(256),
+                     4 * GTILE_BYTES, (hipStream_t)hip_stream, ga);
+  return (int)hipGetLastError();
 }

@@ -30,6 +30,16 @@ def _ret(t, in_arena):
     return None if in_arena else t
 
 
+def _dw_flush(jobs):
+    """Run deferred weight-gradient GEMMs (dy, x, dW, db), all accumulating into zeroed or arena buffers:
+    one grouped launch in bf16, one GEMM per job otherwise (fp32 parity mode)."""
+    if jobs and all(j[0].dtype == torch.bfloat16 and j[1].dtype == torch.bfloat16 for j in jobs):
+        ops.linear_dw_grouped(jobs)
+    else:
+        for dy, x, dW, db in jobs:
+            ops.linear_dw(dy, x, out=dW, accumulate=True, db=db)
+
+
 # ------------------------------------------------------------------------------- generic Linear
 class LinearFn(torch.autograd.Function):
     """y = x W^T + b (f32 out) — SpeechProjector / TextProjector / encoder proj (models/projection.py)."""
@@ -192,7 +202,8 @@ class DecoderBlockFn(torch.autograd.Function):
         W = {k: rt.wt(v_) for k, v_ in (("sa", sa_w), ("so", so_w), ("ca", ca_w), ("co", co_w), ("f0", f0_w),
                                          ("f3", f3_w))}
         # gradient destinations: arena views (accumulated in place) or fresh tensors
-        G = [_gdst(p_, zero=(i >= 12)) for i, p_ in enumerate(params)]  # LN params are atomically summed
+        # (every destination accumulates: the weight gradients are deferred to one grouped launch at the end)
+        G = [_gdst(p_, zero=True) for p_ in params]
         (gsa_w, asa), (gsa_b, _), (gso_w, aso), (gso_b, _), (gca_w, aca), (gca_b, _), (gco_w, aco), (gco_b, _), \
             (gf0_w, af0), (gf0_b, _), (gf3_w, af3), (gf3_b, _), (gn1w, _), (gn1b, _), (gn2w, _), (gn2b, _), \
             (gn3w, _), (gn3b, _) = G
@@ -203,11 +214,11 @@ class DecoderBlockFn(torch.autograd.Function):
         ops.ln_bwd(dx3, s3, m3, r3, n3w, n3b, dres=dx2, dy_t=dy3, dgamma=gn3w, dbeta=gn3b, drop_p=p,
                    seed=seed, rng_stream=st + 6)
         # FF
-        ops.linear_dw(dy3, hact, out=gf3_w, accumulate=af3, db=gf3_b)
+        dw_jobs = [(dy3, hact, gf3_w, gf3_b)]
         FF = f0_w.shape[0]
         dh = torch.empty(N, FF, device=dev, dtype=cd)
         ops.linear_dx(dy3, W["f3"], out=dh, epi=ops.EPI_DGELU, C2=hpre, drop_p=p, seed=seed, rng_stream=st + 5)
-        ops.linear_dw(dh, x2T, out=gf0_w, accumulate=af0, db=gf0_b)
+        dw_jobs.append((dh, x2T, gf0_w, gf0_b))
         ops.linear_dx(dh, W["f0"], out=dx2, accumulate=True)
         # LN2 + FiLM
         dx1 = torch.empty(N, d, device=dev, dtype=F32)
@@ -217,15 +228,14 @@ class DecoderBlockFn(torch.autograd.Function):
         ops.ln_bwd(dx2, s2, m2, r2, n2w, n2b, dres=dx1, dy_t=dyc, dgamma=gn2w, dbeta=gn2b, film_scale=fsc,
                    dfilm=(dfs, dfh), rows_per_batch=L, drop_p=p, seed=seed, rng_stream=st + 4)
         # cross out-proj + attention
-        ops.linear_dw(dyc, oc, out=gco_w, accumulate=aco, db=gco_b)
+        dw_jobs.append((dyc, oc, gco_w, gco_b))
         doc = ops.linear_dx(dyc, W["co"], out_dtype=cd)
         dqc = torch.empty(N, d, device=dev, dtype=cd)
         dkvc = torch.empty(B * S, 2 * d, device=dev, dtype=cd)
         bits_s, bits_c = ctx.bits
         ops.attn_bwd(qc, kvc, kvc[:, d:], oc, doc, lsec, dqc, dkvc, dkvc[:, d:], B, H, L, S, drop_p=p, seed=seed,
                      rng_stream=st + 3, dbits=bits_c)
-        ops.linear_dw(dqc, x1T, out=gca_w[:d], accumulate=aca, db=gca_b[:d])
-        ops.linear_dw(dkvc, cT, out=gca_w[d:], accumulate=aca, db=gca_b[d:])
+        dw_jobs += [(dqc, x1T, gca_w[:d], gca_b[:d]), (dkvc, cT, gca_w[d:], gca_b[d:])]
         ops.linear_dx(dqc, W["ca"][:d], out=dx1, accumulate=True)
         # LN1
         dx = torch.empty(N, d, device=dev, dtype=F32)
@@ -233,17 +243,17 @@ class DecoderBlockFn(torch.autograd.Function):
         ops.ln_bwd(dx1, s1, m1, r1, n1w, n1b, dres=dx, dy_t=dy, dgamma=gn1w, dbeta=gn1b, drop_p=p, seed=seed,
                    rng_stream=st + 2)
         # self out-proj + attention
-        ops.linear_dw(dy, o, out=gso_w, accumulate=aso, db=gso_b)
+        dw_jobs.append((dy, o, gso_w, gso_b))
         do = ops.linear_dx(dy, W["so"], out_dtype=cd)
         dqk = torch.empty(N, 2 * d, device=dev, dtype=cd)
         dv = torch.empty(N, d, device=dev, dtype=cd)
         ops.attn_bwd(qk, qk[:, d:], v, o, do, lse, dqk, dqk[:, d:], dv, B, H, L, L, key_keep=key_keep, drop_p=p,
                      seed=seed, rng_stream=st + 1, dbits=bits_s)
-        ops.linear_dw(dqk, xr, out=gsa_w[: 2 * d], accumulate=asa, db=gsa_b[: 2 * d])
-        ops.linear_dw(dv, xT, out=gsa_w[2 * d:], accumulate=asa, db=gsa_b[2 * d:])
+        dw_jobs += [(dqk, xr, gsa_w[: 2 * d], gsa_b[: 2 * d]), (dv, xT, gsa_w[2 * d:], gsa_b[2 * d:])]
         ops.linear_dx(dv, W["sa"][2 * d:], out=dx, accumulate=True)
         dxr = ops.linear_dx(dqk, W["sa"][: 2 * d])
         ops.rope_bwd(dxr, cos, sin, dx, L)
+        _dw_flush(dw_jobs)
         grads = tuple(_ret(t_, a_) for t_, a_ in G)
         return (dx, None, None, None, dfs, dfh, None) + grads
 

@@ -96,6 +96,29 @@ def linear_dw(dy2d, x2d, out=None, accumulate=False, db=None):
                 ldc=out.stride(0), epi=EPI_ACC if accumulate else EPI_STORE, colsum=db)
 
 
+def linear_dw_grouped(jobs, kchunk=8192):
+    """One launch for several weight-gradient GEMMs, all accumulating: for each (dy [K,M], x [K,N], dW [M,N] f32,
+    db [M] f32 or None): dW += dy^T x, db += sum_k dy. dy/x bf16 with unit inner stride."""
+    import ctypes
+    jobs = [j for j in jobs if j[0].shape[0] > 0]
+    for i in range(0, len(jobs), 12):
+        chunk = jobs[i:i + 12]
+        n = len(chunk)
+        for dy, x, dW, db in chunk:
+            _chk(dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and dW.dtype == torch.float32, "dw dtypes")
+            _chk(dy.shape[0] == x.shape[0] and dW.shape == (dy.shape[1], x.shape[1]), "dw shapes")
+            _chk(dy.stride(1) == 1 and x.stride(1) == 1 and dW.stride(1) == 1, "dw strides")
+            _chk(db is None or (db.dtype == torch.float32 and db.is_contiguous() and db.numel() == dy.shape[1]),
+                 "db")
+        P = ctypes.c_void_p * n
+        L = ctypes.c_long * n
+        call("fddm_gemm_dw_grouped", n, P(*[j[0].data_ptr() for j in chunk]), L(*[j[0].stride(0) for j in chunk]),
+             P(*[j[1].data_ptr() for j in chunk]), L(*[j[1].stride(0) for j in chunk]),
+             P(*[j[2].data_ptr() for j in chunk]), L(*[j[2].stride(0) for j in chunk]),
+             P(*[ptr(j[3]) for j in chunk]), L(*[j[0].shape[1] for j in chunk]), L(*[j[1].shape[1] for j in chunk]),
+             L(*[j[0].shape[0] for j in chunk]), kchunk, stream())
+
+
 def colsum(X2d, out=None, accumulate=False):
     M, N = X2d.shape
     if out is None:

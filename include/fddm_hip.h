@@ -36,6 +36,16 @@ int fddm_gemm(int dtype, int a_dtype, int a_kc, int b_kc, int epi, int out_dtype
               long N, long K, unsigned long long seed, unsigned long long stream, float drop_p, float* colsum,
               void* hip_stream);
 
+/* ---- grouped weight-gradient GEMMs (one launch for the n <= 12 dW GEMMs of a decoder block):
+ *      dw[p][m][n] += sum_k dy[p][k][m] * x[p][k][n]   (dy: [K][M] bf16, x: [K][N] bf16, row strides ldy/ldx;
+ *      dw: f32, row stride lddw), db[p][m] += sum_k dy[p][k][m] (db[p] may be NULL). K is split into
+ *      slices of about `kchunk` tokens (kchunk <= 0: no split); slices combine with f32 atomics.
+ *      Arrays are host arrays of n entries. Replaces the weight/bias gradients autograd computes for the
+ *      block's Linear / MultiheadAttention parameters: models/denoise_decoder.py:129-145 */
+int fddm_gemm_dw_grouped(int n, const void* const* dy, const long* ldy, const void* const* x, const long* ldx,
+                         float* const* dw, const long* lddw, float* const* db, const long* M, const long* N,
+                         const long* K, long kchunk, void* hip_stream);
+
 /* ---- implicit-GEMM Conv1d on channels-last input (epi 0 store / 3 GELU), `groups` along gridDim.z.
  *      HF modeling_wavlm.py:675-693 (conv layers 1..6), 37-90 (positional grouped conv). */
 int fddm_conv1d_gemm(int dtype, int epi, const void* x, long lda, long sAb, long Tin, long Cg, long cstride,

@@ -138,6 +138,43 @@ def test_big_gemm_matches_torch(M, N, K, epi, odt, path, monkeypatch):
     assert (chk - chk2).abs().max().item() <= 1e-2 * want.abs().max().item()
 
 
+def test_grouped_weight_grads_match_torch():
+    """fddm_gemm_dw_grouped: the dW / db GEMMs of a decoder block in one launch (ragged K split across
+    workgroups, strided column slices of one gradient buffer) accumulate like torch in fp64."""
+    o = ops()
+    gen = torch.Generator(device=dev).manual_seed(11)
+    Kt, Kc = 1000, 1996
+    shapes = [(Kt, 64, 256), (Kt, 256, 64), (Kc, 128, 64), (Kt, 64, 64)]
+    dW = torch.randn(256 + 64 + 64, 256, device=dev, generator=gen)  # row slices for several jobs
+    dW0 = dW.clone()
+    db = torch.randn(512, device=dev, generator=gen)
+    db0 = db.clone()
+    jobs, refs = [], []
+    r0 = 0
+    for i, (K, M, N) in enumerate(shapes):
+        dy = torch.randn(K, M, device=dev, generator=gen).bfloat16()
+        x = torch.randn(K, N, device=dev, generator=gen).bfloat16()
+        if i == 0:
+            dst, bdst = dW[r0:r0 + M, :N], db[:M]
+        elif i == 1:
+            dst, bdst = torch.zeros(M, N, device=dev), None
+        elif i == 2:
+            dst, bdst = dW[r0:r0 + M, :N], db[256:256 + M]
+        else:
+            dst, bdst = dW[r0:r0 + M, 64:64 + N], db[448:448 + M]
+        jobs.append((dy, x, dst, bdst))
+        refs.append((dy.double().T @ x.double(), dy.double().sum(0)))
+        if i != 1:
+            r0 += M
+    o.linear_dw_grouped(jobs, kchunk=512)
+    close(jobs[1][2], refs[1][0], rtol=1e-4, what="dW job1")
+    close(dW[0:64, :256], dW0[0:64, :256].double() + refs[0][0], rtol=1e-4, what="dW job0")
+    close(dW[64:192, :64], dW0[64:192, :64].double() + refs[2][0], rtol=1e-4, what="dW job2")
+    close(dW[192:256, 64:128], dW0[192:256, 64:128].double() + refs[3][0], rtol=1e-4, what="dW job3")
+    close(db[:64], db0[:64].double() + refs[0][1], rtol=1e-4, what="db0")
+    close(db[256:384], db0[256:384].double() + refs[2][1], rtol=1e-4, what="db2")
+
+
 def test_gemm256_dropout_gelu_matches_small_path(monkeypatch):
     """EPI_GELU with dropout: the 256x256 epilogue draws the same keep mask (counter-based hash of m*N+n)."""
     o = ops()

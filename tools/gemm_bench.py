@@ -80,6 +80,23 @@ def main():
         db = torch.empty(M, device=dev)
         f = lambda: ops.linear_dw(dy, x, out=o, db=db)  # noqa: E731
         report(name, 2 * M * N * K, timeit(f))
+    if not only or only == "dw":
+        # the 8 weight-gradient GEMMs of one C2 decoder block in one grouped launch
+        T, d, FF, TS = 8192, 512, 2048, 15968
+        specs = [(T, d, FF), (T, FF, d), (T, d, d), (T, d, d), (TS, 2 * d, d), (T, d, d), (T, 2 * d, d), (T, d, d)]
+        jobs, fl = [], 0
+        for K, M, N in specs:
+            jobs.append((torch.randn(K, M, device=dev, dtype=bf), torch.randn(K, N, device=dev, dtype=bf),
+                         torch.zeros(M, N, device=dev), torch.zeros(M, device=dev)))
+            fl += 2 * M * N * K
+        for kc in (0, 8192, 4096, 2048):
+            f = lambda: ops.linear_dw_grouped(jobs, kchunk=kc)  # noqa: E731
+            report(f"dW grouped block (8 GEMMs) kchunk {kc}", fl, timeit(f))
+
+        def seq():
+            for dy, x, o, db in jobs:
+                ops.linear_dw(dy, x, out=o, accumulate=True, db=db)
+        report("dW block as 8 split-K launches", fl, timeit(seq))
     dxs = [("dX dec FF1 8192x512 (K=2048)", 8192, 512, 2048), ("dX head 8192x512 (K=8000, f32 A)", 8192, 512, 8000)]
     for name, M, N, K in dxs:
         if only and only != "dx":
