@@ -658,15 +658,11 @@ static int gemm_path() {
 }
 static bool big_enabled() { return gemm_path() != 2; }
 static bool g256_enabled() { return gemm_path() == 0 || gemm_path() == 3; }
-// 256x256 tiles pay off once they fill the chip: at least ~one tile per CU, and not much worse quantised than
-// 256x128 tiles (rounds of 256 workgroups)
+// the persistent 256x256 kernel wins from about half a round of tiles up (measured at the train step's shapes:
+// 189 tiles of 15968x768x3072 still beat the 256x128 kernel by 1.3x; 64 tiles of 8192x512x512 lose)
 static bool prefer_256(long M, long N) {
   if (gemm_path() == 3) return true;
-  const long t256 = gemm256_tiles(M, N);
-  if (t256 < 192) return false;
-  const long t128 = ((M + 255) / 256) * ((N + 127) / 128);
-  const double r256 = (double)((t256 + 255) / 256), r128 = (double)((t128 + 255) / 256);
-  return r256 <= 0.5 * r128 * 1.15;  // a 256x256 round does twice the work of a 256x128 round
+  return gemm256_tiles(M, N) >= 128;
 }
 static long env_long(const char* name, long dflt) {
   const char* v = getenv(name);

@@ -62,29 +62,9 @@ __device__ __forceinline__ u32x4_t ds_read128_at(unsigned a) {
 }
 template <int V> using IC = std::integral_constant<int, V>;
 
-// leave at most n (rounded down to a coded step) vector-memory instructions of this wave in flight
-template <int N> __device__ __forceinline__ void vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
-__device__ __forceinline__ void wait_vm(int n) {
-  if (n >= 32) {
-    if (n >= 63) vmcnt<63>();
-    else if (n >= 56) vmcnt<56>();
-    else if (n >= 48) vmcnt<48>();
-    else if (n >= 40) vmcnt<40>();
-    else vmcnt<32>();
-  } else if (n >= 12) {
-    if (n >= 28) vmcnt<28>();
-    else if (n >= 24) vmcnt<24>();
-    else if (n >= 20) vmcnt<20>();
-    else if (n >= 16) vmcnt<16>();
-    else vmcnt<12>();
-  } else {
-    if (n >= 10) vmcnt<10>();
-    else if (n >= 8) vmcnt<8>();
-    else if (n >= 6) vmcnt<6>();
-    else if (n >= 4) vmcnt<4>();
-    else if (n >= 2) vmcnt<2>();
-    else vmcnt<0>();
-  }
+// leave at most N vector-memory instructions of this wave in flight (N is always a compile-time count)
+template <int N> __device__ __forceinline__ void vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N < 63 ? N : 63) : "memory");
 }
 
 __device__ __forceinline__ void bar() {
@@ -110,19 +90,21 @@ __global__ void __launch_bounds__(512) gemm256_kernel(GemmArgs g) {
   const int s0 = (int)((long)tiles * Wx / G), s1 = (int)((long)tiles * (Wx + Px) / G);
   const int nmine = (s1 - s0 > jx) ? (s1 - s0 - jx + Px - 1) / Px : 0;
   if (nmine == 0) return;
-  // A ragged last tile is computed as the full tile ending at M (N): it recomputes some rows (columns) of
-  // its neighbour bit-identically and writes the same values, so no load or store needs a bounds check.
-  auto coords = [&](int i, int& m0, int& n0) {  // i-th tile of this workgroup
-    const int s = s0 + jx + i * Px;
+  // i-th tile of this workgroup (clamped to its last one: loads past the end re-read valid data). A ragged
+  // last tile is computed as the full tile ending at M (N): it recomputes some rows (columns) of its
+  // neighbour bit-identically and writes the same values, so no load or store needs a bounds check.
+  auto coords = [&](int i, int& m0, int& n0) {
+    const int s = s0 + jx + min(i, nmine - 1) * Px;
     const int per = GM * nN, grp = s / per, first = grp * GM, gsz = min(GM, nM - first), rr = s - grp * per;
     m0 = min((first + rr % gsz) * BM, (int)g.M - BM);
     n0 = min((rr / gsz) * BN, (int)g.N - BN);
   };
 
-  // LDS-DMA sources: buffer resources over A and B; per-lane byte offsets of the rows a lane fills relative
-  // to the tile origin (half h, instruction i fills image rows (wid*2+i)*8 + lane/8, physical chunk lane%8,
-  // which holds logical chunk (lane%8) ^ ((row>>1)&7)); tile origin, half shift and K offset go in the
-  // scalar soffset. Implicit conv: A rows are (utterance, frame) windows, so their offsets are per tile.
+  // ---------------------------------------------------------------- operand sources
+  // Buffer resources over A and B; per-lane byte offsets of the rows a lane fills relative to the tile
+  // origin (half h, instruction i fills image rows (wid*2+i)*8 + lane/8, physical chunk lane%8, which holds
+  // logical chunk (lane%8) ^ ((row>>1)&7)); tile origin, half shift and K offset go in the scalar soffset.
+  // Implicit conv: A rows are (utterance, frame) windows, so their offsets are per tile and per half.
   const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)g.A, 0, 0x7fffffff, SRD_W3);
   const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)g.B, 0, 0x7fffffff, SRD_W3);
   const int lda = (int)g.lda, ldb = (int)g.ldb, ldc = (int)g.ldc, Nc = (int)g.N;
@@ -134,95 +116,90 @@ __global__ void __launch_bounds__(512) gemm256_kernel(GemmArgs g) {
     va[i] = (((row >> 6) * 128 + (row & 63)) * lda + c * 8) * 2;  // A0 rows; A1 = +64 rows
     vb[i] = (((row >> 5) * 64 + (row & 31)) * ldb + c * 8) * 2;   // B0 rows; B1 = +32 rows
   }
-  int vc1[2] = {0, 0}, vc2[2] = {0, 0};  // conv: A1 rows of stream 1's tile, A0 rows of stream 2's tile
-  auto conv_rows = [&](int (&v)[2], int m0, int h) {
+  int vcc[2][2] = {{0, 0}, {0, 0}}, vcn[2][2] = {{0, 0}, {0, 0}};  // conv: [half][i] of current / next tile
+  auto conv_rows = [&](int (&v)[2][2], int m0) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int row = (wid * 2 + i) * 8 + (lane >> 3);
-      const int c = (lane & 7) ^ ((row >> 1) & 7);
-      const int m = m0 + (row >> 6) * 128 + h * 64 + (row & 63);
-      const int b = m / (int)g.Mi, tt = m - b * (int)g.Mi;
-      v[i] = (b * (int)g.sAb + tt * (int)(g.geo.cstride * g.lda) + c * 8) * 2;
-    }
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = (wid * 2 + i) * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ ((row >> 1) & 7);
+        const int m = m0 + (row >> 6) * 128 + h * 64 + (row & 63);
+        const int b = m / (int)g.Mi, tt = m - b * (int)g.Mi;
+        v[h][i] = (b * (int)g.sAb + tt * (int)(g.geo.cstride * g.lda) + c * 8) * 2;
+      }
   };
-  int vm = 0;  // vector-memory instructions issued by this wave so far
-  auto issue = [&](int h, int buf, const int (&v)[2], int so) {  // so: scalar byte offset
+  auto issue = [&](int h, int buf, int v0, int v1, int so) {  // so: scalar byte offset
     lptr_t d = (lptr_t)(smem + buf * STAGE + h * HALF + wid * 2048);
     const __amdgpu_buffer_rsrc_t& r = h < 2 ? rA : rB;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, d, 16, v[0], so, 0, 0);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lptr_t)((unsigned char*)d + 1024), 16, v[1], so, 0, 0);
-    vm += 2;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, d, 16, v0, so, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lptr_t)((unsigned char*)d + 1024), 16, v1, so, 0, 0);
   };
-  // issue streams: K-tile T+1 (halves B1, A1) and T+2 (A0, B0); each tracks its tile, K-tile, tile origin
-  // (scalar byte offsets into A and B) and, for conv, the (tap, channel) of the K-tile
-  struct Cursor { int ti, kt, tap, c, sa, sb; };
-  const int nk = (int)(g.K / 64), NT = nmine * nk;
-  const int Cg = CONV ? (int)g.geo.Cg : 64;
-  auto advance = [&](Cursor& u) {
-    if (++u.kt == nk) { u.kt = 0; ++u.ti; u.tap = 0; u.c = 0; }
-    else if (CONV) { u.c += 64; if (u.c == Cg) { u.c = 0; ++u.tap; } }
+  const int nk = (int)(g.K / 64);
+  const int cshift = CONV ? __builtin_ctz((unsigned)(g.geo.Cg / 64)) : 0;  // K-tiles per conv tap = 2^cshift
+  auto koffA = [&](int kt) -> int {  // byte offset of K-tile kt in an A row
+    if (!CONV) return kt * 128;
+    return ((kt >> cshift) * lda + (kt & ((1 << cshift) - 1)) * 64) * 2;
   };
-  auto koffA = [&](const Cursor& u) -> int { return (CONV ? u.tap * lda + u.c : u.sa + u.kt * 64) * 2; };
-  auto koffB = [&](const Cursor& u) -> int { return (u.sb + u.kt * 64) * 2; };
-  // at a tile start: the stream's tile origin (and conv row offsets of its A half)
-  auto enter = [&](Cursor& u, int (&vc)[2], int ha) {
-    if (u.kt == 0) {
-      int mm, nn;
-      coords(u.ti, mm, nn);
-      u.sa = mm * lda;
-      u.sb = nn * ldb;
-      if (CONV) conv_rows(vc, mm, ha);
-    }
+  // tile origins: current tile (cm0, cn0) and this workgroup's next tile (nm0, nn0)
+  int cm0, cn0, nm0, nn0;
+  coords(0, cm0, cn0);
+  coords(1, nm0, nn0);
+  if (CONV) {
+    conv_rows(vcc, cm0);
+    conv_rows(vcn, nm0);
+  }
+  // half h of K-tile kt of the tile at (m0, n0) [conv: lane offsets vc]
+  auto issueA = [&](int h, int buf, int kt, int m0, const int (&vc)[2][2]) {
+    if (CONV) issue(h, buf, vc[h][0], vc[h][1], koffA(kt));
+    else issue(h, buf, va[0], va[1], m0 * lda * 2 + h * 64 * lda * 2 + koffA(kt));
   };
-  auto issueA = [&](int h, int buf, const Cursor& u, const int (&vc)[2]) {
-    if (CONV) issue(h, buf, vc, koffA(u));
-    else issue(h, buf, va, koffA(u) + (h == HA1 ? 64 * lda * 2 : 0));
+  auto issueB = [&](int h, int buf, int kt, int n0) {
+    issue(h, buf, vb[0], vb[1], n0 * ldb * 2 + (h - 2) * 32 * ldb * 2 + kt * 128);
   };
-  auto issueB = [&](int h, int buf, const Cursor& u) { issue(h, buf, vb, koffB(u) + (h == HB1 ? 32 * ldb * 2 : 0)); };
 
-  // bias: each wave's 64 columns n0 + wc*64 + 0..63 are brought into its own 256-B LDS slot (one 4-byte
-  // LDS-DMA, one tile ahead) and seed the accumulators
+  // ---------------------------------------------------------------- bias
+  // each wave's 64 columns n0 + wc*64 + 0..63 come into its own 256-B LDS slot (one 4-byte LDS-DMA, one tile
+  // ahead) and seed the accumulators; without a bias the DMA reads A (any valid address) and the seed is 0
+  // Every K-tile issues one such DMA (phase 1); only a tile's last K-tile aims it at the real slot, the others
+  // at a dummy slot, so that all K-tiles issue the same vector-memory sequence.
   const bool has_bias = g.bias != nullptr;
   unsigned char* bslot = smem + LDS_BYTES + wid * 256;
-  int pos_bias = 0;
-  auto load_bias = [&](int n0) {
-    if (has_bias) {
-      const int n = n0 + wc * 64 + lane;
-      __builtin_amdgcn_global_load_lds((gptr_t)(g.bias + n), (lptr_t)bslot, 4, 0, 0);
-      vm += 1;
-    }
-    pos_bias = vm;
+  auto load_bias = [&](int n0, bool real) {
+    const float* src = has_bias ? g.bias + n0 + wc * 64 + lane : (const float*)g.A + lane;
+    __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(real ? bslot : bslot + 2048), 4, 0, 0);
   };
-  // the 4 bias values of block column j for this lane (columns j*16 + 4*fg .. +3); the caller has waited
-  // for the slot's LDS-DMA (vm - pos_bias)
+  // the 4 bias values of block columns jb, jb+1 for this lane (columns j*16 + 4*fg .. +3); the slot's DMA
+  // has been covered by a vmcnt of this wave
   auto bias_pair = [&](int jb, f32x4_t& v0, f32x4_t& v1) {
-    if (has_bias) {
-      const u32x4_t a = ds_read128(bslot + (jb * 16 + 4 * fg) * 4);
-      const u32x4_t b = ds_read128(bslot + ((jb + 1) * 16 + 4 * fg) * 4);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      v0 = __builtin_bit_cast(f32x4_t, a);
-      v1 = __builtin_bit_cast(f32x4_t, b);
-      asm volatile("" : "+v"(v0), "+v"(v1));
-    } else {
+    const u32x4_t a = ds_read128(bslot + (jb * 16 + 4 * fg) * 4);
+    const u32x4_t b = ds_read128(bslot + ((jb + 1) * 16 + 4 * fg) * 4);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    v0 = __builtin_bit_cast(f32x4_t, a);
+    v1 = __builtin_bit_cast(f32x4_t, b);
+    asm volatile("" : "+v"(v0), "+v"(v1));
+    if (!has_bias) {
       v0 = f32x4_t{0.f, 0.f, 0.f, 0.f};
       v1 = v0;
     }
   };
 
-  // stores: buffer stores, lane offset fixed, tile origin and block offset in soffset
+  // ---------------------------------------------------------------- stores
+  // buffer stores: lane offset fixed, tile origin and block offset in soffset
   const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(g.C, 0, 0x7fffffff, SRD_W3);
   const __amdgpu_buffer_rsrc_t rc2 =
       __builtin_amdgcn_make_buffer_rsrc(EPI == EPI_GELU ? g.C2 : g.C, 0, 0x7fffffff, SRD_W3);
   constexpr int ESZ = (int)sizeof(OT);
-  const int vst = ((wr * 128 + fr) * ldc + wc * 64 + 4 * fg) * ESZ;
   constexpr int SPQ = EPI == EPI_GELU ? 16 : 8;  // store instructions per quadrant
+  const int vst = ((wr * 128 + fr) * ldc + wc * 64 + 4 * fg) * ESZ;
 
   u32x4_t af[4][2], b0[2][2], b1[2][2];
   f32x4_t acc[8][4];
 
-  // quadrant q of the finished tile at (em0, en0): blocks i in 4*(q>>1).., j in 2*(q&1)..; then re-seed it
-  auto epi_quadrant = [&](int q, int em0, int en0, bool reseed) {
-    const int ib = (q >> 1) * 4, jb = (q & 1) * 2;
+  // quadrant q of the finished tile at (em0, en0): blocks i in 4*(q>>1).., j in 2*(q&1)..; then (reseed)
+  // seed it with the bias of the tile that follows
+  auto epi_quadrant = [&](auto qc, int em0, int en0, bool reseed) {
+    constexpr int q = decltype(qc)::value, ib = (q >> 1) * 4, jb = (q & 1) * 2;
     f32x4_t bq[2];
     if (reseed) bias_pair(jb, bq[0], bq[1]);
 #pragma unroll
@@ -230,13 +207,12 @@ __global__ void __launch_bounds__(512) gemm256_kernel(GemmArgs g) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int so = ((em0 + (ib + i) * 16) * ldc + en0 + (jb + j) * 16) * ESZ;
-        const int off = vst;
         f32x4_t v = acc[ib + i][jb + j];
         if constexpr (sizeof(OT) == 4) {
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rc, off, so, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rc, vst, so, 0);
         } else {
           if constexpr (EPI == EPI_GELU) {
-            __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3])}, rc, off, so, 0);
+            __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3])}, rc, vst, so, 0);
             const unsigned thr = g.thr16;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -248,19 +224,18 @@ __global__ void __launch_bounds__(512) gemm256_kernel(GemmArgs g) {
               }
               v[e] = a;
             }
-            __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3])}, rc2, off, so, 0);
+            __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3])}, rc2, vst, so, 0);
           } else {
             if constexpr (EPI == EPI_GELU_ONLY) {
 #pragma unroll
               for (int e = 0; e < 4; ++e) v[e] = gelu_f(v[e]);
             }
-            __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3])}, rc, off, so, 0);
+            __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3])}, rc, vst, so, 0);
           }
         }
         if (reseed) acc[ib + i][jb + j] = bq[j];
         __builtin_amdgcn_sched_barrier(0);  // one block at a time: bounds the epilogue's live registers
       }
-    vm += SPQ;
   };
 
   // fragment addresses: swz_kc(base16 + i*16 + fr, s*4 + fg) = (base16 + i*16)*128 + swz_kc(fr, s*4 + fg) for a
@@ -308,30 +283,20 @@ __global__ void __launch_bounds__(512) gemm256_kernel(GemmArgs g) {
   };
 
   // ---------------------------------------------------------------- prologue
-  int m0, n0;
-  coords(0, m0, n0);
-  load_bias(n0);
-  Cursor c1{0, 0, 0, 0, 0, 0}, c2{0, 0, 0, 0, 0, 0};  // both at K-tile 0; c2 moves to K-tile 1 below
-  enter(c1, vc1, HA1);
-  enter(c2, vc2, HA0);
-  int pos_A0, pos_A0_prev, pos_B0, pos_B1, pos_A1;
-  issueA(HA0, 0, c2, vc2);
-  issueB(HB0, 0, c2);
-  const int pos_first = vm;
-  issueB(HB1, 0, c1);
-  pos_B1 = vm;
-  issueA(HA1, 0, c1, vc1);
-  pos_A1 = vm;
-  pos_A0 = pos_B0 = pos_first;
-  advance(c2);  // K-tile 1
-  if (NT > 1) {
-    enter(c2, vc2, HA0);
-    issueA(HA0, 1, c2, vc2);
-    pos_A0 = vm;
-    issueB(HB0, 1, c2);
-    pos_B0 = vm;
+  // VMEM issue order (= the steady-state order of the K loop): bias(tile 0), A0 B0 B1 A1 of K-tile 0,
+  // A0 B0 of K-tile 1
+  load_bias(cn0, true);
+  {
+    const int kt1 = 1 % nk;
+    const int m1 = nk > 1 ? cm0 : nm0, n1 = nk > 1 ? cn0 : nn0;
+    issueA(HA0, 0, 0, cm0, vcc);
+    issueB(HB0, 0, 0, cn0);
+    issueB(HB1, 0, 0, cn0);
+    issueA(HA1, 0, 0, cm0, vcc);
+    issueA(HA0, 1, kt1, m1, nk > 1 ? vcc : vcn);
+    issueB(HB0, 1, kt1, n1);
   }
-  wait_vm(vm - pos_first);  // bias, A0(0), B0(0)
+  vmcnt<8>();  // bias(0), A0(0), B0(0) landed
   bar();
 #pragma unroll
   for (int jb = 0; jb < 4; jb += 2) {
@@ -345,92 +310,91 @@ __global__ void __launch_bounds__(512) gemm256_kernel(GemmArgs g) {
   }
   readB(0, IC<HB0>{}, b0);
   if (wr == 1) bar();  // stagger the wave groups by one barrier
-  // c1 -> K-tile T+1, c2 -> K-tile T+2 at the top of iteration T
-  advance(c1);
-  advance(c2);
 
   // ---------------------------------------------------------------- flattened K loop over all my tiles
-  bool ep = false;  // the previous tile's results are still in acc (stored during this K-tile)
-  int em0 = 0, en0 = 0;
-  int kt = 0, ti = 0;
-  for (int T = 0; T < NT; ++T) {
+  // One K-tile T (kt within tile ti). Issues, in order: phase 1 bias DMA (real slot on a tile's last K-tile),
+  // B1(T+1); phase 2 A1(T+1); phase 3 A0(T+2); phase 4 B0(T+2) — K-tiles past the end re-read valid data.
+  // Each phase then waits for the half its successor reads; the count of younger vector-memory instructions
+  // is exact and compile-time per mode: EP (kt 0 of tiles >= 1) stores the previous tile after each wait,
+  // POST (kt 1) still sees those stores in its windows. Requires nk >= 2.
+  int em0 = 0, en0 = 0, kt = 0, ti = 0;
+  const int NT = nmine * nk;
+  // mode: 0 steady, 1 EP, 2 POST (one body; only the s_waitcnt immediate depends on the mode)
+  auto wait3 = [&](int mode, auto n0c, auto nec, auto npc) {
+    if (mode == 0) vmcnt<decltype(n0c)::value>();
+    else if (mode == 1) vmcnt<decltype(nec)::value>();
+    else vmcnt<decltype(npc)::value>();
+  };
+  auto ktile = [&](int T, int mode) {
+    const bool EP = mode == 1;
     const int bc = T & 1, bn = bc ^ 1;
-    const bool last = kt == nk - 1;
-    const bool more1 = T + 1 < NT, more2 = T + 2 < NT;
-    int nm0 = 0, nn0 = 0;  // next tile of this workgroup (for its bias)
-    if (last && more1) coords(ti + 1, nm0, nn0);
+    // K-tile T+1 is in the next tile iff LAST; T+2 iff kt >= nk-2
+    const bool n1b = kt == nk - 1, n2 = kt >= nk - 2;
+    const int kt1 = n1b ? 0 : kt + 1;
+    const int kt2 = n2 ? kt + 2 - nk : kt + 2;
+    const int m1 = n1b ? nm0 : cm0, n1 = n1b ? nn0 : cn0;
+    const int m2 = n2 ? nm0 : cm0, n2c = n2 ? nn0 : cn0;
     // ---- phase 1: A rows 0..63 x B cols 0..31
-    if (ep) {
-      wait_vm(vm - pos_bias);  // this tile's bias slot (loaded during the previous K-tile)
-      epi_quadrant(0, em0, en0, true);
-    }
     readA(bc, IC<HA0>{});
-    if (last && nk > 1 && more1) load_bias(nn0);
-    {
-      const int prev = pos_B1;  // B1(T), read in phase 2
-      if (more1) {
-        enter(c1, vc1, HA1);
-        issueB(HB1, bn, c1);
-        pos_B1 = vm;
-      }
-      wait_vm(vm - prev);
-    }
+    load_bias(nn0, n1b);
+    issueB(HB1, bn, kt1, n1);
+    wait3(mode, IC<9>{}, IC<9>{}, IC<9 + 4 * SPQ>{});  // B1(T)
+    if (EP) epi_quadrant(IC<0>{}, em0, en0, true);
     mma(0, 0, b0);
     // ---- phase 2: A rows 0..63 x B cols 32..63
-    if (ep) epi_quadrant(1, em0, en0, true);
     readB(bc, IC<HB1>{}, b1);
-    {
-      const int prev = pos_A1;  // A1(T), read in phase 3
-      if (more1) {
-        issueA(HA1, bn, c1, vc1);
-        pos_A1 = vm;
-      }
-      wait_vm(vm - prev);
-    }
+    if (CONV) issueA(HA1, bn, kt1, m1, n1b ? vcn : vcc);
+    else issueA(HA1, bn, kt1, m1, vcc);
+    wait3(mode, IC<9>{}, IC<9 + SPQ>{}, IC<9 + 3 * SPQ>{});  // A1(T)
+    if (EP) epi_quadrant(IC<1>{}, em0, en0, true);
     mma(0, 2, b1);
     // ---- phase 3: A rows 64..127 x B cols 0..31
-    if (ep) epi_quadrant(2, em0, en0, true);
     readA(bc, IC<HA1>{});
-    pos_A0_prev = pos_A0;
-    if (more2) {
-      enter(c2, vc2, HA0);
-      issueA(HA0, bc, c2, vc2);
-      pos_A0 = vm;
-    }
-    if (more1) wait_vm(vm - pos_B0);  // B0(T+1), read in phase 4
+    if (CONV) issueA(HA0, bc, kt2, m2, n2 ? vcn : vcc);
+    else issueA(HA0, bc, kt2, m2, vcc);
+    wait3(mode, IC<7>{}, IC<7 + 2 * SPQ>{}, IC<7 + SPQ>{});  // B0(T+1)
+    if (EP) epi_quadrant(IC<2>{}, em0, en0, true);
     mma(4, 0, b0);
     // ---- phase 4: A rows 64..127 x B cols 32..63; B0 fragments of K-tile T+1
-    if (ep) {
-      epi_quadrant(3, em0, en0, true);
-      ep = false;
-    }
-    if (more1) readB(bn, IC<HB0>{}, b0);
-    if (last && nk == 1 && more1) load_bias(nn0);
-    if (more2) {
-      issueB(HB0, bc, c2);
-      pos_B0 = vm;
-    }
-    if (more1) wait_vm(vm - pos_A0_prev);  // A0(T+1), read in phase 1 of T+1
+    readB(bn, IC<HB0>{}, b0);
+    issueB(HB0, bc, kt2, n2c);
+    wait3(mode, IC<11>{}, IC<11 + 3 * SPQ>{}, IC<11 + 2 * SPQ>{});  // A0(T+1)
+    if (EP) epi_quadrant(IC<3>{}, em0, en0, true);
     mma(4, 2, b1);
-    // ---- advance
-    advance(c1);
-    advance(c2);
-    if (last) {
-      ep = true;
-      em0 = m0;
-      en0 = n0;
-      m0 = nm0;
-      n0 = nn0;
+  };
+  // after a tile's last K-tile: its results move to the epilogue slot, the workgroup's next tile becomes current
+  auto next_tile = [&]() {
+    em0 = cm0;
+    en0 = cn0;
+    cm0 = nm0;
+    cn0 = nn0;
+    coords(ti + 2, nm0, nn0);
+    if (CONV) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) vcc[h][i] = vcn[h][i];
+      conv_rows(vcn, nm0);
+    }
+    ++ti;
+  };
+  for (int T = 0; T < NT; ++T) {
+    const bool later = ti > 0;
+    ktile(T, later ? (kt == 0 ? 1 : kt == 1 ? 2 : 0) : 0);
+    if (kt == nk - 1) {
+      next_tile();
       kt = 0;
-      ++ti;
     } else {
       ++kt;
     }
   }
   if (wr == 0) bar();
-  // the last tile
-#pragma unroll
-  for (int q = 0; q < 4; ++q) epi_quadrant(q, em0, en0, false);
+  // the last tile (its successor "tile" was a clamped re-read: nothing to seed)
+  epi_quadrant(IC<0>{}, em0, en0, false);
+  epi_quadrant(IC<1>{}, em0, en0, false);
+  epi_quadrant(IC<2>{}, em0, en0, false);
+  epi_quadrant(IC<3>{}, em0, en0, false);
+  vmcnt<0>();  // no LDS-DMA may land after the workgroup retires
 }
 
 template <int EPI, typename OT, bool CONV>
@@ -448,7 +412,7 @@ static int launch(const GemmArgs& g, hipStream_t s) {
 #else
   const long grid = tiles < ncu ? tiles : ncu;
 #endif
-  hipLaunchKernelGGL((gemm256_kernel<EPI, OT, CONV>), dim3((unsigned)grid), dim3(512), LDS_BYTES + 2048, s, g);
+  hipLaunchKernelGGL((gemm256_kernel<EPI, OT, CONV>), dim3((unsigned)grid), dim3(512), LDS_BYTES + 4096, s, g);
   return (int)hipGetLastError();
 }
 
@@ -457,7 +421,7 @@ static int launch(const GemmArgs& g, hipStream_t s) {
 long gemm256_tiles(long M, long N) { return ((M + 255) / 256) * ((N + 255) / 256); }
 
 bool gemm256_ok(const GemmArgs& g, int epi, int out_dtype, bool conv) {
-  if (g.K % 64 || g.K <= 0 || g.M <= 0 || g.N <= 0 || g.N % 8 || g.lda % 8 || g.ldb % 8 || g.ldc % 8) return false;
+  if (g.K % 64 || g.K < 128 || g.M <= 0 || g.N <= 0 || g.N % 8 || g.lda % 8 || g.ldb % 8 || g.ldc % 8) return false;
   if (g.alpha != 1.f) return false;
   if ((((uintptr_t)g.A) | ((uintptr_t)g.B) | ((uintptr_t)g.C) | ((uintptr_t)g.C2) | ((uintptr_t)g.bias)) & 15)
     return false;
@@ -468,7 +432,7 @@ bool gemm256_ok(const GemmArgs& g, int epi, int out_dtype, bool conv) {
   if (conv && (g.M % g.Mi || g.geo.cstride * g.lda >= (1L << 31))) return false;
   const long esz = out_dtype == FDDM_F32 ? 4 : 2;
   if (((g.M - 1) * g.ldc + g.N) * esz >= (1L << 31)) return false;  // 32-bit buffer offsets
-  if (conv && (g.geo.cpad != 0 || g.geo.Cg % 64)) return false;
+  if (conv && (g.geo.cpad != 0 || g.geo.Cg % 64 || ((g.geo.Cg / 64) & (g.geo.Cg / 64 - 1)))) return false;
   if (out_dtype == FDDM_F32) return epi == EPI_STORE && !conv;
   if (conv) return epi == EPI_STORE || epi == EPI_GELU_ONLY;
   return epi == EPI_STORE || epi == EPI_GELU || epi == EPI_GELU_ONLY;
