@@ -181,6 +181,92 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
   }
 }
 
+// Fused single pass: a workgroup takes a slab of LNB_ROWS rows (one FiLM batch), each wave its rows as in
+// ln_bwd_kernel, while every lane keeps per-column partial sums of the parameter gradients in registers;
+// the 4 waves combine them through LDS and the slab adds them with one atomic per column and quantity.
+constexpr int LNB_ROWS = 16;
+template <int PL, typename OT>  // PL: row elements per lane (d <= 64*PL)
+__global__ void __launch_bounds__(256) ln_bwd_fused_kernel(LnBwdArgs a) {
+  __shared__ float red[4][4][64 * PL];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long d = a.d;
+  const long r0 = (long)blockIdx.x * LNB_ROWS;
+  const long b = r0 / a.rows_per_batch;
+  float pg[PL], pb[PL], psc[PL], psh[PL], gm[PL], bt[PL], fs[PL];
+#pragma unroll
+  for (int i = 0; i < PL; ++i) {
+    const long c = lane + 64L * i;
+    pg[i] = pb[i] = psc[i] = psh[i] = 0.f;
+    gm[i] = c < d ? a.gamma[c] : 0.f;
+    bt[i] = (c < d && a.beta) ? a.beta[c] : 0.f;
+    fs[i] = (c < d && a.fsc) ? a.fsc[b * d + c] : 0.f;
+  }
+  for (int rr = w; rr < LNB_ROWS; rr += 4) {
+    const long row = r0 + rr;
+    if (row >= a.N) break;
+    const float mean = a.mean[row], rstd = a.rstd[row];
+    float xh[PL], dxh[PL];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < PL; ++i) {
+      const long c = lane + 64L * i;
+      xh[i] = dxh[i] = 0.f;
+      if (c < d) {
+        const float x = (a.s[row * d + c] - mean) * rstd;
+        float go = a.dout[row * d + c];
+        if (a.fsc) {
+          psc[i] += go * (x * gm[i] + bt[i]);
+          psh[i] += go;
+          go *= 1.f + fs[i];
+        }
+        pg[i] += go * x;
+        pb[i] += go;
+        const float gx = go * gm[i];
+        xh[i] = x;
+        dxh[i] = gx;
+        s1 += gx;
+        s2 += gx * x;
+      }
+    }
+    s1 = wave_sum(s1) / (float)d;
+    s2 = wave_sum(s2) / (float)d;
+#pragma unroll
+    for (int i = 0; i < PL; ++i) {
+      const long c = lane + 64L * i;
+      if (c < d) {
+        const float ds = rstd * (dxh[i] - s1 - xh[i] * s2);
+        if (a.dres) a.dres[row * d + c] = ds;
+        if (a.dy_t) {
+          float dy = ds;
+          if (a.thr16) dy = drop_keep(a.seed, a.stream, (uint64_t)(row * d + c), a.thr16) ? dy * a.drop_scale : 0.f;
+          st<OT>((OT*)a.dy_t + row * d + c, dy);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < PL; ++i) {
+    red[0][w][lane + 64 * i] = pg[i];
+    red[1][w][lane + 64 * i] = pb[i];
+    red[2][w][lane + 64 * i] = psc[i];
+    red[3][w][lane + 64 * i] = psh[i];
+  }
+  __syncthreads();
+  for (long c = threadIdx.x; c < d; c += 256) {
+    float v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = red[q][0][c] + red[q][1][c] + red[q][2][c] + red[q][3][c];
+    if (a.dgamma) {
+      atomicAdd(a.dgamma + c, v[0]);
+      atomicAdd(a.dbeta + c, v[1]);
+    }
+    if (a.fsc) {
+      atomicAdd(a.dfsc + b * d + c, v[2]);
+      atomicAdd(a.dfsh + b * d + c, v[3]);
+    }
+  }
+}
+
 // pass 2: parameter gradients as column reductions over row slabs (no per-row atomics):
 //   dgamma[c] += sum dout'*xhat, dbeta[c] += sum dout', dfilm_scale[b][c] += sum dout*lnout,
 //   dfilm_shift[b][c] += sum dout   (dout' = dout * (1 + film_scale[b]))
@@ -270,8 +356,21 @@ FDDM_API int fddm_ln_bwd(int dy_dtype, const float* dout, const float* s, const 
     a.thr16 = (unsigned)llrintf(drop_p * 65536.f);
     a.drop_scale = 1.f / (1.f - drop_p);
   }
-  dim3 grid((unsigned)((N + 3) / 4));
   hipStream_t st_ = (hipStream_t)hs;
+  // parameter gradients wanted and every row slab inside one FiLM batch: the fused single pass
+  if ((dgamma || dfilm_scale) && (!film_scale || a.rows_per_batch % LNB_ROWS == 0) && (!dgamma || (beta && dbeta))) {
+    dim3 fg((unsigned)((N + LNB_ROWS - 1) / LNB_ROWS));
+    const bool small = d <= 512;
+    if (dy_dtype == FDDM_BF16) {
+      if (small) hipLaunchKernelGGL((ln_bwd_fused_kernel<8, bf16_t>), fg, dim3(256), 0, st_, a);
+      else hipLaunchKernelGGL((ln_bwd_fused_kernel<LN_MAXPL, bf16_t>), fg, dim3(256), 0, st_, a);
+    } else {
+      if (small) hipLaunchKernelGGL((ln_bwd_fused_kernel<8, float>), fg, dim3(256), 0, st_, a);
+      else hipLaunchKernelGGL((ln_bwd_fused_kernel<LN_MAXPL, float>), fg, dim3(256), 0, st_, a);
+    }
+    return (int)hipGetLastError();
+  }
+  dim3 grid((unsigned)((N + 3) / 4));
   if (dy_dtype == FDDM_BF16)
     hipLaunchKernelGGL((ln_bwd_kernel<bf16_t>), grid, dim3(256), 0, st_, a);
   else

@@ -135,6 +135,15 @@ def conv1d_gemm(x, W, out, *, lda, sAb, Tin, Cg, cstride, cpad, Bn, Tout, N, K, 
     return out
 
 
+def posconv_gelu(x, W, bias, out, B, S, E, G, kp):
+    """WavLM positional conv + GELU (bf16): x/out [B*S, E], W [G, Cg, kp*Cg], bias [E] f32."""
+    _chk(x.dtype == torch.bfloat16 and W.dtype == torch.bfloat16 and out.dtype == torch.bfloat16, "posconv dtypes")
+    _chk(x.is_contiguous() and W.is_contiguous() and out.is_contiguous() and bias.is_contiguous(), "posconv layout")
+    _chk(x.numel() == B * S * E and out.numel() == B * S * E and W.numel() == E * kp * (E // G), "posconv shapes")
+    call("fddm_posconv_gelu", ptr(x), ptr(W), ptr(bias), ptr(out), B, S, E, G, kp, stream())
+    return out
+
+
 def conv0_gn_gelu(wave, w, gamma, beta, out_dtype, C, K, S, eps=1e-5):
     B, nsamp = wave.shape
     T0 = (nsamp - K) // S + 1

@@ -176,8 +176,11 @@ class WavLMModel(nn.Module):
         Cg = E // G
         kp = c.num_conv_pos_embeddings
         pos = torch.empty(B * S, E, device=wave.device, dtype=cd)
-        ops.conv1d_gemm(x, P["pos"][0], pos, lda=E, sAb=S * E, Tin=S, Cg=Cg, cstride=1, cpad=kp // 2, Bn=B, Tout=S,
-                        N=Cg, K=kp * Cg, groups=G, bias=P["pos"][1], gelu=True)
+        if cd == torch.bfloat16 and Cg % 16 == 0 and Cg <= 64:
+            ops.posconv_gelu(x, P["pos"][0], P["pos"][1], pos, B, S, E, G, kp)   # whole-window LDS kernel
+        else:
+            ops.conv1d_gemm(x, P["pos"][0], pos, lda=E, sAb=S * E, Tin=S, Cg=Cg, cstride=1, cpad=kp // 2, Bn=B,
+                            Tout=S, N=Cg, K=kp * Cg, groups=G, bias=P["pos"][1], gelu=True)
         xn = torch.empty_like(x)
         ops.ln_fwd(x, pos, P["enc_ln"][0], P["enc_ln"][1], out_t=xn, eps=eps)
         x = xn

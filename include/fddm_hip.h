@@ -52,6 +52,12 @@ int fddm_conv1d_gemm(int dtype, int epi, const void* x, long lda, long sAb, long
                      long cpad, const void* W, void* out, long ldc, const float* bias, long Bn, long Tout, long N,
                      long K, int groups, void* hip_stream);
 
+/* ---- WavLM positional conv embedding + GELU (bf16): pos[b][t][g*Cg+n] = gelu(bias + sum_{tap,c}
+ *      x[b][t+tap-kp/2][g*Cg+c] W[g][n][tap*Cg+c]), t < S (the SamePad drops the conv's last frame).
+ *      x/out [B][S][E], W [G][Cg][kp*Cg], Cg = E/G a multiple of 16 (<= 64). HF modeling_wavlm.py:37-90. */
+int fddm_posconv_gelu(const void* x, const void* W, const float* bias, void* out, long B, long S, long E, int G,
+                      int kp, void* hip_stream);
+
 /* ---- conv layer 0 + GroupNorm + GELU. HF modeling_wavlm.py:723-744. ws: zeroed f64 scratch of
  *      B*(K + K*K) + B*C doubles (per-utterance Gram statistics, then the GroupNorm affine). */
 int fddm_conv0_gn_gelu(int out_dtype, const float* x, const float* w, const float* gamma, const float* beta,

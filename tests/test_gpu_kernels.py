@@ -250,6 +250,25 @@ def test_conv1d_gemm_matches_conv(dtype):
     close(out.float().view(B, S, E).transpose(1, 2), F.gelu(ref), rtol=TOL[dtype], what="grouped conv")
 
 
+@pytest.mark.parametrize("S", [37, 499])
+def test_posconv_matches_conv(S):
+    """WavLM positional conv (kernel 128, pad 64, 16 -> here 4 groups of 48, SamePad, GELU) of the bf16
+    whole-window kernel vs torch conv1d in fp64 on the same bf16 operands."""
+    o = ops()
+    B, E, G, kp = 3, 192, 4, 128
+    Cg = E // G
+    gen = torch.Generator().manual_seed(21)
+    x = torch.randn(B, S, E, generator=gen).bfloat16()
+    w = (torch.randn(E, Cg, kp, generator=gen) / math.sqrt(Cg * kp)).bfloat16()
+    bb = torch.randn(E, generator=gen)
+    ref = F.conv1d(x.double().transpose(1, 2), w.double(), bb.double(), padding=kp // 2, groups=G)[:, :, :-1]
+    ref = F.gelu(ref).transpose(1, 2)
+    Wp = w.view(G, Cg, Cg, kp).permute(0, 1, 3, 2).contiguous().to(dev)
+    out = torch.full((B * S, E), float("nan"), device=dev, dtype=torch.bfloat16)
+    o.posconv_gelu(x.to(dev).reshape(B * S, E).contiguous(), Wp, bb.to(dev), out, B, S, E, G, kp)
+    close(out.float().view(B, S, E), ref, rtol=2e-2, what="posconv")
+
+
 # ------------------------------------------------------------------------------------- attention
 def _attn_ref(q, k, v, keep, p_drop, seed, stream, gate=None, table=None):
     """q [B,H,Lq,64] ... float64 reference with the oracle's dropout mask."""
@@ -331,9 +350,12 @@ def test_attention_relbias(dtype):
 
 # ----------------------------------------------------------------------------- LN / RoPE / embed
 @pytest.mark.parametrize("film", [False, True])
-def test_layernorm_fwd_bwd(film):
+@pytest.mark.parametrize("L", [20, 32])
+def test_layernorm_fwd_bwd(film, L):
+    """L=32: FiLM rows fall in whole 16-row slabs -> the fused single-pass backward; L=20 with FiLM -> two
+    passes (row kernel + column-slab parameter kernel)."""
     o = ops()
-    B, L, d = 3, 20, 192
+    B, d = 3, 192
     N = B * L
     x = torch.randn(N, d, generator=g(40))
     y = torch.randn(N, d, generator=g(41))
