@@ -181,76 +181,107 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
   }
 }
 
-// Fused single pass: a workgroup takes a slab of LNB_ROWS rows (one FiLM batch), each wave its rows as in
-// ln_bwd_kernel, while every lane keeps per-column partial sums of the parameter gradients in registers;
-// the 4 waves combine them through LDS and the slab adds them with one atomic per column and quantity.
+// Fused single pass: a workgroup takes a slab of LNB_ROWS rows (one FiLM batch), each wave its rows with 8
+// consecutive columns per lane and chunk (32-B f32 / 16-B bf16 accesses), while every lane keeps per-column
+// partial sums of the parameter gradients in registers; the 4 waves combine them through LDS and the slab
+// adds them with one atomic per column and quantity. CH = 8-column chunks per lane (d <= 512*CH).
 constexpr int LNB_ROWS = 16;
-template <int PL, typename OT>  // PL: row elements per lane (d <= 64*PL)
+// keep bits of the 8 dropout decisions of elements e0..e0+7 (e0 % 8 == 0): two hash words
+__device__ __forceinline__ unsigned keep8(uint64_t seed, uint64_t stream, uint64_t e0, unsigned thr) {
+  unsigned k = 0;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint64_t w = mix64(seed, stream, (e0 >> 2) + h);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) k |= ((((unsigned)(w >> (16 * j))) & 0xFFFFu) >= thr ? 1u : 0u) << (4 * h + j);
+  }
+  return k;
+}
+template <int CH, typename OT>
 __global__ void __launch_bounds__(256) ln_bwd_fused_kernel(LnBwdArgs a) {
-  __shared__ float red[4][4][64 * PL];
+  __shared__ float red[4][4][512 * CH];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const long d = a.d;
+  const long d = a.d, nch = d / 8;
   const long r0 = (long)blockIdx.x * LNB_ROWS;
   const long b = r0 / a.rows_per_batch;
-  float pg[PL], pb[PL], psc[PL], psh[PL], gm[PL], bt[PL], fs[PL];
+  float pg[CH][8], pb[CH][8], psc[CH][8], psh[CH][8], gm[CH][8], bt[CH][8], fs[CH][8];
 #pragma unroll
-  for (int i = 0; i < PL; ++i) {
-    const long c = lane + 64L * i;
-    pg[i] = pb[i] = psc[i] = psh[i] = 0.f;
-    gm[i] = c < d ? a.gamma[c] : 0.f;
-    bt[i] = (c < d && a.beta) ? a.beta[c] : 0.f;
-    fs[i] = (c < d && a.fsc) ? a.fsc[b * d + c] : 0.f;
+  for (int i = 0; i < CH; ++i) {
+    const long ch = lane + 64L * i;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) pg[i][e] = pb[i][e] = psc[i][e] = psh[i][e] = gm[i][e] = bt[i][e] = fs[i][e] = 0.f;
+    if (ch < nch) {
+      ld8<float>(a.gamma + ch * 8, gm[i]);
+      if (a.beta) ld8<float>(a.beta + ch * 8, bt[i]);
+      if (a.fsc) ld8<float>(a.fsc + b * d + ch * 8, fs[i]);
+    }
   }
+#pragma unroll 2
   for (int rr = w; rr < LNB_ROWS; rr += 4) {
     const long row = r0 + rr;
     if (row >= a.N) break;
     const float mean = a.mean[row], rstd = a.rstd[row];
-    float xh[PL], dxh[PL];
+    float xh[CH][8], dxh[CH][8];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int i = 0; i < PL; ++i) {
-      const long c = lane + 64L * i;
-      xh[i] = dxh[i] = 0.f;
-      if (c < d) {
-        const float x = (a.s[row * d + c] - mean) * rstd;
-        float go = a.dout[row * d + c];
-        if (a.fsc) {
-          psc[i] += go * (x * gm[i] + bt[i]);
-          psh[i] += go;
-          go *= 1.f + fs[i];
+    for (int i = 0; i < CH; ++i) {
+      const long ch = lane + 64L * i;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) xh[i][e] = dxh[i][e] = 0.f;
+      if (ch < nch) {
+        float sv[8], go[8];
+        ld8<float>(a.s + row * d + ch * 8, sv);
+        ld8<float>(a.dout + row * d + ch * 8, go);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float x = (sv[e] - mean) * rstd;
+          float g = go[e];
+          if (a.fsc) {
+            psc[i][e] += g * (x * gm[i][e] + bt[i][e]);
+            psh[i][e] += g;
+            g *= 1.f + fs[i][e];
+          }
+          pg[i][e] += g * x;
+          pb[i][e] += g;
+          const float gx = g * gm[i][e];
+          xh[i][e] = x;
+          dxh[i][e] = gx;
+          s1 += gx;
+          s2 += gx * x;
         }
-        pg[i] += go * x;
-        pb[i] += go;
-        const float gx = go * gm[i];
-        xh[i] = x;
-        dxh[i] = gx;
-        s1 += gx;
-        s2 += gx * x;
       }
     }
     s1 = wave_sum(s1) / (float)d;
     s2 = wave_sum(s2) / (float)d;
 #pragma unroll
-    for (int i = 0; i < PL; ++i) {
-      const long c = lane + 64L * i;
-      if (c < d) {
-        const float ds = rstd * (dxh[i] - s1 - xh[i] * s2);
-        if (a.dres) a.dres[row * d + c] = ds;
+    for (int i = 0; i < CH; ++i) {
+      const long ch = lane + 64L * i;
+      if (ch < nch) {
+        float ds[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ds[e] = rstd * (dxh[i][e] - s1 - xh[i][e] * s2);
+        if (a.dres) st8<float>(a.dres + row * d + ch * 8, ds);
         if (a.dy_t) {
-          float dy = ds;
-          if (a.thr16) dy = drop_keep(a.seed, a.stream, (uint64_t)(row * d + c), a.thr16) ? dy * a.drop_scale : 0.f;
-          st<OT>((OT*)a.dy_t + row * d + c, dy);
+          if (a.thr16) {
+            const unsigned k = keep8(a.seed, a.stream, (uint64_t)(row * d + ch * 8), a.thr16);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) ds[e] = ((k >> e) & 1u) ? ds[e] * a.drop_scale : 0.f;
+          }
+          st8<OT>((OT*)a.dy_t + row * d + ch * 8, ds);
         }
       }
     }
   }
 #pragma unroll
-  for (int i = 0; i < PL; ++i) {
-    red[0][w][lane + 64 * i] = pg[i];
-    red[1][w][lane + 64 * i] = pb[i];
-    red[2][w][lane + 64 * i] = psc[i];
-    red[3][w][lane + 64 * i] = psh[i];
-  }
+  for (int i = 0; i < CH; ++i)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = (lane + 64 * i) * 8 + e;
+      red[0][w][c] = pg[i][e];
+      red[1][w][c] = pb[i][e];
+      red[2][w][c] = psc[i][e];
+      red[3][w][c] = psh[i][e];
+    }
   __syncthreads();
   for (long c = threadIdx.x; c < d; c += 256) {
     float v[4];
@@ -358,15 +389,19 @@ FDDM_API int fddm_ln_bwd(int dy_dtype, const float* dout, const float* s, const 
   }
   hipStream_t st_ = (hipStream_t)hs;
   // parameter gradients wanted and every row slab inside one FiLM batch: the fused single pass
-  if ((dgamma || dfilm_scale) && (!film_scale || a.rows_per_batch % LNB_ROWS == 0) && (!dgamma || (beta && dbeta))) {
+  const bool vec_ok = d % 8 == 0 && d <= 1024 &&
+                      !(((uintptr_t)dout | (uintptr_t)s | (uintptr_t)gamma | (uintptr_t)beta | (uintptr_t)film_scale |
+                         (uintptr_t)dres | (uintptr_t)dy_t) & 15);
+  if ((dgamma || dfilm_scale) && (!film_scale || a.rows_per_batch % LNB_ROWS == 0) && (!dgamma || (beta && dbeta)) &&
+      vec_ok) {
     dim3 fg((unsigned)((N + LNB_ROWS - 1) / LNB_ROWS));
     const bool small = d <= 512;
     if (dy_dtype == FDDM_BF16) {
-      if (small) hipLaunchKernelGGL((ln_bwd_fused_kernel<8, bf16_t>), fg, dim3(256), 0, st_, a);
-      else hipLaunchKernelGGL((ln_bwd_fused_kernel<LN_MAXPL, bf16_t>), fg, dim3(256), 0, st_, a);
+      if (small) hipLaunchKernelGGL((ln_bwd_fused_kernel<1, bf16_t>), fg, dim3(256), 0, st_, a);
+      else hipLaunchKernelGGL((ln_bwd_fused_kernel<2, bf16_t>), fg, dim3(256), 0, st_, a);
     } else {
-      if (small) hipLaunchKernelGGL((ln_bwd_fused_kernel<8, float>), fg, dim3(256), 0, st_, a);
-      else hipLaunchKernelGGL((ln_bwd_fused_kernel<LN_MAXPL, float>), fg, dim3(256), 0, st_, a);
+      if (small) hipLaunchKernelGGL((ln_bwd_fused_kernel<1, float>), fg, dim3(256), 0, st_, a);
+      else hipLaunchKernelGGL((ln_bwd_fused_kernel<2, float>), fg, dim3(256), 0, st_, a);
     }
     return (int)hipGetLastError();
   }

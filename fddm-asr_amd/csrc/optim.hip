@@ -31,13 +31,22 @@ __global__ void __launch_bounds__(256) sumsq_kernel(MTTable t, float* total) {
   const long ti = t.chunk_tensor[ci], s0 = t.chunk_start[ci];
   const long n = min(MT_CHUNK, t.numel[ti] - s0);
   const float* g = t.g[ti] + s0;
-  float acc = 0.f;
-  for (long i = threadIdx.x; i < n; i += 256) {
-    const float x = g[i];
-    acc += x * x;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  long i = 0;
+  if ((((uintptr_t)g) & 15) == 0) {  // 16-B loads, 4 independent accumulators
+    const long n4 = n / 4;
+    for (long j = threadIdx.x; j < n4; j += 256) {
+      const float4 x = ((const float4*)g)[j];
+      acc[0] += x.x * x.x;
+      acc[1] += x.y * x.y;
+      acc[2] += x.z * x.z;
+      acc[3] += x.w * x.w;
+    }
+    i = n4 * 4;
   }
-  acc = block_sum(acc, red);
-  if (threadIdx.x == 0) atomicAdd(total, acc);
+  for (long j = i + threadIdx.x; j < n; j += 256) acc[0] += g[j] * g[j];
+  float v = block_sum((acc[0] + acc[1]) + (acc[2] + acc[3]), red);
+  if (threadIdx.x == 0) atomicAdd(total, v);
 }
 
 __global__ void __launch_bounds__(256) adamw_kernel(MTTable t, const float* total, float max_norm, float lr_wd, float b1,
@@ -56,13 +65,35 @@ __global__ void __launch_bounds__(256) adamw_kernel(MTTable t, const float* tota
   float* v = t.v[ti] + s0;
   bf16_t* pb = t.pbf[ti] ? t.pbf[ti] + s0 : nullptr;
   const float ss = t.step_size[ti], bc2s = t.bc2_sqrt[ti];
-  for (long i = threadIdx.x; i < n; i += 256) {
-    const float gg = g[i] * coef;
-    float pp = p[i] * (1.f - lr_wd);
-    const float mm = m[i] + (1.f - b1) * (gg - m[i]);
-    const float vv = v[i] * b2 + (1.f - b2) * gg * gg;
-    const float denom = sqrtf(vv) / bc2s + eps;
-    pp = pp - ss * (mm / denom);
+  auto upd = [&](float gg, float& pp, float& mm, float& vv) {
+    gg *= coef;
+    pp *= 1.f - lr_wd;
+    mm += (1.f - b1) * (gg - mm);
+    vv = vv * b2 + (1.f - b2) * gg * gg;
+    pp -= ss * (mm / (sqrtf(vv) / bc2s + eps));
+  };
+  long i0 = 0;
+  const bool vec = ((((uintptr_t)p) | ((uintptr_t)g) | ((uintptr_t)m) | ((uintptr_t)v)) & 15) == 0 &&
+                   (pb == nullptr || (((uintptr_t)pb) & 7) == 0);
+  if (vec) {  // 4 elements per thread and iteration: 16-B loads/stores, 8-B bf16 copy
+    const long n4 = n / 4;
+    for (long j = threadIdx.x; j < n4; j += 256) {
+      const float4 gg = ((const float4*)g)[j];
+      float4 pp = ((float4*)p)[j], mm = ((float4*)m)[j], vv = ((float4*)v)[j];
+      upd(gg.x, pp.x, mm.x, vv.x);
+      upd(gg.y, pp.y, mm.y, vv.y);
+      upd(gg.z, pp.z, mm.z, vv.z);
+      upd(gg.w, pp.w, mm.w, vv.w);
+      ((float4*)p)[j] = pp;
+      ((float4*)m)[j] = mm;
+      ((float4*)v)[j] = vv;
+      if (pb) ((uint2*)pb)[j] = make_uint2(pk_bf16(pp.x, pp.y), pk_bf16(pp.z, pp.w));
+    }
+    i0 = n4 * 4;
+  }
+  for (long i = i0 + threadIdx.x; i < n; i += 256) {
+    float pp = p[i], mm = m[i], vv = v[i];
+    upd(g[i], pp, mm, vv);
     p[i] = pp;
     m[i] = mm;
     v[i] = vv;
