@@ -25,7 +25,7 @@
 // phases after its DMA. Every vmcnt is exact: the wave counts each vector-memory instruction it issues
 // (DMA, bias loads, stores — all explicit, none compiler-generated) and waits for "issued since X".
 // The MFMAs compute C^T fragments (operands swapped) so a lane owns 4 consecutive columns of one row: the
-// epilogue writes 8-B (bf16) / 16-B (f32) bounds-checked buffer stores straight from the accumulators.
+// epilogue writes 16-B buffer stores straight from the accumulators (bf16: lane pairs trade halves first).
 #include "gemm.h"
 #include <type_traits>
 
@@ -67,11 +67,28 @@ template <int N> __device__ __forceinline__ void vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N < 63 ? N : 63) : "memory");
 }
 
+// 16-B buffer store as inline asm with the wait state gfx950 needs before the store-data VGPRs may be
+// rewritten (a wide store reads its data late: the builtin let hipcc overwrite them in the next instruction,
+// corrupting the last lanes' data)
+__device__ __forceinline__ void store16(const u32x4_t& d, const i32x4_t& srd, int voff, int soff) {
+  asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 1" ::"v"(d), "v"(voff), "s"(srd), "s"(soff)
+               : "memory");
+}
+__device__ __forceinline__ i32x4_t make_srd(const void* base) {
+  const unsigned long a = (unsigned long)base;
+  return i32x4_t{(int)(unsigned)a, (int)(unsigned)(a >> 32), 0x7fffffff, (int)SRD_W3};
+}
+
 __device__ __forceinline__ void bar() {
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
 }
+
+#ifdef G256_STAMPS
+// diagnostic build only: s_memtime at the start of each K-tile of each workgroup (fddm_gemm256_stamps reads it)
+__device__ unsigned long long g256_stamps[256 * G256_STAMPS];
+#endif
 
 template <int EPI, typename OT, bool CONV>
 __global__ void __launch_bounds__(512) gemm256_kernel(GemmArgs g) {
@@ -186,56 +203,79 @@ __global__ void __launch_bounds__(512) gemm256_kernel(GemmArgs g) {
 
   // ---------------------------------------------------------------- stores
   // buffer stores: lane offset fixed, tile origin and block offset in soffset
-  const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(g.C, 0, 0x7fffffff, SRD_W3);
-  const __amdgpu_buffer_rsrc_t rc2 =
-      __builtin_amdgcn_make_buffer_rsrc(EPI == EPI_GELU ? g.C2 : g.C, 0, 0x7fffffff, SRD_W3);
+  const i32x4_t rc = make_srd(g.C);
+  const i32x4_t rc2 = make_srd(EPI == EPI_GELU ? g.C2 : g.C);
   constexpr int ESZ = (int)sizeof(OT);
-  constexpr int SPQ = EPI == EPI_GELU ? 16 : 8;  // store instructions per quadrant
+  // store instructions per quadrant: f32 8 (dwordx4 per block); bf16 4 per output (paired blocks)
+  constexpr int SPQ = sizeof(OT) == 4 ? 8 : (EPI == EPI_GELU ? 8 : 4);
   const int vst = ((wr * 128 + fr) * ldc + wc * 64 + 4 * fg) * ESZ;
+  const int vst2 = vst + ((fg & 1) ? 12 * ESZ : 0);
 
   u32x4_t af[4][2], b0[2][2], b1[2][2];
   f32x4_t acc[8][4];
 
   // quadrant q of the finished tile at (em0, en0): blocks i in 4*(q>>1).., j in 2*(q&1)..; then (reseed)
   // seed it with the bias of the tile that follows
+  // bf16: the two lanes 16 apart (fg, fg^1) trade packed halves (v_permlane16_swap, no LDS) so that each lane
+  // stores 8 consecutive
+  // columns (16 B) — one dwordx4 store per row block and column pair instead of two dwordx2 (store issue, not
+  // bandwidth, bounds the epilogue); odd-fg lanes write the second block of the pair
   auto epi_quadrant = [&](auto qc, int em0, int en0, bool reseed) {
     constexpr int q = decltype(qc)::value, ib = (q >> 1) * 4, jb = (q & 1) * 2;
     f32x4_t bq[2];
     if (reseed) bias_pair(jb, bq[0], bq[1]);
+    const bool odd = fg & 1;
+    auto emit = [&](const f32x4_t& a, const f32x4_t& b, const i32x4_t& r, int so) {
+      const u32x2_t pa = {pk_bf16(a[0], a[1]), pk_bf16(a[2], a[3])};
+      const u32x2_t pb = {pk_bf16(b[0], b[1]), pk_bf16(b[2], b[3])};
+      const u32x2_t x = odd ? pa : pb;
+      // v_permlane16_swap(x, x): odd 16-lane rows get x of lane-16 in [0], even rows x of lane+16 in [1]
+      const auto s0 = __builtin_amdgcn_permlane16_swap(x[0], x[0], false, false);
+      const auto s1 = __builtin_amdgcn_permlane16_swap(x[1], x[1], false, false);
+      const u32x2_t y = odd ? u32x2_t{s0[0], s1[0]} : u32x2_t{s0[1], s1[1]};
+      const u32x4_t d = odd ? u32x4_t{y[0], y[1], pb[0], pb[1]} : u32x4_t{pa[0], pa[1], y[0], y[1]};
+      store16(d, r, vst2, so);
+    };
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i) {
+      const int so = ((em0 + (ib + i) * 16) * ldc + en0 + jb * 16) * ESZ;
+      if constexpr (sizeof(OT) == 4) {
+        store16(__builtin_bit_cast(u32x4_t, acc[ib + i][jb]), rc, vst, so);
+        store16(__builtin_bit_cast(u32x4_t, acc[ib + i][jb + 1]), rc, vst, so + 16 * ESZ);
+      } else {
+        f32x4_t v[2] = {acc[ib + i][jb], acc[ib + i][jb + 1]};
+        if constexpr (EPI == EPI_GELU) {
+          emit(v[0], v[1], rc, so);
+          const unsigned thr = g.thr16;
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int so = ((em0 + (ib + i) * 16) * ldc + en0 + (jb + j) * 16) * ESZ;
-        f32x4_t v = acc[ib + i][jb + j];
-        if constexpr (sizeof(OT) == 4) {
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rc, vst, so, 0);
-        } else {
-          if constexpr (EPI == EPI_GELU) {
-            __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3])}, rc, vst, so, 0);
-            const unsigned thr = g.thr16;
+          for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              float a = gelu_f(v[e]);
+              float a = gelu_f(v[j][e]);
               if (thr) {
                 const unsigned m = (unsigned)(em0 + wr * 128 + (ib + i) * 16 + fr);
                 const unsigned n = (unsigned)(en0 + wc * 64 + (jb + j) * 16 + 4 * fg + e);
                 a = drop_keep(g.seed, g.stream, (uint64_t)m * (uint64_t)Nc + n, thr) ? a * g.drop_scale : 0.f;
               }
-              v[e] = a;
+              v[j][e] = a;
             }
-            __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3])}, rc2, vst, so, 0);
-          } else {
-            if constexpr (EPI == EPI_GELU_ONLY) {
+          emit(v[0], v[1], rc2, so);
+        } else {
+          if constexpr (EPI == EPI_GELU_ONLY) {
 #pragma unroll
-              for (int e = 0; e < 4; ++e) v[e] = gelu_f(v[e]);
-            }
-            __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3])}, rc, vst, so, 0);
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[j][e] = gelu_f(v[j][e]);
           }
+          emit(v[0], v[1], rc, so);
         }
-        if (reseed) acc[ib + i][jb + j] = bq[j];
-        __builtin_amdgcn_sched_barrier(0);  // one block at a time: bounds the epilogue's live registers
       }
+      if (reseed) {
+        acc[ib + i][jb] = bq[0];
+        acc[ib + i][jb + 1] = bq[1];
+      }
+      __builtin_amdgcn_sched_barrier(0);  // one row block at a time: bounds the epilogue's live registers
+    }
   };
 
   // fragment addresses: swz_kc(base16 + i*16 + fr, s*4 + fg) = (base16 + i*16)*128 + swz_kc(fr, s*4 + fg) for a
@@ -380,6 +420,9 @@ __global__ void __launch_bounds__(512) gemm256_kernel(GemmArgs g) {
   };
   for (int T = 0; T < NT; ++T) {
     const bool later = ti > 0;
+#ifdef G256_STAMPS
+    if (tid == 0 && T < G256_STAMPS) g256_stamps[blockIdx.x * G256_STAMPS + T] = __builtin_amdgcn_s_memtime();
+#endif
     ktile(T, later ? (kt == 0 ? 1 : kt == 1 ? 2 : 0) : 0);
     if (kt == nk - 1) {
       next_tile();
@@ -451,3 +494,10 @@ int gemm256_launch(const GemmArgs& g, int epi, int out_dtype, bool conv, hipStre
 }
 
 }  // namespace fddm
+
+#ifdef G256_STAMPS
+FDDM_API int fddm_gemm256_stamps(unsigned long long* host, long n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(fddm::g256::g256_stamps), n * sizeof(unsigned long long), 0,
+                                  hipMemcpyDeviceToHost);
+}
+#endif
