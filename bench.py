@@ -192,7 +192,7 @@ def main():
                                    "dropout 0.1, n_step_fd=4",
                        "global_batch": args.batch * world, "seq_len": args.seq_len, "audio_seconds": args.seconds,
                        "parallelism": f"dp{world}"},
-            "roofline": {"bound": "mfma", "kernel": "WavLM conv layer 1 implicit GEMM (gemm_big_kernel, GELU)",
+            "roofline": {"bound": "mfma", "kernel": "WavLM conv layer 1 implicit GEMM (gemm256_kernel: persistent 256x256, GELU)",
                          "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
                          "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_unit": "B/launch",
                          "traffic_source": traffic_src, "avg_ms": round(kms, 4),

@@ -3,8 +3,8 @@
 
 FETCH_SIZE is in KB and, on gfx950, reports half the bytes of wide coalesced streaming reads
 (MI355X_MICROARCH.md § HBM): traffic = 2 * FETCH_SIZE + WRITE_SIZE (KB -> bytes).
-The dominant launch (WavLM conv layer 1) shares its kernel symbol with conv layers 2-6; it is the
-dispatch of that symbol with the largest grid.
+The dominant launch (WavLM conv layer 1) shares its kernel symbol with conv layers 2-6 (and the persistent
+kernel's grid is one workgroup per CU for all of them); it is the dispatch of that symbol that runs longest.
 
   python tools/pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> <kernel substring> <out.json> <batch>
 """
@@ -22,6 +22,10 @@ def load(path, counter):
         did = r.get("Dispatch_Id") or r.get("Correlation_Id")
         rows[did]["name"] = r.get("Kernel_Name", "")
         rows[did]["grid"] = int(float(r.get("Grid_Size", 0) or 0))
+        try:
+            rows[did]["dur"] = int(r.get("End_Timestamp", 0)) - int(r.get("Start_Timestamp", 0))
+        except ValueError:
+            rows[did]["dur"] = 0
         rows[did][counter] = rows[did].get(counter, 0.0) + float(r["Counter_Value"])
     return rows
 
@@ -30,9 +34,11 @@ def pick(rows, sub, counter):
     sel = [v for v in rows.values() if sub in v["name"] and counter in v]
     if not sel:
         return None, 0, 0
-    gmax = max(v["grid"] for v in sel)
-    vals = [v[counter] for v in sel if v["grid"] == gmax]
-    return sum(vals) / len(vals), len(vals), gmax
+    # the longest dispatches of the symbol (within 20 % of the longest): conv layer 1, once per step
+    dmax = max(v.get("dur", 0) for v in sel)
+    pick_ = [v for v in sel if v.get("dur", 0) >= 0.8 * dmax] if dmax > 0 else sel
+    vals = [v[counter] for v in pick_]
+    return sum(vals) / len(vals), len(vals), pick_[0]["grid"]
 
 
 def main():
