@@ -35,4 +35,20 @@ int gemm256_launch(const GemmArgs& g, int epi, int out_dtype, bool conv, hipStre
 bool gemm256_ok(const GemmArgs& g, int epi, int out_dtype, bool conv);
 long gemm256_tiles(long M, long N);
 
+// 128x128 LDS-DMA ring GEMM (gemm128.hip) for outputs with too few 256x256 tiles. Layouts: A KC + B KC (STORE
+// bf16/f32, GELU, GELU_ONLY, DGELU, ACC_F32), A KC + B MC (STORE bf16/f32, DGELU, ACC_F32), A MC + B MC (ACC_F32, with
+// colsum). nz > 1: split-K slices of g.ksplit (ACC_F32 only, f32 atomics).
+bool gemm128_ok(const GemmArgs& g, bool akc, bool bkc, int epi, int out_dtype);
+int gemm128_launch(const GemmArgs& g, bool akc, bool bkc, int epi, int out_dtype, int nz, hipStream_t s);
+long gemm128_tiles(long M, long N);
+constexpr int G128_GROUP_MAX = 12;
+struct G128Group {
+  int np;
+  int start[G128_GROUP_MAX + 1];
+  int tn[G128_GROUP_MAX], tm[G128_GROUP_MAX], nz[G128_GROUP_MAX];
+  GemmArgs g[G128_GROUP_MAX];
+};
+// A MC + B MC, ACC_F32 (weight gradients): `total` workgroups over the problems of ga
+int gemm128_grouped_dw(const G128Group& ga, int total, hipStream_t s);
+
 }  // namespace fddm

@@ -23,6 +23,12 @@
 // A may be stored in f32 while the MFMA runs in bf16 (TA=float, T=bf16): converted while staging.
 #include "gemm.h"
 #include <algorithm>
+#include <functional>
+#include <vector>
+#include <map>
+#include <mutex>
+#include <queue>
+#include <algorithm>
 #include <cstdlib>
 
 namespace fddm {
@@ -654,10 +660,12 @@ static int gemm_path() {
   if (v[0] == 's') return 2;
   if (v[0] == 'b') return 1;
   if (v[0] == '2') return 3;
+  if (v[0] == '1') return 4;  // "128": the 128x128 LDS-DMA ring kernel wherever its preconditions hold
   return 0;
 }
-static bool big_enabled() { return gemm_path() != 2; }
+static bool big_enabled() { return gemm_path() != 2 && gemm_path() != 4; }
 static bool g256_enabled() { return gemm_path() == 0 || gemm_path() == 3; }
+static bool g128_enabled() { return gemm_path() == 0 || gemm_path() == 4; }
 // the persistent 256x256 kernel wins from about half a round of tiles up (measured at the train step's shapes:
 // 189 tiles of 15968x768x3072 still beat the 256x128 kernel by 1.3x; 64 tiles of 8192x512x512 lose)
 static bool prefer_256(long M, long N) {
@@ -704,6 +712,30 @@ FDDM_API int fddm_gemm(int dtype, int a_dtype, int a_kc, int b_kc, int epi, int 
     g.drop_scale = 1.f / (1.f - drop_p);
   }
   hipStream_t s = (hipStream_t)hip_stream;
+  // bf16 operands: the 256x256 kernel for outputs of >= half a round of its tiles (NT only), else the 128x128
+  // LDS-DMA ring kernel (NT, NN with W as stored, TN weight gradients)
+  if (dtype == FDDM_BF16 && a_dtype == FDDM_BF16 && Mi >= M && g128_enabled() &&
+      !(a_kc && b_kc && !colsum && g256_enabled() && gemm256_ok(g, epi, out_dtype, false) && prefer_256(M, N)) &&
+      gemm128_ok(g, a_kc, b_kc, epi, out_dtype) && (!colsum || !a_kc)) {
+    int nz128 = 1;
+    const long t128 = gemm128_tiles(M, N);
+    // split-K only for long reductions: a split slice adds its 128x128 tile with 64 KB of f32 atomics
+    if (out_dtype == FDDM_F32 && (epi == EPI_STORE || epi == EPI_ACC_F32) && t128 < 192 && K >= 4096) {
+      long want = (256 + t128 - 1) / t128;
+      nz128 = (int)std::max(1L, std::min(want, K / 2048));
+      if (nz128 > 1) {
+        long ks = ((K + nz128 - 1) / nz128 + 63) / 64 * 64;
+        nz128 = (int)((K + ks - 1) / ks);
+        g.ksplit = ks;
+        if (epi == EPI_STORE) {
+          hipError_t e = hipMemset2DAsync(C, ldc * sizeof(float), 0, N * sizeof(float), M, s);
+          if (e != hipSuccess) return (int)e;
+          epi = EPI_ACC_F32;
+        }
+      }
+    }
+    return gemm128_launch(g, a_kc, b_kc, epi, out_dtype, nz128, s);
+  }
   // split-K when the output has too few 128x128 tiles to fill 256 CUs (weight gradients, small N):
   // f32 output only, atomically accumulated; STORE becomes memset + accumulate.
   int nz = 1;
@@ -780,11 +812,117 @@ FDDM_API int fddm_conv1d_gemm(int dtype, int epi, const void* x, long lda, long 
 // bf16 and M/N-contiguous), with the bias gradient db_p[m] += sum_k dY_p[k][m] fused (db_p may be null).
 // One launch for up to 12 problems; a problem's K is split so that every workgroup reduces about
 // `kchunk` tokens (f32 atomics between splits).
+// Split choice for the 128x128 grouped launch: coordinate descent over each problem's split count
+// (1, 2, 4, 8, 16) on the longest-processing-time schedule of all units over the CUs. Unit cost in K-tiles:
+// its K-tiles + 6 (prologue / epilogue) + for split units the f32 atomics of its 128x128 tile (~20 K-tile
+// times) or else a read-modify-write (2). Units run longest first (problem order on the host).
+// The decision depends only on the shapes: cached per (tiles, K-tiles) signature.
+static void g128_balance(int n, const long* tiles, const long* ktiles, int* nz, int ncu) {
+  static std::mutex mu;
+  static std::map<std::vector<long>, std::vector<int>> cache;
+  std::vector<long> key(tiles, tiles + n);
+  key.insert(key.end(), ktiles, ktiles + n);
+  key.push_back(ncu);
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) {
+      std::copy(it->second.begin(), it->second.end(), nz);
+      return;
+    }
+  }
+  auto makespan = [&](const int* z) {
+    std::vector<double> units;
+    for (int p = 0; p < n; ++p)
+      for (long u = 0; u < tiles[p] * z[p]; ++u)
+        units.push_back((double)((ktiles[p] + z[p] - 1) / z[p]) + 6.0 + (z[p] > 1 ? 20.0 : 2.0));
+    std::sort(units.begin(), units.end(), std::greater<double>());
+    std::priority_queue<double, std::vector<double>, std::greater<double>> cu;
+    for (int c = 0; c < ncu; ++c) cu.push(0.0);
+    double mk = 0.0;
+    for (double u : units) {
+      const double t = cu.top() + u;
+      cu.pop();
+      cu.push(t);
+      mk = std::max(mk, t);
+    }
+    return mk;
+  };
+  for (int p = 0; p < n; ++p) nz[p] = 1;
+  double best = makespan(nz);
+  for (int rnd = 0; rnd < 3; ++rnd) {
+    bool changed = false;
+    for (int p = 0; p < n; ++p)
+      for (int c = 1; c <= 16; c *= 2) {
+        if ((ktiles[p] + c - 1) / c < 8) break;
+        const int old = nz[p];
+        nz[p] = c;
+        const double m = makespan(nz);
+        if (m < best - 1e-9) {
+          best = m;
+          changed = true;
+        } else {
+          nz[p] = old;
+        }
+      }
+    if (!changed) break;
+  }
+  std::lock_guard<std::mutex> lk(mu);
+  cache[key] = std::vector<int>(nz, nz + n);
+}
+
+static int g128_ncu() {
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        ncu <= 0)
+      ncu = 256;
+  }
+  return ncu;
+}
+
 FDDM_API int fddm_gemm_dw_grouped(int n, const void* const* dy, const long* ldy, const void* const* x, const long* ldx,
                                   float* const* dw, const long* lddw, float* const* db, const long* M, const long* N,
                                   const long* K, long kchunk, void* hip_stream) {
   if (n <= 0) return 0;
-  if (n > GROUP_MAX) return (int)hipErrorInvalidValue;
+  if (n > GROUP_MAX || n > G128_GROUP_MAX) return (int)hipErrorInvalidValue;
+  bool g128 = g128_enabled() && kchunk <= 0;
+  for (int p = 0; p < n && g128; ++p) {
+    GemmArgs g{dy[p], ldy[p], 1L << 62, 0, x[p], ldx[p], dw[p], lddw[p], nullptr, nullptr, 1.f, M[p], N[p], K[p],
+               0, 0, 0u, 1.f, ConvGeo{1, 0, 0, 0}, 0, 0, 0, 0, K[p], db[p]};
+    g128 = gemm128_ok(g, false, false, EPI_ACC_F32, FDDM_F32);
+  }
+  if (g128) {
+    // problems ordered by decreasing unit length, so the hardware's in-order dispatch approximates LPT
+    long tiles[G128_GROUP_MAX], kt[G128_GROUP_MAX];
+    int nz[G128_GROUP_MAX], ord[G128_GROUP_MAX];
+    for (int p = 0; p < n; ++p) {
+      tiles[p] = gemm128_tiles(M[p], N[p]);
+      kt[p] = (K[p] + 63) / 64;
+      ord[p] = p;
+    }
+    g128_balance(n, tiles, kt, nz, g128_ncu());
+    std::sort(ord, ord + n, [&](int a, int b) { return (kt[a] + nz[a] - 1) / nz[a] > (kt[b] + nz[b] - 1) / nz[b]; });
+    G128Group ga{};
+    ga.np = n;
+    int total = 0;
+    for (int i = 0; i < n; ++i) {
+      const int p = ord[i];
+      GemmArgs g{dy[p], ldy[p], 1L << 62, 0, x[p], ldx[p], dw[p], lddw[p], nullptr, nullptr, 1.f, M[p], N[p], K[p],
+                 0, 0, 0u, 1.f, ConvGeo{1, 0, 0, 0}, 0, 0, 0, 0, K[p], db[p]};
+      if (nz[p] > 1) g.ksplit = ((K[p] + nz[p] - 1) / nz[p] + 63) / 64 * 64;
+      ga.g[i] = g;
+      ga.nz[i] = nz[p] > 1 ? (int)((K[p] + g.ksplit - 1) / g.ksplit) : 1;
+      ga.tn[i] = (int)((N[p] + 127) / 128);
+      ga.tm[i] = (int)((M[p] + 127) / 128);
+      ga.start[i] = total;
+      total += ga.tn[i] * ga.tm[i] * ga.nz[i];
+    }
+    ga.start[n] = total;
+    return gemm128_grouped_dw(ga, total, (hipStream_t)hip_stream);
+  }
+  if (kchunk <= 0) kchunk = 8192;
   GroupArgs ga{};
   ga.np = n;
   int total = 0;

@@ -96,9 +96,11 @@ def linear_dw(dy2d, x2d, out=None, accumulate=False, db=None):
                 ldc=out.stride(0), epi=EPI_ACC if accumulate else EPI_STORE, colsum=db)
 
 
-def linear_dw_grouped(jobs, kchunk=8192):
+def linear_dw_grouped(jobs, kchunk=0):
     """One launch for several weight-gradient GEMMs, all accumulating: for each (dy [K,M], x [K,N], dW [M,N] f32,
-    db [M] f32 or None): dW += dy^T x, db += sum_k dy. dy/x bf16 with unit inner stride."""
+    db [M] f32 or None): dW += dy^T x, db += sum_k dy. dy/x bf16 with unit inner stride.
+    kchunk 0: the library balances split-K over the CUs (128x128 LDS-DMA kernel); kchunk > 0: every workgroup
+    of the 128x128 register-staged kernel reduces about kchunk tokens."""
     import ctypes
     jobs = [j for j in jobs if j[0].shape[0] > 0]
     for i in range(0, len(jobs), 12):

@@ -106,7 +106,7 @@ def test_weight_grad_gemm_with_fused_bias_grad(dtype, M, N, K):
     close(db, dy.to(dtype).double().sum(0), rtol=1e-5 if dtype == torch.float32 else 1e-3, what="db")
 
 
-@pytest.mark.parametrize("path", ["256", "big"])
+@pytest.mark.parametrize("path", ["256", "big", "128"])
 @pytest.mark.parametrize("M,N,K,epi,odt", [(8192, 2048, 512, 0, "bf16"), (15968, 768, 3072, 1, "bf16"),
                                            (8200, 2056, 768, 3, "bf16"), (8192, 8000, 512, 0, "f32"),
                                            (300, 264, 64, 0, "bf16"), (1000, 3072, 192, 1, "bf16")])
@@ -173,6 +173,81 @@ def test_grouped_weight_grads_match_torch():
     close(dW[192:256, 64:128], dW0[192:256, 64:128].double() + refs[3][0], rtol=1e-4, what="dW job3")
     close(db[:64], db0[:64].double() + refs[0][1], rtol=1e-4, what="db0")
     close(db[256:384], db0[256:384].double() + refs[2][1], rtol=1e-4, what="db2")
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 520, 512), (8192, 512, 2048), (128, 128, 64)])
+def test_gemm128_input_grad_layout(M, N, K, monkeypatch):
+    """128x128 LDS-DMA kernel, A K-contiguous x B as stored [K][N] (dX = dY W): f32 store / accumulate,
+    bf16 store, dGELU+dropout epilogue — against torch in fp64 on the same bf16 operands."""
+    o = ops()
+    monkeypatch.setenv("FDDM_GEMM_PATH", "128")
+    gen = torch.Generator(device=dev).manual_seed(21)
+    dy = torch.randn(M, K, device=dev, generator=gen).bfloat16()
+    W = (torch.randn(K, N, device=dev, generator=gen) / math.sqrt(K)).bfloat16()
+    ref = dy.double() @ W.double()
+    out = torch.full((M, N), float("nan"), device=dev)
+    o.linear_dx(dy, W, out=out)
+    close(out, ref, rtol=1e-4, what="dx f32")
+    base = torch.randn(M, N, device=dev, generator=gen)
+    acc = base.clone()
+    o.linear_dx(dy, W, out=acc, accumulate=True)
+    close(acc, base.double() + ref, rtol=1e-4, what="dx acc")
+    ob = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    o.linear_dx(dy, W, out=ob, out_dtype=torch.bfloat16)
+    close(ob.float(), ref, rtol=1e-2, what="dx bf16")
+    pre = torch.randn(M, N, device=dev, generator=gen).bfloat16()
+    dh = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    o.linear_dx(dy, W, out=dh, epi=o.EPI_DGELU, C2=pre, drop_p=0.1, seed=9, rng_stream=4)
+    x = pre.double()
+    gg = 0.5 * (1 + torch.erf(x / math.sqrt(2))) + x * torch.exp(-0.5 * x * x) / math.sqrt(2 * math.pi)
+    keep = O.dropout_keep(9, 4, M * N, 0.1).view(M, N).to(dev)
+    close(dh.float(), ref * gg * keep / 0.9, rtol=2e-2, what="dgelu")
+    monkeypatch.setenv("FDDM_GEMM_PATH", "small")
+    dh2 = torch.empty_like(dh)
+    o.linear_dx(dy, W, out=dh2, epi=o.EPI_DGELU, C2=pre, drop_p=0.1, seed=9, rng_stream=4)
+    assert torch.equal(dh == 0, dh2 == 0)
+
+
+@pytest.mark.parametrize("M,N,K", [(264, 200, 1000), (512, 512, 8192), (128, 128, 4096), (1024, 512, 15968)])
+def test_gemm128_weight_grad_layout(M, N, K, monkeypatch):
+    """128x128 LDS-DMA kernel, both operands token-major (dW = dY^T X): ragged token counts read zeros past the
+    end, split-K slices accumulate atomically, the bias gradient (colsum) is fused."""
+    o = ops()
+    monkeypatch.setenv("FDDM_GEMM_PATH", "128")
+    gen = torch.Generator(device=dev).manual_seed(22)
+    dy = torch.randn(K, M, device=dev, generator=gen).bfloat16()
+    x = torch.randn(K, N, device=dev, generator=gen).bfloat16()
+    ref = dy.double().T @ x.double()
+    dW = torch.full((M, N), float("nan"), device=dev)
+    db = torch.full((M,), float("nan"), device=dev)
+    o.linear_dw(dy, x, out=dW, db=db)
+    close(dW, ref, rtol=1e-4, what="dW")
+    close(db, dy.double().sum(0), rtol=1e-4, what="db")
+    o.linear_dw(dy, x, out=dW, db=db, accumulate=True)
+    close(dW, 2 * ref, rtol=1e-4, what="dW acc")
+    close(db, 2 * dy.double().sum(0), rtol=1e-4, what="db acc")
+
+
+def test_gemm128_grouped_weight_grads(monkeypatch):
+    """The decoder block's 8 weight-gradient GEMMs in one 128x128 grouped launch (automatic split balance):
+    token counts 8192 / 15968 (ragged), column slices of shared gradient buffers, fused bias gradients."""
+    o = ops()
+    monkeypatch.delenv("FDDM_GEMM_PATH", raising=False)
+    gen = torch.Generator(device=dev).manual_seed(23)
+    T, d, FF, TS = 2048, 256, 1024, 3992
+    specs = [(T, d, FF), (T, FF, d), (T, d, d), (T, d, d), (TS, 2 * d, d), (T, d, d), (T, 2 * d, d), (T, d, d)]
+    jobs, refs = [], []
+    for K, M, N in specs:
+        dy = torch.randn(K, M, device=dev, generator=gen).bfloat16()
+        x = torch.randn(K, N, device=dev, generator=gen).bfloat16()
+        dW = torch.randn(M, N + 16, device=dev, generator=gen)[:, 8:8 + N]
+        db = torch.randn(M, device=dev, generator=gen)
+        refs.append((dW.double() + dy.double().T @ x.double(), db.double() + dy.double().sum(0)))
+        jobs.append((dy, x, dW, db))
+    o.linear_dw_grouped(jobs)
+    for i, ((dy, x, dW, db), (rw, rb)) in enumerate(zip(jobs, refs)):
+        close(dW, rw, rtol=1e-4, what=f"dW job{i}")
+        close(db, rb, rtol=1e-4, what=f"db job{i}")
 
 
 def test_gemm256_dropout_gelu_matches_small_path(monkeypatch):

@@ -1,0 +1,62 @@
+"""Diagnostic: s_memtime stamps of the 128x128 GEMM (library variant built with -DG128_STAMPS=48, loaded via
+FDDM_HIP_LIB): kernel start skew, prologue (first K-tile landed), per-K-tile cycles, epilogue, per workgroup."""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "fddm-asr_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from fddm_hip import ops  # noqa: E402
+from fddm_hip._lib import lib  # noqa: E402
+
+NS = 48
+dev = torch.device("cuda:0")
+os.environ["FDDM_GEMM_PATH"] = "128"
+
+
+def run(name, fn, nblk):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    buf = (ctypes.c_ulonglong * (2048 * NS))()
+    assert lib().fddm_gemm128_stamps(buf, ctypes.c_long(2048 * NS)) == 0
+    a = np.frombuffer(buf, dtype=np.uint64).reshape(2048, NS)[:nblk].astype(np.int64)
+    t0 = a[:, 0].min()
+    start = a[:, 0] - t0
+    pro = a[:, 1] - a[:, 0]
+    epi = a[:, NS - 1] - a[:, NS - 2]
+    end = a[:, NS - 1] - t0
+    print(f"{name}: blocks {nblk}  start skew med {np.median(start):.0f} max {start.max()}  prologue med "
+          f"{np.median(pro):.0f}  epilogue med {np.median(epi):.0f}  end med {np.median(end):.0f} max {end.max()}")
+    return a
+
+
+def main():
+    bf = torch.bfloat16
+    for (M, N, K) in [(8192, 512, 2048), (8192, 512, 512)]:
+        dy = torch.randn(M, K, device=dev, dtype=bf)
+        w = torch.randn(K, N, device=dev, dtype=bf)
+        o = torch.empty(M, N, device=dev)
+        a = run(f"dX {M}x{N}x{K}", lambda: ops.linear_dx(dy, w, out=o), (M // 128) * (N // 128))
+        nk = K // 64
+        if os.environ.get("G128_FINE"):
+            f = a[:, 2:42].reshape(-1, 8, 5)
+            st = np.concatenate([np.diff(f, axis=2), (f[:, 1:, :1] - f[:, :-1, 4:5])], axis=None) if False else None
+            d = np.diff(f, axis=2)                     # read->lgkm, lgkm->vm, vm->bar1, bar1->mma end
+            nxt = f[:, 1:, 0] - f[:, :-1, 4]            # mma end -> bar2 -> next top
+            print("   fine (median cycles): reads+lgkm %.0f | vmcnt %.0f | bar1 %.0f | mfma %.0f | bar2 %.0f" %
+                  (np.median(d[:, :, 0]), np.median(d[:, :, 1]), np.median(d[:, :, 2]), np.median(d[:, :, 3]),
+                   np.median(nxt)))
+            continue
+        kt = min(nk, NS - 4)
+        d = np.diff(a[:, 2:2 + kt], axis=1)
+        print("   per-K-tile cycles (median over blocks):", " ".join(f"{int(x)}" for x in np.median(d, axis=0)))
+        last = a[:, NS - 2] - a[:, 2 + kt - 1]
+        print(f"   last stamped K-tile -> epilogue start: med {np.median(last):.0f} ({nk - kt + 1} K-tiles)")
+
+
+if __name__ == "__main__":
+    main()

@@ -68,7 +68,7 @@ def main():
         o = torch.empty(M, N, device=dev, dtype=torch.float32 if epi < 0 else bf)
         e = ops.EPI_STORE if epi < 0 else epi
         f = lambda: ops.gemm(A, Wt, o, M, N, K, lda=K, ldb=K, ldc=N, epi=e)  # noqa: E731
-        report_paths(name, 2 * M * N * K, f)
+        report_paths(name, 2 * M * N * K, f, paths=("auto", "256", "128", "big"))
     dws = [("dW dec FF1 2048x512 (K=8192)", 2048, 512, 8192), ("dW dec out 512x512 (K=8192)", 512, 512, 8192),
            ("dW head 8000x512 (K=8192)", 8000, 512, 8192), ("dW cross kv 1024x512 (K=15968)", 1024, 512, 15968)]
     for name, M, N, K in dws:
@@ -79,7 +79,7 @@ def main():
         o = torch.empty(M, N, device=dev)
         db = torch.empty(M, device=dev)
         f = lambda: ops.linear_dw(dy, x, out=o, db=db)  # noqa: E731
-        report(name, 2 * M * N * K, timeit(f))
+        report_paths(name, 2 * M * N * K, f, paths=("auto", "small"))
     if not only or only == "dw":
         # the 8 weight-gradient GEMMs of one C2 decoder block in one grouped launch
         T, d, FF, TS = 8192, 512, 2048, 15968
@@ -89,7 +89,7 @@ def main():
             jobs.append((torch.randn(K, M, device=dev, dtype=bf), torch.randn(K, N, device=dev, dtype=bf),
                          torch.zeros(M, N, device=dev), torch.zeros(M, device=dev)))
             fl += 2 * M * N * K
-        for kc in (0, 8192, 4096, 2048):
+        for kc in (0, 8192, 4096):
             f = lambda: ops.linear_dw_grouped(jobs, kchunk=kc)  # noqa: E731
             report(f"dW grouped block (8 GEMMs) kchunk {kc}", fl, timeit(f))
 
@@ -97,7 +97,9 @@ def main():
             for dy, x, o, db in jobs:
                 ops.linear_dw(dy, x, out=o, accumulate=True, db=db)
         report("dW block as 8 split-K launches", fl, timeit(seq))
-    dxs = [("dX dec FF1 8192x512 (K=2048)", 8192, 512, 2048), ("dX head 8192x512 (K=8000, f32 A)", 8192, 512, 8000)]
+    dxs = [("dX dec FF1 8192x512 (K=2048)", 8192, 512, 2048), ("dX dec out 8192x512 (K=512)", 8192, 512, 512),
+           ("dX dec qkv 8192x512 (K=1536)", 8192, 512, 1536), ("dX cross kv 15968x512 (K=1024)", 15968, 512, 1024),
+           ("dX dec FF2 8192x2048 (K=512)", 8192, 2048, 512), ("dX head 8192x512 (K=8000, f32 A)", 8192, 512, 8000)]
     for name, M, N, K in dxs:
         if only and only != "dx":
             break
@@ -105,7 +107,7 @@ def main():
         w = torch.randn(K, N, device=dev, dtype=bf)
         o = torch.empty(M, N, device=dev)
         f = lambda: ops.linear_dx(dy, w, out=o)  # noqa: E731
-        report(name, 2 * M * N * K, timeit(f))
+        report_paths(name, 2 * M * N * K, f, paths=("auto", "small"))
 
 
 if __name__ == "__main__":
