@@ -49,6 +49,14 @@ __device__ __forceinline__ bool drop_keep(uint64_t seed, uint64_t stream, uint64
   unsigned u = (unsigned)(h >> (16u * (unsigned)(e & 3u))) & 0xFFFFu;
   return u >= thr16;
 }
+// the keep decisions of the four elements 4*e4 .. 4*e4+3 (one hash): bit i for element 4*e4 + i
+__device__ __forceinline__ unsigned drop_keep4(uint64_t seed, uint64_t stream, uint64_t e4, unsigned thr16) {
+  const uint64_t h = mix64(seed, stream, e4);
+  unsigned k = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) k |= (((unsigned)(h >> (16 * i)) & 0xFFFFu) >= thr16 ? 1u : 0u) << i;
+  return k;
+}
 
 // erf via Abramowitz-Stegun 7.1.26 (|abs err| <= 1.5e-7): exp + rcp + 5 FMA instead of the library
 // erff's branchy rational approximations; exact GELU (torch approximate='none') to ~1e-7.

@@ -330,13 +330,11 @@ __device__ __forceinline__ void tile128(const GemmArgs& g, unsigned char* smem, 
         } else {
           if constexpr (EPI == EPI_GELU) {
             *(uint2*)cp = make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));  // pre-activation
+            const unsigned keep = g.thr16 ? drop_keep4(g.seed, g.stream, ((uint64_t)m * (uint64_t)N + n) >> 2, g.thr16) : 0xfu;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              float a = gelu_f(v[e]);
-              if (g.thr16)
-                a = drop_keep(g.seed, g.stream, (uint64_t)m * (uint64_t)N + (uint64_t)(n + e), g.thr16) ? a * g.drop_scale
-                                                                                                      : 0.f;
-              v[e] = a;
+              const float a = gelu_f(v[e]);
+              v[e] = (keep >> e) & 1u ? (g.thr16 ? a * g.drop_scale : a) : 0.f;
             }
             cp = (OT*)g.C2 + (long)m * ldc + n;
           } else if constexpr (EPI == EPI_GELU_ONLY) {
@@ -346,13 +344,11 @@ __device__ __forceinline__ void tile128(const GemmArgs& g, unsigned char* smem, 
             const uint2 pu = *(const uint2*)((const OT*)g.C2 + (long)m * ldc + n);
             const float pv[4] = {__uint_as_float(pu.x << 16), __uint_as_float(pu.x & 0xffff0000u),
                                  __uint_as_float(pu.y << 16), __uint_as_float(pu.y & 0xffff0000u)};
+            const unsigned keep = g.thr16 ? drop_keep4(g.seed, g.stream, ((uint64_t)m * (uint64_t)N + n) >> 2, g.thr16) : 0xfu;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              float a = v[e] * gelu_grad(pv[e]);
-              if (g.thr16)
-                a = drop_keep(g.seed, g.stream, (uint64_t)m * (uint64_t)N + (uint64_t)(n + e), g.thr16) ? a * g.drop_scale
-                                                                                                      : 0.f;
-              v[e] = a;
+              const float a = v[e] * gelu_grad(pv[e]);
+              v[e] = (keep >> e) & 1u ? (g.thr16 ? a * g.drop_scale : a) : 0.f;
             }
           }
           *(uint2*)cp = make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));

@@ -248,17 +248,19 @@ __global__ void __launch_bounds__(512) gemm256_kernel(GemmArgs g) {
           emit(v[0], v[1], rc, so);
           const unsigned thr = g.thr16;
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
+          for (int j = 0; j < 2; ++j) {
+            unsigned keep = 0xfu;
+            if (thr) {  // 4 consecutive columns (N % 8 == 0): one hash
+              const unsigned m = (unsigned)(em0 + wr * 128 + (ib + i) * 16 + fr);
+              const unsigned n = (unsigned)(en0 + wc * 64 + (jb + j) * 16 + 4 * fg);
+              keep = drop_keep4(g.seed, g.stream, ((uint64_t)m * (uint64_t)Nc + n) >> 2, thr);
+            }
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              float a = gelu_f(v[j][e]);
-              if (thr) {
-                const unsigned m = (unsigned)(em0 + wr * 128 + (ib + i) * 16 + fr);
-                const unsigned n = (unsigned)(en0 + wc * 64 + (jb + j) * 16 + 4 * fg + e);
-                a = drop_keep(g.seed, g.stream, (uint64_t)m * (uint64_t)Nc + n, thr) ? a * g.drop_scale : 0.f;
-              }
-              v[j][e] = a;
+              const float a = gelu_f(v[j][e]);
+              v[j][e] = thr ? ((keep >> e) & 1u ? a * g.drop_scale : 0.f) : a;
             }
+          }
           emit(v[0], v[1], rc2, so);
         } else {
           if constexpr (EPI == EPI_GELU_ONLY) {

@@ -75,11 +75,15 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(LnFwdArgs a) {
       if (y) {
         float yv[8];
         ld8<YT>(y + ch * 8, yv);
+        unsigned keep = 0xffu;  // d % 8 == 0: two hashes per 8 elements
+        if (a.thr16) {
+          const uint64_t e4 = (uint64_t)(row * d + ch * 8) >> 2;
+          keep = drop_keep4(a.seed, a.stream, e4, a.thr16) | (drop_keep4(a.seed, a.stream, e4 + 1, a.thr16) << 4);
+        }
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          float t = yv[e];
-          if (a.thr16) t = drop_keep(a.seed, a.stream, (uint64_t)(row * d + ch * 8 + e), a.thr16) ? t * a.drop_scale : 0.f;
-          v[i][e] += t;
+          const float t = yv[e];
+          v[i][e] += a.thr16 ? ((keep >> e) & 1u ? t * a.drop_scale : 0.f) : t;
         }
       }
 #pragma unroll

@@ -274,8 +274,11 @@ class HeadFn(torch.autograd.Function):
     def backward(ctx, dlogits):
         xT, weight = ctx.saved_tensors
         dl = dlogits.contiguous()
+        if xT.dtype == torch.bfloat16 and dl.dtype == F32:
+            # one cast pass, then both head GEMMs take the bf16 LDS-DMA paths (dx: K = vocab, dW: K = tokens)
+            dl = ops.cast(dl, torch.bfloat16)
         w = rt.wt(weight)
-        dx = ops.linear_dx(dl, w)                 # A = dlogits (f32, converted while staging)
+        dx = ops.linear_dx(dl, w)
         dW, aw = _gdst(weight)
         db, ab = _gdst(ctx.bias[0])
         if aw != ab:
