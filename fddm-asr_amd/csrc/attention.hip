@@ -332,9 +332,12 @@ __global__ void __launch_bounds__(256) fwd2_kernel(AttnArgs a) {
         mma<bf16_t>(s[1][kb], af, qf[1][sub]);
       }
     }
-    // softmax in the exp2 domain: x = s*scale*log2e (+ gate*bias*log2e) (+ 0/-inf mask row)
+    // softmax. Scores stay in raw units x = s (+ (gate/scale)*bias) (+ 0/-inf mask row, only on tiles that
+    // can hold masked keys); the running max m is in raw units and p = 2^(x*sl2 - m*sl2) is one FMA +
+    // v_exp_f32 (no separate scale multiply or subtraction per score).
+    const bool mt = MASK && (a.key_keep != nullptr || t == ntiles - 1);
     float mrow[4][4];
-    if constexpr (MASK) {
+    if (mt) {
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb) {
         const float4 mv4 = *(const float4*)(&mbuf[cur][kb * 16 + 4 * g]);
@@ -345,24 +348,29 @@ __global__ void __launch_bounds__(256) fwd2_kernel(AttnArgs a) {
 #pragma unroll
     for (int gq = 0; gq < 2; ++gq) {
       float tmax = -INFINITY;
-      const float gl = gate[gq] * 1.4426950408889634f;
+      const float graw = REL ? gate[gq] / a.scale : 0.f;
       const int toff = 127 - (q[gq] - qbase);
 #pragma unroll
-      for (int kb = 0; kb < 4; ++kb)
+      for (int kb = 0; kb < 4; ++kb) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int kl = kb * 16 + 4 * g + j;
-          float x = s[gq][kb][j] * sl2;
-          if constexpr (REL) x = fmaf(gl, tbuf[cur][kl + toff], x);
-          if constexpr (MASK) x += mrow[kb][j];
+          float x = s[gq][kb][j];
+          if constexpr (REL) x = fmaf(graw, tbuf[cur][kl + toff], x);
           p[gq][kb][j] = x;
-          tmax = fmaxf(tmax, x);
         }
+        if (mt) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) p[gq][kb][j] += mrow[kb][j];
+        }
+        tmax = fmaxf(tmax, fmaxf(fmaxf(p[gq][kb][0], p[gq][kb][1]), fmaxf(p[gq][kb][2], p[gq][kb][3])));
+      }
       tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
       const float mn = fmaxf(m[gq], tmax);
-      const float mref = (mn == -INFINITY) ? 0.f : mn;  // all-masked so far: exp2(-inf - 0) = 0
-      const float alpha = __builtin_amdgcn_exp2f(m[gq] - mref);
+      const float mref = (mn == -INFINITY) ? 0.f : mn;  // all-masked so far: exp2(-inf) = 0
+      const float nbias = -mref * sl2;
+      const float alpha = __builtin_amdgcn_exp2f((m[gq] - mref) * sl2);
       float ls = 0.f;
       uint64_t bits = 0;
 #pragma unroll
@@ -385,7 +393,7 @@ __global__ void __launch_bounds__(256) fwd2_kernel(AttnArgs a) {
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          float e = __builtin_amdgcn_exp2f(p[gq][kb][j] - mref);
+          float e = __builtin_amdgcn_exp2f(fmaf(p[gq][kb][j], sl2, nbias));
           ls += e;
           if constexpr (DROP) e = ((keep >> j) & 1u) ? e * a.drop_scale : 0.f;
           p[gq][kb][j] = e;
@@ -456,7 +464,8 @@ __global__ void __launch_bounds__(256) fwd2_kernel(AttnArgs a) {
       u2.y = pk(o[gq][d][2] * inv, o[gq][d][3] * inv);
       *(uint2*)(Ob + d * 16 + 4 * g) = u2;
     }
-    if (a.lse && g == 0) a.lse[(long)bh * a.Lq + q[gq]] = (lt > 0.f) ? (m[gq] + __log2f(lt)) * 0.69314718055994531f : NAN;
+    if (a.lse && g == 0)
+      a.lse[(long)bh * a.Lq + q[gq]] = (lt > 0.f) ? (m[gq] * sl2 + __log2f(lt)) * 0.69314718055994531f : NAN;
   }
 }
 

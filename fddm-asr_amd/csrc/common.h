@@ -71,11 +71,31 @@ __device__ __forceinline__ float erf_fast(float x) {
   const float r = 1.0f - p * t * __expf(-ax * ax);
   return copysignf(r, x);
 }
-__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f)); }
+// GELU(x) = x*Phi(x) = max(x, 0) - |x| * r with r = 0.5*erfc(|x|/sqrt2) = t*P(t)*exp(-x^2/2) (A&S 7.1.26 with the
+// 1/sqrt2 and the 0.5 folded into its constants): one rcp, one exp2, 4 FMA + 4 mul/max — no sign select, no
+// separate argument scaling. Same approximation as erf_fast, |abs err of Phi| <= 1e-7.
+__device__ __forceinline__ float gelu_r(float ax, float& e) {
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.23164189f, ax, 1.0f));
+  float p = 0.5307027145f;
+  p = fmaf(p, t, -0.7265760135f);
+  p = fmaf(p, t, 0.7107068705f);
+  p = fmaf(p, t, -0.142248368f);
+  p = fmaf(p, t, 0.127414796f);
+  e = __builtin_amdgcn_exp2f(ax * (ax * -0.72134752044f));  // exp(-x^2/2)
+  return p * t * e;
+}
+__device__ __forceinline__ float gelu_f(float x) {
+  const float ax = fabsf(x);
+  float e;
+  const float r = gelu_r(ax, e);
+  return fmaf(-ax, r, fmaxf(x, 0.f));
+}
+// d/dx GELU = Phi(x) + x * phi(x), phi(x) = exp(-x^2/2)/sqrt(2 pi) (shares the exponential)
 __device__ __forceinline__ float gelu_grad(float x) {
-  const float cdf = 0.5f * (1.0f + erf_fast(x * 0.70710678118654752f));
-  const float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
-  return cdf + x * pdf;
+  float e;
+  const float r = gelu_r(fabsf(x), e);
+  const float cdf = x >= 0.f ? 1.0f - r : r;
+  return fmaf(x * 0.3989422804014327f, e, cdf);
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

@@ -104,19 +104,19 @@ __global__ void conv0_gn_affine_kernel(const double* __restrict__ ws, const floa
 // FMAs, the affine and the GELU polynomial issue as packed v_pk_* f32 instructions.
 typedef float f2_t __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ f2_t gelu2(f2_t x) {
-  const f2_t z = x * 0.70710678118654752f;
-  const f2_t az = {fabsf(z.x), fabsf(z.y)};
-  const f2_t den = az * 0.3275911f + 1.0f;
+__device__ __forceinline__ f2_t gelu2(f2_t x) {  // gelu_f (common.h) on a channel pair
+  const f2_t ax = {fabsf(x.x), fabsf(x.y)};
+  const f2_t den = ax * 0.23164189f + 1.0f;
   const f2_t t = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
-  f2_t p = t * 1.061405429f - 1.453152027f;
-  p = p * t + 1.421413741f;
-  p = p * t - 0.284496736f;
-  p = p * t + 0.254829592f;
-  const f2_t e = {__expf(-az.x * az.x), __expf(-az.y * az.y)};
-  const f2_t r = 1.0f - p * t * e;
-  const f2_t erfz = {copysignf(r.x, z.x), copysignf(r.y, z.y)};
-  return 0.5f * x * (1.0f + erfz);
+  f2_t p = t * 0.5307027145f - 0.7265760135f;
+  p = p * t + 0.7107068705f;
+  p = p * t - 0.142248368f;
+  p = p * t + 0.127414796f;
+  const f2_t u = ax * (ax * -0.72134752044f);
+  const f2_t e = {__builtin_amdgcn_exp2f(u.x), __builtin_amdgcn_exp2f(u.y)};
+  const f2_t r = p * t * e;
+  const f2_t mx = {fmaxf(x.x, 0.f), fmaxf(x.y, 0.f)};
+  return mx - ax * r;
 }
 
 template <typename OT, int K>

@@ -12,6 +12,8 @@ import contextlib
 import math
 import os
 
+import weakref
+
 import torch
 
 from . import ops
@@ -46,7 +48,18 @@ def compute_dtype():
 
 # --------------------------------------------------------------------------------- weight cache
 class _Entry:
-    __slots__ = ("version", "tensor", "ptr")
+    __slots__ = ("version", "tensor", "ptr", "ref")
+
+    def valid_for(self, p) -> bool:
+        # id(p) and the allocator's data_ptr are both reused once p is freed: the weak reference is what
+        # tells a live parameter from a new one that landed on the same id / address
+        return self.ref() is p and self.version == p._version and self.ptr == p.data_ptr()
+
+
+def _entry(p, tensor) -> _Entry:
+    e = _Entry()
+    e.version, e.tensor, e.ptr, e.ref = p._version, tensor, p.data_ptr(), weakref.ref(p)
+    return e
 
 
 _wcache: dict = {}
@@ -63,30 +76,26 @@ def wt(p: torch.Tensor, dtype=None, transform=None, key=None) -> torch.Tensor:
         return p.detach()
     k = (id(p), dtype, key)
     e = _wcache.get(k)
-    if e is not None and e.version == p._version and e.ptr == p.data_ptr():
+    if e is not None and e.valid_for(p):
         return e.tensor
     with torch.no_grad():
         src = transform(p.detach()) if transform is not None else p.detach()
         src = src.contiguous()
         out = src if src.dtype == dtype else ops.cast(src, dtype)
-    e = _Entry()
-    e.version, e.tensor, e.ptr = p._version, out, p.data_ptr()
-    _wcache[k] = e
+    _wcache[k] = _entry(p, out)
     return out
 
 
 def wt_refresh_from(p: torch.Tensor, bf16_copy: torch.Tensor) -> None:
     """Record a bf16 copy written by the fused optimizer as current for `p`."""
-    e = _Entry()
-    e.version, e.tensor, e.ptr = p._version, bf16_copy, p.data_ptr()
-    _wcache[(id(p), torch.bfloat16, None)] = e
+    _wcache[(id(p), torch.bfloat16, None)] = _entry(p, bf16_copy)
 
 
 def wt_bf16_buffer(p: torch.Tensor) -> torch.Tensor:
     """The cached bf16 copy buffer of p (allocating it), for the optimizer to write in place."""
     k = (id(p), torch.bfloat16, None)
     e = _wcache.get(k)
-    if e is None or e.tensor.shape != p.shape:
+    if e is None or e.ref() is not p or e.tensor.shape != p.shape:
         return wt(p, torch.bfloat16)
     return e.tensor
 
@@ -132,18 +141,29 @@ def set_seed_state(state) -> None:
 _tables: dict = {}
 
 
+def _table_get(k, owner):
+    """Cached derived table of `owner` under key k — only while that very tensor is alive (its id is reused
+    once it is freed, so the key alone could hand a new model the old one's table)."""
+    v = _tables.get(k)
+    return v[1] if v is not None and v[0]() is owner else None
+
+
+def _table_put(k, owner, t):
+    _tables[k] = (weakref.ref(owner), t)
+
+
 def rope_tables(L: int, inv_freq: torch.Tensor, device):
     """cos/sin [L, d] exactly as RoPEEmbedding.forward (models/denoise_decoder.py:35-40), computed on
     the host once per (L, d) and kept resident."""
     k = ("rope", L, id(inv_freq), inv_freq._version, inv_freq.numel(), str(device))  # no device read (graph capture)
-    t = _tables.get(k)
+    t = _table_get(k, inv_freq)
     if t is None:
         f = inv_freq.detach().float().cpu()
         pos = torch.arange(L, dtype=f.dtype)
         fr = torch.outer(pos, f)
         emb = torch.cat((fr, fr), dim=-1)
         t = (emb.cos().contiguous().to(device), emb.sin().contiguous().to(device))
-        _tables[k] = t
+        _table_put(k, inv_freq, t)
     return t
 
 
@@ -165,12 +185,12 @@ def rel_bucket(rel: torch.Tensor, num_buckets: int, max_distance: int) -> torch.
 def relbias_table(S: int, embed: torch.Tensor, num_buckets: int, max_distance: int):
     """[H, 2S-1] fp32: table[h][r] = rel_attn_embed[bucket(r - (S-1))][h]  (r = key - query + S - 1)."""
     k = ("rel", S, id(embed), embed._version, num_buckets, max_distance)
-    t = _tables.get(k)
+    t = _table_get(k, embed)
     if t is None:
         rel = torch.arange(-(S - 1), S)
         b = rel_bucket(rel, num_buckets, max_distance).to(embed.device)
         t = embed.detach().float()[b].t().contiguous()
-        _tables[k] = t
+        _table_put(k, embed, t)
     return t
 
 

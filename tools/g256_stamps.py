@@ -13,13 +13,14 @@ from fddm_hip import _lib, ops  # noqa: E402
 
 NS = 64
 M, N, K = (int(a) for a in sys.argv[1:4])
+EPI = int(sys.argv[4]) if len(sys.argv) > 4 else 0
 os.environ["FDDM_GEMM_PATH"] = "256"
 dev = torch.device("cuda:0")
 A = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
 W = torch.randn(N, K, device=dev, dtype=torch.bfloat16) / 30
 o = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
 for _ in range(5):
-    ops.gemm(A, W, o, M, N, K, lda=K, ldb=K, ldc=N)
+    ops.gemm(A, W, o, M, N, K, lda=K, ldb=K, ldc=N, epi=EPI)
 torch.cuda.synchronize()
 buf = (ctypes.c_ulonglong * (256 * NS))()
 f = _lib.lib().fddm_gemm256_stamps
@@ -29,7 +30,7 @@ st = np.frombuffer(buf, dtype=np.uint64).reshape(256, NS).astype(np.int64)
 d = np.diff(st, axis=1)
 ok = (st[:, 1:] > 0) & (st[:, :-1] > 0)
 nk = K // 64
-print(f"M{M} N{N} K{K} nk={nk}: median cycles per K-tile (column = K-tile index within the workgroup)")
+print(f"M{M} N{N} K{K} epi{EPI} nk={nk}: median cycles per K-tile (column = K-tile index within the workgroup)")
 med = [int(np.median(d[ok[:, j], j])) if ok[:, j].any() else -1 for j in range(NS - 1)]
 for j in range(0, NS - 1, 8):
     print(" ".join(f"{v:7d}" for v in med[j:j + 8]))
