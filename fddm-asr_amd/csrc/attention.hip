@@ -245,8 +245,11 @@ __global__ void __launch_bounds__(256) fwd_kernel(AttnArgs a) {
 // with the tile instead of gathered from global memory per score.
 // Template flags: DROP (dropout on P), MASK (key-padding mask and/or a ragged last tile: a 0/-inf bias row
 // per tile in LDS), REL (WavLM gated relative-position bias).
+#ifndef ATTN_FWD_WPS
+#define ATTN_FWD_WPS 2  // waves per SIMD the register allocation targets (measured: 2 beats 1, 3-4 spill)
+#endif
 template <bool DROP, bool MASK, bool REL>
-__global__ void __launch_bounds__(256) fwd2_kernel(AttnArgs a) {
+__global__ void __launch_bounds__(256, ATTN_FWD_WPS) fwd2_kernel(AttnArgs a) {
   constexpr int RB = 128;
   __shared__ __attribute__((aligned(16))) unsigned char kbuf[2][64 * RB];
   __shared__ __attribute__((aligned(16))) unsigned char vbuf[2][64 * RB];
