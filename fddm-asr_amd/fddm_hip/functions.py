@@ -4,7 +4,10 @@ with the residual stream, LayerNorm statistics and softmax log-sum-exps in fp32.
 """
 from __future__ import annotations
 
+import math
+
 import torch
+import torch.nn.functional as F
 
 from . import ops, runtime as rt
 
@@ -111,6 +114,94 @@ class EmbedFn(torch.autograd.Function):
         return None, _ret(dE, aE), dtb, None
 
 
+# ------------------------------------------------------------------------- decoder conditioning
+def sinusoid(t, d, max_steps):
+    """SinusoidalTimeEmbedding's feature map (models/denoise_decoder.py:92-119), same torch ops."""
+    if t.dim() == 0:
+        t = t[None]
+    half = d // 2
+    freqs = torch.exp(torch.linspace(math.log(1.0), math.log(max_steps), half, device=t.device) * (-1))
+    args = t.float().unsqueeze(1) * freqs.unsqueeze(0)
+    emb = torch.cat([torch.sin(args), torch.cos(args)], dim=1)
+    if d % 2 == 1:
+        emb = F.pad(emb, (0, 1))
+    return emb.contiguous()
+
+
+class CondFn(torch.autograd.Function):
+    """The decoder's conditioning path as one Function: t_bias = time_proj(mlp(sinusoid(t)))
+    (models/denoise_decoder.py:92-119, 272-274) and the FiLM projections scale_l / shift_l = pooled W^T + b of
+    every block (:74-89; pooled = time-mean of the acoustic condition, no grad). Forward: 3 fp32 GEMMs for the
+    time MLP and ONE for all 2*NL FiLM projections; backward: the time-MLP chain in fp32 and the FiLM weight /
+    bias gradients as one grouped launch (bf16 mode) straight into the parameters' gradient slots — instead of
+    ~80 small framework kernels (per-layer BLAS calls, bias reductions, gradient accumulations) per step.
+    `gbuf` [2*NL, B, d] (zeroed by the caller) is where the blocks' LayerNorm backward accumulates dFiLM."""
+
+    @staticmethod
+    def forward(ctx, t, pooled, gbuf, d, max_steps, *params):
+        W1, b1, W2, b2, Wp, bp = params[:6]
+        film = params[6:]
+        nf = len(film) // 2
+        # [B, d]-row GEMMs in fp32 on the BLAS library (plain skinny GEMMs; the MFMA kernels target >= 128 rows)
+        with torch.no_grad():
+            emb = sinusoid(t, d, max_steps)
+            pre = torch.addmm(b1, emb, W1.t())
+            h = F.silu(pre)
+            te = torch.addmm(b2, h, W2.t())
+            tb = torch.addmm(bp, te, Wp.t())
+            Wf = torch.cat([w for w in film[0::2]])
+            bf = torch.cat([b for b in film[1::2]])
+            B = pooled.shape[0]
+            fl = torch.addmm(bf, pooled, Wf.t())                                 # [B, nf*d]
+            f12 = fl.view(B, nf, d).transpose(0, 1).contiguous()              # [nf, B, d]
+        ctx.save_for_backward(emb, pre, h, te, pooled, gbuf, *params)
+        ctx.nf = nf
+        return (tb,) + tuple(f12[i] for i in range(nf))
+
+    @staticmethod
+    def backward(ctx, dtb, *dfilm):
+        emb, pre, h, te, pooled, gbuf, *params = ctx.saved_tensors
+        W1, b1, W2, b2, Wp, bp = params[:6]
+        film = params[6:]
+        nf = ctx.nf
+        B, d = pooled.shape
+        dev = pooled.device
+        grads = [None] * len(params)
+        # FiLM: the blocks accumulated into gbuf and handed back its slices; anything else is stacked
+        if all(g is not None and g.data_ptr() == gbuf[i].data_ptr() for i, g in enumerate(dfilm)):
+            dfl = gbuf
+        else:
+            dfl = torch.stack([g if g is not None else torch.zeros(B, d, device=dev) for g in dfilm])
+        G = [_gdst(p_, zero=True) for p_ in film]
+        if rt.compute_dtype() == torch.bfloat16:
+            d16 = ops.cast(dfl.contiguous(), torch.bfloat16)
+            p16 = ops.cast(pooled.contiguous(), torch.bfloat16)
+            ops.linear_dw_grouped([(d16[i], p16, G[2 * i][0], G[2 * i + 1][0]) for i in range(nf)])
+        else:
+            for i in range(nf):
+                ops.linear_dw(dfl[i], pooled, out=G[2 * i][0], accumulate=True, db=G[2 * i + 1][0])
+        for i in range(2 * nf):
+            grads[6 + i] = _ret(*G[i])
+        # time MLP (fp32): tb = te Wp^T + bp, te = h W2^T + b2, h = silu(pre), pre = emb W1^T + b1;
+        # weight gradients accumulated in place (beta = 1) into the gradient slots
+        if dtb is not None:
+            dtb = dtb.contiguous()
+            T = [_gdst(p_, zero=True) for p_ in (W1, b1, W2, b2, Wp, bp)]
+            dte = dtb @ Wp
+            torch.addmm(T[4][0], dtb.t(), te, out=T[4][0])
+            T[5][0].add_(dtb.sum(0))
+            dh = dte @ W2
+            torch.addmm(T[2][0], dte.t(), h, out=T[2][0])
+            T[3][0].add_(dte.sum(0))
+            sg = torch.sigmoid(pre)
+            dpre = dh * sg * (1.0 + pre * (1.0 - sg))
+            torch.addmm(T[0][0], dpre.t(), emb, out=T[0][0])
+            T[1][0].add_(dpre.sum(0))
+            for i in range(6):
+                grads[i] = _ret(*T[i])
+        return (None, None, None, None, None) + tuple(grads)
+
+
 # -------------------------------------------------------------------------------- decoder block
 def _film_split(fs):
     return fs.contiguous()
@@ -127,7 +218,7 @@ class DecoderBlockFn(torch.autograd.Function):
     def forward(ctx, x, xT, cT, key_keep, fscale, fshift, meta, *params):
         (sa_w, sa_b, so_w, so_b, ca_w, ca_b, co_w, co_b, f0_w, f0_b, f3_w, f3_b,
          n1w, n1b, n2w, n2b, n3w, n3b) = params
-        B, L, S, H, layer, p, seed, cos, sin = meta
+        B, L, S, H, layer, p, seed, cos, sin = meta[:9]
         N, d = x.shape
         dev = x.device
         cd = rt.compute_dtype()
@@ -194,7 +285,8 @@ class DecoderBlockFn(torch.autograd.Function):
          key_keep, fsc, *params) = ctx.saved_tensors
         (sa_w, sa_b, so_w, so_b, ca_w, ca_b, co_w, co_b, f0_w, f0_b, f3_w, f3_b,
          n1w, n1b, n2w, n2b, n3w, n3b) = params
-        B, L, S, H, layer, p, seed, cos, sin = ctx.meta
+        B, L, S, H, layer, p, seed, cos, sin = ctx.meta[:9]
+        gfilm = ctx.meta[9] if len(ctx.meta) > 9 else None
         st = 6 * layer
         N, d = dx3.shape
         dev = dx3.device
@@ -223,8 +315,11 @@ class DecoderBlockFn(torch.autograd.Function):
         # LN2 + FiLM
         dx1 = torch.empty(N, d, device=dev, dtype=F32)
         dyc = torch.empty(N, d, device=dev, dtype=cd)
-        dfs = torch.zeros(B, d, device=dev, dtype=F32)
-        dfh = torch.zeros(B, d, device=dev, dtype=F32)
+        if gfilm is not None:   # zeroed slices of CondFn's FiLM-gradient buffer (one fill per step)
+            dfs, dfh = gfilm
+        else:
+            dfs = torch.zeros(B, d, device=dev, dtype=F32)
+            dfh = torch.zeros(B, d, device=dev, dtype=F32)
         ops.ln_bwd(dx2, s2, m2, r2, n2w, n2b, dres=dx1, dy_t=dyc, dgamma=gn2w, dbeta=gn2b, film_scale=fsc,
                    dfilm=(dfs, dfh), rows_per_batch=L, drop_p=p, seed=seed, rng_stream=st + 4)
         # cross out-proj + attention

@@ -119,10 +119,12 @@ class DecoderBlock(nn.Module):
                 self.ff[3].weight, self.ff[3].bias, self.norm1.weight, self.norm1.bias, self.norm2.weight,
                 self.norm2.bias, self.norm3.weight, self.norm3.bias)
 
-    def run(self, x, xT, cT, key_keep, pooled, B, L, S, layer, seed, cos, sin):
-        fscale, fshift = self.film_layer.params(pooled)
+    def run(self, x, xT, cT, key_keep, film, B, L, S, layer, seed, cos, sin):
+        """film = (scale, shift, (dscale, dshift) accumulators or None) from DenoisingTransformerDecoder's
+        conditioning Function."""
+        fscale, fshift, gfilm = film
         p = self.p if self.training else 0.0
-        meta = (B, L, S, self.nhead, layer, p, seed, cos, sin)
+        meta = (B, L, S, self.nhead, layer, p, seed, cos, sin, gfilm)
         return FN.DecoderBlockFn.apply(x, xT, cT, key_keep, fscale, fshift, meta, *self.block_params())
 
 
@@ -155,7 +157,18 @@ class DenoisingTransformerDecoder(nn.Module):
         S = cond.shape[1]
         dev = xt.device
         cd = rt.compute_dtype()
-        t_bias = self.time_proj(self.time_emb(t))                                   # [B, d]  (:272-274)
+        # conditioning (:272-274 time bias, :185 pooled condition -> FiLM of every block) in one Function
+        with torch.no_grad():
+            pooled = cond.detach().float().mean(dim=1)                              # (:185)
+        nb = len(self.blocks)
+        gbuf = torch.zeros(2 * nb, B, self.d_model, device=dev, dtype=torch.float32)
+        te = self.time_emb
+        film_params = [q for blk in self.blocks for lin in (blk.film_layer.scale_proj, blk.film_layer.shift_proj)
+                       for q in (lin.weight, lin.bias)]
+        outs = FN.CondFn.apply(t, pooled, gbuf, self.d_model, te.max_steps, te.mlp[0].weight, te.mlp[0].bias,
+                               te.mlp[2].weight, te.mlp[2].bias, self.time_proj.weight, self.time_proj.bias,
+                               *film_params)
+        t_bias, films = outs[0], outs[1:]
         if t_bias.shape[0] != B:
             t_bias = t_bias.expand(B, -1)
         x, xT = FN.EmbedFn.apply(xt, self.tok_emb.weight, t_bias, self.pad_id)      # (:254)
@@ -165,11 +178,11 @@ class DenoisingTransformerDecoder(nn.Module):
         with torch.no_grad():
             c = cond.detach()
             cT = (c if c.dtype == cd else c.to(cd)).reshape(B * S, -1).contiguous()
-            pooled = c.float().mean(dim=1)                                          # (:185)
         cos, sin = self.pos_emb(L, dev)
         seed = rt.next_seed()
         for i, blk in enumerate(self.blocks):
-            x, xT = blk.run(x, xT, cT, key_keep, pooled, B, L, S, i, seed, cos, sin)
+            film = (films[2 * i], films[2 * i + 1], (gbuf[2 * i], gbuf[2 * i + 1]))
+            x, xT = blk.run(x, xT, cT, key_keep, film, B, L, S, i, seed, cos, sin)
         logits = FN.HeadFn.apply(x, xT, self.head.weight, self.head.bias)           # (:286)
         return logits.view(B, L, -1)
 
