@@ -258,7 +258,10 @@ __device__ __forceinline__ void tile128(const GemmArgs& g, unsigned char* smem, 
   bar();       // ... for every wave: the ring is free
   STAMP(NSTAMP - 2);
 
-  // ------------------------------------------------------------------ k-half reduction, epilogue (group 0)
+  // ------------------------------------------------------------------ k-half reduction, epilogue
+  // Each group finalises half of its wave tile's rows (group g: row blocks 2g, 2g+1): it parks the partial
+  // sums of the other half in LDS for its partner, and adds the partner's parked half of its own rows. The
+  // epilogue's global loads (bias, dGELU pre-activation) are issued before the exchange barrier.
   const int mw = m0 + wr * 64, nw = n0 + wc * 64;
   if (!AKC && do_cs) {
     // lanes fr, fr+16, fr+32, fr+48 hold partial sums of row 16i + fr (each group its k-half)
@@ -271,90 +274,101 @@ __device__ __forceinline__ void tile128(const GemmArgs& g, unsigned char* smem, 
       if (fg == 0 && m >= by * BM) atomicAdd(g.colsum + m, v);
     }
   }
-  {
-    f32x4_t* red = (f32x4_t*)smem + w4 * 1024;  // [i][j][lane], 16 KB per wave pair
-    if (grp == 1) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) red[(i * 4 + j) * 64 + lane] = acc[i][j];
-    }
-    bar();
-    if (grp == 1) return;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] += red[(i * 4 + j) * 64 + lane];
-  }
+  f32x4_t* red = (f32x4_t*)smem + w4 * 1024;  // [i][j][lane], 16 KB per wave pair
   const float alpha = g.alpha;
-  if constexpr (EPI == EPI_ACC_F32) {
-    // park the wave's 64x64 f32 sub-tile in LDS (chunk c of row r at c ^ (r & 15)), then add one 256-B row per
-    // instruction: split-K slices atomically, a single slice by read-modify-write
-    float* tl = (float*)(smem + 65536) + w4 * 4096;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int r = 16 * i + fr, c = 4 * j + fg;
-        *(f32x4_t*)(tl + r * 64 + ((c ^ (r & 15)) << 2)) = acc[i][j];
-      }
-    const int n = nw + lane;
-    const int mlo = by * BM;
-    const bool nok = n >= bx * BN;
-    float* C = (float*)g.C;
-    const long ldc = g.ldc;
-    for (int r = 0; r < 64; ++r) {
-      const int m = mw + r;
-      const float v = tl[r * 64 + ((((lane >> 2) ^ (r & 15)) << 2) | (lane & 3))] * alpha;
-      if (nok && m >= mlo) {
-        float* c = C + (long)m * ldc + n;
-        if (nz > 1) atomicAdd(c, v);
-        else *c += v;
-      }
-    }
-  } else {
-    const long ldc = g.ldc;
+  const long ldc = g.ldc;
+  auto finish = [&](auto gc) {
+    constexpr int G = decltype(gc)::value, I0 = 2 * G, P0 = 2 - 2 * G;  // own / partner's row blocks
     f32x4_t bv[4];
+    uint2 pre[2][4];
+    if constexpr (EPI != EPI_ACC_F32) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      bv[j] = g.bias ? *(const f32x4_t*)(g.bias + nw + 16 * j + 4 * fg) : f32x4_t{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < 4; ++j)
+        bv[j] = g.bias ? *(const f32x4_t*)(g.bias + nw + 16 * j + 4 * fg) : f32x4_t{0.f, 0.f, 0.f, 0.f};
+    }
+    if constexpr (EPI == EPI_DGELU) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+      for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int m = mw + 16 * i + fr, n = nw + 16 * j + 4 * fg;
-        f32x4_t v = acc[i][j] * alpha + bv[j];
-        OT* cp = (OT*)g.C + (long)m * ldc + n;
-        if constexpr (sizeof(OT) == 4) {
-          *(f32x4_t*)cp = v;
-        } else {
-          if constexpr (EPI == EPI_GELU) {
-            *(uint2*)cp = make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));  // pre-activation
-            const unsigned keep = g.thr16 ? drop_keep4(g.seed, g.stream, ((uint64_t)m * (uint64_t)N + n) >> 2, g.thr16) : 0xfu;
+        for (int j = 0; j < 4; ++j)
+          pre[ii][j] = *(const uint2*)((const OT*)g.C2 + (long)(mw + 16 * (I0 + ii) + fr) * ldc + nw + 16 * j + 4 * fg);
+    }
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float a = gelu_f(v[e]);
-              v[e] = (keep >> e) & 1u ? (g.thr16 ? a * g.drop_scale : a) : 0.f;
-            }
-            cp = (OT*)g.C2 + (long)m * ldc + n;
-          } else if constexpr (EPI == EPI_GELU_ONLY) {
+    for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = gelu_f(v[e]);
-          } else if constexpr (EPI == EPI_DGELU) {
-            const uint2 pu = *(const uint2*)((const OT*)g.C2 + (long)m * ldc + n);
-            const float pv[4] = {__uint_as_float(pu.x << 16), __uint_as_float(pu.x & 0xffff0000u),
-                                 __uint_as_float(pu.y << 16), __uint_as_float(pu.y & 0xffff0000u)};
-            const unsigned keep = g.thr16 ? drop_keep4(g.seed, g.stream, ((uint64_t)m * (uint64_t)N + n) >> 2, g.thr16) : 0xfu;
+      for (int j = 0; j < 4; ++j) red[((P0 + ii) * 4 + j) * 64 + lane] = acc[P0 + ii][j];
+    bar();
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float a = v[e] * gelu_grad(pv[e]);
-              v[e] = (keep >> e) & 1u ? (g.thr16 ? a * g.drop_scale : a) : 0.f;
-            }
-          }
-          *(uint2*)cp = make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[I0 + ii][j] += red[((I0 + ii) * 4 + j) * 64 + lane];
+    if constexpr (EPI == EPI_ACC_F32) {
+      // park the finished 32x64 f32 rows in LDS (chunk c of row r at c ^ (r & 15)), then add one 256-B row per
+      // instruction: split-K slices atomically, a single slice by read-modify-write
+      float* tl = (float*)(smem + 65536) + wid * 2048;
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int r = 16 * ii + fr, c = 4 * j + fg;
+          *(f32x4_t*)(tl + r * 64 + ((c ^ (r & 15)) << 2)) = acc[I0 + ii][j];
+        }
+      const int n = nw + lane;
+      const int mlo = by * BM;
+      const bool nok = n >= bx * BN;
+      float* C = (float*)g.C;
+      for (int r = 0; r < 32; ++r) {
+        const int m = mw + 32 * G + r;
+        const float v = tl[r * 64 + ((((lane >> 2) ^ (r & 15)) << 2) | (lane & 3))] * alpha;
+        if (nok && m >= mlo) {
+          float* c = C + (long)m * ldc + n;
+          if (nz > 1) atomicAdd(c, v);
+          else *c += v;
         }
       }
-  }
+    } else {
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int m = mw + 16 * (I0 + ii) + fr, n = nw + 16 * j + 4 * fg;
+          f32x4_t v = acc[I0 + ii][j] * alpha + bv[j];
+          OT* cp = (OT*)g.C + (long)m * ldc + n;
+          if constexpr (sizeof(OT) == 4) {
+            *(f32x4_t*)cp = v;
+          } else {
+            if constexpr (EPI == EPI_GELU) {
+              *(uint2*)cp = make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));  // pre-activation
+              const unsigned keep =
+                  g.thr16 ? drop_keep4(g.seed, g.stream, ((uint64_t)m * (uint64_t)N + n) >> 2, g.thr16) : 0xfu;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const float a = gelu_f(v[e]);
+                v[e] = (keep >> e) & 1u ? (g.thr16 ? a * g.drop_scale : a) : 0.f;
+              }
+              cp = (OT*)g.C2 + (long)m * ldc + n;
+            } else if constexpr (EPI == EPI_GELU_ONLY) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = gelu_f(v[e]);
+            } else if constexpr (EPI == EPI_DGELU) {
+              const uint2 pu = pre[ii][j];
+              const float pv[4] = {__uint_as_float(pu.x << 16), __uint_as_float(pu.x & 0xffff0000u),
+                                   __uint_as_float(pu.y << 16), __uint_as_float(pu.y & 0xffff0000u)};
+              const unsigned keep =
+                  g.thr16 ? drop_keep4(g.seed, g.stream, ((uint64_t)m * (uint64_t)N + n) >> 2, g.thr16) : 0xfu;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const float a = v[e] * gelu_grad(pv[e]);
+                v[e] = (keep >> e) & 1u ? (g.thr16 ? a * g.drop_scale : a) : 0.f;
+              }
+            }
+            *(uint2*)cp = make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
+          }
+        }
+    }
+  };
+  if (grp == 0) finish(IC<0>{});
+  else finish(IC<1>{});
   STAMP(NSTAMP - 1);
 }
 
