@@ -5,6 +5,7 @@ with the residual stream, LayerNorm statistics and softmax log-sum-exps in fp32.
 from __future__ import annotations
 
 import math
+import weakref
 
 import torch
 import torch.nn.functional as F
@@ -354,6 +355,13 @@ class DecoderBlockFn(torch.autograd.Function):
 
 
 # --------------------------------------------------------------------------------------- head
+# bf16 mode: the KL backward writes its logits gradient straight in bf16 for the head backward (the head GEMMs
+# run on bf16 operands) instead of an fp32 [B*L, V] tensor plus a cast pass. The hand-over is keyed by the
+# address of a live HeadFn output; autograd sees a stride-0 zero gradient on that path.
+_head_outputs: dict = {}     # data_ptr -> weakref to a HeadFn output (bf16 mode)
+_dlogits_bf16: dict = {}     # data_ptr -> bf16 gradient left by KLFn.backward
+
+
 class HeadFn(torch.autograd.Function):
     """logits = h W^T + b in fp32 (models/denoise_decoder.py:286)."""
 
@@ -363,15 +371,28 @@ class HeadFn(torch.autograd.Function):
         logits = ops.linear(xT, w, bias, out_dtype=F32)
         ctx.save_for_backward(xT, weight)
         ctx.bias = (bias,)
+        ctx.out_ptr = logits.data_ptr()
+        if xT.dtype == torch.bfloat16:
+            for k in [k for k, r in _head_outputs.items() if r() is None]:   # outputs freed without a backward
+                _head_outputs.pop(k, None)
+                _dlogits_bf16.pop(k, None)
+            _head_outputs[ctx.out_ptr] = weakref.ref(logits)
         return logits
 
     @staticmethod
     def backward(ctx, dlogits):
         xT, weight = ctx.saved_tensors
-        dl = dlogits.contiguous()
-        if xT.dtype == torch.bfloat16 and dl.dtype == F32:
-            # one cast pass, then both head GEMMs take the bf16 LDS-DMA paths (dx: K = vocab, dW: K = tokens)
-            dl = ops.cast(dl, torch.bfloat16)
+        _head_outputs.pop(ctx.out_ptr, None)
+        dz16 = _dlogits_bf16.pop(ctx.out_ptr, None)
+        if dz16 is not None and all(st == 0 for st in dlogits.stride()):
+            dl = dz16                                     # the KL gradient alone, already bf16
+        elif dz16 is not None:
+            dl = (dlogits + dz16.view(dlogits.shape)).to(torch.bfloat16).contiguous()  # + L_fd's contribution
+        else:
+            dl = dlogits.contiguous()
+            if xT.dtype == torch.bfloat16 and dl.dtype == F32:
+                # one cast pass, then both head GEMMs take the bf16 LDS-DMA paths (dx: K = vocab, dW: K = tokens)
+                dl = ops.cast(dl, torch.bfloat16)
         w = rt.wt(weight)
         dx = ops.linear_dx(dl, w)
         dW, aw = _gdst(weight)
@@ -402,6 +423,14 @@ class KLFn(torch.autograd.Function):
         l2, xt, x0, t, w, betas = ctx.saved_tensors
         B, L, V = ctx.shape
         gs = g.reshape(1).to(F32).contiguous()
+        ptr = l2.data_ptr()
+        ref = _head_outputs.get(ptr)
+        owner = ref() if ref is not None else None
+        if owner is not None and owner.data_ptr() == ptr and ptr not in _dlogits_bf16:
+            # logits of a live bf16-mode HeadFn: hand it the gradient in bf16 (HeadFn.backward picks it up)
+            _dlogits_bf16[ptr] = ops.kl_bwd(l2, xt.reshape(-1).contiguous(), x0.reshape(-1).contiguous(),
+                                            t.contiguous(), betas, w, gs, L, out_dtype=torch.bfloat16)
+            return torch.zeros((), device=l2.device, dtype=F32).expand(B, L, V), None, None, None, None, None
         dz = ops.kl_bwd(l2, xt.reshape(-1).contiguous(), x0.reshape(-1).contiguous(), t.contiguous(), betas, w, gs, L)
         return dz.view(B, L, V), None, None, None, None, None
 

@@ -189,3 +189,44 @@ def test_train_step_fp32_matches_reference(tag, geom, V, d, H, NL, FF, Tn, monke
         if "p." + n in g and "in_proj_bias" not in n:
             err = (p.double() - T(g["p." + n]).double()).abs()
             assert (err > 4e-6).float().mean().item() < 0.02, n
+
+
+@pytest.mark.parametrize("with_lfd", [False, True])
+def test_bf16_kl_gradient_handover_matches_fp32_gradient_path(with_lfd):
+    """bf16 mode hands the KL's logits gradient to the head backward in bf16 (functions.KLFn / HeadFn);
+    the decoder gradients must equal those of the plain path (fp32 dlogits through autograd, cast in the
+    head backward) — alone and summed with an L_fd-style second consumer of the logits."""
+    from fddm_hip import functions as FN
+    from fddm_hip import runtime as rt_
+    from fddm.sched.diffusion_scheduler import DiscreteDiffusionScheduler
+    import train as T_
+    gen = torch.Generator().manual_seed(5)
+    V, d, B, L, S = 1000, 128, 2, 16, 20
+    xt = torch.randint(1, V, (B, L), generator=gen).to(dev)
+    x0 = torch.randint(1, V, (B, L), generator=gen).to(dev)
+    t = torch.tensor([3, 7]).to(dev)
+    cond = torch.randn(B, S, d, generator=gen).to(dev)
+    R = torch.randn(B, L, V, generator=gen).to(dev)
+    sch = T_.SchedulerAdapter(DiscreteDiffusionScheduler(K=V, T=10, device=dev))
+    grads = []
+    for handover in (True, False):
+        with rt_.use_precision("bf16"):
+            dec = make_decoder(V, d, 2, 2, 256)
+            dec.train()
+            if not handover:
+                saved = FN._head_outputs
+                FN._head_outputs = type("NoReg", (dict,), {"__setitem__": lambda self, k, v: None})()
+            try:
+                logits = dec(xt, t, cond)
+                loss = sch.kl_term(xt, x0, logits, t)
+                if with_lfd:
+                    loss = loss + 1e-3 * (logits * R).sum()
+                loss.backward()
+            finally:
+                if not handover:
+                    FN._head_outputs = saved
+            grads.append({n: p.grad.detach().clone() for n, p in dec.named_parameters() if p.grad is not None})
+    assert grads[0].keys() == grads[1].keys()
+    for n in grads[0]:
+        close(grads[0][n], grads[1][n], rtol=2e-2, atol=1e-6, what=n)
+    assert any(g.abs().max().item() > 0 for g in grads[0].values())
