@@ -145,6 +145,9 @@ struct AttnArgs {
   const unsigned char* key_keep;  // [B][Lk] or null
   const float* gate;              // [B*H][Lq] or null (WavLM)
   const float* table;             // [H][2*Lk-1]
+  const void* graw;               // WavLM gate pre-activations (bf16) at graw + (b*Lq + q)*sgr + h*8 + o, or null
+  long sgr;
+  const float* gconst;            // [H] gru_rel_pos_const
   int B, H, Lq, Lk;
   float scale;
   uint64_t seed, stream;
@@ -272,6 +275,16 @@ __global__ void __launch_bounds__(256, ATTN_FWD_WPS) fwd2_kernel(AttnArgs a) {
     qv[gq] = q[gq] < a.Lq;
     row_frags<bf16_t>(qf[gq], Qb, a.sq, qv[gq] ? q[gq] : 0, qv[gq], lane);
     gate[gq] = (a.gate && qv[gq]) ? a.gate[(long)bh * a.Lq + q[gq]] : 0.f;
+    if (REL && a.graw && qv[gq]) {
+      // gate from the 8 pre-activations the Q|K|V projection appended (HF modeling_wavlm.py:177-186)
+      const uint4 u = *(const uint4*)((const bf16_t*)a.graw + ((long)b * a.Lq + q[gq]) * a.sgr + h * 8);
+      const float ra = bf2f((bf16_t)(u.x & 0xffff)) + bf2f((bf16_t)(u.x >> 16)) + bf2f((bf16_t)(u.y & 0xffff)) +
+                       bf2f((bf16_t)(u.y >> 16));
+      const float rb = bf2f((bf16_t)(u.z & 0xffff)) + bf2f((bf16_t)(u.z >> 16)) + bf2f((bf16_t)(u.w & 0xffff)) +
+                       bf2f((bf16_t)(u.w >> 16));
+      const float ga = 1.f / (1.f + __expf(-ra)), gb = 1.f / (1.f + __expf(-rb));
+      gate[gq] = ga * (gb * a.gconst[h] - 1.f) + 2.f;
+    }
   }
   // tile loader: 512 16-B chunks of K and of V per tile, 2 each per thread
   uint4 kr[2], vr[2];
@@ -991,7 +1004,7 @@ static int run(int which, AttnArgs& a, hipStream_t s) {
       if (!getenv("FDDM_ATTN_V1")) {
         dim3 grid((a.Lq + 127) / 128, a.B * a.H);
         const bool drop = a.thr16 != 0, mask = a.key_keep != nullptr || (a.Lk % 64) != 0;
-        const bool rel = a.table != nullptr && a.gate != nullptr;
+        const bool rel = a.table != nullptr && (a.gate != nullptr || a.graw != nullptr);
 #define FWD2(D, M, R) hipLaunchKernelGGL((fwd2_kernel<D, M, R>), grid, dim3(256), 0, s, a)
         if (rel) {
           if (drop) { if (mask) FWD2(true, true, true); else FWD2(true, false, true); }
@@ -1077,6 +1090,20 @@ FDDM_API int fddm_attn_fwd(int dtype, const void* Q, long sq, const void* K, lon
   a.key_keep = key_keep; a.gate = gate; a.table = table;
   a.B = B; a.H = H; a.Lq = Lq; a.Lk = Lk; a.scale = scale; a.seed = seed; a.stream = stream;
   return attn_dispatch(0, dtype, a, drop_p, hs);
+}
+
+// WavLM forward with the gate computed in the kernel from 8 bf16 pre-activations per (token, head) that the Q|K|V
+// projection appended as extra columns (graw, row stride sgr; gconst [H]): no separate gate pass over the input.
+FDDM_API int fddm_attn_fwd_relgate(const void* Q, long sq, const void* K, long sk, const void* V, long sv, void* O,
+                                   long so, const void* graw, long sgr, const float* gconst, const float* table, int B,
+                                   int H, int Lq, int Lk, float scale, void* hs) {
+  if (!graw || !gconst || !table || (((uintptr_t)graw) & 15) || sgr % 8) return (int)hipErrorInvalidValue;
+  AttnArgs a{};
+  a.Q = Q; a.K = K; a.V = V; a.Out = O;
+  a.sq = sq; a.sk = sk; a.sv = sv; a.so = so;
+  a.graw = graw; a.sgr = sgr; a.gconst = gconst; a.table = table;
+  a.B = B; a.H = H; a.Lq = Lq; a.Lk = Lk; a.scale = scale;
+  return attn_dispatch(0, FDDM_BF16, a, 0.f, hs);
 }
 
 // Backward: dQ (query-owned kernel) and dK/dV (key-owned kernel). lse from the forward.

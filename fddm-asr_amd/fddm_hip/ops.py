@@ -182,6 +182,17 @@ def attn_fwd(q, k, v, out, lse, B, H, Lq, Lk, *, key_keep=None, gate=None, table
     return out
 
 
+def attn_fwd_relgate(q, k, v, out, graw, gconst, table, B, H, L, scale=None):
+    """WavLM attention (bf16) with the gate computed in the kernel from graw [B*L, >= H*8] (row stride
+    graw.stride(0)): 8 gru_rel_pos_linear pre-activations per (token, head)."""
+    _chk(q.dtype == k.dtype == v.dtype == out.dtype == graw.dtype == torch.bfloat16, "relgate attention is bf16")
+    _chk(graw.stride(-1) == 1 and graw.shape[1] >= H * 8 and graw.data_ptr() % 16 == 0, "graw layout")
+    sc = 1.0 / math.sqrt(64) if scale is None else scale
+    call("fddm_attn_fwd_relgate", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out),
+         out.stride(0), ptr(graw), graw.stride(0), ptr(gconst), ptr(table), B, H, L, L, float(sc), stream())
+    return out
+
+
 def attn_bwd(q, k, v, o, do, lse, dq, dk, dv, B, H, Lq, Lk, *, key_keep=None, drop_p=0.0, seed=0, rng_stream=0,
              dbits=None):
     delta = torch.empty(B * H, Lq, device=q.device, dtype=torch.float32)

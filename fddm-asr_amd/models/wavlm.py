@@ -119,11 +119,23 @@ class WavLMModel(nn.Module):
             P["pos"] = (T(w.view(G, Cg, Cg, -1).permute(0, 1, 3, 2)), pc.bias.detach().float().contiguous())
             P["enc_ln"] = (self.encoder.layer_norm.weight.detach().float(), self.encoder.layer_norm.bias.detach().float())
             layers = []
+            H = c.num_attention_heads
             for L in self.encoder.layers:
                 a = L.attention
+                qkv_w = [a.q_proj.weight, a.k_proj.weight, a.v_proj.weight]
+                qkv_b = [a.q_proj.bias, a.k_proj.bias, a.v_proj.bias]
+                if cd == torch.bfloat16:
+                    # gate pre-activations of every head as 8*H extra output columns (block-diagonal copies of
+                    # gru_rel_pos_linear), consumed by the attention kernel (no separate gate pass)
+                    gw = a.gru_rel_pos_linear.weight.detach().float()
+                    blk = torch.zeros(8 * H, E, device=gw.device, dtype=torch.float32)
+                    for h in range(H):
+                        blk[8 * h:8 * h + 8, h * (E // H):(h + 1) * (E // H)] = gw
+                    qkv_w = qkv_w + [blk]
+                    qkv_b = qkv_b + [a.gru_rel_pos_linear.bias.detach().float().repeat(H)]
                 layers.append(dict(
-                    qkv=T(torch.cat([a.q_proj.weight, a.k_proj.weight, a.v_proj.weight], 0)),
-                    bqkv=torch.cat([a.q_proj.bias, a.k_proj.bias, a.v_proj.bias], 0).detach().float().contiguous(),
+                    qkv=T(torch.cat([w.detach().float() for w in qkv_w], 0)),
+                    bqkv=torch.cat([b.detach().float() for b in qkv_b], 0).contiguous(),
                     o=(T(a.out_proj.weight), a.out_proj.bias.detach().float()),
                     gru=(a.gru_rel_pos_linear.weight.detach().float().contiguous(),
                          a.gru_rel_pos_linear.bias.detach().float().contiguous(),
@@ -187,10 +199,13 @@ class WavLMModel(nn.Module):
         table = rt.relbias_table(S, self.encoder.layers[0].attention.rel_attn_embed.weight, c.num_buckets,
                                  c.max_bucket_distance)
         for Lp in P["layers"]:
-            gate = ops.wavlm_gate(x, Lp["gru"][0], Lp["gru"][1], Lp["gru"][2], B, S, H)
             qkv = ops.linear(x, Lp["qkv"], Lp["bqkv"], out_dtype=cd)
             o = torch.empty(B * S, E, device=wave.device, dtype=cd)
-            ops.attn_fwd(qkv, qkv[:, E:], qkv[:, 2 * E:], o, None, B, H, S, S, gate=gate, table=table)
+            if cd == torch.bfloat16:
+                ops.attn_fwd_relgate(qkv, qkv[:, E:], qkv[:, 2 * E:], o, qkv[:, 3 * E:], Lp["gru"][2], table, B, H, S)
+            else:
+                gate = ops.wavlm_gate(x, Lp["gru"][0], Lp["gru"][1], Lp["gru"][2], B, S, H)
+                ops.attn_fwd(qkv, qkv[:, E:], qkv[:, 2 * E:], o, None, B, H, S, S, gate=gate, table=table)
             y = ops.linear(o, Lp["o"][0], Lp["o"][1], out_dtype=cd)
             x1 = torch.empty_like(x)
             ops.ln_fwd(x, y, Lp["ln1"][0], Lp["ln1"][1], out_t=x1, eps=eps)

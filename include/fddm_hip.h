@@ -78,6 +78,12 @@ int fddm_attn_fwd(int dtype, const void* Q, long sq, const void* K, long sk, con
                   float* lse, const unsigned char* key_keep, const float* gate, const float* table, int B, int H,
                   int Lq, int Lk, float scale, float drop_p, unsigned long long seed, unsigned long long stream,
                   unsigned long long* drop_bits, void* hip_stream);
+/* WavLM variant (bf16): the gate is computed in the kernel from the 8 gru_rel_pos_linear pre-activations per
+ * (token, head) stored at graw + (b*Lq+q)*sgr + h*8 (bf16, appended to the Q|K|V projection's output) and
+ * gconst [H] (gru_rel_pos_const) — HF modeling_wavlm.py:177-186. */
+int fddm_attn_fwd_relgate(const void* Q, long sq, const void* K, long sk, const void* V, long sv, void* O, long so,
+                          const void* graw, long sgr, const float* gconst, const float* table, int B, int H, int Lq,
+                          int Lk, float scale, void* hip_stream);
 int fddm_attn_bwd(int dtype, const void* Q, long sq, const void* K, long sk, const void* V, long sv, const void* O,
                   long so, const void* dO, long sdo, const float* lse, void* dQ, long sdq, void* dK, long sdk,
                   void* dV, long sdv, float* delta_ws, const unsigned char* key_keep, int B, int H, int Lq, int Lk,

@@ -423,6 +423,42 @@ def test_attention_relbias(dtype):
     close(od.float(), ref.transpose(1, 2).reshape(B * S, D), rtol=TOL[dtype], what="relbias attn")
 
 
+@pytest.mark.parametrize("S", [75, 499])
+def test_attention_relgate_matches_gate_kernel_path(S):
+    """WavLM attention with the gate computed in the kernel from 8 bf16 pre-activations per (token, head)
+    appended to the projection output (fddm_attn_fwd_relgate) vs the two-pass path (fddm_wavlm_gate +
+    fddm_attn_fwd) and vs float64 torch on the same bf16 inputs."""
+    o = ops()
+    B, H, E = 2, 12, 768
+    gen = torch.Generator(device=dev).manual_seed(40)
+    x = torch.randn(B * S, E, device=dev, generator=gen).bfloat16()
+    qkv = torch.randn(B * S, 3 * E, device=dev, generator=gen).bfloat16()
+    W = torch.randn(8, 64, device=dev, generator=gen) * 0.2
+    bias = torch.randn(8, device=dev, generator=gen) * 0.1
+    cst = torch.rand(H, device=dev, generator=gen) + 0.5
+    table = torch.randn(H, 2 * S - 1, device=dev, generator=gen)
+    # pre-activations as the fused projection produces them (bf16)
+    graw = torch.einsum("nhd,od->nho", x.float().view(B * S, H, 64), W) + bias
+    buf = torch.zeros(B * S, 3 * E + 8 * H + 8, device=dev, dtype=torch.bfloat16)   # padded row stride
+    buf[:, :3 * E] = qkv
+    buf[:, 3 * E:3 * E + 8 * H] = graw.reshape(B * S, 8 * H).bfloat16()
+    out = torch.empty(B * S, E, device=dev, dtype=torch.bfloat16)
+    o.attn_fwd_relgate(buf, buf[:, E:], buf[:, 2 * E:], out, buf[:, 3 * E:], cst, table, B, H, S)
+    gate = o.wavlm_gate(x, W, bias, cst, B, S, H)
+    out2 = torch.empty_like(out)
+    o.attn_fwd(qkv, qkv[:, E:], qkv[:, 2 * E:], out2, None, B, H, S, S, gate=gate, table=table)
+    close(out.float(), out2.float(), rtol=2e-2, what="relgate vs gate kernel")
+    r = buf[:, 3 * E:3 * E + 8 * H].double().view(B, S, H, 8)
+    ga, gb = torch.sigmoid(r[..., :4].sum(-1)), torch.sigmoid(r[..., 4:].sum(-1))
+    gref = (ga * (gb * cst.double() - 1) + 2).permute(0, 2, 1)                      # [B, H, S]
+    hv = lambda t: t.double().view(B, S, H, 64).transpose(1, 2)  # noqa: E731
+    q_, k_, v_ = hv(qkv[:, :E]), hv(qkv[:, E:2 * E]), hv(qkv[:, 2 * E:])
+    rel = torch.arange(S, device=dev)[None, :] - torch.arange(S, device=dev)[:, None] + S - 1   # key - query + S-1
+    sc = q_ @ k_.transpose(-1, -2) / 8.0 + gref[..., None] * table.double()[:, rel][None]
+    ref = torch.softmax(sc, -1) @ v_
+    close(out.float(), ref.transpose(1, 2).reshape(B * S, E), rtol=2e-2, what="relgate vs float64")
+
+
 # ----------------------------------------------------------------------------- LN / RoPE / embed
 @pytest.mark.parametrize("film", [False, True])
 @pytest.mark.parametrize("L", [20, 32])
