@@ -46,7 +46,10 @@ __device__ __forceinline__ KlRow kl_consts(const float* betas, long tv, long xt,
   return c;
 }
 
-// NPT = row elements held per thread (V <= 256 * NPT)
+// NPT = row elements held per thread (V <= 256 * NPT).
+// Every index k other than x_t and x0 has M_k = b_t and Q_k = Qg = b_t b_p / dq, so the row pass evaluates that
+// generic form for all k (one log per element forward; one rcp per element backward, kept in registers for the
+// output pass) and the at most two special indices are corrected with scalar terms afterwards.
 template <int NPT, bool BWD, typename OT>
 __global__ void __launch_bounds__(256) kl_kernel(const float* __restrict__ logits, const long* __restrict__ xt_,
                                                  const long* __restrict__ x0_, const long* __restrict__ t_,
@@ -79,32 +82,71 @@ __global__ void __launch_bounds__(256) kl_kernel(const float* __restrict__ logit
   s = block_sum(s, red);
   const float inv_s = 1.f / s;
   const float xhat_xt = __expf(z[xt] - mx) * inv_s;
+  const float xhat_x0 = __expf(z[x0] - mx) * inv_s;
   const float dp = c.b_t + c.a_t * xhat_xt;
   const float inv_dp = 1.f / (dp + eps);
-  // pass over the row: KL, S1 = sum Q P/(P+eps), G0 = sum g0 xhat
-  float kl = 0.f, s1 = 0.f, g0s = 0.f;
+  const float Qg = c.b_t * c.b_p * c.inv_dq;
+  // the exact per-index terms (P, Q, KL term, S1 term, g0 term) of index k with normalised probability xh
+  auto special = [&](long k, float xh, float& P, float& Q, float& M) {
+    M = c.b_t + (k == xt ? c.a_t : 0.f);
+    Q = M * ((k == x0 ? c.a_p : 0.f) + c.b_p) * c.inv_dq;
+    P = M * (c.a_p * xh + c.b_p) * inv_dp;
+  };
+  auto generic_P = [&](float xh) { return c.b_t * (c.a_p * xh + c.b_p) * inv_dp; };
+
+  if (!BWD) {
+    // KL = sum_k Q (log(Q+eps) - log(P+eps)): generic form for all k, then the special indices swapped in
+    const float LQg = __logf(Qg + eps);
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) {
+      const long k = tid + 256L * i;
+      if (k < V) acc += LQg - __logf(generic_P(v[i] * inv_s) + eps);
+    }
+    acc = block_sum(acc, red);
+    if (tid == 0) {
+      float kl = Qg * acc;
+      const long ks[2] = {xt, x0};
+      const float xs[2] = {xhat_xt, xhat_x0};
+      for (int j = 0; j < (xt == x0 ? 1 : 2); ++j) {
+        float P, Q, M;
+        special(ks[j], xs[j], P, Q, M);
+        kl += Q * (__logf(Q + eps) - __logf(P + eps)) - Qg * (LQg - __logf(generic_P(xs[j]) + eps));
+      }
+      kl_tok[row] = kl;
+    }
+    return;
+  }
+  // backward: S1 = sum Q P/(P+eps), G0 = sum -Q M a_p/(P+eps) inv_dp xh
+  float r[NPT];
+  float a1 = 0.f, a2 = 0.f;
 #pragma unroll
   for (int i = 0; i < NPT; ++i) {
     const long k = tid + 256L * i;
+    const float xh = v[i] * inv_s;
+    v[i] = xh;
+    const float P = generic_P(xh);
+    r[i] = 1.f / (P + eps);
     if (k < V) {
-      const float xh = v[i] * inv_s;
-      const float M = c.b_t + (k == xt ? c.a_t : 0.f);
-      const float Q = M * ((k == x0 ? c.a_p : 0.f) + c.b_p) * c.inv_dq;
-      const float P = M * (c.a_p * xh + c.b_p) * inv_dp;
-      const float rP = 1.f / (P + eps);
-      kl += Q * (__logf(Q + eps) - __logf(P + eps));
-      s1 += Q * P * rP;
-      if (BWD) g0s += -Q * M * c.a_p * rP * inv_dp * xh;
-      v[i] = xh;
+      a1 += P * r[i];
+      a2 += xh * r[i];
     }
   }
-  if (!BWD) {
-    kl = block_sum(kl, red);
-    if (tid == 0) kl_tok[row] = kl;
-    return;
+  a1 = block_sum(a1, red);
+  a2 = block_sum(a2, red);
+  const float gc = -Qg * c.b_t * c.a_p * inv_dp;  // generic g0 factor: g0_k = gc * xh_k / (P_k + eps)
+  float s1 = Qg * a1, g0s = gc * a2;
+  {
+    const long ks[2] = {xt, x0};
+    const float xs[2] = {xhat_xt, xhat_x0};
+    for (int j = 0; j < (xt == x0 ? 1 : 2); ++j) {
+      float P, Q, M;
+      special(ks[j], xs[j], P, Q, M);
+      const float Pg = generic_P(xs[j]);
+      s1 += Q * P / (P + eps) - Qg * Pg / (Pg + eps);
+      g0s += -Q * M * c.a_p / (P + eps) * inv_dp * xs[j] - gc * xs[j] / (Pg + eps);
+    }
   }
-  s1 = block_sum(s1, red);
-  g0s = block_sum(g0s, red);
   const float gxt = c.a_t * s1 * inv_dp;
   const float G = g0s + xhat_xt * gxt;
   const float wr = w[row] * (gscale ? gscale[0] : 1.f);
@@ -114,10 +156,12 @@ __global__ void __launch_bounds__(256) kl_kernel(const float* __restrict__ logit
     const long k = tid + 256L * i;
     if (k < V) {
       const float xh = v[i];
-      const float M = c.b_t + (k == xt ? c.a_t : 0.f);
-      const float Q = M * ((k == x0 ? c.a_p : 0.f) + c.b_p) * c.inv_dq;
-      const float P = M * (c.a_p * xh + c.b_p) * inv_dp;
-      float g = -Q * M * c.a_p / (P + eps) * inv_dp + (k == xt ? gxt : 0.f);
+      float g = gc * r[i];
+      if (k == xt || k == x0) {
+        float P, Q, M;
+        special(k, xh, P, Q, M);
+        g = -Q * M * c.a_p / (P + eps) * inv_dp + (k == xt ? gxt : 0.f);
+      }
       st<OT>(out + k, wr * xh * (g - G));
     }
   }

@@ -570,6 +570,31 @@ def test_sampler_bit_exact_and_kl():
     close(dz.view(Bk, Lk, Vk), 2 * T(gk["dlogits"]), rtol=1e-4, atol=1e-10, what="kl grad")
 
 
+def test_kl_full_vocab_matches_oracle():
+    """C2 vocabulary (V=8000): the kernel's generic-index form with the x_t / x0 corrections vs the closed form
+    over every index (oracle, fp32), incl. t=1 (beta_p = 0), t=T, x_t == x0 rows and a masked row."""
+    o = ops()
+    K, Tn, B, L = 8000, 200, 4, 256
+    betas, _ = O.sched_tables(Tn)
+    logits = 3.0 * torch.randn(B, L, K, generator=g(70))
+    x0 = torch.randint(1, K, (B, L), generator=g(71))
+    xt = torch.randint(1, K, (B, L), generator=g(72))
+    xt[:, ::3] = x0[:, ::3]
+    t = torch.tensor([1, 2, 117, 200])
+    xm = torch.ones(B, L, dtype=torch.bool)
+    xm[2, 200:] = False
+    ref_loss, ref_dz = O.kl_term(logits, xt, x0, t, xm, betas)
+    valid = xm.float()
+    w = (valid / (valid.sum(1, keepdim=True) + 1e-8) / B).reshape(-1)
+    kl_tok = o.kl_fwd(logits.view(-1, K).to(dev), xt.reshape(-1).to(dev), x0.reshape(-1).to(dev), t.to(dev),
+                      betas.to(dev), L)
+    close((kl_tok.cpu() * w).sum(), ref_loss, rtol=1e-4, what="kl loss V=8000")
+    dz = o.kl_bwd(logits.view(-1, K).to(dev), xt.reshape(-1).to(dev), x0.reshape(-1).to(dev), t.to(dev),
+                  betas.to(dev), w.to(dev), None, L)
+    err = (dz.view(B, L, K).cpu() - ref_dz).abs().max() / ref_dz.abs().max()
+    assert err < 1e-4, f"kl grad V=8000 rel err {err:.2e}"
+
+
 def test_lfd_kernels_match_reference():
     from helpers import load, T
     from fddm_hip import runtime as rt
