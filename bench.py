@@ -103,6 +103,37 @@ def dominant_flops(args):
     return 2.0 * args.batch * T1 * 512 * 3 * 512
 
 
+def encoder_frames(seconds):
+    n = int(16000 * seconds)
+    for k, st in zip((10, 3, 3, 3, 3, 2, 2), (5, 2, 2, 2, 2, 2, 2)):
+        n = (n - k) // st + 1
+    return n
+
+
+ATTN_PROBES = ("decoder.self_attn_fwd", "decoder.cross_attn_fwd", "decoder.self_attn_bwd", "decoder.cross_attn_bwd")
+
+
+def decoder_attention(args, probes, peak):
+    """Decoder attention launches timed with HIP events on their stream: algorithmic FLOPs per launch (dense
+    Lq x Lk scores, head_dim = d_model / heads; forward 4 Lq Lk dh, backward 10 Lq Lk dh per (b, h): QK^T
+    recompute, dP, dQ, dK, dV) / average launch time, against the dense bf16 MFMA peak (BASELINE north_star:
+    >= 30 % on the decoder attention)."""
+    L, S = args.seq_len, encoder_frames(args.seconds)
+    dh = args.d_model // args.heads
+    out = {}
+    for name in ATTN_PROBES:
+        ev = probes.get(name) or []
+        if not ev:
+            continue
+        ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+        lk = L if "self" in name else S
+        fl = (10 if name.endswith("bwd") else 4) * args.batch * args.heads * L * lk * dh
+        tf = fl / (ms * 1e-3) / 1e12
+        out[name.split(".", 1)[1]] = {"avg_us": round(1e3 * ms, 1), "gflop_per_launch": round(fl / 1e9, 3),
+                                      "tflops": round(tf, 1), "frac": round(tf / peak, 4), "launches": len(ev)}
+    return out
+
+
 def cpu_baseline(args, models):
     """The CPU oracle (plain torch fp32 restatement of the reference step) timed on the host cores on a
     bounded sample: 2 utterances of the same geometry, `cpu_steps` steps (kind "port")."""
@@ -160,7 +191,7 @@ def main():
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    with rt.probing(["wavlm.conv1"]) as probes:   # HIP events around the dominant launch, on its stream
+    with rt.probing(["wavlm.conv1", *ATTN_PROBES]) as probes:   # HIP events around the dominant launch, on its stream
         gs, avg_loss = T_.train_one_epoch(enc, dec, sp, te, tp, sch, loader_t, opt, device, cfg, gs, None, 1, False)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
@@ -197,6 +228,7 @@ def main():
                          "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_unit": "B/launch",
                          "traffic_source": traffic_src, "avg_ms": round(kms, 4),
                          "launches_timed": len(ev), "flops_per_launch": kflops},
+            "decoder_attention": decoder_attention(args, probes, peak),
             "step_mfma_frac": round(step_tflops / peak, 4),
             "step_tflops": round(step_tflops, 1),
             "avg_loss": round(avg_loss, 4),

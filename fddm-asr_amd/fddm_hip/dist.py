@@ -9,6 +9,64 @@ import torch
 import torch.distributed as dist
 
 BUCKET_BYTES = 64 << 20
+OVERLAP_BUCKET_BYTES = 16 << 20
+
+
+class OverlapReducer:
+    """Gradient all-reduce overlapped with backward (BASELINE configs[2]: "grad all-reduce overlap").
+
+    The grad arena's slots are laid out in the order backward finalises them (runtime.GradArena `order`:
+    head, last decoder block, ..., first block, then FiLM / embeddings / time MLP). Backward Functions call
+    runtime.grads_ready(params) once they have enqueued everything that accumulates into those slots; the
+    reducer then tracks the finished prefix of the arena and, whenever it has grown by a bucket, enqueues an
+    async all-reduce of that slice. RCCL orders the collective after the kernels already on the compute
+    stream and runs it on its own stream, so it proceeds under the remaining blocks' backward. `finish()`
+    (from allreduce_grads, after backward) launches the tail, makes the compute stream wait for every slice
+    and averages. All ranks run the same backward sequence, so they issue identical collectives in the same
+    order."""
+
+    def __init__(self, arena, bucket_bytes: int = OVERLAP_BUCKET_BYTES):
+        self.arena = arena
+        self.bucket = max(1, bucket_bytes // 4)
+        self.W = world()
+        self.reset()
+        arena.on_ready = self.on_ready
+        arena.reducer = self
+
+    def reset(self):
+        self.ready = [False] * len(self.arena.params)
+        self.next = 0
+        self.launched = 0
+        self.works = []
+
+    def on_ready(self, params):
+        a = self.arena
+        for p in params:
+            i = a.slot.get(id(p))
+            if i is not None:
+                self.ready[i] = True
+        while self.next < len(self.ready) and self.ready[self.next]:
+            self.next += 1
+        hi = a.offs[self.next]
+        if hi - self.launched >= self.bucket:
+            self._launch(hi)
+
+    def _launch(self, hi):
+        lo = self.launched
+        if hi <= lo:
+            return
+        sl = self.arena.flat[lo:hi]
+        self.works.append((dist.all_reduce(sl, op=dist.ReduceOp.SUM, async_op=True), sl))
+        self.launched = hi
+
+    def finish(self):
+        n = self.arena.offs[-1]
+        while self.launched < n:
+            self._launch(min(n, self.launched + self.bucket))
+        for w, sl in self.works:
+            w.wait()
+            sl.mul_(1.0 / self.W)
+        self.reset()
 
 
 def world() -> int:
@@ -22,8 +80,12 @@ def allreduce_grads(params, bucket_bytes: int = BUCKET_BYTES) -> None:
         return
     params = list(params)
     arena = next((a for a in (getattr(p, "_fddm_arena", None) for p in params) if a is not None), None)
-    if arena is not None and all(p.grad is not None and p.grad.data_ptr() == v.data_ptr()
-                                 for p, v in zip(arena.params, arena.views)):
+    if arena is not None and getattr(arena, "reducer", None) is not None:
+        arena.reducer.finish()     # slices already in flight since backward; launch the tail, wait
+        inside = set(id(p) for p in arena.params)
+        params = [p for p in params if id(p) not in inside]
+    elif arena is not None and all(p.grad is not None and p.grad.data_ptr() == v.data_ptr()
+                                   for p, v in zip(arena.params, arena.views)):
         # the arena is already flat: all-reduce it in place in bucket-sized slices
         flat = arena.flat
         step = max(1, bucket_bytes // 4)

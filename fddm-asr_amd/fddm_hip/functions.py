@@ -234,8 +234,9 @@ class DecoderBlockFn(torch.autograd.Function):
         o = torch.empty(N, d, device=dev, dtype=cd)
         lse = torch.empty(B * H, L, device=dev, dtype=F32)
         bits_s = ops.drop_bits(B, H, L, L, dev) if p > 0 else None
-        ops.attn_fwd(qk, qk[:, d:], v, o, lse, B, H, L, L, key_keep=key_keep, drop_p=p, seed=seed, rng_stream=st + 1,
-                     dbits=bits_s)
+        with rt.probe("decoder.self_attn_fwd"):
+            ops.attn_fwd(qk, qk[:, d:], v, o, lse, B, H, L, L, key_keep=key_keep, drop_p=p, seed=seed,
+                         rng_stream=st + 1, dbits=bits_s)
         y = ops.linear(o, W["so"], so_b, out_dtype=cd)
         s1 = torch.empty(N, d, device=dev, dtype=F32)
         m1 = torch.empty(N, device=dev, dtype=F32)
@@ -250,7 +251,9 @@ class DecoderBlockFn(torch.autograd.Function):
         oc = torch.empty(N, d, device=dev, dtype=cd)
         lsec = torch.empty(B * H, L, device=dev, dtype=F32)
         bits_c = ops.drop_bits(B, H, L, S, dev) if p > 0 else None
-        ops.attn_fwd(qc, kvc, kvc[:, d:], oc, lsec, B, H, L, S, drop_p=p, seed=seed, rng_stream=st + 3, dbits=bits_c)
+        with rt.probe("decoder.cross_attn_fwd"):
+            ops.attn_fwd(qc, kvc, kvc[:, d:], oc, lsec, B, H, L, S, drop_p=p, seed=seed, rng_stream=st + 3,
+                         dbits=bits_c)
         yc = ops.linear(oc, W["co"], co_b, out_dtype=cd)
         s2 = torch.empty(N, d, device=dev, dtype=F32)
         m2 = torch.empty(N, device=dev, dtype=F32)
@@ -329,8 +332,9 @@ class DecoderBlockFn(torch.autograd.Function):
         dqc = torch.empty(N, d, device=dev, dtype=cd)
         dkvc = torch.empty(B * S, 2 * d, device=dev, dtype=cd)
         bits_s, bits_c = ctx.bits
-        ops.attn_bwd(qc, kvc, kvc[:, d:], oc, doc, lsec, dqc, dkvc, dkvc[:, d:], B, H, L, S, drop_p=p, seed=seed,
-                     rng_stream=st + 3, dbits=bits_c)
+        with rt.probe("decoder.cross_attn_bwd"):
+            ops.attn_bwd(qc, kvc, kvc[:, d:], oc, doc, lsec, dqc, dkvc, dkvc[:, d:], B, H, L, S, drop_p=p, seed=seed,
+                         rng_stream=st + 3, dbits=bits_c)
         dw_jobs += [(dqc, x1T, gca_w[:d], gca_b[:d]), (dkvc, cT, gca_w[d:], gca_b[d:])]
         ops.linear_dx(dqc, W["ca"][:d], out=dx1, accumulate=True)
         # LN1
@@ -343,13 +347,15 @@ class DecoderBlockFn(torch.autograd.Function):
         do = ops.linear_dx(dy, W["so"], out_dtype=cd)
         dqk = torch.empty(N, 2 * d, device=dev, dtype=cd)
         dv = torch.empty(N, d, device=dev, dtype=cd)
-        ops.attn_bwd(qk, qk[:, d:], v, o, do, lse, dqk, dqk[:, d:], dv, B, H, L, L, key_keep=key_keep, drop_p=p,
-                     seed=seed, rng_stream=st + 1, dbits=bits_s)
+        with rt.probe("decoder.self_attn_bwd"):
+            ops.attn_bwd(qk, qk[:, d:], v, o, do, lse, dqk, dqk[:, d:], dv, B, H, L, L, key_keep=key_keep, drop_p=p,
+                         seed=seed, rng_stream=st + 1, dbits=bits_s)
         dw_jobs += [(dqk, xr, gsa_w[: 2 * d], gsa_b[: 2 * d]), (dv, xT, gsa_w[2 * d:], gsa_b[2 * d:])]
         ops.linear_dx(dv, W["sa"][2 * d:], out=dx, accumulate=True)
         dxr = ops.linear_dx(dqk, W["sa"][: 2 * d])
         ops.rope_bwd(dxr, cos, sin, dx, L)
         _dw_flush(dw_jobs)
+        rt.grads_ready(params)
         grads = tuple(_ret(t_, a_) for t_, a_ in G)
         return (dx, None, None, None, dfs, dfh, None) + grads
 
@@ -400,6 +406,7 @@ class HeadFn(torch.autograd.Function):
         if aw != ab:
             raise RuntimeError("head weight and bias must share the grad arena")
         ops.linear_dw(dl, xT, out=dW, accumulate=aw, db=db)
+        rt.grads_ready((weight, ctx.bias[0]))
         return dx, None, _ret(dW, aw), _ret(db, ab)
 
 

@@ -23,10 +23,11 @@ class FusedAdamW(torch.optim.Optimizer):
         self.last_total_sq = None
         self.arena = None
 
-    def use_grad_arena(self, params):
+    def use_grad_arena(self, params, order=None):
         """Back the grads of `params` (parameters that get a gradient every step) by one flat buffer
-        (runtime.GradArena); zero_grad() then zeroes it with a single fill instead of dropping grads."""
-        self.arena = rt.GradArena(params)
+        (runtime.GradArena, slots laid out in `order` if given); zero_grad() then zeroes it with a single fill
+        instead of dropping grads."""
+        self.arena = rt.GradArena(params, order)
         return self.arena
 
     def zero_grad(self, set_to_none: bool = True):

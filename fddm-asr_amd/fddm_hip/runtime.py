@@ -205,16 +205,25 @@ class GradArena:
 
     ALIGN = 64
 
-    def __init__(self, params):
+    def __init__(self, params, order=None):
         self.params = [p for p in params if p.requires_grad]
         if not self.params:
             raise ValueError("empty grad arena")
+        if order is not None:
+            # lay the slots out in the order backward finalises them (head, last block ... first block, rest), so
+            # the DP all-reduce can start on a finished prefix while backward still runs (dist.OverlapReducer)
+            rank = {id(p): i for i, p in enumerate(order)}
+            self.params.sort(key=lambda p: rank.get(id(p), len(rank)))
         offs, n = [], 0
         for p in self.params:
             offs.append(n)
             n += (p.numel() + self.ALIGN - 1) // self.ALIGN * self.ALIGN
         dev = self.params[0].device
         self.flat = torch.zeros(n, device=dev, dtype=torch.float32)
+        self.offs = offs + [n]
+        self.slot = {id(p): i for i, p in enumerate(self.params)}
+        self.on_ready = None     # set by dist.OverlapReducer (DP runs): called by grads_ready()
+        self.reducer = None
         self.views = []
         for p, o in zip(self.params, offs):
             v = self.flat[o:o + p.numel()].view_as(p)
@@ -231,6 +240,16 @@ class GradArena:
     def zero_(self):
         self.attach()
         self.flat.zero_()
+
+
+def grads_ready(params) -> None:
+    """Called by a backward Function once the gradients of `params` are final for this step (everything that
+    accumulates into their arena slots has been enqueued on the current stream)."""
+    for p in params:
+        a = getattr(p, "_fddm_arena", None)
+        if a is not None and a.on_ready is not None:
+            a.on_ready(params)
+            return
 
 
 def grad_slot(p: torch.Tensor):

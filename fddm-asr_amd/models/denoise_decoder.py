@@ -186,6 +186,16 @@ class DenoisingTransformerDecoder(nn.Module):
         logits = FN.HeadFn.apply(x, xT, self.head.weight, self.head.bias)           # (:286)
         return logits.view(B, L, -1)
 
+    def grad_ready_order(self):
+        """Parameters in the order backward finalises their gradients: head, the blocks from last to first (their
+        own weights; FiLM projections are reduced by the conditioning Function at the very end), then the rest.
+        The grad arena is laid out in this order so the DP all-reduce overlaps backward (fddm_hip.dist)."""
+        out = [self.head.weight, self.head.bias]
+        for blk in reversed(self.blocks):
+            out += [p for n, p in blk.named_parameters() if not n.startswith("film_layer.")]
+        seen = set(id(p) for p in out)
+        return out + [p for p in self.parameters() if id(p) not in seen]
+
     @torch.no_grad()
     def predict_x0(self, xt, t, cond, x_mask=None, c_mask=None) -> torch.Tensor:
         return self.forward(xt, t, cond, x_mask, c_mask).softmax(dim=-1)

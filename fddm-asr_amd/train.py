@@ -121,7 +121,11 @@ def train_one_epoch(encoder, decoder, s_proj, t_embed, t_proj, scheduler, loader
         opt_ids = set(id(p) for g in optimizer.param_groups for p in g["params"])
         dparams = [p for p in decoder.parameters() if p.requires_grad]
         if all(id(p) in opt_ids for p in dparams):
-            optimizer.use_grad_arena(dparams)
+            order = decoder.grad_ready_order() if hasattr(decoder, "grad_ready_order") else None
+            optimizer.use_grad_arena(dparams, order)
+    arena = getattr(optimizer, "arena", None)
+    if arena is not None and fdist.world() > 1 and arena.reducer is None:
+        fdist.OverlapReducer(arena)     # gradient all-reduce overlapped with backward
     pbar = loader
     if tqdm is not None and print_epoch_summary:
         pbar = tqdm(loader, desc=f"Epoch {epoch} [train]", leave=False)

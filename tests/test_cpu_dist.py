@@ -53,3 +53,55 @@ def test_allreduce_grads_gloo_world2():
         exp = sum(torch.randn(s, generator=torch.Generator().manual_seed(100 * r + i)) for r in range(world)) / world
         for r in range(world):
             torch.testing.assert_close(got[r][i], exp, rtol=1e-6, atol=1e-6)
+
+
+def _overlap_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from fddm_hip import dist as fdist
+        from fddm_hip import runtime as rt
+        shapes = [(40, 3), (7,), (2, 9, 2), (64,), (5, 5), (33,)]
+        params = [torch.nn.Parameter(torch.zeros(s)) for s in shapes]
+        order = [params[i] for i in (4, 1, 5, 0, 3, 2)]       # "backward" finalises them in this order
+        arena = rt.GradArena(params, order)
+        red = fdist.OverlapReducer(arena, bucket_bytes=256)   # tiny buckets: slices launch mid-"backward"
+        inflight = []
+        for step in range(2):
+            arena.zero_()
+            for i, p in enumerate(order):
+                g = torch.Generator().manual_seed(1000 * step + 100 * rank + i)
+                p.grad.add_(torch.randn(p.shape, generator=g))
+                rt.grads_ready([p])
+                inflight.append(len(red.works))
+            fdist.allreduce_grads(params)
+            q.put((rank, step, [p.grad.clone() for p in order], max(inflight)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_overlap_reducer_gloo_world2():
+    """Arena laid out in backward order; slices all-reduced asynchronously as soon as a bucket's worth of
+    slots is final (fddm_hip.dist.OverlapReducer), the tail at allreduce_grads; two steps (reset between)."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_overlap_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(2 * world):
+        r, step, gs, nin = q.get(timeout=120)
+        got[(r, step)] = gs
+        assert nin > 0, "no slice was in flight before allreduce_grads"
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    shapes = [(40, 3), (7,), (2, 9, 2), (64,), (5, 5), (33,)]
+    order_shapes = [shapes[i] for i in (4, 1, 5, 0, 3, 2)]
+    for step in range(2):
+        for i, s in enumerate(order_shapes):
+            exp = sum(torch.randn(s, generator=torch.Generator().manual_seed(1000 * step + 100 * r + i))
+                      for r in range(world)) / world
+            for r in range(world):
+                torch.testing.assert_close(got[(r, step)][i], exp, rtol=1e-6, atol=1e-6)
