@@ -103,6 +103,13 @@ def dominant_flops(args):
     return 2.0 * args.batch * T1 * 512 * 3 * 512
 
 
+def workload_name(args):
+    c2 = (args.layers, args.d_model, args.heads, args.seq_len, args.batch, args.seconds) == (6, 512, 8, 256, 32, 10.0)
+    tag = "fddm_zhTW_base C2" if c2 else "custom"
+    return (f"{tag}: WavLM-base + {args.layers}L d{args.d_model} H{args.heads} ff2048 decoder, V=8000, T=200, "
+            f"dropout 0.1, n_step_fd=4")
+
+
 def encoder_frames(seconds):
     n = int(16000 * seconds)
     for k, st in zip((10, 3, 3, 3, 3, 2, 2), (5, 2, 2, 2, 2, 2, 2)):
@@ -219,8 +226,7 @@ def main():
             "value": round(value, 2), "unit": "utterances/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": args.precision, "data": "synthetic (random-init WavLM-base, random audio/tokens)",
-            "config": {"workload": "fddm_zhTW_base C2: WavLM-base + 6L d512 H8 ff2048 decoder, V=8000, T=200, "
-                                   "dropout 0.1, n_step_fd=4",
+            "config": {"workload": workload_name(args),
                        "global_batch": args.batch * world, "seq_len": args.seq_len, "audio_seconds": args.seconds,
                        "parallelism": f"dp{world}"},
             "roofline": {"bound": "mfma", "kernel": "WavLM conv layer 1 implicit GEMM (gemm256_kernel: persistent 256x256, GELU)",
