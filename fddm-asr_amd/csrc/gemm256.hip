@@ -442,6 +442,11 @@ __global__ void __launch_bounds__(512) gemm256_kernel(GemmArgs g) {
   vmcnt<0>();  // no LDS-DMA may land after the workgroup retires
 }
 
+// Workgroup cap of the persistent grid (0 = one per CU). Set around launches that share the chip with another
+// stream (train.py runs the frozen encoder of the next step beside the decoder): fewer persistent workgroups
+// leave whole CUs to the other stream's short launches instead of making them queue behind 132 KB-LDS tiles.
+static int g_grid_cap = 0;
+
 template <int EPI, typename OT, bool CONV>
 static int launch(const GemmArgs& g, hipStream_t s) {
   static int ncu = 0;
@@ -455,7 +460,8 @@ static int launch(const GemmArgs& g, hipStream_t s) {
 #ifdef G256_NOPERSIST
   const long grid = tiles;
 #else
-  const long grid = tiles < ncu ? tiles : ncu;
+  const long cap = (g_grid_cap > 0 && g_grid_cap < ncu) ? g_grid_cap : ncu;
+  const long grid = tiles < cap ? tiles : cap;
 #endif
   hipLaunchKernelGGL((gemm256_kernel<EPI, OT, CONV>), dim3((unsigned)grid), dim3(512), LDS_BYTES + 4096, s, g);
   return (int)hipGetLastError();
@@ -496,6 +502,12 @@ int gemm256_launch(const GemmArgs& g, int epi, int out_dtype, bool conv, hipStre
 }
 
 }  // namespace fddm
+
+FDDM_API int fddm_gemm_persistent_cap(int cap) {
+  const int prev = fddm::g256::g_grid_cap;
+  fddm::g256::g_grid_cap = cap > 0 ? (cap & ~7) : 0;  // multiple of 8: the tile order is XCD-chunked
+  return prev;
+}
 
 #ifdef G256_STAMPS
 FDDM_API int fddm_gemm256_stamps(unsigned long long* host, long n) {

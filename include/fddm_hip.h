@@ -7,7 +7,8 @@
  *
  * Conventions
  *  - All pointers are device pointers owned by the caller (torch tensors); the library allocates
- *    nothing and keeps no global state. Every call is asynchronous on `stream` (a hipStream_t).
+ *    nothing and keeps no global state other than the persistent-GEMM workgroup cap below. Every call is
+ *    asynchronous on `stream` (a hipStream_t).
  *  - dtype codes: 0 = f32, 1 = bf16. "T" below means the selected compute/storage dtype.
  *  - Return value: hipError_t as int (0 = success); fddm_error_string() describes it.
  *  - Randomness: counter-based (seed, stream, element index) splitmix64 — see oracle/fddm_oracle.py.
@@ -35,6 +36,12 @@ int fddm_gemm(int dtype, int a_dtype, int a_kc, int b_kc, int epi, int out_dtype
               long sAb, const void* B, long ldb, void* C, long ldc, void* C2, const float* bias, float alpha, long M,
               long N, long K, unsigned long long seed, unsigned long long stream, float drop_p, float* colsum,
               void* hip_stream);
+
+/* ---- launch shape of the persistent 256x256 GEMM: at most `cap` workgroups (rounded down to a multiple
+ *      of 8; 0 = one per CU). Returns the previous cap. train.py lowers it while it enqueues the frozen
+ *      encoder of the next batch on a second stream, so the decoder's launches keep CUs of their own
+ *      (reference: train.py:359 `encoder(wave)` inside the step loop). */
+int fddm_gemm_persistent_cap(int cap);
 
 /* ---- grouped weight-gradient GEMMs (one launch for the n <= 12 dW GEMMs of a decoder block):
  *      dw[p][m][n] += sum_k dy[p][k][m] * x[p][k][n]   (dy: [K][M] bf16, x: [K][N] bf16, row strides ldy/ldx;
