@@ -461,7 +461,11 @@ static int launch(const GemmArgs& g, hipStream_t s) {
   const long grid = tiles;
 #else
   const long cap = (g_grid_cap > 0 && g_grid_cap < ncu) ? g_grid_cap : ncu;
-  const long grid = tiles < cap ? tiles : cap;
+  // as few workgroups as give the same number of tile rounds (e.g. 630 tiles on 256 CUs: 3 rounds either
+  // way, 216 workgroups instead of 256): the launch takes as long, and the spare CUs go to the other stream
+  const long rounds = (tiles + cap - 1) / cap;
+  const long need = ((tiles + rounds - 1) / rounds + 7) & ~7L;
+  const long grid = tiles < cap ? tiles : (need < cap ? need : cap);
 #endif
   hipLaunchKernelGGL((gemm256_kernel<EPI, OT, CONV>), dim3((unsigned)grid), dim3(512), LDS_BYTES + 4096, s, g);
   return (int)hipGetLastError();

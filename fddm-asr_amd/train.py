@@ -214,8 +214,8 @@ def train_one_epoch(encoder, decoder, s_proj, t_embed, t_proj, scheduler, loader
         optimizer.zero_grad(set_to_none=True)
         if scaler is not None:
             scaler.scale(loss).backward()
+            fdist.allreduce_grads(trainable)    # before unscale_: overlapped slices may still be in flight
             scaler.unscale_(optimizer)
-            fdist.allreduce_grads(trainable)
             torch.nn.utils.clip_grad_norm_([p for p in trainable if p.grad is not None], max_norm=5.0)
             scaler.step(optimizer)
             scaler.update()
