@@ -251,7 +251,7 @@ __global__ void __launch_bounds__(256) fwd_kernel(AttnArgs a) {
 #ifndef ATTN_FWD_WPS
 #define ATTN_FWD_WPS 2  // waves per SIMD the register allocation targets (measured: 2 beats 1, 3-4 spill)
 #endif
-template <bool DROP, bool MASK, bool REL>
+template <bool DROP, bool MASK, bool REL, int NG = 2>
 __global__ void __launch_bounds__(256, ATTN_FWD_WPS) fwd2_kernel(AttnArgs a) {
   constexpr int RB = 128;
   __shared__ __attribute__((aligned(16))) unsigned char kbuf[2][64 * RB];
@@ -260,18 +260,18 @@ __global__ void __launch_bounds__(256, ATTN_FWD_WPS) fwd2_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) float mbuf[2][64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, i = lane & 15;
   const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
-  const int qbase = blockIdx.x * 128;
+  const int qbase = blockIdx.x * (64 * NG);
   const bf16_t* Qb = (const bf16_t*)a.Q + (long)b * a.Lq * a.sq + h * DH;
   const bf16_t* Kb = (const bf16_t*)a.K + (long)b * a.Lk * a.sk + h * DH;
   const bf16_t* Vb = (const bf16_t*)a.V + (long)b * a.Lk * a.sv + h * DH;
   const float* tabh = REL ? a.table + (long)h * (2 * a.Lk - 1) : nullptr;
-  int q[2];
-  bool qv[2];
-  uint4 qf[2][2];
-  float gate[2];
+  int q[NG];
+  bool qv[NG];
+  uint4 qf[NG][2];
+  float gate[NG];
 #pragma unroll
-  for (int gq = 0; gq < 2; ++gq) {
-    q[gq] = qbase + w * 32 + gq * 16 + i;
+  for (int gq = 0; gq < NG; ++gq) {
+    q[gq] = qbase + w * (16 * NG) + gq * 16 + i;
     qv[gq] = q[gq] < a.Lq;
     row_frags<bf16_t>(qf[gq], Qb, a.sq, qv[gq] ? q[gq] : 0, qv[gq], lane);
     gate[gq] = (a.gate && qv[gq]) ? a.gate[(long)bh * a.Lq + q[gq]] : 0.f;
@@ -321,12 +321,15 @@ __global__ void __launch_bounds__(256, ATTN_FWD_WPS) fwd2_kernel(AttnArgs a) {
   };
 
   const float sl2 = a.scale * 1.4426950408889634f;  // running max m is kept in log2 units
-  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
-  f32x4_t o[2][4];
+  float m[NG], l[NG];
+  f32x4_t o[NG][4];
 #pragma unroll
-  for (int gq = 0; gq < 2; ++gq)
+  for (int gq = 0; gq < NG; ++gq) {
+    m[gq] = -INFINITY;
+    l[gq] = 0.f;
 #pragma unroll
     for (int d = 0; d < 4; ++d) o[gq][d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  }
 
   load(0);
   store(0);
@@ -337,15 +340,16 @@ __global__ void __launch_bounds__(256, ATTN_FWD_WPS) fwd2_kernel(AttnArgs a) {
     if (t + 1 < ntiles) load(k0 + 64);
     const unsigned char* kimg = kbuf[cur];
     const unsigned char* vimg = vbuf[cur];
-    f32x4_t s[2][4];
+    f32x4_t s[NG][4];
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
-      s[0][kb] = s[1][kb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int gq = 0; gq < NG; ++gq) s[gq][kb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub) {
         const uint4 af = *(const uint4*)(kimg + kc_off(RB, kb * 16 + i, sub * 4 + g));
-        mma<bf16_t>(s[0][kb], af, qf[0][sub]);
-        mma<bf16_t>(s[1][kb], af, qf[1][sub]);
+#pragma unroll
+        for (int gq = 0; gq < NG; ++gq) mma<bf16_t>(s[gq][kb], af, qf[gq][sub]);
       }
     }
     // softmax. Scores stay in raw units x = s (+ (gate/scale)*bias) (+ 0/-inf mask row, only on tiles that
@@ -360,9 +364,9 @@ __global__ void __launch_bounds__(256, ATTN_FWD_WPS) fwd2_kernel(AttnArgs a) {
         mrow[kb][0] = mv4.x; mrow[kb][1] = mv4.y; mrow[kb][2] = mv4.z; mrow[kb][3] = mv4.w;
       }
     }
-    float p[2][4][4];
+    float p[NG][4][4];
 #pragma unroll
-    for (int gq = 0; gq < 2; ++gq) {
+    for (int gq = 0; gq < NG; ++gq) {
       float tmax = -INFINITY;
       const float graw = REL ? gate[gq] / a.scale : 0.f;
       const int toff = 127 - (q[gq] - qbase);
@@ -436,9 +440,9 @@ __global__ void __launch_bounds__(256, ATTN_FWD_WPS) fwd2_kernel(AttnArgs a) {
       typedef __attribute__((address_space(3))) s16x4_t* lp;
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss) {
-        uint4 bq[2];
+        uint4 bq[NG];
 #pragma unroll
-        for (int gq = 0; gq < 2; ++gq) {
+        for (int gq = 0; gq < NG; ++gq) {
           bq[gq].x = pk(p[gq][2 * ss][0], p[gq][2 * ss][1]);
           bq[gq].y = pk(p[gq][2 * ss][2], p[gq][2 * ss][3]);
           bq[gq].z = pk(p[gq][2 * ss + 1][0], p[gq][2 * ss + 1][1]);
@@ -455,8 +459,8 @@ __global__ void __launch_bounds__(256, ATTN_FWD_WPS) fwd2_kernel(AttnArgs a) {
           af.y = (unsigned)(unsigned short)lo[2] | ((unsigned)(unsigned short)lo[3] << 16);
           af.z = (unsigned)(unsigned short)hi[0] | ((unsigned)(unsigned short)hi[1] << 16);
           af.w = (unsigned)(unsigned short)hi[2] | ((unsigned)(unsigned short)hi[3] << 16);
-          mma<bf16_t>(o[0][db], af, bq[0]);
-          mma<bf16_t>(o[1][db], af, bq[1]);
+#pragma unroll
+          for (int gq = 0; gq < NG; ++gq) mma<bf16_t>(o[gq][db], af, bq[gq]);
         }
       }
     }
@@ -466,7 +470,7 @@ __global__ void __launch_bounds__(256, ATTN_FWD_WPS) fwd2_kernel(AttnArgs a) {
     }
   }
 #pragma unroll
-  for (int gq = 0; gq < 2; ++gq) {
+  for (int gq = 0; gq < NG; ++gq) {
     float lt = l[gq];
     lt += __shfl_xor(lt, 16, 64);
     lt += __shfl_xor(lt, 32, 64);
@@ -1002,9 +1006,22 @@ static int run(int which, AttnArgs& a, hipStream_t s) {
   if (which == 0) {
     if constexpr (sizeof(T) == 2) {
       if (!getenv("FDDM_ATTN_V1")) {
-        dim3 grid((a.Lq + 127) / 128, a.B * a.H);
         const bool drop = a.thr16 != 0, mask = a.key_keep != nullptr || (a.Lk % 64) != 0;
         const bool rel = a.table != nullptr && (a.gate != nullptr || a.graw != nullptr);
+        // FDDM_ATTN_NG=1: 64-query workgroups (one 16-query group per wave). Measured at the decoder's
+        // Lq = 256 (tools/attn_bench.py): no faster with dropout (24.4 vs 24.0 us), slower without (19.4 vs
+        // 15.1 us) — the launch is not short of workgroups; kept as a probe, off by default.
+        const char* ng_env = getenv("FDDM_ATTN_NG");
+        const int ng = ng_env ? atoi(ng_env) : 2;
+        if (ng == 1 && !rel) {
+          dim3 grid1((a.Lq + 63) / 64, a.B * a.H);
+#define FWD1(D, M) hipLaunchKernelGGL((fwd2_kernel<D, M, false, 1>), grid1, dim3(256), 0, s, a)
+          if (drop) { if (mask) FWD1(true, true); else FWD1(true, false); }
+          else { if (mask) FWD1(false, true); else FWD1(false, false); }
+#undef FWD1
+          return (int)hipGetLastError();
+        }
+        dim3 grid((a.Lq + 127) / 128, a.B * a.H);
 #define FWD2(D, M, R) hipLaunchKernelGGL((fwd2_kernel<D, M, R>), grid, dim3(256), 0, s, a)
         if (rel) {
           if (drop) { if (mask) FWD2(true, true, true); else FWD2(true, false, true); }
