@@ -169,13 +169,39 @@ def drop_bits(B, H, Lq, Lk, device):
     return torch.empty(B * H * Lq * ((Lk + 63) // 64), device=device, dtype=torch.int64)
 
 
+def _heads(x, rows, H, dh):
+    """[rows, H*dh] view (any row stride) as [rows, H, dh]."""
+    return x[:rows, : H * dh].unflatten(1, (H, dh))
+
+
+def _pad64(x, rows, H, dh):
+    """Head slots widened to the kernels' 64 lanes with zeros: [rows, H*64]. Zero q/k columns add nothing to
+    Q K^T and zero v columns give zero output columns, so the attention of the first dh columns is unchanged."""
+    xp = torch.zeros(rows, H, 64, device=x.device, dtype=x.dtype)
+    xp[:, :, :dh] = _heads(x, rows, H, dh)
+    return xp.view(rows, H * 64)
+
+
 def attn_fwd(q, k, v, out, lse, B, H, Lq, Lk, *, key_keep=None, gate=None, table=None, drop_p=0.0, seed=0,
              rng_stream=0, scale=None, dbits=None):
-    """q: [B*Lq, >=H*64] row stride q.stride(0); k/v: [B*Lk, ...]; out [B*Lq, H*64]; lse [B*H, Lq].
-    dbits (optional, drop_bits()): records the dropout keep bits for the backward."""
+    """q: [B*Lq, >=H*dh] row stride q.stride(0); k/v: [B*Lk, ...]; out [B*Lq, H*dh]; lse [B*H, Lq], dh =
+    out.shape[1] // H. dbits (optional, drop_bits()): records the dropout keep bits for the backward.
+    The kernels are built for head_dim 64; a smaller head_dim (the reference's nn.MultiheadAttention takes any
+    d_model / nhead) runs them on zero-padded 64-wide head slots — the scores, the softmax, the dropout
+    element indices (b, h, query, key) and hence the RNG stream are those of the unpadded heads."""
     _chk(q.stride(-1) == 1 and k.stride(-1) == 1 and v.stride(-1) == 1, "attention inputs need unit inner stride")
     _chk(q.dtype == k.dtype == v.dtype == out.dtype, "attention dtype mismatch")
-    sc = 1.0 / math.sqrt(64) if scale is None else scale
+    _chk(out.shape[1] % H == 0, "attention output width must be H * head_dim")
+    dh = out.shape[1] // H
+    _chk(1 <= dh <= 64, f"head_dim {dh} > 64 is not built")
+    sc = 1.0 / math.sqrt(dh) if scale is None else scale
+    if dh != 64:
+        op = torch.empty(B * Lq, H * 64, device=out.device, dtype=out.dtype)
+        attn_fwd(_pad64(q, B * Lq, H, dh), _pad64(k, B * Lk, H, dh), _pad64(v, B * Lk, H, dh), op, lse, B, H, Lq,
+                 Lk, key_keep=key_keep, gate=gate, table=table, drop_p=drop_p, seed=seed, rng_stream=rng_stream,
+                 scale=sc, dbits=dbits)
+        _heads(out, B * Lq, H, dh).copy_(op.view(B * Lq, H, 64)[:, :, :dh])
+        return out
     call("fddm_attn_fwd", code(q), ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out),
          out.stride(0), ptr(lse), ptr(key_keep), ptr(gate), ptr(table), B, H, Lq, Lk, float(sc), float(drop_p), seed,
          rng_stream, ptr(dbits), stream())
@@ -194,11 +220,27 @@ def attn_fwd_relgate(q, k, v, out, graw, gconst, table, B, H, L, scale=None):
 
 
 def attn_bwd(q, k, v, o, do, lse, dq, dk, dv, B, H, Lq, Lk, *, key_keep=None, drop_p=0.0, seed=0, rng_stream=0,
-             dbits=None):
+             dbits=None, scale=None):
+    """Gradients of attn_fwd (same layouts; head_dim = o.shape[1] // H, padded to 64 as in attn_fwd)."""
+    _chk(o.shape[1] % H == 0, "attention output width must be H * head_dim")
+    dh = o.shape[1] // H
+    _chk(1 <= dh <= 64, f"head_dim {dh} > 64 is not built")
+    sc = 1.0 / math.sqrt(dh) if scale is None else scale
+    if dh != 64:
+        rq, rk = B * Lq, B * Lk
+        dqp = torch.empty(rq, H * 64, device=dq.device, dtype=dq.dtype)
+        dkp = torch.empty(rk, H * 64, device=dk.device, dtype=dk.dtype)
+        dvp = torch.empty(rk, H * 64, device=dv.device, dtype=dv.dtype)
+        attn_bwd(_pad64(q, rq, H, dh), _pad64(k, rk, H, dh), _pad64(v, rk, H, dh), _pad64(o, rq, H, dh),
+                 _pad64(do, rq, H, dh), lse, dqp, dkp, dvp, B, H, Lq, Lk, key_keep=key_keep, drop_p=drop_p, seed=seed,
+                 rng_stream=rng_stream, dbits=dbits, scale=sc)
+        for g, gp, r in ((dq, dqp, rq), (dk, dkp, rk), (dv, dvp, rk)):
+            _heads(g, r, H, dh).copy_(gp.view(r, H, 64)[:, :, :dh])
+        return
     delta = torch.empty(B * H, Lq, device=q.device, dtype=torch.float32)
     call("fddm_attn_bwd", code(q), ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(o),
          o.stride(0), ptr(do), do.stride(0), ptr(lse), ptr(dq), dq.stride(0), ptr(dk), dk.stride(0), ptr(dv),
-         dv.stride(0), ptr(delta), ptr(key_keep), B, H, Lq, Lk, float(1.0 / 8.0), float(drop_p), seed, rng_stream,
+         dv.stride(0), ptr(delta), ptr(key_keep), B, H, Lq, Lk, float(sc), float(drop_p), seed, rng_stream,
          ptr(dbits), stream())
 
 

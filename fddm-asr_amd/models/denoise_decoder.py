@@ -5,7 +5,8 @@ Same constructor signature, forward signature, submodule names and state_dict ke
 autograd Function per DecoderBlock (fddm_hip.functions.DecoderBlockFn) over libfddm_hip kernels.
 
 Deviations (documented in DESIGN.md): only pos_emb_type="rope" is built (the only type the reference's
-train.py constructs, train.py:517-526); head_dim must be 64; the gradient w.r.t. `cond` is not
+train.py constructs, train.py:517-526); head_dim <= 64 (the attention kernels are built for 64-wide heads;
+smaller heads run on zero-padded slots, fddm_hip.ops.attn_fwd); the gradient w.r.t. `cond` is not
 produced (the encoder is frozen and its projection is never optimised, train.py:543).
 """
 from __future__ import annotations
@@ -99,8 +100,8 @@ class DecoderBlock(nn.Module):
         super().__init__()
         if pos_emb_type != "rope" or not use_film:
             raise NotImplementedError("only the reference's default block (rope + FiLM) is built")
-        if d_model // nhead != 64 or d_model % nhead:
-            raise NotImplementedError("head_dim must be 64 on this build")
+        if d_model % nhead or d_model // nhead > 64:
+            raise NotImplementedError("head_dim = d_model / nhead must divide d_model and be <= 64 on this build")
         self.use_film, self.pos_emb_type = use_film, pos_emb_type
         self.nhead, self.p = nhead, dropout
         self.self_attn = _MHAParams(d_model, nhead, dropout)
