@@ -182,9 +182,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # FDDM_DIST_BACKEND=gloo rehearses the N > 1 path with every rank on one GPU (local % device_count);
+    # the driver's multi-GPU runs use the default: RCCL ("nccl"), one GPU per rank
+    backend = os.environ.get("FDDM_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % torch.cuda.device_count()
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     device = torch.device("cuda", local)
     torch.manual_seed(1337 + rank)
     T_, cfg, models, opt = build(args, device)
