@@ -108,11 +108,7 @@ __device__ __forceinline__ void trans_times_vals(f32x4_t (&out)[4], const unsign
         const int u = db * 4 + p;
         const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(img + k1 * 128 + ((u ^ hatt(k1)) << 3)));
         const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(img + k2 * 128 + ((u ^ hatt(k2)) << 3)));
-        uint4 a;
-        a.x = (unsigned)(unsigned short)lo[0] | ((unsigned)(unsigned short)lo[1] << 16);
-        a.y = (unsigned)(unsigned short)lo[2] | ((unsigned)(unsigned short)lo[3] << 16);
-        a.z = (unsigned)(unsigned short)hi[0] | ((unsigned)(unsigned short)hi[1] << 16);
-        a.w = (unsigned)(unsigned short)hi[2] | ((unsigned)(unsigned short)hi[3] << 16);
+        const uint4 a = join_tr(lo, hi);
         mma<bf16_t>(out[db], a, b);
       }
     }
@@ -321,6 +317,9 @@ __global__ void __launch_bounds__(256, ATTN_FWD_WPS) fwd2_kernel(AttnArgs a) {
   };
 
   const float sl2 = a.scale * 1.4426950408889634f;  // running max m is kept in log2 units
+  float graw[NG];  // bias multiplier in raw score units (gate / scale), once per query instead of per tile
+#pragma unroll
+  for (int gq = 0; gq < NG; ++gq) graw[gq] = REL ? gate[gq] / a.scale : 0.f;
   float m[NG], l[NG];
   f32x4_t o[NG][4];
 #pragma unroll
@@ -352,36 +351,39 @@ __global__ void __launch_bounds__(256, ATTN_FWD_WPS) fwd2_kernel(AttnArgs a) {
         for (int gq = 0; gq < NG; ++gq) mma<bf16_t>(s[gq][kb], af, qf[gq][sub]);
       }
     }
-    // softmax. Scores stay in raw units x = s (+ (gate/scale)*bias) (+ 0/-inf mask row, only on tiles that
-    // can hold masked keys); the running max m is in raw units and p = 2^(x*sl2 - m*sl2) is one FMA +
-    // v_exp_f32 (no separate scale multiply or subtraction per score).
-    const bool mt = MASK && (a.key_keep != nullptr || t == ntiles - 1);
-    float mrow[4][4];
-    if (mt) {
+    // softmax. Scores stay in raw units x = s (+ (gate/scale)*bias) (+ the tile's 0/-inf mask row); the running
+    // max m is in raw units and p = 2^(x*sl2 - m*sl2) is one FMA + v_exp_f32 per score. Score pairs are carried
+    // as float2 so the bias FMA, the mask add, the exponent FMA and the row sum issue as packed v_pk_* f32
+    // instructions. MASK kernels add the mask row on every tile (0 where keys are valid): a per-tile condition
+    // compiled to an add plus a select per score on every tile. The dropout scale 1/(1-p) is applied to O once
+    // at the end, not per kept probability.
+    f32x2_t mrow[4][2];
+    if constexpr (MASK) {
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb) {
         const float4 mv4 = *(const float4*)(&mbuf[cur][kb * 16 + 4 * g]);
-        mrow[kb][0] = mv4.x; mrow[kb][1] = mv4.y; mrow[kb][2] = mv4.z; mrow[kb][3] = mv4.w;
+        mrow[kb][0] = f32x2_t{mv4.x, mv4.y};
+        mrow[kb][1] = f32x2_t{mv4.z, mv4.w};
       }
     }
     float p[NG][4][4];
 #pragma unroll
     for (int gq = 0; gq < NG; ++gq) {
       float tmax = -INFINITY;
-      const float graw = REL ? gate[gq] / a.scale : 0.f;
       const int toff = 127 - (q[gq] - qbase);
+      const f32x2_t gr2 = {graw[gq], graw[gq]};
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int kl = kb * 16 + 4 * g + j;
-          float x = s[gq][kb][j];
-          if constexpr (REL) x = fmaf(graw, tbuf[cur][kl + toff], x);
-          p[gq][kb][j] = x;
-        }
-        if (mt) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) p[gq][kb][j] += mrow[kb][j];
+        for (int jj = 0; jj < 2; ++jj) {
+          f32x2_t x = {s[gq][kb][2 * jj], s[gq][kb][2 * jj + 1]};
+          if constexpr (REL) {
+            const int kl = kb * 16 + 4 * g + 2 * jj + toff;
+            x = gr2 * f32x2_t{tbuf[cur][kl], tbuf[cur][kl + 1]} + x;
+          }
+          if constexpr (MASK) x += mrow[kb][jj];
+          p[gq][kb][2 * jj] = x.x;
+          p[gq][kb][2 * jj + 1] = x.y;
         }
         tmax = fmaxf(tmax, fmaxf(fmaxf(p[gq][kb][0], p[gq][kb][1]), fmaxf(p[gq][kb][2], p[gq][kb][3])));
       }
@@ -391,34 +393,58 @@ __global__ void __launch_bounds__(256, ATTN_FWD_WPS) fwd2_kernel(AttnArgs a) {
       const float mref = (mn == -INFINITY) ? 0.f : mn;  // all-masked so far: exp2(-inf) = 0
       const float nbias = -mref * sl2;
       const float alpha = __builtin_amdgcn_exp2f((m[gq] - mref) * sl2);
-      float ls = 0.f;
+      const f32x2_t sl2v = {sl2, sl2}, nb2 = {nbias, nbias};
+      f32x2_t ls2 = {0.f, 0.f};
       uint64_t bits = 0;
+      // dropout hash words: the lane's 4 consecutive keys e0..e0+3 of block kb span word e0>>2 (h0[kb]) and, when
+      // Lk % 4 != 0, word (e0>>2)+1 (h1[kb]) — which is the h0 of the lane 16 up (the next 4 keys) or, for the
+      // last key quad of a block, of block kb+1 in lane g = 0: one 64-bit lane rotation per block and one extra
+      // hash instead of a second hash per block. Lk % 4 == 0 (a wave-uniform branch) needs h0 only.
+      uint64_t e0q = 0, h0[4] = {0, 0, 0, 0}, h1[4] = {0, 0, 0, 0};
+      if constexpr (DROP) {
+        e0q = ((uint64_t)bh * a.Lq + q[gq]) * a.Lk + (k0 + 4 * g);
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) h0[kb] = mix64(a.seed, a.stream, (e0q + kb * 16) >> 2);
+        if (a.Lk & 3) {
+          const uint64_t hx = mix64(a.seed, a.stream, (e0q + 64) >> 2);  // "h0[4]", read by g = 3 at kb = 3
+          const int src = (lane + 16) & 63;
+#pragma unroll
+          for (int kb = 0; kb < 4; ++kb) {
+            const uint64_t v = g == 0 ? (kb < 3 ? h0[kb + 1] : hx) : h0[kb];
+            const unsigned lo = __shfl((unsigned)v, src, 64), hi = __shfl((unsigned)(v >> 32), src, 64);
+            h1[kb] = ((uint64_t)hi << 32) | lo;
+          }
+        }
+      }
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb) {
         unsigned keep = 0xF;
         if constexpr (DROP) {
-          // elements e0..e0+3 (consecutive keys) span at most two 64-bit hash words
-          const uint64_t e0 = ((uint64_t)bh * a.Lq + q[gq]) * a.Lk + (k0 + kb * 16 + 4 * g);
-          const uint64_t h0 = mix64(a.seed, a.stream, e0 >> 2);
-          const uint64_t h1 = ((e0 & 3) == 0) ? h0 : mix64(a.seed, a.stream, (e0 >> 2) + 1);
+          const unsigned r = (unsigned)(e0q & 3);  // same for every block (16 | kb*16)
           keep = 0;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const unsigned sl = (unsigned)((e0 & 3) + j);
-            const uint64_t hw = sl < 4 ? h0 : h1;
+            const unsigned sl = r + j;
+            const uint64_t hw = sl < 4 ? h0[kb] : h1[kb];
             const unsigned u = (unsigned)(hw >> (16u * (sl & 3u))) & 0xFFFFu;
             keep |= (u >= a.thr16 ? 1u : 0u) << j;
           }
           bits |= (uint64_t)keep << (kb * 16 + 4 * g);
         }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          float e = __builtin_amdgcn_exp2f(fmaf(p[gq][kb][j], sl2, nbias));
-          ls += e;
-          if constexpr (DROP) e = ((keep >> j) & 1u) ? e * a.drop_scale : 0.f;
-          p[gq][kb][j] = e;
+        for (int jj = 0; jj < 2; ++jj) {
+          const f32x2_t arg = f32x2_t{p[gq][kb][2 * jj], p[gq][kb][2 * jj + 1]} * sl2v + nb2;
+          f32x2_t e = {__builtin_amdgcn_exp2f(arg.x), __builtin_amdgcn_exp2f(arg.y)};
+          ls2 += e;
+          if constexpr (DROP) {
+            e.x = ((keep >> (2 * jj)) & 1u) ? e.x : 0.f;
+            e.y = ((keep >> (2 * jj + 1)) & 1u) ? e.y : 0.f;
+          }
+          p[gq][kb][2 * jj] = e.x;
+          p[gq][kb][2 * jj + 1] = e.y;
         }
       }
+      const float ls = ls2.x + ls2.y;
       if constexpr (DROP) {
         if (a.dbits) {  // the 4 lanes of a query hold disjoint key nibbles: OR them into the tile's 64-bit word
           unsigned lo = (unsigned)bits, hi = (unsigned)(bits >> 32);
@@ -454,11 +480,7 @@ __global__ void __launch_bounds__(256, ATTN_FWD_WPS) fwd2_kernel(AttnArgs a) {
           const int u = db * 4 + pp;
           const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(vimg + k1 * 128 + ((u ^ hatt(k1)) << 3)));
           const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(vimg + k2 * 128 + ((u ^ hatt(k2)) << 3)));
-          uint4 af;
-          af.x = (unsigned)(unsigned short)lo[0] | ((unsigned)(unsigned short)lo[1] << 16);
-          af.y = (unsigned)(unsigned short)lo[2] | ((unsigned)(unsigned short)lo[3] << 16);
-          af.z = (unsigned)(unsigned short)hi[0] | ((unsigned)(unsigned short)hi[1] << 16);
-          af.w = (unsigned)(unsigned short)hi[2] | ((unsigned)(unsigned short)hi[3] << 16);
+          const uint4 af = join_tr(lo, hi);
 #pragma unroll
           for (int gq = 0; gq < NG; ++gq) mma<bf16_t>(o[gq][db], af, bq[gq]);
         }
@@ -475,7 +497,8 @@ __global__ void __launch_bounds__(256, ATTN_FWD_WPS) fwd2_kernel(AttnArgs a) {
     lt += __shfl_xor(lt, 16, 64);
     lt += __shfl_xor(lt, 32, 64);
     if (!qv[gq]) continue;
-    const float inv = (lt > 0.f) ? 1.f / lt : NAN;  // fully masked row -> NaN like softmax(all -inf)
+    // fully masked row -> NaN like softmax(all -inf); the dropout scale of the kept probabilities goes here
+    const float inv = (lt > 0.f) ? (DROP ? a.drop_scale : 1.f) / lt : NAN;
     bf16_t* Ob = (bf16_t*)a.Out + ((long)b * a.Lq + q[gq]) * a.so + h * DH;
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
@@ -667,11 +690,7 @@ __device__ __forceinline__ void trans_times_vals2(f32x4_t (&out)[2][4], const un
       const int u = db * 4 + pp;
       const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(img + k1 * 128 + ((u ^ hatt(k1)) << 3)));
       const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(img + k2 * 128 + ((u ^ hatt(k2)) << 3)));
-      uint4 af;
-      af.x = (unsigned)(unsigned short)lo[0] | ((unsigned)(unsigned short)lo[1] << 16);
-      af.y = (unsigned)(unsigned short)lo[2] | ((unsigned)(unsigned short)lo[3] << 16);
-      af.z = (unsigned)(unsigned short)hi[0] | ((unsigned)(unsigned short)hi[1] << 16);
-      af.w = (unsigned)(unsigned short)hi[2] | ((unsigned)(unsigned short)hi[3] << 16);
+      const uint4 af = join_tr(lo, hi);
       mma<bf16_t>(out[0][db], af, bq[0]);
       mma<bf16_t>(out[1][db], af, bq[1]);
     }

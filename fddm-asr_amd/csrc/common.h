@@ -16,6 +16,11 @@ typedef __attribute__((ext_vector_type(4))) short s16x4_t;
 namespace fddm {
 
 __device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((unsigned)v) << 16); }
+// two ds_read_b64_tr_b16 results (4 bf16 each) as one 8-bf16 MFMA operand: a register reinterpretation (no VALU)
+__device__ __forceinline__ uint4 join_tr(s16x4_t lo, s16x4_t hi) {
+  const uint2 l = __builtin_bit_cast(uint2, lo), h = __builtin_bit_cast(uint2, hi);
+  return make_uint4(l.x, l.y, h.x, h.y);
+}
 typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
 typedef __attribute__((ext_vector_type(2))) float f32x2_t;
 // round-to-nearest-even f32 -> bf16 with the gfx950 hardware convert (v_cvt_pk_bf16_f32)

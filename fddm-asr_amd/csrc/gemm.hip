@@ -170,11 +170,7 @@ struct Operand {
       typedef __attribute__((address_space(3))) s16x4_t* lp;
       const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(s + k * 256 + ((u ^ hk(k)) << 3)));
       const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(s + (k + 4) * 256 + ((u ^ hk(k + 4)) << 3)));
-      uint4 o;
-      o.x = (unsigned)(unsigned short)lo[0] | ((unsigned)(unsigned short)lo[1] << 16);
-      o.y = (unsigned)(unsigned short)lo[2] | ((unsigned)(unsigned short)lo[3] << 16);
-      o.z = (unsigned)(unsigned short)hi[0] | ((unsigned)(unsigned short)hi[1] << 16);
-      o.w = (unsigned)(unsigned short)hi[2] | ((unsigned)(unsigned short)hi[3] << 16);
+      const uint4 o = join_tr(lo, hi);
       return o;
     } else {
       const int k = sub * 16 + 4 * g;
