@@ -760,7 +760,7 @@ __global__ void __launch_bounds__(256, 2) dq2_kernel(AttnArgs a) {
     lse2[gq] = qv[gq] ? a.lse[(long)bh * a.Lq + q[gq]] * 1.4426950408889634f : 0.f;
   }
   uint4 kr[2], vr[2];
-  float mv = 1.f;
+  float mv = 0.f;
   auto load = [&](int k0) {
     const int nv = min(64, a.Lk - k0);
 #pragma unroll
@@ -772,7 +772,7 @@ __global__ void __launch_bounds__(256, 2) dq2_kernel(AttnArgs a) {
         vr[u] = *(const uint4*)(Vb + (long)(k0 + r) * a.sv + c * 8);
       }
     }
-    if (MASK && tid >= 192) mv = key_ok(a, b, k0 + tid - 192) ? 1.f : 0.f;
+    if (MASK && tid >= 192) mv = key_ok(a, b, k0 + tid - 192) ? 0.f : -INFINITY;  // added to the exponent
   };
   auto store = [&](int buf) {
 #pragma unroll
@@ -823,7 +823,10 @@ __global__ void __launch_bounds__(256, 2) dq2_kernel(AttnArgs a) {
 #pragma unroll
       for (int gq = 0; gq < 2; ++gq) wbits[gq] = qv[gq] ? a.dbits[((long)bh * ntiles + t) * a.Lq + q[gq]] : 0;
     }
+    // dS = P (dP' - delta), P = 2^(s*sl2 - lse2 + mask) (the 0/-inf mask row in the exponent instead of a select),
+    // dP' = dP & keep (sign-extended keep bit, v_bfe_i32) * 1/(1-p); score pairs as float2 (packed v_pk_* f32)
     float ds[2][4][4];
+    const f32x2_t sl2v = {sl2, sl2}, dscv = {a.drop_scale, a.drop_scale};
 #pragma unroll
     for (int gq = 0; gq < 2; ++gq)
 #pragma unroll
@@ -831,13 +834,24 @@ __global__ void __launch_bounds__(256, 2) dq2_kernel(AttnArgs a) {
         unsigned keep = 0xF;
         if constexpr (DM == 2) keep = (unsigned)(wbits[gq] >> (kb * 16 + 4 * g)) & 0xFu;
         if constexpr (DM == 1) keep = keep4(a, ((uint64_t)bh * a.Lq + q[gq]) * a.Lk + (k0 + kb * 16 + 4 * g));
+        const f32x2_t ndl = {-delta[gq], -delta[gq]};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          float pr = __builtin_amdgcn_exp2f(s[gq][kb][j] * sl2 - lse2[gq]);
-          if constexpr (MASK) pr = mrow[kb][j] != 0.f ? pr : 0.f;
-          float dpv = dp[gq][kb][j];
-          if constexpr (DROP) dpv = ((keep >> j) & 1u) ? dpv * a.drop_scale : 0.f;
-          ds[gq][kb][j] = pr * (dpv - delta[gq]);
+        for (int jj = 0; jj < 2; ++jj) {
+          f32x2_t off = {-lse2[gq], -lse2[gq]};
+          if constexpr (MASK) off += f32x2_t{mrow[kb][2 * jj], mrow[kb][2 * jj + 1]};
+          const f32x2_t arg = f32x2_t{s[gq][kb][2 * jj], s[gq][kb][2 * jj + 1]} * sl2v + off;
+          const f32x2_t pr = {__builtin_amdgcn_exp2f(arg.x), __builtin_amdgcn_exp2f(arg.y)};
+          f32x2_t dpv = {dp[gq][kb][2 * jj], dp[gq][kb][2 * jj + 1]};
+          if constexpr (DROP) {
+            dpv.x = __int_as_float(__float_as_int(dpv.x) & __builtin_amdgcn_sbfe((int)keep, 2 * jj, 1));
+            dpv.y = __int_as_float(__float_as_int(dpv.y) & __builtin_amdgcn_sbfe((int)keep, 2 * jj + 1, 1));
+            dpv = dpv * dscv + ndl;
+          } else {
+            dpv += ndl;
+          }
+          const f32x2_t d2 = pr * dpv;
+          ds[gq][kb][2 * jj] = d2.x;
+          ds[gq][kb][2 * jj + 1] = d2.y;
         }
       }
     trans_times_vals2(dq, kt[cur], ds, lane);
@@ -955,44 +969,58 @@ __global__ void __launch_bounds__(256, (DM == 1 ? 1 : 2)) dkv2_kernel(AttnArgs a
         mma<bf16_t>(dp[1][qb], ao, vf[1][sub]);
       }
     }
+    // P = 2^(s*sl2 - lse2); P' = P & keep, dS = P (dP & keep * 1/(1-p) - delta) (the keep bit sign-extended by
+    // v_bfe_i32; the 1/(1-p) of P' goes on dV once at the end). Query pairs as float2 (packed v_pk_* f32). The
+    // lane owns one key: a masked key's P is not zeroed per score — its dK/dV column is written as zeros.
     float pd[2][4][4], ds[2][4][4];
-    const int kbit = (w * 32 + i) & 63;  // key bit within its tile (groups gq add 16)
+    const int kbit = (w * 32 + i) & 63;  // key bit within its tile (groups gq add 16): the word half is w & 1
+    const f32x2_t sl2v = {sl2, sl2}, dscv = {a.drop_scale, a.drop_scale};
 #pragma unroll
     for (int qb = 0; qb < 4; ++qb) {
       const float4 l4 = *(const float4*)(&lse_s[cur][qb * 16 + 4 * g]);
       const float4 d4 = *(const float4*)(&del_s[cur][qb * 16 + 4 * g]);
-      const float lr[4] = {l4.x, l4.y, l4.z, l4.w}, dr[4] = {d4.x, d4.y, d4.z, d4.w};
-      uint64_t wq[4] = {0, 0, 0, 0};
+      const f32x2_t nl[2] = {f32x2_t{-l4.x, -l4.y}, f32x2_t{-l4.z, -l4.w}};
+      const f32x2_t nd[2] = {f32x2_t{-d4.x, -d4.y}, f32x2_t{-d4.z, -d4.w}};
+      unsigned wq[4] = {0, 0, 0, 0};  // the 32-bit half of each query's keep word holding this wave's keys
       if constexpr (DM == 2) {
-        {
-          const uint64_t* src = &wb_s[cur][w >> 1][qb * 16 + 4 * g];
-          const uint4 u0 = *(const uint4*)src, u1 = *(const uint4*)(src + 2);
-          wq[0] = ((uint64_t)u0.y << 32) | u0.x;
-          wq[1] = ((uint64_t)u0.w << 32) | u0.z;
-          wq[2] = ((uint64_t)u1.y << 32) | u1.x;
-          wq[3] = ((uint64_t)u1.w << 32) | u1.z;
-        }
+        const unsigned* src = (const unsigned*)&wb_s[cur][w >> 1][qb * 16 + 4 * g] + (w & 1);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) wq[j] = src[2 * j];
       }
 #pragma unroll
-      for (int gq = 0; gq < 2; ++gq)
+      for (int gq = 0; gq < 2; ++gq) {
+        const int kb5 = (kbit + 16 * gq) & 31;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          float pr = __builtin_amdgcn_exp2f(s[gq][qb][j] * sl2 - lr[j]);
-          pr = kok[gq] ? pr : 0.f;
-          float keep = 1.f;
+        for (int jj = 0; jj < 2; ++jj) {
+          const f32x2_t arg = f32x2_t{s[gq][qb][2 * jj], s[gq][qb][2 * jj + 1]} * sl2v + nl[jj];
+          f32x2_t pr = {__builtin_amdgcn_exp2f(arg.x), __builtin_amdgcn_exp2f(arg.y)};
+          f32x2_t dpv = {dp[gq][qb][2 * jj], dp[gq][qb][2 * jj + 1]};
+          f32x2_t pdv = pr;
           if constexpr (DROP) {
-            bool kp;
+            int m0, m1;
             if constexpr (DM == 2) {
-              kp = (wq[j] >> (kbit + 16 * gq)) & 1u;
+              m0 = __builtin_amdgcn_sbfe((int)wq[2 * jj], kb5, 1);
+              m1 = __builtin_amdgcn_sbfe((int)wq[2 * jj + 1], kb5, 1);
             } else {
-              const int qq = q0 + qb * 16 + 4 * g + j;
-              kp = drop_keep(a.seed, a.stream, ((uint64_t)bh * a.Lq + qq) * a.Lk + key[gq], a.thr16);
+              const int qq = q0 + qb * 16 + 4 * g + 2 * jj;
+              m0 = drop_keep(a.seed, a.stream, ((uint64_t)bh * a.Lq + qq) * a.Lk + key[gq], a.thr16) ? -1 : 0;
+              m1 = drop_keep(a.seed, a.stream, ((uint64_t)bh * a.Lq + qq + 1) * a.Lk + key[gq], a.thr16) ? -1 : 0;
             }
-            keep = kp ? a.drop_scale : 0.f;
+            pdv.x = __int_as_float(__float_as_int(pr.x) & m0);
+            pdv.y = __int_as_float(__float_as_int(pr.y) & m1);
+            dpv.x = __int_as_float(__float_as_int(dpv.x) & m0);
+            dpv.y = __int_as_float(__float_as_int(dpv.y) & m1);
+            dpv = dpv * dscv + nd[jj];
+          } else {
+            dpv += nd[jj];
           }
-          pd[gq][qb][j] = pr * keep;
-          ds[gq][qb][j] = pr * (dp[gq][qb][j] * keep - dr[j]);
+          const f32x2_t d2 = pr * dpv;
+          pd[gq][qb][2 * jj] = pdv.x;
+          pd[gq][qb][2 * jj + 1] = pdv.y;
+          ds[gq][qb][2 * jj] = d2.x;
+          ds[gq][qb][2 * jj + 1] = d2.y;
         }
+      }
     }
     trans_times_vals2(dv, ot[cur], pd, lane);
     trans_times_vals2(dk, qt[cur], ds, lane);
@@ -1006,13 +1034,15 @@ __global__ void __launch_bounds__(256, (DM == 1 ? 1 : 2)) dkv2_kernel(AttnArgs a
     if (!kvld[gq]) continue;
     bf16_t* dKb = (bf16_t*)a.dK + ((long)b * a.Lk + key[gq]) * a.sdk + h * DH;
     bf16_t* dVb = (bf16_t*)a.dV + ((long)b * a.Lk + key[gq]) * a.sdv + h * DH;
+    // masked key: zero gradient (its P was never zeroed); dV carries the dropout scale of P'
+    const float ksc = kok[gq] ? a.scale : 0.f, vsc = kok[gq] ? (DROP ? a.drop_scale : 1.f) : 0.f;
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
       uint2 uk, uv;
-      uk.x = pk(dk[gq][d][0] * a.scale, dk[gq][d][1] * a.scale);
-      uk.y = pk(dk[gq][d][2] * a.scale, dk[gq][d][3] * a.scale);
-      uv.x = pk(dv[gq][d][0], dv[gq][d][1]);
-      uv.y = pk(dv[gq][d][2], dv[gq][d][3]);
+      uk.x = pk(kok[gq] ? dk[gq][d][0] * ksc : 0.f, kok[gq] ? dk[gq][d][1] * ksc : 0.f);
+      uk.y = pk(kok[gq] ? dk[gq][d][2] * ksc : 0.f, kok[gq] ? dk[gq][d][3] * ksc : 0.f);
+      uv.x = pk(kok[gq] ? dv[gq][d][0] * vsc : 0.f, kok[gq] ? dv[gq][d][1] * vsc : 0.f);
+      uv.y = pk(kok[gq] ? dv[gq][d][2] * vsc : 0.f, kok[gq] ? dv[gq][d][3] * vsc : 0.f);
       *(uint2*)(dKb + d * 16 + 4 * g) = uk;
       *(uint2*)(dVb + d * 16 + 4 * g) = uv;
     }
