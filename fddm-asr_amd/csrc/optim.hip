@@ -77,7 +77,34 @@ __global__ void __launch_bounds__(256) adamw_kernel(MTTable t, const float* tota
                    (pb == nullptr || (((uintptr_t)pb) & 7) == 0);
   if (vec) {  // 4 elements per thread and iteration: 16-B loads/stores, 8-B bf16 copy
     const long n4 = n / 4;
-    for (long j = threadIdx.x; j < n4; j += 256) {
+    // a block owns a 64 K-element chunk (~2.5 blocks per CU for the decoder): 4 iterations' loads are issued
+    // before any update so each thread keeps 16 loads in flight instead of 4
+    constexpr int U = 4;
+    long j0 = threadIdx.x;
+    for (; j0 + 256 * (U - 1) < n4; j0 += 256 * U) {
+      float4 gg[U], pp[U], mm[U], vv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long j = j0 + 256 * u;
+        gg[u] = ((const float4*)g)[j];
+        pp[u] = ((float4*)p)[j];
+        mm[u] = ((float4*)m)[j];
+        vv[u] = ((float4*)v)[j];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long j = j0 + 256 * u;
+        upd(gg[u].x, pp[u].x, mm[u].x, vv[u].x);
+        upd(gg[u].y, pp[u].y, mm[u].y, vv[u].y);
+        upd(gg[u].z, pp[u].z, mm[u].z, vv[u].z);
+        upd(gg[u].w, pp[u].w, mm[u].w, vv[u].w);
+        ((float4*)p)[j] = pp[u];
+        ((float4*)m)[j] = mm[u];
+        ((float4*)v)[j] = vv[u];
+        if (pb) ((uint2*)pb)[j] = make_uint2(pk_bf16(pp[u].x, pp[u].y), pk_bf16(pp[u].z, pp[u].w));
+      }
+    }
+    for (long j = j0; j < n4; j += 256) {
       const float4 gg = ((const float4*)g)[j];
       float4 pp = ((float4*)p)[j], mm = ((float4*)m)[j], vv = ((float4*)v)[j];
       upd(gg.x, pp.x, mm.x, vv.x);

@@ -20,6 +20,8 @@ class FusedAdamW(torch.optim.Optimizer):
     def __init__(self, params, lr=2e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
         self._tables = {}
+        self._ring = None        # pinned host slots for the per-step bias-correction scalars (see _upload)
+        self._ring_i = 0
         self.last_total_sq = None
         self.arena = None
 
@@ -46,10 +48,12 @@ class FusedAdamW(torch.optim.Optimizer):
     def _table(self, group, plist):
         dev = plist[0].device
         cd = rt.compute_dtype()
-        key = tuple((p.data_ptr(), p.grad.data_ptr()) for p in plist) + (cd,)
-        t = self._tables.get(id(group))
-        if t is not None and t[0] == key:
-            return t[1]
+        key = (id(group),) + tuple((p.data_ptr(), p.grad.data_ptr()) for p in plist) + (cd,)
+        t = self._tables.get(key)
+        if t is not None:
+            return t
+        if len(self._tables) >= 8:  # the train step alternates between a few parameter sets (L_fd steps add the
+            self._tables.clear()    # projectors): keep each set's device table instead of rebuilding it per switch
         ct, cs, numel, pp, gp, mp, vp, bp = [], [], [], [], [], [], [], []
         for i, p in enumerate(plist):
             st = self.state[p]
@@ -68,8 +72,29 @@ class FusedAdamW(torch.optim.Optimizer):
                 bp.append(0)
         L = lambda v: torch.tensor(v, dtype=torch.int64).pin_memory().to(dev, non_blocking=True)  # noqa: E731
         tab = dict(ct=L(ct), cs=L(cs), numel=L(numel), p=L(pp), g=L(gp), m=L(mp), v=L(vp), b=L(bp), n=len(ct))
-        self._tables[id(group)] = (key, tab)
+        self._tables[key] = tab
         return tab
+
+    def _upload(self, vals, dev):
+        """Host floats -> device f32 tensor through a ring of reused pinned slots (no pinned allocation per step);
+        a slot is reused only after the copy that last read it has completed (its event)."""
+        R, n = 8, len(vals)
+        if self._ring is None or self._ring[0].shape[1] < n:
+            cap = max(n, 256)
+            self._ring = (torch.empty(R, cap, dtype=torch.float32).pin_memory(), [None] * R,
+                          torch.empty(R, cap, dtype=torch.float32, device=dev))
+        host, evs, devbuf = self._ring
+        i = self._ring_i % R
+        self._ring_i += 1
+        if evs[i] is not None:
+            evs[i].synchronize()
+        host[i, :n] = torch.tensor(vals, dtype=torch.float32)
+        out = devbuf[i, :n]
+        out.copy_(host[i, :n], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dev))
+        evs[i] = ev
+        return out
 
     @torch.no_grad()
     def clip_and_step(self, max_norm: float | None = None):
@@ -106,8 +131,8 @@ class FusedAdamW(torch.optim.Optimizer):
                 st["step"] += 1
                 ss.append(group["lr"] / (1 - b1 ** st["step"]))
                 b2s.append(math.sqrt(1 - b2 ** st["step"]))
-            ss_t = torch.tensor(ss, dtype=torch.float32).pin_memory().to(dev, non_blocking=True)
-            b2_t = torch.tensor(b2s, dtype=torch.float32).pin_memory().to(dev, non_blocking=True)
+            sb = self._upload(ss + b2s, dev)      # one copy for both per-tensor scalar arrays
+            ss_t, b2_t = sb[: len(ss)], sb[len(ss):]
             call("fddm_adamw", tab["ct"].data_ptr(), tab["cs"].data_ptr(), tab["numel"].data_ptr(), tab["p"].data_ptr(),
                  tab["g"].data_ptr(), tab["m"].data_ptr(), tab["v"].data_ptr(), tab["b"].data_ptr(), ss_t.data_ptr(),
                  b2_t.data_ptr(), tab["n"], total.data_ptr() if total is not None else 0,
