@@ -10,7 +10,10 @@ runs on a second HIP stream beside step i's decoder (train._encoded); every time
 once inside the timed region (the first one without overlap).
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
-  N>1: launched by torch.distributed.run, one rank per GPU (RCCL); per-GPU batch fixed ("weak").
+  N>1: one rank per GPU over RCCL, per-GPU batch fixed ("weak"). Under torch.distributed.run (WORLD_SIZE set)
+  the ranks come from the launcher; `python bench.py --gpus N` alone starts that launcher itself (a child
+  process, before this process touches the GPU) and exits with its status. The world size the process group
+  reports must equal N.
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -29,7 +32,6 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-GFLOP_PER_UTT = 193.87          # SURVEY §8(d), C2 (torch.utils.flop_counter on the reference)
 BF16_PEAK_TFLOPS = 2500.0       # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 F32_PEAK_TFLOPS = 157.3
 
@@ -47,8 +49,58 @@ def parse():
     ap.add_argument("--heads", type=int, default=8)
     ap.add_argument("--precision", default="bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--cpu-steps", type=int, default=4)
+    ap.add_argument("--cpu-batch", type=int, default=4)
+    ap.add_argument("--lfd-sync", action="store_true",
+                    help="DP: L_fd / w_t statistics over the global batch (lfd.sync_batch_stats)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="initialise the process group, report the launch shape, do no GPU work")
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        return s_.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """`--gpus N` without a launcher: run this script under torch.distributed.run with N local ranks (one per
+    GPU) as a child process and return its exit status. Nothing here initialises the GPU."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    import subprocess
+    return subprocess.run(cmd, env=dict(os.environ)).returncode
+
+
+def gflop_per_utt(args, S=None):
+    """Algorithmic GFLOP per utterance of one train step (necessary work, SURVEY §8(d) accounting: 2MNK per GEMM
+    / conv, 4 Lq Lk d per attention forward; decoder backward = 2x forward minus the never-applied gradient into
+    the frozen encoder's output (cross K/V projection dX, FiLM pooled dX); L_fd (fwd + bwd) amortised over
+    n_step_fd = 4; WavLM's gated-bias attention is not in the survey's count (its SDPA call escapes
+    torch.utils.flop_counter), so it is left out here too). Reproduces the survey's C2 193.87 / C4 491.68."""
+    d, NL, L, V, FF, P = args.d_model, args.layers, args.seq_len, 8000, 2048, 256
+    S = encoder_frames(args.seconds) if S is None else S
+    n = int(16000 * args.seconds)
+    conv = 0.0
+    cin = 1
+    for k, st in zip((10, 3, 3, 3, 3, 2, 2), (5, 2, 2, 2, 2, 2, 2)):
+        n = (n - k) // st + 1
+        conv += 2.0 * n * 512 * k * cin
+        cin = 512
+    E, EF = 768, 3072
+    enc = conv + 2.0 * S * 512 * E + 2.0 * S * E * 48 * 128 + 12 * (2.0 * S * E * 4 * E + 4.0 * S * E * EF +
+                                                                       2.0 * S * 64 * 8 * 12)
+    if d != E:
+        enc += 2.0 * S * E * d
+    blk = (2.0 * L * d * 3 * d + 4.0 * L * L * d + 2.0 * L * d * d + 2.0 * L * d * d + 2.0 * S * d * 2 * d +
+           4.0 * L * S * d + 2.0 * L * d * d + 4.0 * d * d + 4.0 * L * d * FF)
+    fwd = NL * blk + 2.0 * L * d * V + 2.0 * (4 * d * d * 2 + d * d)
+    bwd = 2.0 * fwd - NL * (2.0 * S * d * 2 * d + 4.0 * d * d)
+    lfd_f = 2.0 * L * V * P + 2.0 * L * P * P + 2.0 * S * d * P + 2.0 * L * P * P
+    lfd_b = 2 * 2.0 * L * V * P + 2 * 2.0 * L * P * P + 2.0 * S * d * P + 2 * 2.0 * L * P * P
+    return (enc + fwd + bwd + (lfd_f + lfd_b) / 4) / 1e9
 
 
 def build(args, device):
@@ -105,9 +157,17 @@ def dominant_flops(args):
     return 2.0 * args.batch * T1 * 512 * 3 * 512
 
 
+def config_tag(args):
+    geom = (args.layers, args.d_model, args.heads, args.seq_len, args.seconds)
+    if geom == (6, 512, 8, 256, 10.0) and args.batch == 32:
+        return "fddm_zhTW_base C2"
+    if geom == (12, 768, 12, 512, 10.0) and args.batch == 16:
+        return "C4 (BASELINE configs[3], per GPU)"
+    return "custom"
+
+
 def workload_name(args):
-    c2 = (args.layers, args.d_model, args.heads, args.seq_len, args.batch, args.seconds) == (6, 512, 8, 256, 32, 10.0)
-    tag = "fddm_zhTW_base C2" if c2 else "custom"
+    tag = config_tag(args)
     return (f"{tag}: WavLM-base + {args.layers}L d{args.d_model} H{args.heads} ff2048 decoder, V=8000, T=200, "
             f"dropout 0.1, n_step_fd=4")
 
@@ -149,6 +209,7 @@ def cpu_baseline(args, models):
     from oracle import fddm_oracle as O
     ncores = min(16, len(os.sched_getaffinity(0)))
     torch.set_num_threads(ncores)
+    nthreads = torch.get_num_threads()
     enc, dec, sp, te, tp, sch = models
     enc_sd = {k: v.detach().float().cpu() for k, v in enc.state_dict().items()}
     w = enc.backbone.encoder.pos_conv_embed.conv.weight.detach().float().cpu()
@@ -161,7 +222,7 @@ def cpu_baseline(args, models):
     cfg = dict(d_model=args.d_model, nhead=args.heads, num_layers=args.layers, pad_id=0, n_step_fd=4, tau=1.0,
                lambda_offdiag=5e-3)
     g = torch.Generator().manual_seed(0)
-    Bc, L = 2, args.seq_len
+    Bc, L = args.cpu_batch, args.seq_len
     ns = int(16000 * args.seconds)
     del w
     t0 = time.perf_counter()
@@ -172,30 +233,56 @@ def cpu_baseline(args, models):
         xt = O.sample_xt(x0, t, 8000, ab, seed=i)
         O.oracle_train_step(params, enc_sd, geom, wave, x0, t, xt, cfg, opt, i + 4, betas, ab)
     dt = time.perf_counter() - t0
-    return {"value": round(Bc * args.cpu_steps / dt, 4), "unit": "utterances/s", "cores": ncores, "kind": "port",
+    return {"value": round(Bc * args.cpu_steps / dt, 4), "unit": "utterances/s", "cores": nthreads, "kind": "port",
+            "torch_threads": nthreads, "affinity_cpus": len(os.sched_getaffinity(0)),
             "sample": f"oracle train step (CPU fp32 restatement), {args.cpu_steps} steps x {Bc} utt x "
-                      f"{args.seconds:g} s, C2 geometry, incl. one L_fd step; {dt:.1f} s wall"}
+                      f"{args.seconds:g} s, same geometry as the GPU line, global steps 4..{3 + args.cpu_steps} "
+                      f"(L_fd on 1 in 4); {dt:.1f} s wall"}
 
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     # FDDM_DIST_BACKEND=gloo rehearses the N > 1 path with every rank on one GPU (local % device_count);
     # the driver's multi-GPU runs use the default: RCCL ("nccl"), one GPU per rank
     backend = os.environ.get("FDDM_DIST_BACKEND", "nccl")
-    if backend != "nccl":
-        local = local % torch.cuda.device_count()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        if backend == "nccl" and not args.dry_run and torch.cuda.device_count() < args.gpus:
+            sys.exit(f"bench.py: --gpus {args.gpus} but only {torch.cuda.device_count()} GPU(s) visible")
+        sys.exit(launch_ranks(args.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: launcher started {world} rank(s) but --gpus is {args.gpus}")
     if world > 1:
-        torch.cuda.set_device(local)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        from datetime import timedelta
+        timeout = timedelta(seconds=int(os.environ.get("FDDM_DIST_TIMEOUT_S", "600")))
+        if args.dry_run:
+            dist.init_process_group("gloo", timeout=timeout)
         else:
-            dist.init_process_group(backend)
+            if backend != "nccl":
+                local = local % torch.cuda.device_count()
+            torch.cuda.set_device(local)
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=timeout)
+            else:
+                dist.init_process_group(backend, timeout=timeout)
+        world = dist.get_world_size()
+        if world != args.gpus:
+            sys.exit(f"bench.py: process group has {world} rank(s), --gpus is {args.gpus}")
+    if args.dry_run:
+        if rank == 0:
+            print(json.dumps({"n_gpus": world, "parallelism": f"dp{world}", "backend": backend,
+                              "global_batch": args.batch * world}), flush=True)
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
     device = torch.device("cuda", local)
     torch.manual_seed(1337 + rank)
     T_, cfg, models, opt = build(args, device)
+    if args.lfd_sync:
+        cfg.lfd["sync_batch_stats"] = True
     from fddm_hip import runtime as rt
     rt.reseed(1337 + rank)
     enc, dec, sp, te, tp, sch = models
@@ -241,7 +328,8 @@ def main():
         iev = aprobes["wavlm.conv1"]
         iso_ms = sum(a.elapsed_time(b) for a, b in iev) / max(1, len(iev))
         iso = kflops / (iso_ms * 1e-3) / 1e12
-        step_tflops = value / world * GFLOP_PER_UTT / 1e3
+        gpu_utt = gflop_per_utt(args)
+        step_tflops = value / world * gpu_utt / 1e3
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(args, models)
@@ -263,6 +351,8 @@ def main():
             "decoder_attention": decoder_attention(args, aprobes, peak),
             "step_mfma_frac": round(step_tflops / peak, 4),
             "step_tflops": round(step_tflops, 1),
+            "gflop_per_utt": round(gpu_utt, 2),
+            "lfd_batch_stats": "global" if (args.lfd_sync and world > 1) else "local",
             "avg_loss": round(avg_loss, 4),
             "cpu_baseline": cpu,
         }

@@ -43,6 +43,67 @@ __global__ void lfd_std_bwd_kernel(const float* __restrict__ dzt, const T* __res
   for (long b = 0; b < B; ++b) dz[b * C + c] = (dzt[b * C + c] - m1 - ld<T>(zt + b * C + c) * m2) * is;
 }
 
+// ---- data-parallel form: the batch statistics of the standardisation span every rank's rows.
+// Each rank reduces its own rows per column; the caller all-reduces the partial sums between the passes.
+// pass 1 (mean_sum == null): out[c] = sum_b z[b][c];  pass 2: out[c] = sum_b (z[b][c] - mean_sum[c]*inv_n)^2
+__global__ void lfd_colstat_kernel(const float* __restrict__ z, float* __restrict__ out, const float* __restrict__ mean_sum,
+                                   float inv_n, long B, long C) {
+  const long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float acc = 0.f;
+  if (mean_sum == nullptr) {
+    for (long b = 0; b < B; ++b) acc += z[b * C + c];
+  } else {
+    const float m = mean_sum[c] * inv_n;
+    for (long b = 0; b < B; ++b) {
+      const float t = z[b * C + c] - m;
+      acc += t * t;
+    }
+  }
+  out[c] = acc;
+}
+
+// z~ = (z - S1*inv_n) / sqrt(S2*inv_n + eps) from the global column sums S1 (sum z) and S2 (centred squares)
+template <typename OT>
+__global__ void lfd_std_apply_kernel(const float* __restrict__ z, OT* __restrict__ zt, float* __restrict__ inv_std,
+                                     const float* __restrict__ s1, const float* __restrict__ s2, float inv_n, float eps,
+                                     long B, long C) {
+  const long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float m = s1[c] * inv_n;
+  const float is = 1.f / sqrtf(s2[c] * inv_n + eps);
+  inv_std[c] = is;
+  for (long b = 0; b < B; ++b) st<OT>(zt + b * C + c, (z[b * C + c] - m) * is);
+}
+
+// backward partial sums: out[c] = sum_b dz~, out[C + c] = sum_b dz~ * z~
+template <typename T>
+__global__ void lfd_bwd_colstat_kernel(const float* __restrict__ dzt, const T* __restrict__ zt, float* __restrict__ out,
+                                       long B, long C) {
+  const long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float m1 = 0.f, m2 = 0.f;
+  for (long b = 0; b < B; ++b) {
+    const float g = dzt[b * C + c];
+    m1 += g;
+    m2 += g * ld<T>(zt + b * C + c);
+  }
+  out[c] = m1;
+  out[C + c] = m2;
+}
+
+// dz = scale * (dz~ - S1*inv_n - z~ * S2*inv_n) * inv_std   (S1, S2: global sums of lfd_bwd_colstat)
+template <typename T>
+__global__ void lfd_std_bwd_apply_kernel(const float* __restrict__ dzt, const T* __restrict__ zt,
+                                         const float* __restrict__ inv_std, const float* __restrict__ sums, float inv_n,
+                                         float scale, float* __restrict__ dz, long B, long C) {
+  const long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float m1 = sums[c] * inv_n, m2 = sums[C + c] * inv_n;
+  const float is = inv_std[c] * scale;
+  for (long b = 0; b < B; ++b) dz[b * C + c] = (dzt[b * C + c] - m1 - ld<T>(zt + b * C + c) * m2) * is;
+}
+
 // loss = sum_j (1 - C_jj)^2 + lambda * sum_{j!=k} C_jk^2   (single block)
 __global__ void __launch_bounds__(256) lfd_loss_kernel(const float* __restrict__ Cm, float* __restrict__ loss, long D,
                                                        float lam) {
@@ -105,5 +166,48 @@ FDDM_API int fddm_lfd_dloss(int out_dtype, const float* Cm, const float* gscale,
     hipLaunchKernelGGL((lfd_dloss_kernel<bf16_t>), g, dim3(256), 0, (hipStream_t)hs, Cm, gscale, (bf16_t*)dC, D, lam);
   else
     hipLaunchKernelGGL((lfd_dloss_kernel<float>), g, dim3(256), 0, (hipStream_t)hs, Cm, gscale, (float*)dC, D, lam);
+  return (int)hipGetLastError();
+}
+
+FDDM_API int fddm_lfd_colstat(const float* z, float* out, const float* mean_sum, float inv_n, long B, long C, void* hs) {
+  if (C <= 0) return 0;
+  hipLaunchKernelGGL(lfd_colstat_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, (hipStream_t)hs, z, out,
+                     mean_sum, inv_n, B, C);
+  return (int)hipGetLastError();
+}
+
+FDDM_API int fddm_lfd_std_apply(int out_dtype, const float* z, void* zt, float* inv_std, const float* s1, const float* s2,
+                                float inv_n, float eps, long B, long C, void* hs) {
+  if (C <= 0) return 0;
+  dim3 g((unsigned)((C + 255) / 256));
+  if (out_dtype == FDDM_BF16)
+    hipLaunchKernelGGL((lfd_std_apply_kernel<bf16_t>), g, dim3(256), 0, (hipStream_t)hs, z, (bf16_t*)zt, inv_std, s1, s2,
+                       inv_n, eps, B, C);
+  else
+    hipLaunchKernelGGL((lfd_std_apply_kernel<float>), g, dim3(256), 0, (hipStream_t)hs, z, (float*)zt, inv_std, s1, s2,
+                       inv_n, eps, B, C);
+  return (int)hipGetLastError();
+}
+
+FDDM_API int fddm_lfd_bwd_colstat(int zt_dtype, const float* dzt, const void* zt, float* out, long B, long C, void* hs) {
+  if (C <= 0) return 0;
+  dim3 g((unsigned)((C + 255) / 256));
+  if (zt_dtype == FDDM_BF16)
+    hipLaunchKernelGGL((lfd_bwd_colstat_kernel<bf16_t>), g, dim3(256), 0, (hipStream_t)hs, dzt, (const bf16_t*)zt, out, B, C);
+  else
+    hipLaunchKernelGGL((lfd_bwd_colstat_kernel<float>), g, dim3(256), 0, (hipStream_t)hs, dzt, (const float*)zt, out, B, C);
+  return (int)hipGetLastError();
+}
+
+FDDM_API int fddm_lfd_std_bwd_apply(int zt_dtype, const float* dzt, const void* zt, const float* inv_std, const float* sums,
+                                    float inv_n, float scale, float* dz, long B, long C, void* hs) {
+  if (C <= 0) return 0;
+  dim3 g((unsigned)((C + 255) / 256));
+  if (zt_dtype == FDDM_BF16)
+    hipLaunchKernelGGL((lfd_std_bwd_apply_kernel<bf16_t>), g, dim3(256), 0, (hipStream_t)hs, dzt, (const bf16_t*)zt, inv_std,
+                       sums, inv_n, scale, dz, B, C);
+  else
+    hipLaunchKernelGGL((lfd_std_bwd_apply_kernel<float>), g, dim3(256), 0, (hipStream_t)hs, dzt, (const float*)zt, inv_std,
+                       sums, inv_n, scale, dz, B, C);
   return (int)hipGetLastError();
 }

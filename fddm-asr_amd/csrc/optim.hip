@@ -4,8 +4,12 @@
 //      p *= (1 - lr*wd); m = lerp(m, g', 1-b1); v = b2 v + (1-b2) g'^2;
 //      p -= (lr/bc1) * m / (sqrt(v)/sqrt(bc2) + eps)          (torch.optim.AdamW single-tensor form)
 //      and optionally a bf16 copy of p for the next forward's MFMA operands.
-// No host synchronisation: the clip coefficient is read on the device. Tensors whose grad is None
-// are simply not in the list (set_to_none semantics, train.py:400).
+//   3) per tensor: step += 1 (device-side step counters, torch's AdamW `state["step"]`).
+// No host synchronisation: the clip coefficient and the bias corrections (from the device step counters, in
+// double like torch's host arithmetic) are computed on the device. Non-finite guard: when the gradient sum of
+// squares is inf/NaN the whole step is skipped — no parameter, moment or step-counter update — as
+// GradScaler.step skips it on the reference's GPU path (train.py:401-413); `skipped` counts such steps.
+// Tensors whose grad is None are simply not in the list (set_to_none semantics, train.py:400).
 #include "common.h"
 
 namespace fddm {
@@ -19,8 +23,7 @@ struct MTTable {
   float* const* m;
   float* const* v;
   bf16_t* const* pbf;        // entries may be null
-  const float* step_size;    // [ntensors] lr / bc1
-  const float* bc2_sqrt;     // [ntensors]
+  float* const* step;        // [ntensors] device step counters (0-d fp32 tensors)
 };
 
 constexpr long MT_CHUNK = 65536;
@@ -49,22 +52,28 @@ __global__ void __launch_bounds__(256) sumsq_kernel(MTTable t, float* total) {
   if (threadIdx.x == 0) atomicAdd(total, v);
 }
 
-__global__ void __launch_bounds__(256) adamw_kernel(MTTable t, const float* total, float max_norm, float lr_wd, float b1,
-                                                    float b2, float eps) {
+__global__ void __launch_bounds__(256) adamw_kernel(MTTable t, const float* total, float max_norm, float lr, float lr_wd,
+                                                    float b1, float b2, float eps) {
   const long ci = blockIdx.x;
   const long ti = t.chunk_tensor[ci], s0 = t.chunk_start[ci];
   const long n = min(MT_CHUNK, t.numel[ti] - s0);
   float coef = 1.f;
   if (total) {
-    coef = max_norm / (sqrtf(total[0]) + 1e-6f);
-    coef = fminf(coef, 1.f);
+    if (!isfinite(total[0])) return;  // non-finite gradients: skip the step (GradScaler semantics)
+    if (max_norm > 0.f) {
+      coef = max_norm / (sqrtf(total[0]) + 1e-6f);
+      coef = fminf(coef, 1.f);
+    }
   }
+  // bias corrections of this step (torch: step_size = lr / (1 - b1^step), bc2_sqrt = sqrt(1 - b2^step), in double)
+  const double stp = (double)t.step[ti][0] + 1.0;
+  const float ss = (float)((double)lr / (1.0 - pow((double)b1, stp)));
+  const float bc2s = (float)sqrt(1.0 - pow((double)b2, stp));
   float* p = t.p[ti] + s0;
   const float* g = t.g[ti] + s0;
   float* m = t.m[ti] + s0;
   float* v = t.v[ti] + s0;
   bf16_t* pb = t.pbf[ti] ? t.pbf[ti] + s0 : nullptr;
-  const float ss = t.step_size[ti], bc2s = t.bc2_sqrt[ti];
   auto upd = [&](float gg, float& pp, float& mm, float& vv) {
     gg *= coef;
     pp *= 1.f - lr_wd;
@@ -128,6 +137,15 @@ __global__ void __launch_bounds__(256) adamw_kernel(MTTable t, const float* tota
   }
 }
 
+// step counters advance after every chunk of the step has read them (separate launch); a skipped step leaves them
+__global__ void __launch_bounds__(256) adamw_step_kernel(float* const* step, long ntensors, const float* total,
+                                                         int* skipped) {
+  const bool ok = total == nullptr || isfinite(total[0]);
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < ntensors; i += (long)gridDim.x * blockDim.x)
+    if (ok) step[i][0] += 1.f;
+  if (!ok && skipped && blockIdx.x == 0 && threadIdx.x == 0) skipped[0] += 1;
+}
+
 }  // namespace fddm
 
 using namespace fddm;
@@ -135,18 +153,21 @@ using namespace fddm;
 FDDM_API int fddm_grad_sumsq(const long* chunk_tensor, const long* chunk_start, const long* numel, const float* const* g,
                              long nchunks, float* total, void* hs) {
   if (nchunks <= 0) return 0;
-  MTTable t{chunk_tensor, chunk_start, numel, nullptr, g, nullptr, nullptr, nullptr, nullptr, nullptr};
+  MTTable t{chunk_tensor, chunk_start, numel, nullptr, g, nullptr, nullptr, nullptr, nullptr};
   hipLaunchKernelGGL(sumsq_kernel, dim3((unsigned)nchunks), dim3(256), 0, (hipStream_t)hs, t, total);
   return (int)hipGetLastError();
 }
 
 FDDM_API int fddm_adamw(const long* chunk_tensor, const long* chunk_start, const long* numel, float* const* p,
-                        const float* const* g, float* const* m, float* const* v, bf16_t* const* pbf,
-                        const float* step_size, const float* bc2_sqrt, long nchunks, const float* total, float max_norm,
-                        float lr_wd, float b1, float b2, float eps, void* hs) {
+                        const float* const* g, float* const* m, float* const* v, bf16_t* const* pbf, float* const* step,
+                        long ntensors, long nchunks, const float* total, float max_norm, float lr, float lr_wd, float b1,
+                        float b2, float eps, int* skipped, void* hs) {
   if (nchunks <= 0) return 0;
-  MTTable t{chunk_tensor, chunk_start, numel, p, g, m, v, pbf, step_size, bc2_sqrt};
-  hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)nchunks), dim3(256), 0, (hipStream_t)hs, t, total, max_norm, lr_wd, b1,
-                     b2, eps);
+  MTTable t{chunk_tensor, chunk_start, numel, p, g, m, v, pbf, step};
+  hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)nchunks), dim3(256), 0, (hipStream_t)hs, t, total, max_norm, lr, lr_wd,
+                     b1, b2, eps);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(adamw_step_kernel, dim3(1), dim3(256), 0, (hipStream_t)hs, step, ntensors, total, skipped);
   return (int)hipGetLastError();
 }

@@ -73,6 +73,19 @@ def world() -> int:
     return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
 
 
+def default_group():
+    return dist.group.WORLD
+
+
+@torch.no_grad()
+def global_mean(x: torch.Tensor, group=None) -> torch.Tensor:
+    """Mean over ranks of a per-rank batch mean (equal local batches): w_t's batch mean (train.py:390) of the
+    global batch under DP."""
+    y = x.detach().float().reshape(1).clone()
+    dist.all_reduce(y, group=group)
+    return (y / dist.get_world_size(group)).reshape(x.shape)
+
+
 @torch.no_grad()
 def allreduce_grads(params, bucket_bytes: int = BUCKET_BYTES) -> None:
     W = world()

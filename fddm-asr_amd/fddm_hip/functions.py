@@ -471,34 +471,71 @@ class TextEmbedFn(torch.autograd.Function):
 
 # ---------------------------------------------------------------------------------------- L_fd
 class LfdFn(torch.autograd.Function):
-    """lfd_loss (losses/fddm_losses.py:29-58): batch-dim standardisation + C = za~^T zb~ /(B T)."""
+    """lfd_loss (losses/fddm_losses.py:29-58): batch-dim standardisation + C = za~^T zb~ /(B T).
+
+    `group` (a torch.distributed process group, or None): data-parallel form with the statistics of the GLOBAL
+    batch — the column sums of the standardisation (two passes), the [D, D] cross-correlation and,
+    in backward, the two column sums of the standardisation gradient are all-reduced (~1 MB per L_fd step at C2),
+    so every rank gets the loss of the whole batch; each rank's input gradient is that of the global loss w.r.t.
+    its own rows, scaled by the world size so the DP gradient average (sum / W) yields the global-batch gradient."""
 
     @staticmethod
-    def forward(ctx, z_a, z_b, lam, eps):
+    def forward(ctx, z_a, z_b, lam, eps, group=None):
         B, T, D = z_a.shape
         cd = rt.compute_dtype()
-        za, isa = ops.lfd_std_fwd(z_a.reshape(B, T * D).float().contiguous(), cd, eps)
-        zb, isb = ops.lfd_std_fwd(z_b.reshape(B, T * D).float().contiguous(), cd, eps)
+        a2 = z_a.reshape(B, T * D).float().contiguous()
+        b2 = z_b.reshape(B, T * D).float().contiguous()
+        if group is None:
+            za, isa = ops.lfd_std_fwd(a2, cd, eps)
+            zb, isb = ops.lfd_std_fwd(b2, cd, eps)
+            N, W = B, 1
+        else:
+            import torch.distributed as dist
+            W = dist.get_world_size(group)
+            N = B * W          # every rank holds B rows (the DP contract the KL average already relies on)
+            C = T * D
+            st = torch.empty(2 * C, device=z_a.device, dtype=F32)
+            ops.lfd_colstat(a2, st[:C])
+            ops.lfd_colstat(b2, st[C:])
+            dist.all_reduce(st, group=group)
+            sq = torch.empty(2 * C, device=z_a.device, dtype=F32)
+            ops.lfd_colstat(a2, sq[:C], st[:C], 1.0 / N)
+            ops.lfd_colstat(b2, sq[C:], st[C:], 1.0 / N)
+            dist.all_reduce(sq, group=group)
+            za, isa = ops.lfd_std_apply(a2, cd, st[:C], sq[:C], 1.0 / N, eps)
+            zb, isb = ops.lfd_std_apply(b2, cd, st[C:], sq[C:], 1.0 / N, eps)
         za2, zb2 = za.view(B * T, D), zb.view(B * T, D)
         Cm = torch.empty(D, D, device=z_a.device, dtype=F32)
-        ops.gemm(za2, zb2, Cm, D, D, B * T, a_kc=False, b_kc=False, lda=D, ldb=D, ldc=D, alpha=1.0 / (B * T))
+        ops.gemm(za2, zb2, Cm, D, D, B * T, a_kc=False, b_kc=False, lda=D, ldb=D, ldc=D, alpha=1.0 / (N * T))
+        if group is not None:
+            dist.all_reduce(Cm, group=group)
         loss = ops.lfd_loss(Cm, lam)
         ctx.save_for_backward(za, zb, isa, isb, Cm)
-        ctx.args = (B, T, D, lam)
+        ctx.args = (B, T, D, lam, N, W, group)
         return loss
 
     @staticmethod
     def backward(ctx, g):
         za, zb, isa, isb, Cm = ctx.saved_tensors
-        B, T, D, lam = ctx.args
+        B, T, D, lam, N, W, group = ctx.args
         cd = rt.compute_dtype()
         dC = ops.lfd_dloss(Cm, g.reshape(1).to(F32).contiguous(), lam, cd)
         za2, zb2 = za.view(B * T, D), zb.view(B * T, D)
         dza = torch.empty(B * T, D, device=za.device, dtype=F32)
         dzb = torch.empty(B * T, D, device=za.device, dtype=F32)
-        # dza~[n][i] = sum_j dC[i][j] zb~[n][j] / BT ;  dzb~[n][j] = sum_i za~[n][i] dC[i][j] / BT
-        ops.gemm(zb2, dC, dza, B * T, D, D, a_kc=True, b_kc=True, lda=D, ldb=D, ldc=D, alpha=1.0 / (B * T))
-        ops.gemm(za2, dC, dzb, B * T, D, D, a_kc=True, b_kc=False, lda=D, ldb=D, ldc=D, alpha=1.0 / (B * T))
-        ga = ops.lfd_std_bwd(dza.view(B, T * D), za, isa).view(B, T, D)
-        gb = ops.lfd_std_bwd(dzb.view(B, T * D), zb, isb).view(B, T, D)
-        return ga, gb, None, None
+        # dza~[n][i] = sum_j dC[i][j] zb~[n][j] / NT ;  dzb~[n][j] = sum_i za~[n][i] dC[i][j] / NT
+        ops.gemm(zb2, dC, dza, B * T, D, D, a_kc=True, b_kc=True, lda=D, ldb=D, ldc=D, alpha=1.0 / (N * T))
+        ops.gemm(za2, dC, dzb, B * T, D, D, a_kc=True, b_kc=False, lda=D, ldb=D, ldc=D, alpha=1.0 / (N * T))
+        if group is None:
+            ga = ops.lfd_std_bwd(dza.view(B, T * D), za, isa).view(B, T, D)
+            gb = ops.lfd_std_bwd(dzb.view(B, T * D), zb, isb).view(B, T, D)
+        else:
+            import torch.distributed as dist
+            C = T * D
+            sums = torch.empty(4 * C, device=za.device, dtype=F32)
+            ops.lfd_bwd_colstat(dza.view(B, C), za, sums[:2 * C])
+            ops.lfd_bwd_colstat(dzb.view(B, C), zb, sums[2 * C:])
+            dist.all_reduce(sums, group=group)
+            ga = ops.lfd_std_bwd_apply(dza.view(B, C), za, isa, sums[:2 * C], 1.0 / N, float(W)).view(B, T, D)
+            gb = ops.lfd_std_bwd_apply(dzb.view(B, C), zb, isb, sums[2 * C:], 1.0 / N, float(W)).view(B, T, D)
+        return ga, gb, None, None, None

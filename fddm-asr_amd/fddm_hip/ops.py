@@ -348,6 +348,37 @@ def lfd_std_bwd(dzt, zt, inv_std):
     return dz
 
 
+def lfd_colstat(z2d, out, mean_sum=None, inv_n=0.0):
+    B, C = z2d.shape
+    _chk(out.numel() >= C and out.dtype == torch.float32, "lfd_colstat out")
+    call("fddm_lfd_colstat", ptr(z2d), ptr(out), ptr(mean_sum), float(inv_n), B, C, stream())
+    return out
+
+
+def lfd_std_apply(z2d, out_dtype, s1, s2, inv_n, eps=1e-5):
+    B, C = z2d.shape
+    zt = torch.empty(B, C, device=z2d.device, dtype=out_dtype)
+    inv_std = torch.empty(C, device=z2d.device, dtype=torch.float32)
+    call("fddm_lfd_std_apply", code(zt), ptr(z2d), ptr(zt), ptr(inv_std), ptr(s1), ptr(s2), float(inv_n), float(eps), B,
+         C, stream())
+    return zt, inv_std
+
+
+def lfd_bwd_colstat(dzt, zt, out):
+    B, C = dzt.shape
+    _chk(out.numel() >= 2 * C and out.dtype == torch.float32, "lfd_bwd_colstat out")
+    call("fddm_lfd_bwd_colstat", code(zt), ptr(dzt), ptr(zt), ptr(out), B, C, stream())
+    return out
+
+
+def lfd_std_bwd_apply(dzt, zt, inv_std, sums, inv_n, scale=1.0):
+    B, C = dzt.shape
+    dz = torch.empty(B, C, device=dzt.device, dtype=torch.float32)
+    call("fddm_lfd_std_bwd_apply", code(zt), ptr(dzt), ptr(zt), ptr(inv_std), ptr(sums), float(inv_n), float(scale),
+         ptr(dz), B, C, stream())
+    return dz
+
+
 def lfd_loss(Cm, lam):
     D = Cm.shape[0]
     loss = torch.empty((), device=Cm.device, dtype=torch.float32)

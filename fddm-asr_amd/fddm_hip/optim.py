@@ -1,8 +1,10 @@
-"""Fused clip_grad_norm_ + AdamW (train.py:411-423) over libfddm_hip: two launches per step, no
-host synchronisation, and the bf16 weight copies for the next forward written in the same pass."""
-from __future__ import annotations
+"""Fused clip_grad_norm_ + AdamW (train.py:411-423) over libfddm_hip: three launches per step, no
+host synchronisation, and the bf16 weight copies for the next forward written in the same pass.
 
-import math
+`state["step"]` is a 0-d fp32 tensor on the parameter's device (torch.optim.AdamW keeps a 0-d fp32 tensor
+too; its capturable/fused variants keep it on the device), advanced by the kernel, so a step skipped by the
+non-finite guard (GradScaler semantics, reference train.py:401-413) leaves the bias corrections exact."""
+from __future__ import annotations
 
 import torch
 
@@ -20,10 +22,9 @@ class FusedAdamW(torch.optim.Optimizer):
     def __init__(self, params, lr=2e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
         self._tables = {}
-        self._ring = None        # pinned host slots for the per-step bias-correction scalars (see _upload)
-        self._ring_i = 0
         self.last_total_sq = None
         self.arena = None
+        self._skipped = None     # device int32: steps skipped by the non-finite guard
 
     def use_grad_arena(self, params, order=None):
         """Back the grads of `params` (parameters that get a gradient every step) by one flat buffer
@@ -45,16 +46,32 @@ class FusedAdamW(torch.optim.Optimizer):
                         p.grad.zero_()
         self.arena.zero_()
 
+    @staticmethod
+    def _bufs_live(plist, bufs) -> bool:
+        """The bf16 copies a table writes are still the runtime cache's live entries for their parameters."""
+        for p, b in zip(plist, bufs):
+            if b is not None and rt.bf16_entry(p) is not b:
+                return False
+        return True
+
     def _table(self, group, plist):
         dev = plist[0].device
         cd = rt.compute_dtype()
-        key = (id(group),) + tuple((p.data_ptr(), p.grad.data_ptr()) for p in plist) + (cd,)
+        key = (id(group),) + tuple((p.data_ptr(), p.grad.data_ptr(), self.state[p]["step"].data_ptr())
+                                   for p in plist) + (cd,)
         t = self._tables.get(key)
         if t is not None:
-            return t
+            # the runtime replaced or dropped cached bf16 copies since the table was built (clear_cache, a
+            # parameter changed in place): rebuild, so the kernel never writes a copy the forward no longer reads
+            if t["gen"] == rt.wcache_generation():
+                return t
+            if self._bufs_live(plist, t["bufs"]):
+                t["gen"] = rt.wcache_generation()
+                return t
+            del self._tables[key]
         if len(self._tables) >= 8:  # the train step alternates between a few parameter sets (L_fd steps add the
             self._tables.clear()    # projectors): keep each set's device table instead of rebuilding it per switch
-        ct, cs, numel, pp, gp, mp, vp, bp = [], [], [], [], [], [], [], []
+        ct, cs, numel, pp, gp, mp, vp, bp, sp, bufs = [], [], [], [], [], [], [], [], [], []
         for i, p in enumerate(plist):
             st = self.state[p]
             n = p.numel()
@@ -66,35 +83,42 @@ class FusedAdamW(torch.optim.Optimizer):
             gp.append(p.grad.data_ptr())
             mp.append(st["exp_avg"].data_ptr())
             vp.append(st["exp_avg_sq"].data_ptr())
+            sp.append(st["step"].data_ptr())
             if cd == torch.bfloat16 and p.dim() >= 2:
-                bp.append(rt.wt_bf16_buffer(p).data_ptr())
+                b = rt.wt_bf16_buffer(p)
+                bufs.append(b)               # held by the table: the kernel never writes freed memory
+                bp.append(b.data_ptr())
             else:
+                bufs.append(None)
                 bp.append(0)
         L = lambda v: torch.tensor(v, dtype=torch.int64).pin_memory().to(dev, non_blocking=True)  # noqa: E731
-        tab = dict(ct=L(ct), cs=L(cs), numel=L(numel), p=L(pp), g=L(gp), m=L(mp), v=L(vp), b=L(bp), n=len(ct))
+        tab = dict(ct=L(ct), cs=L(cs), numel=L(numel), p=L(pp), g=L(gp), m=L(mp), v=L(vp), b=L(bp), s=L(sp),
+                   n=len(ct), nt=len(plist), bufs=bufs, gen=rt.wcache_generation())
         self._tables[key] = tab
         return tab
 
-    def _upload(self, vals, dev):
-        """Host floats -> device f32 tensor through a ring of reused pinned slots (no pinned allocation per step);
-        a slot is reused only after the copy that last read it has completed (its event)."""
-        R, n = 8, len(vals)
-        if self._ring is None or self._ring[0].shape[1] < n:
-            cap = max(n, 256)
-            self._ring = (torch.empty(R, cap, dtype=torch.float32).pin_memory(), [None] * R,
-                          torch.empty(R, cap, dtype=torch.float32, device=dev))
-        host, evs, devbuf = self._ring
-        i = self._ring_i % R
-        self._ring_i += 1
-        if evs[i] is not None:
-            evs[i].synchronize()
-        host[i, :n] = torch.tensor(vals, dtype=torch.float32)
-        out = devbuf[i, :n]
-        out.copy_(host[i, :n], non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(dev))
-        evs[i] = ev
-        return out
+    def _init_state(self, p):
+        st = self.state[p]
+        if not st:
+            st["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
+            st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+        elif not (torch.is_tensor(st["step"]) and st["step"].device == p.device and st["step"].dtype == torch.float32
+                  and st["step"].dim() == 0):
+            st["step"] = torch.tensor(float(st["step"]), dtype=torch.float32, device=p.device)
+        return st
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        self._tables.clear()
+        for group in self.param_groups:
+            for p in group["params"]:
+                if self.state.get(p):
+                    self._init_state(p)
+
+    def skipped_steps(self):
+        """Device int32 count of steps skipped by the non-finite guard (None before the first step)."""
+        return self._skipped
 
     @torch.no_grad()
     def clip_and_step(self, max_norm: float | None = None):
@@ -106,40 +130,29 @@ class FusedAdamW(torch.optim.Optimizer):
             if not plist:
                 continue
             for p in plist:
-                st = self.state[p]
-                if not st:
-                    st["step"] = 0
-                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                self._init_state(p)
                 if p.grad.dtype != torch.float32 or not p.grad.is_contiguous():
                     p.grad = p.grad.float().contiguous()
             groups.append((group, plist, self._table(group, plist)))
         if not groups:
             return None
         dev = groups[0][1][0].device
-        total = None
-        if max_norm is not None:
-            total = torch.zeros(1, device=dev, dtype=torch.float32)
-            for group, plist, tab in groups:
-                call("fddm_grad_sumsq", tab["ct"].data_ptr(), tab["cs"].data_ptr(), tab["numel"].data_ptr(),
-                     tab["g"].data_ptr(), tab["n"], total.data_ptr(), stream())
+        if self._skipped is None:
+            self._skipped = torch.zeros(1, device=dev, dtype=torch.int32)
+        # the gradient sum of squares feeds both the clip coefficient and the non-finite guard
+        total = torch.zeros(1, device=dev, dtype=torch.float32)
+        for group, plist, tab in groups:
+            call("fddm_grad_sumsq", tab["ct"].data_ptr(), tab["cs"].data_ptr(), tab["numel"].data_ptr(),
+                 tab["g"].data_ptr(), tab["n"], total.data_ptr(), stream())
         for group, plist, tab in groups:
             b1, b2 = group["betas"]
-            ss, b2s = [], []
-            for p in plist:
-                st = self.state[p]
-                st["step"] += 1
-                ss.append(group["lr"] / (1 - b1 ** st["step"]))
-                b2s.append(math.sqrt(1 - b2 ** st["step"]))
-            sb = self._upload(ss + b2s, dev)      # one copy for both per-tensor scalar arrays
-            ss_t, b2_t = sb[: len(ss)], sb[len(ss):]
             call("fddm_adamw", tab["ct"].data_ptr(), tab["cs"].data_ptr(), tab["numel"].data_ptr(), tab["p"].data_ptr(),
-                 tab["g"].data_ptr(), tab["m"].data_ptr(), tab["v"].data_ptr(), tab["b"].data_ptr(), ss_t.data_ptr(),
-                 b2_t.data_ptr(), tab["n"], total.data_ptr() if total is not None else 0,
-                 float(max_norm or 0.0), float(group["lr"] * group["weight_decay"]), float(b1), float(b2),
-                 float(group["eps"]), stream())
+                 tab["g"].data_ptr(), tab["m"].data_ptr(), tab["v"].data_ptr(), tab["b"].data_ptr(), tab["s"].data_ptr(),
+                 tab["nt"], tab["n"], total.data_ptr(), float(max_norm or 0.0), float(group["lr"]),
+                 float(group["lr"] * group["weight_decay"]), float(b1), float(b2), float(group["eps"]),
+                 self._skipped.data_ptr(), stream())
         self.last_total_sq = total
-        return None if total is None else total.sqrt()
+        return total.sqrt()
 
     @torch.no_grad()
     def step(self, closure=None):

@@ -63,6 +63,17 @@ def _entry(p, tensor) -> _Entry:
 
 
 _wcache: dict = {}
+_wcache_gen = 0          # bumped whenever an entry is created, replaced or dropped (optimizer tables check it)
+
+
+def wcache_generation() -> int:
+    return _wcache_gen
+
+
+def bf16_entry(p: torch.Tensor):
+    """The cached bf16 copy currently served for p (None if there is none)."""
+    e = _wcache.get((id(p), torch.bfloat16, None))
+    return e.tensor if e is not None and e.ref() is p else None
 
 
 def wt(p: torch.Tensor, dtype=None, transform=None, key=None) -> torch.Tensor:
@@ -82,13 +93,17 @@ def wt(p: torch.Tensor, dtype=None, transform=None, key=None) -> torch.Tensor:
         src = transform(p.detach()) if transform is not None else p.detach()
         src = src.contiguous()
         out = src if src.dtype == dtype else ops.cast(src, dtype)
+    global _wcache_gen
     _wcache[k] = _entry(p, out)
+    _wcache_gen += 1
     return out
 
 
 def wt_refresh_from(p: torch.Tensor, bf16_copy: torch.Tensor) -> None:
     """Record a bf16 copy written by the fused optimizer as current for `p`."""
+    global _wcache_gen
     _wcache[(id(p), torch.bfloat16, None)] = _entry(p, bf16_copy)
+    _wcache_gen += 1
 
 
 def wt_bf16_buffer(p: torch.Tensor) -> torch.Tensor:
@@ -101,7 +116,9 @@ def wt_bf16_buffer(p: torch.Tensor) -> torch.Tensor:
 
 
 def clear_cache():
+    global _wcache_gen
     _wcache.clear()
+    _wcache_gen += 1
     _tables.clear()
 
 

@@ -2,6 +2,11 @@
 
 lfd_loss keeps the reference signature and assertion; the standardisation, the [D x D]
 cross-correlation (MFMA GEMM over B*T rows) and the loss/gradient run on libfddm_hip.
+
+Additive keyword `group` (a torch.distributed process group): under data parallelism the batch-dim
+statistics span every rank's rows, so an N-rank step computes the loss of the global batch exactly as one
+process would (functions.LfdFn). Default None: the batch the caller holds (the reference's
+single-process semantics; under DP that is the documented "local-batch L_fd").
 """
 from __future__ import annotations
 
@@ -20,7 +25,8 @@ def _standardize(x: torch.Tensor, eps: float = 1e-5) -> Tuple[torch.Tensor, torc
     return (x - mean) / std, mean, std
 
 
-def lfd_loss(z_a: torch.Tensor, z_b: torch.Tensor, lambda_offdiag: float = 5.0e-3, eps: float = 1e-5) -> torch.Tensor:
+def lfd_loss(z_a: torch.Tensor, z_b: torch.Tensor, lambda_offdiag: float = 5.0e-3, eps: float = 1e-5, *,
+             group=None) -> torch.Tensor:
     B, T, D = z_a.shape
     assert z_b.shape == (B, T, D), "z_b must have the same shape as z_a"
-    return FN.LfdFn.apply(z_a, z_b, float(lambda_offdiag), float(eps))
+    return FN.LfdFn.apply(z_a, z_b, float(lambda_offdiag), float(eps), group)

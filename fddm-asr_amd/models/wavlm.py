@@ -221,10 +221,32 @@ class WavLMModel(nn.Module):
         return SimpleNamespace(last_hidden_state=self.forward_hidden(input_values))
 
     # ------------------------------------------------------------------ loading
+    random_init = True      # False once weights were loaded from a checkpoint
+
+    @staticmethod
+    def hf_state_dict(sd: dict) -> dict:
+        """A transformers WavLM checkpoint's state_dict in this module's names: strips the `wavlm.` prefix of
+        task-head checkpoints (dropping the heads), and maps the legacy weight-norm names of the positional conv
+        (`weight_g` / `weight_v`, torch.nn.utils.weight_norm) to the parametrization names
+        (`parametrizations.weight.original0/1`, torch.nn.utils.parametrizations.weight_norm) that HF
+        modeling_wavlm.py:45-66 registers on current torch."""
+        if any(k.startswith("wavlm.") for k in sd):
+            sd = {k[len("wavlm."):]: v for k, v in sd.items() if k.startswith("wavlm.")}
+        out = {}
+        for k, v in sd.items():
+            if k.endswith("pos_conv_embed.conv.weight_g"):
+                k = k[: -len("weight_g")] + "parametrizations.weight.original0"
+            elif k.endswith("pos_conv_embed.conv.weight_v"):
+                k = k[: -len("weight_v")] + "parametrizations.weight.original1"
+            out[k] = v
+        return out
+
     @classmethod
     def from_pretrained(cls, name_or_path, geometry: dict | None = None):
-        """Local directory with config.json (+ model.safetensors / pytorch_model.bin) -> loaded weights.
-        Anything else (e.g. a hub name; there is no network) -> WavLM-base geometry, random init."""
+        """Local directory with config.json + model.safetensors / pytorch_model.bin -> loaded weights (strict:
+        a missing or unexpected key raises). A dict -> that geometry, random init. Anything else (a hub name;
+        there is no network) -> WavLM-base geometry, random init. `random_init` tells the two apart (train.py
+        refuses a random-init encoder unless asked to allow it)."""
         if isinstance(name_or_path, dict):
             return cls(wavlm_config(**name_or_path))
         path = str(name_or_path)
@@ -239,8 +261,15 @@ class WavLMModel(nn.Module):
                 sd = load_file(st_path)
             elif os.path.exists(bin_path):
                 sd = torch.load(bin_path, map_location="cpu", weights_only=True)
-            if sd is not None:
-                sd = {k[len("wavlm."):] if k.startswith("wavlm.") else k: v for k, v in sd.items()}
-                m.load_state_dict(sd, strict=False)
+            if sd is None:
+                raise FileNotFoundError(f"{path}: config.json but no model.safetensors / pytorch_model.bin")
+            sd = cls.hf_state_dict(sd)
+            if "masked_spec_embed" not in sd and hasattr(m, "masked_spec_embed"):
+                sd["masked_spec_embed"] = m.masked_spec_embed.detach().clone()   # unused in eval (HF:1006)
+            missing, unexpected = m.load_state_dict(sd, strict=False)
+            if missing or unexpected:
+                raise RuntimeError(f"{path}: WavLM checkpoint does not match the geometry: missing {missing[:8]}, "
+                                   f"unexpected {unexpected[:8]}")
+            m.random_init = False
             return m
         return cls(wavlm_config(**(geometry or {})))

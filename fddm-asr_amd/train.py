@@ -191,6 +191,9 @@ def train_one_epoch(encoder, decoder, s_proj, t_embed, t_proj, scheduler, loader
     arena = getattr(optimizer, "arena", None)
     if arena is not None and fdist.world() > 1 and arena.reducer is None:
         fdist.OverlapReducer(arena)     # gradient all-reduce overlapped with backward
+    # DP: L_fd's batch-dim statistics and w_t's batch mean over the GLOBAL batch (additive lfd.sync_batch_stats,
+    # SURVEY §8(e)); default: each rank's own batch (documented "local-batch L_fd")
+    lfd_group = fdist.default_group() if (fdist.world() > 1 and cfg.lfd.get("sync_batch_stats", False)) else None
     pbar = loader
     if tqdm is not None and print_epoch_summary:
         pbar = tqdm(loader, desc=f"Epoch {epoch} [train]", leave=False)
@@ -209,7 +212,11 @@ def train_one_epoch(encoder, decoder, s_proj, t_embed, t_proj, scheduler, loader
             z_text = t_proj(t_embed(logits))
             z_speech = align_speech(s_proj(c), L)
             w_t = scheduler.w_t(t).mean()
-            loss_fd = lfd_loss(z_speech, z_text, lambda_offdiag=lambda_off)
+            if lfd_group is not None:
+                w_t = fdist.global_mean(w_t, lfd_group)
+                loss_fd = lfd_loss(z_speech, z_text, lambda_offdiag=lambda_off, group=lfd_group)
+            else:
+                loss_fd = lfd_loss(z_speech, z_text, lambda_offdiag=lambda_off)
             loss = loss + tau * w_t * loss_fd
         optimizer.zero_grad(set_to_none=True)
         if scaler is not None:
@@ -318,6 +325,9 @@ def main():
     ap.add_argument("--config", type=str, required=True)
     ap.add_argument("--device", type=str, default="cuda" if torch.cuda.is_available() else "cpu")
     ap.add_argument("--resume", type=str, default=None, help="checkpoint to resume from (additive option)")
+    ap.add_argument("--allow-random-encoder", action="store_true",
+                    help="train against a random-init WavLM when model.encoder.wavlm_name does not load weights "
+                         "(no network: hub names cannot be fetched)")
     args = ap.parse_args()
     setup_logging()
     with open(args.config, "r", encoding="utf-8") as f:
@@ -331,22 +341,28 @@ def main():
     if device.type != "cuda":
         raise RuntimeError("the MI355X build runs on a HIP device only (no CPU fallback)")
     distributed = int(os.environ.get("WORLD_SIZE", "1")) > 1
+    import torch.distributed as tdist
     if distributed:
-        import torch.distributed as tdist
         local = int(os.environ.get("LOCAL_RANK", "0"))
         device = torch.device("cuda", local)
         torch.cuda.set_device(device)
-        tdist.init_process_group("nccl", device_id=device)
+        from datetime import timedelta
+        tdist.init_process_group("nccl", device_id=device,
+                                 timeout=timedelta(seconds=int(os.environ.get("FDDM_DIST_TIMEOUT_S", "1800"))))
         rt.reseed(cfg.seed + tdist.get_rank())
     rank0 = not distributed or int(os.environ.get("RANK", "0")) == 0
     encoder, decoder, s_proj, t_embed, t_proj, sched = build_models(cfg, device)
+    if getattr(encoder.backbone, "random_init", False) and not args.allow_random_encoder:
+        raise RuntimeError(f"model.encoder.wavlm_name={cfg.model['encoder'].get('wavlm_name')!r} loaded no weights "
+                           "(hub names need a network; give a local HF WavLM directory), so the frozen encoder would "
+                           "be random; pass --allow-random-encoder to train against it anyway")
     params = list(decoder.parameters()) + list(s_proj.parameters()) + list(t_embed.parameters()) + \
         list(t_proj.parameters())
     optim = FusedAdamW(params, lr=cfg.optim["lr"], weight_decay=cfg.optim["weight_decay"])
 
     from data_io import CVZhTWDataset  # real-data input path (librosa / sentencepiece)
     train_json = cfg.data.get("train_json", "data/processed/train.json")
-    val_json = cfg.data.get("val_json", "data/processed/val.json")
+    val_json = cfg.data.get("val_json", "data/processed/validation.json")    # reference train.py:555
     test_json = cfg.data.get("test_json", "data/processed/test.json")
     tok_path = cfg.data.get("tokenizer_model_path", "data/tokenizer/zh-TW_A/spm_zhTW_A.model")
 
@@ -362,6 +378,9 @@ def main():
     train_loader = _loader(train_json, True)
     val_loader = _loader(val_json, False) if os.path.exists(val_json) else None
     test_loader = _loader(test_json, False) if os.path.exists(test_json) else None
+    for what, path, ld in (("validation", val_json, val_loader), ("test", test_json, test_loader)):
+        if ld is None:
+            logging.warning(f"{what} manifest {path!r} not found: {what} evaluation is skipped")
     tokenizer = _tokenizer(cfg, tok_path) if (val_loader or test_loader) else None
     os.makedirs(cfg.log["ckpt_dir"], exist_ok=True)
     global_step, start_epoch = 1, 1
@@ -393,10 +412,11 @@ def main():
         if rank0:
             save_checkpoint(os.path.join(cfg.log["ckpt_dir"], f"ep{epoch:03d}.pt"), decoder, s_proj, t_embed, t_proj,
                             global_step, epoch, raw, optimizer=optim)
+        if distributed:
+            tdist.barrier()     # the other ranks wait here, not inside the next epoch's first all-reduce
     if rank0:
         logging.info(f"Best validation CER: {best_val_cer:.4f} (Epoch {best_epoch})")
     if distributed:
-        import torch.distributed as tdist
         tdist.destroy_process_group()
 
 

@@ -147,14 +147,27 @@ int fddm_lfd_std_bwd(int zt_dtype, const float* dzt, const void* zt, const float
                      void* hip_stream);
 int fddm_lfd_loss(const float* Cm, float* loss, long D, float lam, void* hip_stream);
 int fddm_lfd_dloss(int out_dtype, const float* Cm, const float* gscale, void* dC, long D, float lam, void* hip_stream);
+/*      data-parallel L_fd with global-batch statistics (fddm_losses.py:23-24 standardises over the
+ *      whole batch): per-rank column partial sums, all-reduced by the caller between the passes (inv_n = 1/N_global).
+ *      colstat: mean_sum == NULL -> out = sum_b z; else out = sum_b (z - mean_sum*inv_n)^2.
+ *      bwd_colstat: out[0:C] = sum_b dz~, out[C:2C] = sum_b dz~ z~.  std_bwd_apply multiplies dz by `scale`. */
+int fddm_lfd_colstat(const float* z, float* out, const float* mean_sum, float inv_n, long B, long C, void* hip_stream);
+int fddm_lfd_std_apply(int out_dtype, const float* z, void* zt, float* inv_std, const float* s1, const float* s2,
+                       float inv_n, float eps, long B, long C, void* hip_stream);
+int fddm_lfd_bwd_colstat(int zt_dtype, const float* dzt, const void* zt, float* out, long B, long C, void* hip_stream);
+int fddm_lfd_std_bwd_apply(int zt_dtype, const float* dzt, const void* zt, const float* inv_std, const float* sums,
+                           float inv_n, float scale, float* dz, long B, long C, void* hip_stream);
 
-/* ---- clip_grad_norm_ + AdamW (train.py:411-423), multi-tensor over a chunk table */
+/* ---- clip_grad_norm_ + AdamW (train.py:411-423), multi-tensor over a chunk table.
+ *      fddm_adamw: bias corrections from the per-tensor device step counters `step` (advanced by the call);
+ *      max_norm > 0 clips by the gradient norm sqrt(*total); a non-finite *total skips the whole step (the
+ *      reference's GradScaler skip, train.py:401-413) and increments *skipped (optional). */
 int fddm_grad_sumsq(const long* chunk_tensor, const long* chunk_start, const long* numel, const float* const* g,
                     long nchunks, float* total, void* hip_stream);
 int fddm_adamw(const long* chunk_tensor, const long* chunk_start, const long* numel, float* const* p,
                const float* const* g, float* const* m, float* const* v, unsigned short* const* pbf,
-               const float* step_size, const float* bc2_sqrt, long nchunks, const float* total, float max_norm,
-               float lr_wd, float b1, float b2, float eps, void* hip_stream);
+               float* const* step, long ntensors, long nchunks, const float* total, float max_norm, float lr,
+               float lr_wd, float b1, float b2, float eps, int* skipped, void* hip_stream);
 
 /* ---- jumpy sampler denoise step (sampler/jumpy_sampler.py:167-215 + q_posterior_multi_step,
  *      fddm/sched/diffusion_scheduler.py:106-208): x_next = argmax (or a tempered draw) of the

@@ -455,10 +455,11 @@ def oracle_train_step(params: Dict[str, torch.Tensor], enc_sd, enc_geom, wave, x
     for n, p in leaves.items():
         # projector grads are None on non-L_fd steps (set_to_none semantics)
         grads[n] = p.grad.detach().clone() if p.grad is not None else None
+    raw = {n: (None if g is None else g.clone()) for n, g in grads.items()}
     clip_grads(grads, 5.0)
     optim.step(params, grads)
     return dict(kl=float(kl.detach()), lfd=None if lfd_v is None else float(lfd_v.detach()), loss=float(loss.detach()), c=c,
-                logits=logits.detach())
+                logits=logits.detach(), grads=raw)
 
 
 # ------------------------------------------------------------------------------------------------

@@ -68,7 +68,10 @@ def test_projection_and_loss_api():
     assert set(SpeechProjector(512, 256).state_dict()) == {"proj.net.0.weight", "proj.net.0.bias"}
     assert set(TextEmbedding(8000, 256).state_dict()) == {"proj.weight"}
     assert set(TextProjector(256, 256).state_dict()) == {"proj.net.0.weight", "proj.net.0.bias"}
-    assert list(inspect.signature(lfd_loss).parameters) == ["z_a", "z_b", "lambda_offdiag", "eps"]
+    sig = inspect.signature(lfd_loss).parameters
+    assert list(sig)[:4] == ["z_a", "z_b", "lambda_offdiag", "eps"]       # the reference's (fddm_losses.py:29)
+    # additive: the data-parallel process group, keyword-only with a default (reference calls are unchanged)
+    assert all(p.kind is p.KEYWORD_ONLY and p.default is None for p in list(sig.values())[4:])
 
 
 def test_train_surface():
@@ -157,3 +160,39 @@ def test_checkpoint_layout_and_resume_roundtrip(tmp_path):
     st2 = opt2.state[next(iter(dec2.parameters()))]
     assert st2["step"] == 3 and float(st2["exp_avg_sq"][0]) == 2.0
     assert rt.next_seed() == expect_next
+
+
+def test_wavlm_checkpoint_loading_maps_legacy_names_strictly(tmp_path):
+    """A local HF WavLM directory loads strictly: `wavlm.`-prefixed task checkpoints lose their heads, the
+    legacy weight-norm names (weight_g / weight_v) of the positional conv map to the parametrization names, and
+    a checkpoint of another geometry raises instead of leaving the frozen encoder partly random."""
+    import json as _json
+
+    import pytest
+    from safetensors.torch import save_file
+    from transformers import WavLMConfig, WavLMModel as HFWavLM
+    from models.wavlm import WavLMModel
+    torch.manual_seed(3)
+    hf = HFWavLM(WavLMConfig(**SMALL_WAVLM)).eval()
+    sd = {}
+    for k, v in hf.state_dict().items():
+        k = k.replace("parametrizations.weight.original0", "weight_g").replace("parametrizations.weight.original1",
+                                                                              "weight_v")
+        sd["wavlm." + k] = v.contiguous()
+    sd["lm_head.weight"] = torch.zeros(3, 3)
+    d = tmp_path / "wavlm"
+    d.mkdir()
+    save_file(sd, str(d / "model.safetensors"))
+    (d / "config.json").write_text(_json.dumps(dict(SMALL_WAVLM, conv_dim=list(SMALL_WAVLM["conv_dim"]))))
+    m = WavLMModel.from_pretrained(str(d))
+    assert not m.random_init
+    ours = m.state_dict()
+    for k, v in hf.state_dict().items():
+        assert torch.equal(ours[k], v), k
+    bad = tmp_path / "bad"
+    bad.mkdir()
+    save_file({k: v for k, v in sd.items() if "pos_conv" not in k}, str(bad / "model.safetensors"))
+    (bad / "config.json").write_text((d / "config.json").read_text())
+    with pytest.raises(RuntimeError, match="does not match"):
+        WavLMModel.from_pretrained(str(bad))
+    assert WavLMModel.from_pretrained("microsoft/wavlm-large").random_init

@@ -94,3 +94,124 @@ def test_overlapped_allreduce_matches_full_batch_gradient():
         for r in range(world):
             err = (torch.from_numpy(got[r][0][n]) - g).abs().max().item() / scale
             assert err < 1e-4, f"{n} rank {r}: rel err {err:.2e}"
+
+
+# ------------------------------------------------------------------ a full DP train step with a global-batch L_fd
+SV, Sd, SH, SNL, SFF, SL, ST = 600, 128, 2, 2, 256, 20, 10
+NOISE_ONLY = ("s_proj.proj.net.0.bias", "t_proj.proj.net.0.bias")
+
+
+def _step_batches():
+    g = torch.Generator().manual_seed(21)
+    out = []
+    for i in range(2):
+        wave = 0.1 * torch.randn(4, 16000, generator=g)
+        x0 = torch.randint(1, SV, (4, SL), generator=g)
+        x0[1, 14:] = 0
+        x0[2, 9:] = 0
+        xt = torch.randint(1, SV, (4, SL), generator=g)
+        t = torch.tensor([1, 3, 7, 10]) if i == 0 else torch.tensor([10, 2, 5, 1])
+        out.append((wave, x0, xt, t))
+    return out
+
+
+def _train_two_steps(rank, world, sync):
+    """train_one_epoch over global steps 4 (L_fd) and 5 on this rank's rows (all 4 when world == 1), encoder on
+    its side stream, decoder gradients all-reduced by the overlapped reducer; returns final params and L_fd."""
+    import train as T_
+    from fddm.sched.diffusion_scheduler import DiscreteDiffusionScheduler
+    from fddm_hip import runtime as rt
+    from fddm_hip.optim import FusedAdamW
+    from helpers import SMALL_WAVLM, _step_params
+    from models.projection import SpeechProjector, TextEmbedding, TextProjector
+    from test_gpu_models import _encoder, make_decoder
+    dev = torch.device("cuda:0")
+    sl = slice(None) if world == 1 else slice(2 * rank, 2 * rank + 2)
+    data = [tuple(v[sl] for v in b) for b in _step_batches()]
+    rec = []
+    with rt.use_precision("fp32"):
+        enc = _encoder(SMALL_WAVLM, Sd)
+        dec = make_decoder(SV, Sd, SH, SNL, SFF)
+        params = _step_params(SV, Sd, SNL, SFF, SH)
+        sp, te, tp = SpeechProjector(Sd, 256), TextEmbedding(SV, 256), TextProjector(256, 256)
+        for pre, m in (("s_proj.", sp), ("t_embed.", te), ("t_proj.", tp)):
+            m.load_state_dict({n: params[pre + n] for n, _ in m.named_parameters()})
+            m.to(dev)
+        xq = iter([b[2].to(dev) for b in data])
+        tq = iter([b[3].to(dev) for b in data])
+
+        class TF(T_.SchedulerAdapter):
+            def sample_q(self, x0, t):
+                return next(xq)
+
+        orig = T_.lfd_loss
+
+        def rl(*a, **k):
+            v = orig(*a, **k)
+            rec.append(float(v))
+            return v
+
+        T_.lfd_loss = rl
+        try:
+            trainable = list(dec.parameters()) + list(sp.parameters()) + list(te.parameters()) + \
+                list(tp.parameters())
+            opt = FusedAdamW(trainable, lr=2e-4, weight_decay=0.01)
+            cfg = T_.Config(seed=1, data={"pad_id": 0}, model={}, diffusion={"T": ST}, inference={}, optim={},
+                            lfd={"n_step_fd": 4, "tau": 1.0, "lambda_offdiag": 5e-3, "sync_batch_stats": sync},
+                            log={"log_every": 1000})
+            sch = TF(DiscreteDiffusionScheduler(K=SV, T=ST, device=dev))
+            T_.train_one_epoch(enc, dec, sp, te, tp, sch, [(b[0], b[1]) for b in data], opt, dev, cfg, 4, None, 1,
+                               False, draw_t=lambda B: next(tq))
+            torch.cuda.synchronize()
+        finally:
+            T_.lfd_loss = orig
+    final = {("decoder." + n): p.detach().cpu().clone() for n, p in dec.named_parameters()}
+    for pre, m in (("s_proj.", sp), ("t_embed.", te), ("t_proj.", tp)):
+        final.update({pre + n: p.detach().cpu().clone() for n, p in m.named_parameters()})
+    return final, rec, params
+
+
+def _step_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import datetime
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=120))
+    try:
+        final, rec, _ = _train_two_steps(rank, world, True)
+        q.put((rank, {n: v.numpy() for n, v in final.items()}, rec))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_train_step_global_batch_lfd_matches_full_batch():
+    """Two ranks x 2 utterances through train_one_epoch (L_fd step, then a KL-only step whose projector grads
+    are None on both ranks), encoder side stream on, lfd.sync_batch_stats: the global-batch L_fd, w_t mean and
+    the averaged gradients make every rank's parameters equal those of one process on all 4 utterances
+    (reference losses/fddm_losses.py:18-58, train.py:390 over the whole batch)."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_step_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(world):
+        r, fin, rec = q.get(timeout=240)
+        got[r] = (fin, rec)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref, ref_rec, init = _train_two_steps(0, 1, False)
+    assert len(ref_rec) == 1
+    for r in range(world):
+        assert len(got[r][1]) == 1
+        assert abs(got[r][1][0] - ref_rec[0]) <= 1e-4 * abs(ref_rec[0]), (r, got[r][1], ref_rec)
+        for n, p in ref.items():
+            if n in NOISE_ONLY:
+                continue
+            a = torch.from_numpy(got[r][0][n]).double()
+            da = ((a - init[n].double()) ** 2).sum().item()
+            db = ((p.double() - init[n].double()) ** 2).sum().item()
+            assert abs(da - db) <= 5e-3 * db + 1e-12, f"rank {r} {n}: update {da:.4e} vs {db:.4e}"
+            if "in_proj_bias" not in n:
+                assert ((a - p.double()).abs() > 4e-6).float().mean().item() < 0.02, f"rank {r} {n}"

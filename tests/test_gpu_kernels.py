@@ -645,3 +645,61 @@ def test_softmax_rows_and_bwd():
     yr = torch.softmax(x.double(), -1)
     ref = yr * (dy.double() - (yr * dy.double()).sum(-1, keepdim=True))
     close(dz, ref, rtol=1e-5, what="softmax bwd")
+
+
+def test_fused_adamw_nonfinite_guard_skips_whole_step():
+    """A non-finite gradient norm skips the whole step on the device — parameters, moments and the step
+    counters stay as they were (GradScaler.step's skip on the reference's GPU path, train.py:401-413) — and the
+    next finite step continues exactly as if the skipped one never happened."""
+    from fddm_hip.optim import FusedAdamW
+    from fddm_hip import runtime as rt
+    torch.manual_seed(1)
+    shapes = [(64, 33), (33,)]
+    ps = [torch.randn(*s) for s in shapes]
+    grads = [[10 * torch.randn(*s) for s in shapes] for _ in range(3)]
+    grads[1][0][3, 5] = float("nan")
+    with rt.use_precision("fp32"):
+        dps = [torch.nn.Parameter(p.clone().to(dev)) for p in ps]
+        opt = FusedAdamW(dps, lr=2e-4, weight_decay=0.01)
+        ref = {str(i): p.clone() for i, p in enumerate(ps)}
+        ro = O.OracleAdamW()
+        for step in range(3):
+            for p, gr in zip(dps, grads[step]):
+                p.grad = gr.to(dev)
+            opt.clip_and_step(max_norm=5.0)
+            if step == 1:
+                torch.cuda.synchronize()
+                assert int(opt.skipped_steps()[0]) == 1
+                assert all(float(opt.state[p]["step"]) == 1.0 for p in dps)
+                continue
+            gd = {str(i): grads[step][i].clone() for i in range(2)}
+            O.clip_grads(gd, 5.0)
+            ro.step(ref, gd)
+    for i, p in enumerate(dps):
+        close(p, ref[str(i)], rtol=1e-5, atol=1e-7, what=f"guarded adamw p{i}")
+    assert all(float(opt.state[p]["step"]) == 2.0 for p in dps)
+
+
+def test_fused_adamw_follows_replaced_bf16_copies():
+    """The optimizer writes each weight's bf16 copy for the next forward; when the runtime cache replaces that
+    copy (clear_cache after a checkpoint load, an in-place change of the parameter), the optimizer's device
+    table must follow the live copy instead of writing the old buffer (stale pointer)."""
+    from fddm_hip.optim import FusedAdamW
+    from fddm_hip import runtime as rt
+    torch.manual_seed(2)
+    with rt.use_precision("bf16"):
+        w = torch.nn.Parameter(torch.randn(128, 96, device=dev))
+        opt = FusedAdamW([w], lr=1e-2)
+        rt.wt(w)
+        for step in range(3):
+            w.grad = torch.randn(128, 96, device=dev)
+            opt.clip_and_step(max_norm=None)
+            if step == 0:
+                rt.clear_cache()
+                rt.wt(w)                    # the forward's new bf16 copy
+            if step == 1:
+                with torch.no_grad():
+                    w.mul_(0.5)             # version bump: the next forward re-casts
+                rt.wt(w)
+            torch.cuda.synchronize()
+            assert torch.equal(rt.wt(w), w.detach().to(torch.bfloat16)), f"step {step}"

@@ -1,0 +1,194 @@
+"""Full train-step parity at the benchmark geometries (BASELINE.json configs[1] = C2, configs[3] = C4).
+
+Two teacher-forced steps of `train.train_one_epoch` (global steps 3 and 4, so the second one takes the L_fd
+branch, reference train.py:372-397) on B = 2 utterances of 10 s synthetic audio, against the CPU oracle's
+`oracle_train_step` (oracle/fddm_oracle.py, a restatement of train.py:342-423 pinned by the 4-step reference
+fixtures in tests/golden/step_*.npz):
+
+* C2: WavLM-base encoder (10 s -> S = 499) + 6-layer d_model 512 / 8 heads / ff 2048 decoder, L = 256,
+  V = 8000, T = 200 (reference train.py:340-443, models/denoise_decoder.py:147-192);
+* C4: the same encoder (hidden 768 = d_model, so AcousticEncoder.proj is the identity) + 12-layer d_model 768 /
+  12 heads decoder, L = 512 > S = 499, which takes the repeat branch of the S -> L alignment
+  (train.py:382-387) at full size.
+
+Checked per step: the KL and L_fd values, and every trainable parameter's gradient as clip_grad_norm_ sees it
+(before clipping; None on the same parameters — the projectors on the KL-only step, train.py:400), as a
+norm-wise relative error ||g - g_ref|| <= rtol * max(||g_ref||, 1e-3 * ||G_ref||) with G the global gradient
+(the floor covers gradients that are analytically zero — the key third of in_proj_bias, whose value is pure
+rounding noise). After the two AdamW steps the per-parameter update norms are compared too.
+fp32 (parity) mode: KL and L_fd within 1e-4 relative, gradients rtol 1e-4 on the KL step and 3e-4 on the L_fd
+step (measured worst 1.2e-4 at C4: the B = 2 batch-dim standardisation of L_fd, 1/sqrt(var + eps) per column,
+scales up summation-order differences), global gradient norm 1e-5, update norms within 5e-3.
+bf16 mode (the benchmark's precision): KL within 2e-2 relative, L_fd within 3e-2, gradients rtol 5e-2 on the KL
+step and 1.5e-1 on the L_fd step, global gradient norm within 2e-2 (measured worst 3.6e-2 / 1.2e-1: bf16
+operands carry 8 mantissa bits and the comparison is end to end — the bf16 WavLM output the decoder and the
+speech projector consume already differs from the fp32 oracle's by ~1e-2, tests/test_gpu_models.py). Update
+norms are not compared in bf16: AdamW's first steps are ~lr * sign(g), so elements whose gradient is at the
+rounding-noise level (directions with an analytically zero gradient, e.g. the mean-key direction of the K
+projection) move by O(lr) in a direction the noise picks. Elementwise parameter values are not compared at these
+sizes for the same reason (the C1 / S<L fixtures at 1e-4 cover that, tests/test_gpu_models.py)."""
+import pytest
+import torch
+
+from helpers import _step_params, close, wavlm_sd
+from oracle import fddm_oracle as O
+
+pytestmark = pytest.mark.gpu
+dev = torch.device("cuda:0")
+
+CONFIGS = {
+    #       V     d    H  NL   FF    L    T
+    "C2": (8000, 512, 8, 6, 2048, 256, 200),
+    "C4": (8000, 768, 12, 12, 2048, 512, 200),
+}
+NOISE_ONLY = ("s_proj.proj.net.0.bias", "t_proj.proj.net.0.bias")   # d/dbias of a batch-standardised input is 0
+
+
+def _inputs(L, V, Tn, B=2, seconds=10.0):
+    g = torch.Generator().manual_seed(2024)
+    waves, x0s, ts = [], [], []
+    for _ in range(2):
+        waves.append(0.1 * torch.randn(B, int(16000 * seconds), generator=g))
+        x0 = torch.randint(1, V, (B, L), generator=g)
+        lens = torch.randint(L // 2, L + 1, (B,), generator=g)
+        x0 = torch.where(torch.arange(L)[None] < lens[:, None], x0, torch.zeros_like(x0))
+        x0s.append(x0)
+    ts = [torch.tensor([1, 137]), torch.tensor([200, 58])]       # t = 1 (beta_{t-1} = 0 rule) and t = T included
+    return waves, x0s, ts
+
+
+def _run(cfg_name, prec, monkeypatch):
+    import train as T_
+    from fddm.sched.diffusion_scheduler import DiscreteDiffusionScheduler
+    from fddm_hip import runtime as rt
+    from fddm_hip.optim import FusedAdamW
+    from models.projection import SpeechProjector, TextEmbedding, TextProjector
+    from test_gpu_models import _encoder, make_decoder
+    V, d, H, NL, FF, L, Tn = CONFIGS[cfg_name]
+    waves, x0s, ts = _inputs(L, V, Tn)
+    betas, ab = O.sched_tables(Tn)
+    xts = [O.sample_xt(x0, t, V, ab, seed=50 + i) for i, (x0, t) in enumerate(zip(x0s, ts))]
+    params = _step_params(V, d, NL, FF, H)
+    # ---- GPU: the drop-in train_one_epoch
+    rec = {"kl": [], "lfd": []}
+    with rt.use_precision(prec):
+        enc = _encoder({}, d)
+        dec = make_decoder(V, d, H, NL, FF)
+        sp, te, tp = SpeechProjector(d, 256), TextEmbedding(V, 256), TextProjector(256, 256)
+        for pre, m in (("s_proj.", sp), ("t_embed.", te), ("t_proj.", tp)):
+            m.load_state_dict({n: params[pre + n] for n, _ in m.named_parameters()})
+            m.to(dev)
+        xq = iter([x.to(dev) for x in xts])
+        tq = iter([t.to(dev) for t in ts])
+
+        class TF(T_.SchedulerAdapter):
+            def sample_q(self, x0, t):
+                return next(xq)
+
+            def kl_term(self, *a, **k):
+                v = super().kl_term(*a, **k)
+                rec["kl"].append(v)
+                return v
+
+        orig = T_.lfd_loss
+
+        def rl(*a, **k):
+            v = orig(*a, **k)
+            rec["lfd"].append(v)
+            return v
+
+        monkeypatch.setattr(T_, "lfd_loss", rl)
+        named = [("decoder." + n, p) for n, p in dec.named_parameters()]
+        for pre, m in (("s_proj.", sp), ("t_embed.", te), ("t_proj.", tp)):
+            named += [(pre + n, p) for n, p in m.named_parameters()]
+        trainable = [p for _, p in named]
+        opt = FusedAdamW(trainable, lr=2e-4, weight_decay=0.01)
+        step_grads = []
+        inner = opt.clip_and_step
+
+        def snap(*a, **k):      # the gradients clip_grad_norm_ + AdamW see, before clipping
+            step_grads.append({n: (None if p.grad is None else p.grad.detach().cpu().clone()) for n, p in named})
+            return inner(*a, **k)
+
+        opt.clip_and_step = snap
+        cfg = T_.Config(seed=1, data={"pad_id": 0}, model={}, diffusion={"T": Tn}, inference={}, optim={},
+                        lfd={"n_step_fd": 4, "tau": 1.0, "lambda_offdiag": 5e-3}, log={"log_every": 1000})
+        sch = TF(DiscreteDiffusionScheduler(K=V, T=Tn, device=dev))
+        loader = list(zip(waves, x0s))
+        gs, _ = T_.train_one_epoch(enc, dec, sp, te, tp, sch, loader, opt, dev, cfg, 3, None, 1, False,
+                                   draw_t=lambda B: next(tq))
+        torch.cuda.synchronize()
+    assert gs == 5 and len(rec["kl"]) == 2 and len(rec["lfd"]) == 1
+    final = {("decoder." + n): p.detach().cpu() for n, p in dec.named_parameters()}
+    for pre, m in (("s_proj.", sp), ("t_embed.", te), ("t_proj.", tp)):
+        final.update({pre + n: p.detach().cpu() for n, p in m.named_parameters()})
+    got = dict(kl=[float(v) for v in rec["kl"]], lfd=float(rec["lfd"][0]), final=final, grads=step_grads)
+    del enc, dec, sp, te, tp, opt
+    torch.cuda.empty_cache()
+    # ---- CPU oracle: the same two steps
+    init = {k: v.clone() for k, v in params.items()}
+    enc_sd = wavlm_sd(O.wavlm_geometry(), d)
+    ocfg = dict(d_model=d, nhead=H, num_layers=NL, pad_id=0, n_step_fd=4, tau=1.0, lambda_offdiag=5e-3)
+    oopt = O.OracleAdamW()
+    ref = []
+    for i in range(2):
+        ref.append(O.oracle_train_step(params, enc_sd, O.wavlm_geometry(), waves[i], x0s[i], ts[i], xts[i], ocfg,
+                                       oopt, 3 + i, betas, ab))
+    assert ref[0]["lfd"] is None and ref[1]["lfd"] is not None
+    if cfg_name == "C4":
+        assert ref[1]["c"].shape[1] < L, "C4 must take the S < L repeat branch"
+    return got, ref, init, params
+
+
+def _check_grads(got, ref, rtols, gtol, what):
+    """Per step i: same None pattern, global norm within gtol, every parameter's norm-wise relative error within
+    rtols[i] (NOISE_ONLY parameters excluded: their exact gradient is 0). Reports the worst parameters."""
+    for i, rtol in enumerate(rtols):
+        g, r = got["grads"][i], ref[i]["grads"]
+        assert g.keys() == r.keys()
+        assert {n for n in g if g[n] is None} == {n for n in r if r[n] is None}, f"{what} step {i}: None grads"
+        if i == 0:
+            assert all(g[n] is None for n in g if not n.startswith("decoder.")), "projectors skipped on KL steps"
+        G = sum(float((v.double() ** 2).sum()) for v in r.values() if v is not None) ** 0.5
+        Gg = sum(float((v.double() ** 2).sum()) for v in g.values() if v is not None) ** 0.5
+        assert abs(Gg - G) <= gtol * G, f"{what} step {i}: global grad norm {Gg:.6e} vs {G:.6e}"
+        ratios = {}
+        for n in g:
+            if g[n] is None or n in NOISE_ONLY:
+                continue
+            rn = float(r[n].double().norm())
+            err = float((g[n].double() - r[n].double()).norm())
+            ratios[n] = err / max(rn, 1e-3 * G)
+        worst = sorted(ratios.items(), key=lambda kv: -kv[1])[:6]
+        print(f"{what} step {i}: worst grad rel err " + ", ".join(f"{n} {v:.2e}" for n, v in worst))
+        assert worst[0][1] <= rtol, f"{what} step {i}: grad rel err above {rtol}: {worst}"
+
+
+def _updates(final, init, ref_params):
+    out = {}
+    for n, p in final.items():
+        if n in NOISE_ONLY:
+            continue
+        out[n] = (((p.double() - init[n].double()) ** 2).sum().item(),
+                  ((ref_params[n].double() - init[n].double()) ** 2).sum().item())
+    return out
+
+
+@pytest.mark.parametrize("cfg_name", ["C2", "C4"])
+def test_train_step_fp32_matches_oracle(cfg_name, monkeypatch):
+    got, ref, init, ref_params = _run(cfg_name, "fp32", monkeypatch)
+    for i in range(2):
+        close(got["kl"][i], ref[i]["kl"], rtol=1e-4, what=f"{cfg_name} KL step {i}")
+    close(got["lfd"], ref[1]["lfd"], rtol=1e-4, what=f"{cfg_name} L_fd")
+    _check_grads(got, ref, (1e-4, 3e-4), 1e-5, f"{cfg_name} fp32")
+    for n, (a, b) in _updates(got["final"], init, ref_params).items():
+        close(a, b, rtol=5e-3, atol=1e-12, what=f"{cfg_name} update {n}")
+
+
+@pytest.mark.parametrize("cfg_name", ["C2", "C4"])
+def test_train_step_bf16_matches_oracle(cfg_name, monkeypatch):
+    got, ref, init, ref_params = _run(cfg_name, "bf16", monkeypatch)
+    for i in range(2):
+        close(got["kl"][i], ref[i]["kl"], rtol=2e-2, what=f"{cfg_name} bf16 KL step {i}")
+    close(got["lfd"], ref[1]["lfd"], rtol=3e-2, what=f"{cfg_name} bf16 L_fd")
+    _check_grads(got, ref, (5e-2, 1.5e-1), 2e-2, f"{cfg_name} bf16")

@@ -3,7 +3,7 @@
 mkdir -p gpurun_out
 for f in "$@"; do
   name=$(basename "$f" .py)
-  timeout -k 10 900 python -m pytest "$f" -q -m gpu -rf --tb=short > gpurun_out/$name.log 2>&1
+  timeout -k 10 900 python -u -m pytest "$f" -q -m gpu -rf -p no:cacheprovider --tb=short --timeout 300 --timeout-method thread -s > gpurun_out/$name.log 2>&1
   rc=$?
   echo "$f rc=$rc"; tail -5 gpurun_out/$name.log
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP: crash or timeout in $f"; exit $rc; fi
