@@ -131,6 +131,34 @@ __device__ __forceinline__ void trans_times_vals(f32x4_t (&out)[4], const unsign
   }
 }
 
+// cross-row reductions of the 16x16 C layout (lanes l, l^16, l^32, l^48 hold one query's keys) with the gfx950
+// lane-swap instructions: v_permlane16_swap / v_permlane32_swap exchange a value between lanes l and l^16 (l^32) in
+// the VALU, so r[0] and r[1] hold {own, partner} in some order — no LDS round trip (__shfl_xor's ds_bpermute)
+__device__ __forceinline__ float xmax16(float x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xmax32(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xsum16(float x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float xsum32(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ unsigned xor16(unsigned x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+  return r[0] | r[1];
+}
+__device__ __forceinline__ unsigned xor32(unsigned x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+  return r[0] | r[1];
+}
+
 struct AttnArgs {
   const void *Q, *K, *V, *O, *dO;
   void *Out, *dQ, *dK, *dV;
@@ -153,6 +181,38 @@ struct AttnArgs {
 
 __device__ __forceinline__ bool key_ok(const AttnArgs& a, int b, int key) {
   return key < a.Lk && (a.key_keep == nullptr || a.key_keep[(long)b * a.Lk + key]);
+}
+
+// Attention-probability dropout: RNG contract v2 (oracle/fddm_oracle.py: attn_dropout_keep). Per (b, h) three
+// tables of R = 4096 16-bit words, T_tau[j] = bits 16*(j&3).. of mix64(seed, stream, TAB0 + (bh*3 + tau)*1024 +
+// (j>>2)); per query row r = bh*Lq + q three offsets o_tau = (mix64(seed, stream, OFF0 + r) >> 16*tau) & 0xFFC;
+// the element (q, key) draws u = T_0[(o_0 + key) & 4095] ^ T_1[(o_1 + key) & 4095] ^ T_2[(o_2 + key) & 4095] and
+// is kept iff u >= round(p * 65536). Within a row the 16-bit draws are distinct table entries (Lk <= 4096); two
+// rows repeat each other's draws (shifted) only if all three offset differences coincide (2^-20 per pair). The
+// forward kernel holds the three tables in LDS (24 KB, built once per workgroup): 3 ds_read_b64 + 2 64-bit XORs
+// per 4 keys, instead of a 64-bit splitmix64 hash per 4 keys.
+constexpr int ATTN_R = 4096;
+constexpr uint64_t ATTN_TAB0 = 1ull << 62, ATTN_OFF0 = 3ull << 62;
+__device__ __forceinline__ uint64_t attn_offsets(const AttnArgs& a, int bh, int q) {
+  return mix64(a.seed, a.stream, ATTN_OFF0 + (uint64_t)bh * a.Lq + q);
+}
+// the 4 keep bits of keys k0..k0+3 (k0 % 4 == 0) of query q: generic form (4 hashes), for the kernels that do not
+// stage the tables
+__device__ __forceinline__ unsigned attn_keep4(const AttnArgs& a, int bh, int q, int k0) {
+  const uint64_t off = attn_offsets(a, bh, q);
+  uint64_t w = 0;
+#pragma unroll
+  for (int tau = 0; tau < 3; ++tau) {
+    const unsigned j = ((unsigned)((off >> (16 * tau)) & 0xFFCu) + (unsigned)k0) & (ATTN_R - 1);
+    w ^= mix64(a.seed, a.stream, ATTN_TAB0 + ((uint64_t)bh * 3 + tau) * (ATTN_R / 4) + (j >> 2));
+  }
+  unsigned keep = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) keep |= (((unsigned)(w >> (16 * j)) & 0xFFFFu) >= a.thr16 ? 1u : 0u) << j;
+  return keep;
+}
+__device__ __forceinline__ bool attn_keep(const AttnArgs& a, int bh, int q, int key) {
+  return (attn_keep4(a, bh, q, key & ~3) >> (key & 3)) & 1u;
 }
 
 // ------------------------------------------------------------------------------------------- fwd
@@ -200,8 +260,8 @@ __global__ void __launch_bounds__(256) fwd_kernel(AttnArgs a) {
         p[kb][j] = x;
         tmax = fmaxf(tmax, x);
       }
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    tmax = xmax16(tmax);
+    tmax = xmax32(tmax);
     const float mn = fmaxf(m, tmax);
     const float alpha = (mn == -INFINITY) ? 1.f : __expf(m - mn);
     float ls = 0.f;
@@ -213,8 +273,7 @@ __global__ void __launch_bounds__(256) fwd_kernel(AttnArgs a) {
         ls += e;
         if (a.thr16) {
           const int key = k0 + kb * 16 + 4 * g + j;
-          const uint64_t idx = ((uint64_t)bh * a.Lq + q) * a.Lk + key;
-          e = drop_keep(a.seed, a.stream, idx, a.thr16) ? e * a.drop_scale : 0.f;
+          e = attn_keep(a, bh, q, key) ? e * a.drop_scale : 0.f;
         }
         p[kb][j] = e;
       }
@@ -224,8 +283,8 @@ __global__ void __launch_bounds__(256) fwd_kernel(AttnArgs a) {
     for (int d = 0; d < 4; ++d) o[d] *= alpha;
     trans_times_vals<T>(o, vimg, p, lane);
   }
-  l += __shfl_xor(l, 16, 64);
-  l += __shfl_xor(l, 32, 64);
+  l = xsum16(l);
+  l = xsum32(l);
   if (!qv) return;
   const float inv = (l > 0.f) ? 1.f / l : NAN;  // fully masked row -> NaN like softmax(all -inf)
   T* Ob = (T*)a.Out + ((long)b * a.Lq + q) * a.so + h * DH;
@@ -387,8 +446,8 @@ __global__ void __launch_bounds__(256, ATTN_FWD_WPS) fwd2_kernel(AttnArgs a) {
         }
         tmax = fmaxf(tmax, fmaxf(fmaxf(p[gq][kb][0], p[gq][kb][1]), fmaxf(p[gq][kb][2], p[gq][kb][3])));
       }
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      tmax = xmax16(tmax);
+      tmax = xmax32(tmax);
       const float mn = fmaxf(m[gq], tmax);
       const float mref = (mn == -INFINITY) ? 0.f : mn;  // all-masked so far: exp2(-inf) = 0
       const float nbias = -mref * sl2;
@@ -396,39 +455,12 @@ __global__ void __launch_bounds__(256, ATTN_FWD_WPS) fwd2_kernel(AttnArgs a) {
       const f32x2_t sl2v = {sl2, sl2}, nb2 = {nbias, nbias};
       f32x2_t ls2 = {0.f, 0.f};
       uint64_t bits = 0;
-      // dropout hash words: the lane's 4 consecutive keys e0..e0+3 of block kb span word e0>>2 (h0[kb]) and, when
-      // Lk % 4 != 0, word (e0>>2)+1 (h1[kb]) — which is the h0 of the lane 16 up (the next 4 keys) or, for the
-      // last key quad of a block, of block kb+1 in lane g = 0: one 64-bit lane rotation per block and one extra
-      // hash instead of a second hash per block. Lk % 4 == 0 (a wave-uniform branch) needs h0 only.
-      uint64_t e0q = 0, h0[4] = {0, 0, 0, 0}, h1[4] = {0, 0, 0, 0};
-      if constexpr (DROP) {
-        e0q = ((uint64_t)bh * a.Lq + q[gq]) * a.Lk + (k0 + 4 * g);
-#pragma unroll
-        for (int kb = 0; kb < 4; ++kb) h0[kb] = mix64(a.seed, a.stream, (e0q + kb * 16) >> 2);
-        if (a.Lk & 3) {
-          const uint64_t hx = mix64(a.seed, a.stream, (e0q + 64) >> 2);  // "h0[4]", read by g = 3 at kb = 3
-          const int src = (lane + 16) & 63;
-#pragma unroll
-          for (int kb = 0; kb < 4; ++kb) {
-            const uint64_t v = g == 0 ? (kb < 3 ? h0[kb + 1] : hx) : h0[kb];
-            const unsigned lo = __shfl((unsigned)v, src, 64), hi = __shfl((unsigned)(v >> 32), src, 64);
-            h1[kb] = ((uint64_t)hi << 32) | lo;
-          }
-        }
-      }
+      // dropout keep bits of the lane's 4 keys per block (generic contract form; fwd3 stages the tables in LDS)
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb) {
         unsigned keep = 0xF;
         if constexpr (DROP) {
-          const unsigned r = (unsigned)(e0q & 3);  // same for every block (16 | kb*16)
-          keep = 0;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const unsigned sl = r + j;
-            const uint64_t hw = sl < 4 ? h0[kb] : h1[kb];
-            const unsigned u = (unsigned)(hw >> (16u * (sl & 3u))) & 0xFFFFu;
-            keep |= (u >= a.thr16 ? 1u : 0u) << j;
-          }
+          keep = attn_keep4(a, bh, q[gq], k0 + kb * 16 + 4 * g);
           bits |= (uint64_t)keep << (kb * 16 + 4 * g);
         }
 #pragma unroll
@@ -448,10 +480,10 @@ __global__ void __launch_bounds__(256, ATTN_FWD_WPS) fwd2_kernel(AttnArgs a) {
       if constexpr (DROP) {
         if (a.dbits) {  // the 4 lanes of a query hold disjoint key nibbles: OR them into the tile's 64-bit word
           unsigned lo = (unsigned)bits, hi = (unsigned)(bits >> 32);
-          lo |= __shfl_xor(lo, 16, 64);
-          hi |= __shfl_xor(hi, 16, 64);
-          lo |= __shfl_xor(lo, 32, 64);
-          hi |= __shfl_xor(hi, 32, 64);
+          lo = xor16(lo);
+          hi = xor16(hi);
+          lo = xor32(lo);
+          hi = xor32(hi);
           if (g == 0 && qv[gq]) a.dbits[((long)bh * ntiles + t) * a.Lq + q[gq]] = ((uint64_t)hi << 32) | lo;
         }
       }
@@ -494,10 +526,257 @@ __global__ void __launch_bounds__(256, ATTN_FWD_WPS) fwd2_kernel(AttnArgs a) {
 #pragma unroll
   for (int gq = 0; gq < NG; ++gq) {
     float lt = l[gq];
-    lt += __shfl_xor(lt, 16, 64);
-    lt += __shfl_xor(lt, 32, 64);
+    lt = xsum16(lt);
+    lt = xsum32(lt);
     if (!qv[gq]) continue;
     // fully masked row -> NaN like softmax(all -inf); the dropout scale of the kept probabilities goes here
+    const float inv = (lt > 0.f) ? (DROP ? a.drop_scale : 1.f) / lt : NAN;
+    bf16_t* Ob = (bf16_t*)a.Out + ((long)b * a.Lq + q[gq]) * a.so + h * DH;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      uint2 u2;
+      u2.x = pk(o[gq][d][0] * inv, o[gq][d][1] * inv);
+      u2.y = pk(o[gq][d][2] * inv, o[gq][d][3] * inv);
+      *(uint2*)(Ob + d * 16 + 4 * g) = u2;
+    }
+    if (a.lse && g == 0)
+      a.lse[(long)bh * a.Lq + q[gq]] = (lt > 0.f) ? (m[gq] * sl2 + __log2f(lt)) * 0.69314718055994531f : NAN;
+  }
+}
+
+// ------------------------------------------------------------------------------- fwd (bf16, v3)
+// K/V resident in LDS: for Lk <= 512 the whole key range of one (b, h) fits (2 x Lk_pad x 128 B <= 128 KB), so
+// the workgroup streams every K and V row into LDS once, by LDS-DMA issued up front in tile order (8 rows of
+// 128 B per wave instruction, the XOR swizzles applied to the per-lane SOURCE addresses), and the tile loop
+// then runs on LDS reads, MFMAs and VALU only: no per-tile register staging, no per-tile workgroup barrier
+// once the tiles have landed (a tile's barrier is passed while later tiles are still in flight). The per-key
+// mask row (key padding, keys >= Lk) and, for WavLM, the relative-bias slice of the workgroup's whole query
+// range are staged once as well. NW waves x 2 query groups x 16 = 32*NW queries per workgroup; the per-tile
+// softmax / dropout / P.V code is that of fwd2_kernel.
+template <bool DROP, bool MASK, bool REL, int NW>
+__global__ void __launch_bounds__(64 * NW, 1) fwd3_kernel(AttnArgs a) {
+  constexpr int NG = 2, QW = 32 * NW;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem3[];
+  const int ntiles = (a.Lk + 63) / 64, LkP = ntiles * 64;
+  unsigned char* kres = smem3;                                  // [LkP][128 B] KC image
+  unsigned char* vres = smem3 + LkP * 128;                      // [LkP][128 B] tr-read image
+  float* mfull = (float*)(smem3 + 2 * LkP * 128);               // [LkP] 0 / -inf
+  float* tfull = mfull + LkP;                                   // [LkP + QW] relative-bias slice (REL)
+  unsigned char* dtab = (unsigned char*)(mfull + LkP + (REL ? LkP + QW : 0));  // [3][4096] u16 (DROP)
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
+            i = lane & 15;
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int qbase = blockIdx.x * QW;
+  const bf16_t* Qb = (const bf16_t*)a.Q + (long)b * a.Lq * a.sq + h * DH;
+  const bf16_t* Kb = (const bf16_t*)a.K + (long)b * a.Lk * a.sk + h * DH;
+  const bf16_t* Vb = (const bf16_t*)a.V + (long)b * a.Lk * a.sv + h * DH;
+  // ---- LDS-DMA fill, tile order: wave w's instruction for tile t covers rows 64t + 8w' .. +7 for w' = w, w+NW..
+  {
+    typedef __attribute__((address_space(1))) const void* gp_t;
+    typedef __attribute__((address_space(3))) void* lp_t;
+    for (int t = 0; t < ntiles; ++t) {
+#pragma unroll
+      for (int u = 0; u < 8 / NW; ++u) {
+        const int R = 64 * t + 8 * (w + NW * u);
+        const int r = R + (lane >> 3), pch = lane & 7;
+        const int rr = min(r, a.Lk - 1);
+        const int ck = pch ^ ((r >> 1) & 7), cv = pch ^ (((r >> 1) & 3) << 1);
+        __builtin_amdgcn_global_load_lds((gp_t)(Kb + (long)rr * a.sk + ck * 8), (lp_t)(kres + R * 128), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((gp_t)(Vb + (long)rr * a.sv + cv * 8), (lp_t)(vres + R * 128), 16, 0, 0);
+      }
+    }
+  }
+  for (int k = tid; k < LkP; k += 64 * NW) mfull[k] = (MASK && !key_ok(a, b, k)) ? -INFINITY : 0.f;
+  if constexpr (DROP) {  // the (b, h) draw tables of the dropout contract: one hash per 4 entries
+    for (int wi = tid; wi < 3 * ATTN_R / 4; wi += 64 * NW) {
+      const int tau = wi / (ATTN_R / 4), jw = wi % (ATTN_R / 4);
+      *(uint64_t*)(dtab + (size_t)wi * 8) =
+          mix64(a.seed, a.stream, ATTN_TAB0 + ((uint64_t)bh * 3 + tau) * (ATTN_R / 4) + jw);
+    }
+  }
+  if constexpr (REL) {
+    const float* tabh = a.table + (long)h * (2 * a.Lk - 1);
+    const long off0 = (long)(a.Lk - 1) - (qbase + QW - 1);  // tfull[j] = table[h][off0 + j]
+    for (int j = tid; j < LkP + QW; j += 64 * NW) {
+      const long ti = off0 + j;
+      tfull[j] = (ti >= 0 && ti < 2L * a.Lk - 1) ? tabh[ti] : 0.f;
+    }
+  }
+  int q[NG];
+  bool qv[NG];
+  uint4 qf[NG][2];
+  float gate[NG];
+#pragma unroll
+  for (int gq = 0; gq < NG; ++gq) {
+    q[gq] = qbase + w * (16 * NG) + gq * 16 + i;
+    qv[gq] = q[gq] < a.Lq;
+    row_frags<bf16_t>(qf[gq], Qb, a.sq, qv[gq] ? q[gq] : 0, qv[gq], lane);
+    gate[gq] = 0.f;
+    if (REL && a.graw && qv[gq]) {
+      const uint4 u = *(const uint4*)((const bf16_t*)a.graw + ((long)b * a.Lq + q[gq]) * a.sgr + h * 8);
+      const float ra = bf2f((bf16_t)(u.x & 0xffff)) + bf2f((bf16_t)(u.x >> 16)) + bf2f((bf16_t)(u.y & 0xffff)) +
+                       bf2f((bf16_t)(u.y >> 16));
+      const float rb = bf2f((bf16_t)(u.z & 0xffff)) + bf2f((bf16_t)(u.z >> 16)) + bf2f((bf16_t)(u.w & 0xffff)) +
+                       bf2f((bf16_t)(u.w >> 16));
+      const float ga = 1.f / (1.f + __expf(-ra)), gb = 1.f / (1.f + __expf(-rb));
+      gate[gq] = ga * (gb * a.gconst[h] - 1.f) + 2.f;
+    } else if (REL && a.gate && qv[gq]) {
+      gate[gq] = a.gate[(long)bh * a.Lq + q[gq]];
+    }
+  }
+  const float sl2 = a.scale * 1.4426950408889634f;
+  float graw[NG];
+#pragma unroll
+  for (int gq = 0; gq < NG; ++gq) graw[gq] = REL ? gate[gq] / a.scale : 0.f;
+  unsigned ooff[NG][3];  // the rows' table offsets (dropout contract)
+#pragma unroll
+  for (int gq = 0; gq < NG; ++gq) {
+    const uint64_t off = DROP ? attn_offsets(a, bh, q[gq]) : 0;
+#pragma unroll
+    for (int tau = 0; tau < 3; ++tau) ooff[gq][tau] = (unsigned)((off >> (16 * tau)) & 0xFFCu);
+  }
+  float m[NG], l[NG];
+  f32x4_t o[NG][4];
+#pragma unroll
+  for (int gq = 0; gq < NG; ++gq) {
+    m[gq] = -INFINITY;
+    l[gq] = 0.f;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) o[gq][d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int k0 = t * 64;
+    const unsigned char* kimg = kres + k0 * 128;
+    const unsigned char* vimg = vres + k0 * 128;
+    f32x4_t s[NG][4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+#pragma unroll
+      for (int gq = 0; gq < NG; ++gq) s[gq][kb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub) {
+        const uint4 af = *(const uint4*)(kimg + kc_off(128, kb * 16 + i, sub * 4 + g));
+#pragma unroll
+        for (int gq = 0; gq < NG; ++gq) mma<bf16_t>(s[gq][kb], af, qf[gq][sub]);
+      }
+    }
+    f32x2_t mrow[4][2];
+    if constexpr (MASK) {
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        const float4 mv4 = *(const float4*)(&mfull[k0 + kb * 16 + 4 * g]);
+        mrow[kb][0] = f32x2_t{mv4.x, mv4.y};
+        mrow[kb][1] = f32x2_t{mv4.z, mv4.w};
+      }
+    }
+    float p[NG][4][4];
+#pragma unroll
+    for (int gq = 0; gq < NG; ++gq) {
+      float tmax = -INFINITY;
+      const int toff = (QW - 1) - (q[gq] - qbase) + k0;
+      const f32x2_t gr2 = {graw[gq], graw[gq]};
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          f32x2_t x = {s[gq][kb][2 * jj], s[gq][kb][2 * jj + 1]};
+          if constexpr (REL) {
+            const int kl = kb * 16 + 4 * g + 2 * jj + toff;
+            x = gr2 * f32x2_t{tfull[kl], tfull[kl + 1]} + x;
+          }
+          if constexpr (MASK) x += mrow[kb][jj];
+          p[gq][kb][2 * jj] = x.x;
+          p[gq][kb][2 * jj + 1] = x.y;
+        }
+        tmax = fmaxf(tmax, fmaxf(fmaxf(p[gq][kb][0], p[gq][kb][1]), fmaxf(p[gq][kb][2], p[gq][kb][3])));
+      }
+      tmax = xmax16(tmax);
+      tmax = xmax32(tmax);
+      const float mn = fmaxf(m[gq], tmax);
+      const float mref = (mn == -INFINITY) ? 0.f : mn;
+      const float nbias = -mref * sl2;
+      const float alpha = __builtin_amdgcn_exp2f((m[gq] - mref) * sl2);
+      const f32x2_t sl2v = {sl2, sl2}, nb2 = {nbias, nbias};
+      f32x2_t ls2 = {0.f, 0.f};
+      uint64_t bits = 0;
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        unsigned keep = 0xF;
+        if constexpr (DROP) {
+          // 4 x 16-bit draws of keys k0+kb*16+4g .. +3: one aligned 8-byte word from each table, XORed
+          const int kq = k0 + kb * 16 + 4 * g;
+          const uint64_t w = *(const uint64_t*)(dtab + (((ooff[gq][0] + kq) & (ATTN_R - 1)) << 1)) ^
+                             *(const uint64_t*)(dtab + ATTN_R * 2 + (((ooff[gq][1] + kq) & (ATTN_R - 1)) << 1)) ^
+                             *(const uint64_t*)(dtab + ATTN_R * 4 + (((ooff[gq][2] + kq) & (ATTN_R - 1)) << 1));
+          keep = 0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) keep |= (((unsigned)(w >> (16 * j)) & 0xFFFFu) >= a.thr16 ? 1u : 0u) << j;
+          bits |= (uint64_t)keep << (kb * 16 + 4 * g);
+        }
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          const f32x2_t arg = f32x2_t{p[gq][kb][2 * jj], p[gq][kb][2 * jj + 1]} * sl2v + nb2;
+          f32x2_t e = {__builtin_amdgcn_exp2f(arg.x), __builtin_amdgcn_exp2f(arg.y)};
+          ls2 += e;
+          if constexpr (DROP) {
+            e.x = ((keep >> (2 * jj)) & 1u) ? e.x : 0.f;
+            e.y = ((keep >> (2 * jj + 1)) & 1u) ? e.y : 0.f;
+          }
+          p[gq][kb][2 * jj] = e.x;
+          p[gq][kb][2 * jj + 1] = e.y;
+        }
+      }
+      const float ls = ls2.x + ls2.y;
+      if constexpr (DROP) {
+        if (a.dbits) {
+          unsigned lo = (unsigned)bits, hi = (unsigned)(bits >> 32);
+          lo = xor16(lo);
+          hi = xor16(hi);
+          lo = xor32(lo);
+          hi = xor32(hi);
+          if (g == 0 && qv[gq]) a.dbits[((long)bh * ntiles + t) * a.Lq + q[gq]] = ((uint64_t)hi << 32) | lo;
+        }
+      }
+      l[gq] = l[gq] * alpha + ls;
+      m[gq] = mn;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) o[gq][d] *= alpha;
+    }
+    {
+      const int qq = i >> 2, pp = i & 3;
+      typedef __attribute__((address_space(3))) s16x4_t* lp;
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        uint4 bq[NG];
+#pragma unroll
+        for (int gq = 0; gq < NG; ++gq) {
+          bq[gq].x = pk(p[gq][2 * ss][0], p[gq][2 * ss][1]);
+          bq[gq].y = pk(p[gq][2 * ss][2], p[gq][2 * ss][3]);
+          bq[gq].z = pk(p[gq][2 * ss + 1][0], p[gq][2 * ss + 1][1]);
+          bq[gq].w = pk(p[gq][2 * ss + 1][2], p[gq][2 * ss + 1][3]);
+        }
+        const int k1 = 32 * ss + 4 * g + qq, k2 = k1 + 16;
+#pragma unroll
+        for (int db = 0; db < 4; ++db) {
+          const int u = db * 4 + pp;
+          const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(vimg + k1 * 128 + ((u ^ hatt(k1)) << 3)));
+          const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(vimg + k2 * 128 + ((u ^ hatt(k2)) << 3)));
+          const uint4 af = join_tr(lo, hi);
+#pragma unroll
+          for (int gq = 0; gq < NG; ++gq) mma<bf16_t>(o[gq][db], af, bq[gq]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int gq = 0; gq < NG; ++gq) {
+    float lt = l[gq];
+    lt = xsum16(lt);
+    lt = xsum32(lt);
+    if (!qv[gq]) continue;
     const float inv = (lt > 0.f) ? (DROP ? a.drop_scale : 1.f) / lt : NAN;
     bf16_t* Ob = (bf16_t*)a.Out + ((long)b * a.Lq + q[gq]) * a.so + h * DH;
 #pragma unroll
@@ -544,8 +823,8 @@ __global__ void __launch_bounds__(256) dq_kernel(AttnArgs a) {
 #pragma unroll
     for (int e = 0; e < Cfg<T>::ECH; ++e) delta += ld<T>(x + e) * ld<T>(y + e);
   }
-  delta += __shfl_xor(delta, 16, 64);
-  delta += __shfl_xor(delta, 32, 64);
+  delta = xsum16(delta);
+  delta = xsum32(delta);
   if (qv && g == 0) a.delta[(long)bh * a.Lq + q] = delta;
   const float lse = qv ? a.lse[(long)bh * a.Lq + q] : 0.f;
 
@@ -571,10 +850,7 @@ __global__ void __launch_bounds__(256) dq_kernel(AttnArgs a) {
         float pr = 0.f;
         if (key_ok(a, b, key) && qv) pr = __expf(s[kb][j] * a.scale - lse);
         float dpv = dp[kb][j];
-        if (a.thr16) {
-          const uint64_t idx = ((uint64_t)bh * a.Lq + q) * a.Lk + key;
-          dpv = drop_keep(a.seed, a.stream, idx, a.thr16) ? dpv * a.drop_scale : 0.f;
-        }
+        if (a.thr16) dpv = attn_keep(a, bh, q, key) ? dpv * a.drop_scale : 0.f;
         ds[kb][j] = pr * (dpv - delta);
       }
     trans_times_vals<T>(dq, ktimg, ds, lane);
@@ -645,10 +921,7 @@ __global__ void __launch_bounds__(256) dkv_kernel(AttnArgs a) {
         float pr = 0.f;
         if (kok && qq < a.Lq) pr = __expf(s[qb][j] * a.scale - lse_s[ql]);
         float keep = 1.f;
-        if (a.thr16) {
-          const uint64_t idx = ((uint64_t)bh * a.Lq + qq) * a.Lk + key;
-          keep = drop_keep(a.seed, a.stream, idx, a.thr16) ? a.drop_scale : 0.f;
-        }
+        if (a.thr16) keep = attn_keep(a, bh, qq, key) ? a.drop_scale : 0.f;
         pd[qb][j] = pr * keep;
         ds[qb][j] = pr * (dp[qb][j] * keep - del_s[ql]);
       }
@@ -697,20 +970,6 @@ __device__ __forceinline__ void trans_times_vals2(f32x4_t (&out)[2][4], const un
   }
 }
 
-// keep bits of 4 consecutive dropout elements e0..e0+3 (at most two hash words)
-__device__ __forceinline__ unsigned keep4(const AttnArgs& a, uint64_t e0) {
-  const uint64_t h0 = mix64(a.seed, a.stream, e0 >> 2);
-  const uint64_t h1 = ((e0 & 3) == 0) ? h0 : mix64(a.seed, a.stream, (e0 >> 2) + 1);
-  unsigned keep = 0;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const unsigned sl = (unsigned)((e0 & 3) + j);
-    const uint64_t hw = sl < 4 ? h0 : h1;
-    keep |= (((unsigned)(hw >> (16u * (sl & 3u))) & 0xFFFFu) >= a.thr16 ? 1u : 0u) << j;
-  }
-  return keep;
-}
-
 // dQ, query-owned: 128 queries per workgroup (two 16-query groups per wave), K/V tiles double-buffered.
 // S^T = K Q^T and dP^T = V dO^T share the LDS row reads across both groups; dS = P (dP' - delta);
 // dQ^T += K^T dS^T from the K MC image. Writes delta = rowsum(dO*O) for the dK/dV kernel.
@@ -753,8 +1012,8 @@ __global__ void __launch_bounds__(256, 2) dq2_kernel(AttnArgs a) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) dl += bf2f(x[e]) * bf2f(y[e]);
     }
-    dl += __shfl_xor(dl, 16, 64);
-    dl += __shfl_xor(dl, 32, 64);
+    dl = xsum16(dl);
+    dl = xsum32(dl);
     delta[gq] = dl;
     if (qv[gq] && g == 0) a.delta[(long)bh * a.Lq + q[gq]] = dl;
     lse2[gq] = qv[gq] ? a.lse[(long)bh * a.Lq + q[gq]] * 1.4426950408889634f : 0.f;
@@ -833,7 +1092,7 @@ __global__ void __launch_bounds__(256, 2) dq2_kernel(AttnArgs a) {
       for (int kb = 0; kb < 4; ++kb) {
         unsigned keep = 0xF;
         if constexpr (DM == 2) keep = (unsigned)(wbits[gq] >> (kb * 16 + 4 * g)) & 0xFu;
-        if constexpr (DM == 1) keep = keep4(a, ((uint64_t)bh * a.Lq + q[gq]) * a.Lk + (k0 + kb * 16 + 4 * g));
+        if constexpr (DM == 1) keep = attn_keep4(a, bh, q[gq], k0 + kb * 16 + 4 * g);
         const f32x2_t ndl = {-delta[gq], -delta[gq]};
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj) {
@@ -1003,8 +1262,8 @@ __global__ void __launch_bounds__(256, (DM == 1 ? 1 : 2)) dkv2_kernel(AttnArgs a
               m1 = __builtin_amdgcn_sbfe((int)wq[2 * jj + 1], kb5, 1);
             } else {
               const int qq = q0 + qb * 16 + 4 * g + 2 * jj;
-              m0 = drop_keep(a.seed, a.stream, ((uint64_t)bh * a.Lq + qq) * a.Lk + key[gq], a.thr16) ? -1 : 0;
-              m1 = drop_keep(a.seed, a.stream, ((uint64_t)bh * a.Lq + qq + 1) * a.Lk + key[gq], a.thr16) ? -1 : 0;
+              m0 = attn_keep(a, bh, qq, key[gq]) ? -1 : 0;
+              m1 = attn_keep(a, bh, qq + 1, key[gq]) ? -1 : 0;
             }
             pdv.x = __int_as_float(__float_as_int(pr.x) & m0);
             pdv.y = __int_as_float(__float_as_int(pr.y) & m1);
@@ -1068,6 +1327,30 @@ static int run(int which, AttnArgs& a, hipStream_t s) {
           if (drop) { if (mask) FWD1(true, true); else FWD1(true, false); }
           else { if (mask) FWD1(false, true); else FWD1(false, false); }
 #undef FWD1
+          return (int)hipGetLastError();
+        }
+        // v3 (K/V resident in LDS) for Lk <= 512 unless FDDM_ATTN_V2 is set; 8 waves (256 queries) when that
+        // still leaves >= 2 workgroups per CU-round, else 4 (128 queries)
+        if (a.Lk <= 512 && !rel && !getenv("FDDM_ATTN_V2")) {  // WavLM (rel): fwd2's 2 workgroups per CU measure faster
+          const int LkP = (a.Lk + 63) / 64 * 64;
+          const char* nw_env = getenv("FDDM_ATTN_NW");
+          const int nw = nw_env ? atoi(nw_env) : 8;
+          const int QW = 32 * nw;
+          const size_t lds = (size_t)LkP * 256 + (size_t)LkP * 4 + (rel ? (size_t)(LkP + QW) * 4 : 0) +
+                             (drop ? (size_t)3 * ATTN_R * 2 : 0);
+          const bool mask3 = a.key_keep != nullptr || (a.Lk % 64) != 0;
+          dim3 grid3((a.Lq + QW - 1) / QW, a.B * a.H);
+#define FWD3(D, M, R, W) hipLaunchKernelGGL((fwd3_kernel<D, M, R, W>), grid3, dim3(64 * W), lds, s, a)
+#define FWD3W(D, M, R) do { if (nw == 4) FWD3(D, M, R, 4); else FWD3(D, M, R, 8); } while (0)
+          if (rel) {
+            if (mask3) FWD3W(false, true, true); else FWD3W(false, false, true);
+          } else if (drop) {
+            if (mask3) FWD3W(true, true, false); else FWD3W(true, false, false);
+          } else {
+            if (mask3) FWD3W(false, true, false); else FWD3W(false, false, false);
+          }
+#undef FWD3W
+#undef FWD3
           return (int)hipGetLastError();
         }
         dim3 grid((a.Lq + 127) / 128, a.B * a.H);

@@ -1,0 +1,269 @@
+// Small per-batch kernels of the decoder step (rows = the batch, B <= 64): the time-embedding MLP and the FiLM
+// projections (models/denoise_decoder.py:74-119, 179-186, 272-274), the pooled acoustic condition (:185), and the
+// KL term's masked batch reduction (train.py:247-253). Each is a handful of small launches on the main stream in
+// place of ~40 framework launches (sinusoid ops, BLAS calls on 32-row operands, bias sums, concatenations,
+// masked means). All arithmetic is fp32 (the reference's precision for these ops).
+#include "common.h"
+
+namespace fddm {
+namespace small {
+
+constexpr int MAXJ = 16;  // jobs per launch
+
+// ------------------------------------------------------------------------------------------ pooled mean
+// out[b][j] = mean_s x[b][s][j]; block = 64 columns x 4 S-slices (LDS reduction, fixed order)
+template <typename T>
+__global__ void __launch_bounds__(256) rows_mean_kernel(const T* __restrict__ x, float* __restrict__ out, long S,
+                                                        long d) {
+  __shared__ float part[4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const long b = blockIdx.y, j = (long)blockIdx.x * 64 + tx;
+  float acc = 0.f;
+  if (j < d)
+    for (long s = ty; s < S; s += 4) acc += ld<T>(x + (b * S + s) * d + j);
+  part[ty][tx] = acc;
+  __syncthreads();
+  if (ty == 0 && j < d) out[b * d + j] = ((part[0][tx] + part[1][tx]) + (part[2][tx] + part[3][tx])) / (float)S;
+}
+
+// ------------------------------------------------------------------------------------------ time embedding
+// emb[b] = [sin(t f), cos(t f)], f_k = exp(-k * ln(max_steps) / (half - 1)) (SinusoidalTimeEmbedding.forward,
+// models/denoise_decoder.py:108-116: torch.linspace(log 1, log max_steps, half) * -1 then exp; odd d pads a 0)
+__global__ void time_embed_kernel(const long* __restrict__ t, float* __restrict__ emb, long B, long d,
+                                  float log_max) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= B * d) return;
+  const long b = e / d, k = e % d, half = d / 2;
+  float v = 0.f;
+  if (k < 2 * half) {
+    const long kk = k < half ? k : k - half;
+    // torch.linspace(start, end, steps): start + i * step with step = (end - start) / (steps - 1)
+    const float step = half > 1 ? log_max / (float)(half - 1) : 0.f;
+    const float lin = (kk < half / 2) ? (float)kk * step : log_max - (float)(half - 1 - kk) * step;
+    const float f = expf(-lin);
+    const float a = (float)t[b] * f;
+    v = k < half ? sinf(a) : cosf(a);
+  }
+  emb[e] = v;
+}
+
+// ------------------------------------------------------------------------------------------ linear family
+// Job j: out_j[r][n] = act( sum_k in[r][k] * W_j(n, k) + b_j[n] ),  W_j(n, k) = W_j[n*ldw + k] (TW = 0) or
+// W_j[k*ldw + n] (TW = 1, i.e. in @ W).  act 0: none; 1: out = pre, out2 = silu(pre); 2: out = acc * silu'(aux[r][n])
+struct LinJobs {
+  const float* W[MAXJ];
+  const float* b[MAXJ];
+  float* out[MAXJ];
+  float* out2[MAXJ];
+};
+
+template <bool TW>
+__global__ void __launch_bounds__(256) linear_kernel(const float* __restrict__ in, long ldi, LinJobs J, long ldw,
+                                                     long ldo, const float* __restrict__ aux, long R, long N, long K,
+                                                     int act) {
+  // tile: 32 rows x 16 columns, K in chunks of 32; thread = column (t & 15) x rows 2*(t >> 4) .. +1
+  __shared__ float Is[32][33];
+  __shared__ float Ws[16][33];
+  const int tid = threadIdx.x, c = tid & 15, rg = tid >> 4;
+  const long n0 = (long)blockIdx.x * 16, r0 = (long)blockIdx.z * 32;
+  const int j = blockIdx.y;
+  const float* W = J.W[j];
+  float acc[2] = {0.f, 0.f};
+  for (long k0 = 0; k0 < K; k0 += 32) {
+    for (int e = tid; e < 32 * 32; e += 256) {
+      const int rr = e >> 5, kk = e & 31;
+      const long r = r0 + rr, k = k0 + kk;
+      Is[rr][kk] = (r < R && k < K) ? in[r * ldi + k] : 0.f;
+    }
+    for (int e = tid; e < 16 * 32; e += 256) {
+      int cc, kk;
+      if (TW) { kk = e >> 4; cc = e & 15; } else { cc = e >> 5; kk = e & 31; }
+      const long n = n0 + cc, k = k0 + kk;
+      Ws[cc][kk] = (n < N && k < K) ? (TW ? W[k * ldw + n] : W[n * ldw + k]) : 0.f;
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int kk = 0; kk < 32; ++kk) {
+      const float w = Ws[c][kk];
+      acc[0] = fmaf(Is[2 * rg][kk], w, acc[0]);
+      acc[1] = fmaf(Is[2 * rg + 1][kk], w, acc[1]);
+    }
+    __syncthreads();
+  }
+  const long n = n0 + c;
+  if (n >= N) return;
+  const float bias = J.b[j] ? J.b[j][n] : 0.f;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const long r = r0 + 2 * rg + i;
+    if (r >= R) continue;
+    float v = acc[i] + bias;
+    if (act == 1) {
+      J.out[j][r * ldo + n] = v;
+      J.out2[j][r * ldo + n] = v / (1.f + expf(-v));
+    } else if (act == 2) {
+      const float x = aux[r * ldo + n];
+      const float sg = 1.f / (1.f + expf(-x));
+      J.out[j][r * ldo + n] = acc[i] * (sg * (1.f + x * (1.f - sg)));
+    } else {
+      J.out[j][r * ldo + n] = v;
+    }
+  }
+}
+
+// Job j: dW_j[n][k] += sum_r dy_j[r][n] * x_j[r][k];  db_j[n] += sum_r dy_j[r][n]   (accumulating: gradient slots)
+struct DwJobs {
+  const float* dy[MAXJ];
+  const float* x[MAXJ];
+  float* dW[MAXJ];
+  float* db[MAXJ];
+  long N[MAXJ], K[MAXJ], lddy[MAXJ], ldx[MAXJ];
+};
+
+__global__ void __launch_bounds__(256) dw_kernel(DwJobs J, long R) {
+  // tile 32 (n) x 32 (k); rows staged in chunks of 32
+  __shared__ float Ds[32][33];
+  __shared__ float Xs[32][33];
+  const int j = blockIdx.z;
+  const long N = J.N[j], K = J.K[j];
+  const long n0 = (long)blockIdx.y * 32, k0 = (long)blockIdx.x * 32;
+  if (n0 >= N || k0 >= K) return;
+  const int tid = threadIdx.x, kc = tid & 31, ng = tid >> 5;  // thread: column k0+kc, rows n0 + 4*ng .. +3
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  float bacc = 0.f;
+  for (long rr0 = 0; rr0 < R; rr0 += 32) {
+    for (int e = tid; e < 32 * 32; e += 256) {
+      const int rr = e >> 5, cc = e & 31;
+      const long r = rr0 + rr;
+      Ds[rr][cc] = (r < R && n0 + cc < N) ? J.dy[j][r * J.lddy[j] + n0 + cc] : 0.f;
+      Xs[rr][cc] = (r < R && k0 + cc < K) ? J.x[j][r * J.ldx[j] + k0 + cc] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int rr = 0; rr < 32; ++rr) {
+      const float xv = Xs[rr][kc];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i] = fmaf(Ds[rr][4 * ng + i], xv, acc[i]);
+    }
+    if (J.db[j] && blockIdx.x == 0 && tid < 32)
+      for (int rr = 0; rr < 32; ++rr) bacc += Ds[rr][tid];
+    __syncthreads();
+  }
+  const long k = k0 + kc;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const long n = n0 + 4 * ng + i;
+    if (n < N && k < K) J.dW[j][n * K + k] += acc[i];
+  }
+  if (J.db[j] && blockIdx.x == 0 && tid < 32 && n0 + tid < N) J.db[j][n0 + tid] += bacc;
+}
+
+// ------------------------------------------------------------------------------------------ KL reduction
+// SchedulerAdapter.kl_term's batch reduction (train.py:247-253): per[b] = sum_l m kl / (sum_l m + eps) (mask) or
+// mean_l kl (no mask); loss = mean_b per[b]; w[b][l] = d loss / d kl[b][l] for the backward. One wave per
+// utterance, fixed summation order (deterministic); one launch of 1024 threads.
+__global__ void __launch_bounds__(1024) kl_reduce_kernel(const float* __restrict__ kl, const unsigned char* __restrict__ mask,
+                                                         float* __restrict__ w, float* __restrict__ loss, long B,
+                                                         long L) {
+  __shared__ float per[1024];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const float eps = 1e-8f;
+  for (long b = wv; b < B; b += 16) {
+    float s = 0.f, m = 0.f;
+    for (long l = lane; l < L; l += 64) {
+      const float mv = mask ? (mask[b * L + l] ? 1.f : 0.f) : 1.f;
+      s += mv * kl[b * L + l];
+      m += mv;
+    }
+    s = wave_sum(s);
+    m = wave_sum(m);
+    const float den = mask ? m + eps : (float)L;
+    for (long l = lane; l < L; l += 64) {
+      const float mv = mask ? (mask[b * L + l] ? 1.f : 0.f) : 1.f;
+      w[b * L + l] = mask ? mv / den / (float)B : 1.f / ((float)L * (float)B);
+    }
+    if (lane == 0) per[b] = s / den;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float acc = 0.f;
+    for (long b = 0; b < B; ++b) acc += per[b];
+    loss[0] = acc / (float)B;
+  }
+}
+
+}  // namespace small
+}  // namespace fddm
+
+using namespace fddm;
+using namespace fddm::small;
+
+FDDM_API int fddm_rows_mean(int dtype, const void* x, float* out, long B, long S, long d, void* hs) {
+  if (B <= 0 || d <= 0) return 0;
+  dim3 g((unsigned)((d + 63) / 64), (unsigned)B);
+  if (dtype == FDDM_BF16)
+    hipLaunchKernelGGL(rows_mean_kernel<bf16_t>, g, dim3(256), 0, (hipStream_t)hs, (const bf16_t*)x, out, S, d);
+  else
+    hipLaunchKernelGGL(rows_mean_kernel<float>, g, dim3(256), 0, (hipStream_t)hs, (const float*)x, out, S, d);
+  return (int)hipGetLastError();
+}
+
+FDDM_API int fddm_time_embed(const long* t, float* emb, long B, long d, float max_steps, void* hs) {
+  if (B <= 0 || d <= 0) return 0;
+  const long n = B * d;
+  // the end point of torch.linspace(log 1, log max_steps, half): math.log in double, then the fp32 tensor value
+  hipLaunchKernelGGL(time_embed_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)hs, t, emb, B, d,
+                     (float)log((double)max_steps));
+  return (int)hipGetLastError();
+}
+
+FDDM_API int fddm_small_linear(const float* in, long ldi, int njobs, const float* const* W, const float* const* bias,
+                               float* const* out, float* const* out2, long ldw, long ldo, const float* aux, long R, long N,
+                               long K, int act, int transpose_w, void* hs) {
+  if (njobs <= 0 || njobs > MAXJ || R <= 0 || N <= 0) return njobs > MAXJ ? (int)hipErrorInvalidValue : 0;
+  LinJobs J{};
+  for (int j = 0; j < njobs; ++j) {
+    J.W[j] = W[j];
+    J.b[j] = bias ? bias[j] : nullptr;
+    J.out[j] = out[j];
+    J.out2[j] = out2 ? out2[j] : nullptr;
+    if (act == 1 && !J.out2[j]) return (int)hipErrorInvalidValue;
+  }
+  if (act == 2 && !aux) return (int)hipErrorInvalidValue;
+  dim3 g((unsigned)((N + 15) / 16), (unsigned)njobs, (unsigned)((R + 31) / 32));
+  if (transpose_w)
+    hipLaunchKernelGGL(linear_kernel<true>, g, dim3(256), 0, (hipStream_t)hs, in, ldi, J, ldw, ldo, aux, R, N, K, act);
+  else
+    hipLaunchKernelGGL(linear_kernel<false>, g, dim3(256), 0, (hipStream_t)hs, in, ldi, J, ldw, ldo, aux, R, N, K, act);
+  return (int)hipGetLastError();
+}
+
+FDDM_API int fddm_small_dw(int njobs, const float* const* dy, const long* lddy, const float* const* x, const long* ldx,
+                           float* const* dW, float* const* db, const long* N, const long* K, long R, void* hs) {
+  if (njobs <= 0 || njobs > MAXJ || R <= 0) return njobs > MAXJ ? (int)hipErrorInvalidValue : 0;
+  DwJobs J{};
+  long nmax = 1, kmax = 1;
+  for (int j = 0; j < njobs; ++j) {
+    J.dy[j] = dy[j];
+    J.x[j] = x[j];
+    J.dW[j] = dW[j];
+    J.db[j] = db ? db[j] : nullptr;
+    J.N[j] = N[j];
+    J.K[j] = K[j];
+    J.lddy[j] = lddy[j];
+    J.ldx[j] = ldx[j];
+    nmax = N[j] > nmax ? N[j] : nmax;
+    kmax = K[j] > kmax ? K[j] : kmax;
+  }
+  dim3 g((unsigned)((kmax + 31) / 32), (unsigned)((nmax + 31) / 32), (unsigned)njobs);
+  hipLaunchKernelGGL(dw_kernel, g, dim3(256), 0, (hipStream_t)hs, J, R);
+  return (int)hipGetLastError();
+}
+
+FDDM_API int fddm_kl_reduce(const float* kl_tok, const unsigned char* mask, float* w, float* loss, long B, long L,
+                            void* hs) {
+  if (B <= 0 || L <= 0) return 0;
+  if (B > 1024) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(kl_reduce_kernel, dim3(1), dim3(1024), 0, (hipStream_t)hs, kl_tok, mask, w, loss, B, L);
+  return (int)hipGetLastError();
+}

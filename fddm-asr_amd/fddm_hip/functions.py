@@ -97,6 +97,7 @@ class EmbedFn(torch.autograd.Function):
         cd = rt.compute_dtype()
         xT = torch.empty(B * L, d, device=E.device, dtype=cd)
         ops.embed_fwd(xt.contiguous(), E.detach(), tbias.detach().contiguous(), x, xT, L)
+        ctx.set_materialize_grads(False)     # xT is non-differentiable: no zero-filled gradient for it
         ctx.save_for_backward(xt)
         ctx.E = (E,)
         ctx.pad_id, ctx.L, ctx.V = pad_id, L, E.shape[0]
@@ -117,44 +118,42 @@ class EmbedFn(torch.autograd.Function):
 
 # ------------------------------------------------------------------------- decoder conditioning
 def sinusoid(t, d, max_steps):
-    """SinusoidalTimeEmbedding's feature map (models/denoise_decoder.py:92-119), same torch ops."""
+    """SinusoidalTimeEmbedding's feature map (models/denoise_decoder.py:92-119), on the device (fddm_time_embed)."""
     if t.dim() == 0:
         t = t[None]
-    half = d // 2
-    freqs = torch.exp(torch.linspace(math.log(1.0), math.log(max_steps), half, device=t.device) * (-1))
-    args = t.float().unsqueeze(1) * freqs.unsqueeze(0)
-    emb = torch.cat([torch.sin(args), torch.cos(args)], dim=1)
-    if d % 2 == 1:
-        emb = F.pad(emb, (0, 1))
-    return emb.contiguous()
+    return ops.time_embed(t.to(torch.int64).contiguous(), d, max_steps)
 
 
 class CondFn(torch.autograd.Function):
     """The decoder's conditioning path as one Function: t_bias = time_proj(mlp(sinusoid(t)))
     (models/denoise_decoder.py:92-119, 272-274) and the FiLM projections scale_l / shift_l = pooled W^T + b of
-    every block (:74-89; pooled = time-mean of the acoustic condition, no grad). Forward: 3 fp32 GEMMs for the
-    time MLP and ONE for all 2*NL FiLM projections; backward: the time-MLP chain in fp32 and the FiLM weight /
-    bias gradients as one grouped launch (bf16 mode) straight into the parameters' gradient slots — instead of
-    ~80 small framework kernels (per-layer BLAS calls, bias reductions, gradient accumulations) per step.
-    `gbuf` [2*NL, B, d] (zeroed by the caller) is where the blocks' LayerNorm backward accumulates dFiLM."""
+    every block (:74-89; pooled = time-mean of the acoustic condition, no grad). All of it runs on the small
+    row-batch fp32 kernels (csrc/small.hip): forward = time embedding + 3 Linears (SiLU fused) + ONE launch for all
+    2*NL FiLM projections; backward = the two input-gradient Linears (SiLU' fused) and the weight / bias gradients
+    of all of them in one launch, straight into the parameters' gradient slots. `gbuf` [2*NL, B, d] (zeroed by the
+    caller) is where the blocks' LayerNorm backward accumulates dFiLM."""
 
     @staticmethod
     def forward(ctx, t, pooled, gbuf, d, max_steps, *params):
         W1, b1, W2, b2, Wp, bp = params[:6]
         film = params[6:]
         nf = len(film) // 2
-        # [B, d]-row GEMMs in fp32 on the BLAS library (plain skinny GEMMs; the MFMA kernels target >= 128 rows)
         with torch.no_grad():
-            emb = sinusoid(t, d, max_steps)
-            pre = torch.addmm(b1, emb, W1.t())
-            h = F.silu(pre)
-            te = torch.addmm(b2, h, W2.t())
-            tb = torch.addmm(bp, te, Wp.t())
-            Wf = torch.cat([w for w in film[0::2]])
-            bf = torch.cat([b for b in film[1::2]])
+            emb = sinusoid(t, d, max_steps)                                      # [B, d]
+            Bt = emb.shape[0]
+            dev = emb.device
+            pre = torch.empty(Bt, W1.shape[0], device=dev, dtype=F32)
+            h = torch.empty_like(pre)
+            ops.small_linear(emb, [W1.detach()], [b1.detach()], [pre], [h], act=1)
+            te = torch.empty(Bt, W2.shape[0], device=dev, dtype=F32)
+            ops.small_linear(h, [W2.detach()], [b2.detach()], [te])
+            tb = torch.empty(Bt, Wp.shape[0], device=dev, dtype=F32)
+            ops.small_linear(te, [Wp.detach()], [bp.detach()], [tb])
             B = pooled.shape[0]
-            fl = torch.addmm(bf, pooled, Wf.t())                                 # [B, nf*d]
-            f12 = fl.view(B, nf, d).transpose(0, 1).contiguous()              # [nf, B, d]
+            f12 = torch.empty(nf, B, d, device=dev, dtype=F32)
+            if nf:
+                ops.small_linear(pooled.contiguous(), [w.detach() for w in film[0::2]], [b.detach() for b in film[1::2]],
+                                 [f12[i] for i in range(nf)])
         ctx.save_for_backward(emb, pre, h, te, pooled, gbuf, *params)
         ctx.nf = nf
         return (tb,) + tuple(f12[i] for i in range(nf))
@@ -174,30 +173,23 @@ class CondFn(torch.autograd.Function):
         else:
             dfl = torch.stack([g if g is not None else torch.zeros(B, d, device=dev) for g in dfilm])
         G = [_gdst(p_, zero=True) for p_ in film]
-        if rt.compute_dtype() == torch.bfloat16:
-            d16 = ops.cast(dfl.contiguous(), torch.bfloat16)
-            p16 = ops.cast(pooled.contiguous(), torch.bfloat16)
-            ops.linear_dw_grouped([(d16[i], p16, G[2 * i][0], G[2 * i + 1][0]) for i in range(nf)])
-        else:
-            for i in range(nf):
-                ops.linear_dw(dfl[i], pooled, out=G[2 * i][0], accumulate=True, db=G[2 * i + 1][0])
-        for i in range(2 * nf):
-            grads[6 + i] = _ret(*G[i])
-        # time MLP (fp32): tb = te Wp^T + bp, te = h W2^T + b2, h = silu(pre), pre = emb W1^T + b1;
-        # weight gradients accumulated in place (beta = 1) into the gradient slots
+        jobs = [(dfl[i], pooled, G[2 * i][0], G[2 * i + 1][0]) for i in range(nf)]
+        T = None
         if dtb is not None:
             dtb = dtb.contiguous()
             T = [_gdst(p_, zero=True) for p_ in (W1, b1, W2, b2, Wp, bp)]
-            dte = dtb @ Wp
-            torch.addmm(T[4][0], dtb.t(), te, out=T[4][0])
-            T[5][0].add_(dtb.sum(0))
-            dh = dte @ W2
-            torch.addmm(T[2][0], dte.t(), h, out=T[2][0])
-            T[3][0].add_(dte.sum(0))
-            sg = torch.sigmoid(pre)
-            dpre = dh * sg * (1.0 + pre * (1.0 - sg))
-            torch.addmm(T[0][0], dpre.t(), emb, out=T[0][0])
-            T[1][0].add_(dpre.sum(0))
+            jobs.append((dtb, te, T[4][0], T[5][0]))
+        ops.small_dw(jobs)                                        # FiLM + time_proj weight / bias gradients
+        for i in range(2 * nf):
+            grads[6 + i] = _ret(*G[i])
+        if dtb is not None:
+            # tb = te Wp^T + bp, te = h W2^T + b2, h = silu(pre), pre = emb W1^T + b1
+            Bt = dtb.shape[0]
+            dte = torch.empty(Bt, Wp.shape[1], device=dev, dtype=F32)
+            ops.small_linear(dtb, [Wp.detach()], None, [dte], transpose_w=True)
+            dpre = torch.empty(Bt, W2.shape[1], device=dev, dtype=F32)
+            ops.small_linear(dte, [W2.detach()], None, [dpre], act=2, aux=pre, transpose_w=True)
+            ops.small_dw([(dte, h, T[2][0], T[3][0]), (dpre, emb, T[0][0], T[1][0])])
             for i in range(6):
                 grads[i] = _ret(*T[i])
         return (None, None, None, None, None) + tuple(grads)
@@ -281,6 +273,7 @@ class DecoderBlockFn(torch.autograd.Function):
         ctx.meta = meta
         ctx.bits = (bits_s, bits_c)
         ctx.mark_non_differentiable(x3T)
+        ctx.set_materialize_grads(False)     # x3T's gradient is never used: no zero fill per block
         return x3, x3T
 
     @staticmethod
@@ -416,11 +409,12 @@ class KLFn(torch.autograd.Function):
     produced in backward by a second fused pass that reads the upstream scalar on the device."""
 
     @staticmethod
-    def forward(ctx, logits, xt, x0, t, w, betas):
+    def forward(ctx, logits, xt, x0, t, mask_u8, betas):
+        """mask_u8: x_mask as uint8 [B*L] (or None: plain mean over L, train.py:253)."""
         B, L, V = logits.shape
         l2 = logits.reshape(B * L, V)
         kl_tok = ops.kl_fwd(l2, xt.reshape(-1).contiguous(), x0.reshape(-1).contiguous(), t.contiguous(), betas, L)
-        loss = (kl_tok * w).sum()
+        loss, w = ops.kl_reduce(kl_tok, mask_u8, B, L)       # masked mean over L, mean over B; w = dloss/dkl_tok
         ctx.save_for_backward(l2, xt, x0, t, w, betas)
         ctx.shape = (B, L, V)
         return loss

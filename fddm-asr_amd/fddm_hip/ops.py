@@ -393,6 +393,82 @@ def lfd_dloss(Cm, gscale, lam, out_dtype):
     return dC
 
 
+# ----------------------------------------------------------------------------- small per-batch ops
+def rows_mean(x3d):
+    """[B, S, d] (f32 / bf16, contiguous) -> f32 [B, d] mean over S."""
+    B, S, d = x3d.shape
+    _chk(x3d.is_contiguous(), "rows_mean: contiguous input")
+    out = torch.empty(B, d, device=x3d.device, dtype=torch.float32)
+    call("fddm_rows_mean", code(x3d), ptr(x3d), ptr(out), B, S, d, stream())
+    return out
+
+
+def time_embed(t, d, max_steps):
+    """SinusoidalTimeEmbedding features of int64 t [B] -> f32 [B, d]."""
+    _chk(t.dtype == torch.int64 and t.is_contiguous() and t.dim() == 1, "time_embed: int64 [B]")
+    emb = torch.empty(t.numel(), d, device=t.device, dtype=torch.float32)
+    call("fddm_time_embed", ptr(t), ptr(emb), t.numel(), d, float(max_steps), stream())
+    return emb
+
+
+def _parr(ts):
+    import ctypes
+    return (ctypes.c_void_p * len(ts))(*[ptr(x) for x in ts])
+
+
+def small_linear(inp, Ws, bs, outs, outs2=None, act=0, aux=None, transpose_w=False):
+    """out_j = act(inp @ W_j^T + b_j) (transpose_w: inp @ W_j) for a few row-batch (R <= 64 per tile) fp32 Linears
+    sharing one input; act 1 also writes silu into outs2; act 2 multiplies by silu'(aux)."""
+    R, K = inp.shape
+    W0 = Ws[0]
+    N = W0.shape[0]
+    if transpose_w:
+        N = W0.shape[1]
+        _chk(W0.shape[0] == K, "small_linear shapes")
+    else:
+        _chk(W0.shape[1] == K, "small_linear shapes")
+    for W, o in zip(Ws, outs):
+        _chk(W.dtype == torch.float32 and W.is_contiguous() and W.shape == W0.shape, "small_linear weights")
+        _chk(o.dtype == torch.float32 and o.shape == (R, N) and o.stride(1) == 1 and o.stride(0) == N, "small_linear out")
+    _chk(inp.dtype == torch.float32 and inp.stride(1) == 1, "small_linear input")
+    ldw = W0.shape[1]
+    for i in range(0, len(Ws), 16):
+        sl = slice(i, i + 16)
+        n = len(Ws[sl])
+        call("fddm_small_linear", ptr(inp), inp.stride(0), n, _parr(Ws[sl]), _parr(bs[sl]) if bs is not None else None,
+             _parr(outs[sl]), _parr(outs2[sl]) if outs2 is not None else None, ldw, N, ptr(aux), R, N, K, act,
+             int(transpose_w), stream())
+
+
+def small_dw(jobs):
+    """For (dy [R, N], x [R, K], dW [N, K], db [N] or None): dW += dy^T x, db += colsum(dy) (fp32, R rows)."""
+    import ctypes
+    if not jobs:
+        return
+    R = jobs[0][0].shape[0]
+    for dy, x, dW, db in jobs:
+        _chk(dy.dtype == x.dtype == dW.dtype == torch.float32 and dy.shape[0] == x.shape[0] == R, "small_dw dtypes")
+        _chk(dW.shape == (dy.shape[1], x.shape[1]) and dW.is_contiguous() and dy.stride(1) == 1 and x.stride(1) == 1,
+             "small_dw shapes")
+        _chk(db is None or (db.numel() == dy.shape[1] and db.is_contiguous()), "small_dw bias")
+    for i in range(0, len(jobs), 16):
+        ch = jobs[i:i + 16]
+        L = ctypes.c_long * len(ch)
+        call("fddm_small_dw", len(ch), _parr([j[0] for j in ch]), L(*[j[0].stride(0) for j in ch]),
+             _parr([j[1] for j in ch]), L(*[j[1].stride(0) for j in ch]), _parr([j[2] for j in ch]),
+             _parr([j[3] for j in ch]), L(*[j[0].shape[1] for j in ch]), L(*[j[1].shape[1] for j in ch]), R, stream())
+
+
+def kl_reduce(kl_tok, mask_u8, B, L):
+    """Masked batch mean of the per-token KL (train.py:247-253) -> (loss f32 scalar, w [B*L] = d loss / d kl_tok)."""
+    _chk(kl_tok.numel() == B * L and (mask_u8 is None or (mask_u8.numel() == B * L and mask_u8.dtype == torch.uint8)),
+         "kl_reduce shapes")
+    loss = torch.empty((), device=kl_tok.device, dtype=torch.float32)
+    w = torch.empty(B * L, device=kl_tok.device, dtype=torch.float32)
+    call("fddm_kl_reduce", ptr(kl_tok), ptr(mask_u8), ptr(w), ptr(loss), B, L, stream())
+    return loss, w
+
+
 JUMP_FAST, JUMP_SAMPLE = 1, 2
 
 

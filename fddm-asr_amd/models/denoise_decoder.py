@@ -20,6 +20,7 @@ import torch.nn.functional as F
 
 from fddm_hip import functions as FN
 from fddm_hip import runtime as rt
+from fddm_hip.ops import rows_mean as ops_rows_mean
 
 
 class RoPEEmbedding(nn.Module):
@@ -160,7 +161,8 @@ class DenoisingTransformerDecoder(nn.Module):
         cd = rt.compute_dtype()
         # conditioning (:272-274 time bias, :185 pooled condition -> FiLM of every block) in one Function
         with torch.no_grad():
-            pooled = cond.detach().float().mean(dim=1)                              # (:185)
+            cc = cond.detach()
+            pooled = ops_rows_mean(cc if cc.is_contiguous() else cc.contiguous())   # (:185) mean over S, f32
         nb = len(self.blocks)
         gbuf = torch.zeros(2 * nb, B, self.d_model, device=dev, dtype=torch.float32)
         te = self.time_emb
@@ -175,7 +177,8 @@ class DenoisingTransformerDecoder(nn.Module):
         x, xT = FN.EmbedFn.apply(xt, self.tok_emb.weight, t_bias, self.pad_id)      # (:254)
         if x_mask is None:
             x_mask = xt != self.pad_id                                             # (:277-278)
-        key_keep = x_mask.to(torch.uint8).contiguous()
+        key_keep = x_mask.contiguous().view(torch.uint8) if x_mask.dtype == torch.bool else \
+            x_mask.to(torch.uint8).contiguous()
         with torch.no_grad():
             c = cond.detach()
             cT = (c if c.dtype == cd else c.to(cd)).reshape(B * S, -1).contiguous()

@@ -70,15 +70,15 @@ class SchedulerAdapter:
     def kl_term(self, xt, x0, logits_x0, t, x_mask=None) -> torch.Tensor:
         if not hasattr(self.sch, "betas"):
             raise ValueError("scheduler must provide betas [T] to build the posterior")
-        B, L, V = logits_x0.shape
-        eps = 1e-8
-        if x_mask is not None:
-            valid = x_mask.float()
-            w = (valid / (valid.sum(dim=1, keepdim=True) + eps) / B).reshape(-1).contiguous()
-        else:
-            w = torch.full((B * L,), 1.0 / (L * B), device=logits_x0.device)
-        betas = self.sch.betas.to(logits_x0.device).float().contiguous()
-        return FN.KLFn.apply(logits_x0.float(), xt, x0, t, w, betas)
+        mask = None
+        if x_mask is not None:   # masked mean over L (train.py:247-251), reduced on the device with the KL
+            mask = x_mask.contiguous().view(torch.uint8) if x_mask.dtype == torch.bool else \
+                (x_mask != 0).contiguous().view(torch.uint8)
+            mask = mask.reshape(-1)
+        betas = self.sch.betas
+        if betas.device != logits_x0.device or betas.dtype != torch.float32:
+            betas = betas.to(logits_x0.device).float().contiguous()
+        return FN.KLFn.apply(logits_x0.float(), xt, x0, t, mask, betas)
 
     def w_t(self, t: torch.Tensor) -> torch.Tensor:
         if hasattr(self.sch, "alpha_bar"):

@@ -11,7 +11,9 @@
  *    asynchronous on `stream` (a hipStream_t).
  *  - dtype codes: 0 = f32, 1 = bf16. "T" below means the selected compute/storage dtype.
  *  - Return value: hipError_t as int (0 = success); fddm_error_string() describes it.
- *  - Randomness: counter-based (seed, stream, element index) splitmix64 — see oracle/fddm_oracle.py.
+ *  - Randomness: counter-based (seed, stream, element index) splitmix64 — see oracle/fddm_oracle.py; the
+ *    attention-probability dropout draws from per-(b, h) splitmix64 tables with per-row offsets (contract v2,
+ *    oracle attn_dropout_keep).
  */
 #ifndef FDDM_HIP_H
 #define FDDM_HIP_H
@@ -168,6 +170,25 @@ int fddm_adamw(const long* chunk_tensor, const long* chunk_start, const long* nu
                const float* const* g, float* const* m, float* const* v, unsigned short* const* pbf,
                float* const* step, long ntensors, long nchunks, const float* total, float max_norm, float lr,
                float lr_wd, float b1, float b2, float eps, int* skipped, void* hip_stream);
+
+/* ---- small per-batch ops (rows = the batch, fp32): the decoder's conditioning path and the KL reduction.
+ *      rows_mean: out[b][j] = mean_s x[b][s][j] — the pooled condition of FiLM (models/denoise_decoder.py:185).
+ *      time_embed: SinusoidalTimeEmbedding features (models/denoise_decoder.py:108-116).
+ *      small_linear: for each of njobs weight sets, out_j = act(in W_j^T + b_j) (transpose_w: in W_j), act 0 none,
+ *        1 out = pre and out2 = silu(pre), 2 out = acc * silu'(aux) — the time MLP and FiLM Linears
+ *        (models/denoise_decoder.py:89,98-100,274) and their input gradients; njobs <= 16.
+ *      small_dw: dW_j += dy_j^T x_j, db_j += colsum(dy_j) over R rows — their weight gradients.
+ *      kl_reduce: SchedulerAdapter.kl_term's masked mean over L and mean over B of kl_tok (train.py:247-253),
+ *        plus w = d loss / d kl_tok for the closed-form gradient; mask may be NULL (plain mean). */
+int fddm_rows_mean(int dtype, const void* x, float* out, long B, long S, long d, void* hip_stream);
+int fddm_time_embed(const long* t, float* emb, long B, long d, float max_steps, void* hip_stream);
+int fddm_small_linear(const float* in, long ldi, int njobs, const float* const* W, const float* const* bias,
+                      float* const* out, float* const* out2, long ldw, long ldo, const float* aux, long R, long N, long K,
+                      int act, int transpose_w, void* hip_stream);
+int fddm_small_dw(int njobs, const float* const* dy, const long* lddy, const float* const* x, const long* ldx,
+                  float* const* dW, float* const* db, const long* N, const long* K, long R, void* hip_stream);
+int fddm_kl_reduce(const float* kl_tok, const unsigned char* mask, float* w, float* loss, long B, long L,
+                   void* hip_stream);
 
 /* ---- jumpy sampler denoise step (sampler/jumpy_sampler.py:167-215 + q_posterior_multi_step,
  *      fddm/sched/diffusion_scheduler.py:106-208): x_next = argmax (or a tempered draw) of the

@@ -46,6 +46,34 @@ def dropout_keep(seed: int, stream: int, numel: int, p: float) -> torch.Tensor:
     return torch.from_numpy(u >= np.uint64(thr))
 
 
+ATTN_R = 4096
+_ATTN_TAB0 = np.uint64(1 << 62)
+_ATTN_OFF0 = np.uint64(3 << 62)
+
+
+def attn_dropout_keep(seed: int, stream: int, B: int, H: int, Lq: int, Lk: int, p: float) -> torch.Tensor:
+    """Keep-mask [B, H, Lq, Lk] of the attention-probability dropout (RNG contract v2, the dropout on
+    softmax(QK^T) inside nn.MultiheadAttention, models/denoise_decoder.py:129-130; csrc/attention.hip).
+    Per (b, h) = bh three tables of R = 4096 16-bit draws, T_tau[j] = bits 16*(j&3).. of
+    mix64(seed, stream, 2^62 + (bh*3 + tau)*1024 + (j>>2)); per query row r = bh*Lq + q three offsets
+    o_tau = (mix64(seed, stream, 3*2^62 + r) >> 16*tau) & 0xFFC; element (q, k) keeps iff
+    T_0[(o_0+k)%R] ^ T_1[(o_1+k)%R] ^ T_2[(o_2+k)%R] >= round(p*65536)."""
+    thr = int(round(p * 65536.0))
+    BH = B * H
+    words = mix64(seed, stream, _ATTN_TAB0 + np.arange(BH * 3 * (ATTN_R // 4), dtype=np.uint64))
+    shifts = (np.uint64(16) * np.arange(4, dtype=np.uint64))
+    tab = ((words[:, None] >> shifts[None, :]) & np.uint64(0xFFFF)).reshape(BH, 3, ATTN_R)     # [BH, 3, R]
+    rows = np.arange(BH * Lq, dtype=np.uint64)
+    off = mix64(seed, stream, _ATTN_OFF0 + rows).reshape(BH, Lq)
+    k = np.arange(Lk, dtype=np.int64)
+    u = np.zeros((BH, Lq, Lk), dtype=np.uint64)
+    for tau in range(3):
+        o = ((off >> np.uint64(16 * tau)) & np.uint64(0xFFC)).astype(np.int64)                  # [BH, Lq]
+        j = (o[:, :, None] + k[None, None, :]) % ATTN_R
+        u ^= np.take_along_axis(tab[:, tau, :], j.reshape(BH, -1), axis=1).reshape(BH, Lq, Lk)
+    return torch.from_numpy(u >= np.uint64(thr)).view(B, H, Lq, Lk)
+
+
 # ------------------------------------------------------------------------------------------------
 # Scheduler — fddm/sched/diffusion_scheduler.py:18-29 (cosine betas, cumprod alpha_bar, fp32)
 # ------------------------------------------------------------------------------------------------
@@ -186,7 +214,7 @@ def mha(q_in, k_in, v_in, W, bias, Wo, bo, H, key_keep=None, drop_p=0.0, drop=No
         s = s.masked_fill(~key_keep[:, None, None, :], float("-inf"))
     p = torch.softmax(s, -1)
     if drop is not None and drop_p > 0:
-        p = drop(p)
+        p = drop.attn(p)
     o = (p @ v).transpose(1, 2).reshape(B, Lq, d)
     return F.linear(o, Wo, bo)
 
@@ -203,6 +231,15 @@ class _Dropper:
             return x
         keep = dropout_keep(self.seed, self.site, x.numel(), self.p).view(x.shape)
         return x * keep.float() * (1.0 / (1.0 - self.p))
+
+    def attn(self, p: torch.Tensor) -> torch.Tensor:
+        """Attention-probability site (p [B, H, Lq, Lk]): RNG contract v2 (attn_dropout_keep)."""
+        self.site += 1
+        if self.p <= 0:
+            return p
+        B, H, Lq, Lk = p.shape
+        keep = attn_dropout_keep(self.seed, self.site, B, H, Lq, Lk, self.p)
+        return p * keep.to(p.dtype) * (1.0 / (1.0 - self.p))
 
 
 def decoder_block(sd, pre, x, cond, x_mask, cos, sin, H, drop: Optional[_Dropper] = None, c_mask=None):

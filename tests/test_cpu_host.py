@@ -196,3 +196,24 @@ def test_wavlm_checkpoint_loading_maps_legacy_names_strictly(tmp_path):
     with pytest.raises(RuntimeError, match="does not match"):
         WavLMModel.from_pretrained(str(bad))
     assert WavLMModel.from_pretrained("microsoft/wavlm-large").random_init
+
+
+def test_attention_dropout_contract_v2():
+    """Attention-probability dropout draws (oracle attn_dropout_keep, csrc/attention.hip): keep rate 1 - p, rows
+    and heads with different masks, no row a shifted copy of another, seeds and streams independent."""
+    B, H, Lq, Lk, p = 2, 3, 64, 300, 0.1
+    k = O.attn_dropout_keep(11, 1, B, H, Lq, Lk, p)
+    assert k.shape == (B, H, Lq, Lk) and k.dtype == torch.bool
+    assert abs(k.float().mean().item() - 0.9) < 0.01
+    flat = k.reshape(-1, Lk).numpy()
+    for r in range(0, flat.shape[0], 7):            # no row equals a shift of another (within the overlap)
+        for s in range(r + 1, min(flat.shape[0], r + 40)):
+            for d in (0, 4, 8):
+                a, b = flat[r, d:], flat[s, :Lk - d]
+                assert (a != b).mean() > 0.05
+    k2 = O.attn_dropout_keep(11, 3, B, H, Lq, Lk, p)
+    k3 = O.attn_dropout_keep(12, 1, B, H, Lq, Lk, p)
+    assert (k != k2).float().mean().item() > 0.1 and (k != k3).float().mean().item() > 0.1
+    # pairwise independence of neighbouring keys: P(both kept) ~ 0.81
+    both = (k[..., 1:] & k[..., :-1]).float().mean().item()
+    assert abs(both - 0.81) < 0.015

@@ -357,7 +357,7 @@ def _attn_ref(q, k, v, keep, p_drop, seed, stream, gate=None, table=None):
         s = s.masked_fill(~keep[:, None, None, :], float("-inf"))
     pr = torch.softmax(s, -1)
     if p_drop > 0:
-        m = O.dropout_keep(seed, stream, B * H * Lq * Lk, p_drop).view(B, H, Lq, Lk).double()
+        m = O.attn_dropout_keep(seed, stream, B, H, Lq, Lk, p_drop).double()
         pr = pr * m / (1 - p_drop)
     return pr @ v
 
@@ -703,3 +703,67 @@ def test_fused_adamw_follows_replaced_bf16_copies():
                 rt.wt(w)
             torch.cuda.synchronize()
             assert torch.equal(rt.wt(w), w.detach().to(torch.bfloat16)), f"step {step}"
+
+
+# ------------------------------------------------------------------------------ small per-batch ops
+def test_small_linear_and_dw_match_torch():
+    """csrc/small.hip: the time-MLP / FiLM Linears (one launch for several weight sets, SiLU fused, transposed
+    weights for input gradients, SiLU' fused) and their weight / bias gradients vs float64 torch."""
+    o = ops()
+    gen = torch.Generator().manual_seed(40)
+    R, K, N = 32, 96, 200
+    x = torch.randn(R, K, generator=gen)
+    Ws = [torch.randn(N, K, generator=gen) / 10 for _ in range(3)]
+    bs = [torch.randn(N, generator=gen) for _ in range(3)]
+    outs = [torch.empty(R, N, device=dev) for _ in range(3)]
+    o.small_linear(x.to(dev), [w.to(dev) for w in Ws], [b.to(dev) for b in bs], outs)
+    for w, b, out in zip(Ws, bs, outs):
+        close(out, x.double() @ w.double().T + b.double(), rtol=1e-5, what="small_linear")
+    pre, act = torch.empty(R, N, device=dev), torch.empty(R, N, device=dev)
+    o.small_linear(x.to(dev), [Ws[0].to(dev)], [bs[0].to(dev)], [pre], [act], act=1)
+    ref = x.double() @ Ws[0].double().T + bs[0].double()
+    close(pre, ref, rtol=1e-5, what="pre")
+    close(act, torch.nn.functional.silu(ref), rtol=1e-5, what="silu")
+    dy = torch.randn(R, N, generator=gen)
+    dx = torch.empty(R, K, device=dev)
+    o.small_linear(dy.to(dev), [Ws[1].to(dev)], None, [dx], transpose_w=True)
+    close(dx, dy.double() @ Ws[1].double(), rtol=1e-5, what="dx")
+    aux = torch.randn(R, K, generator=gen)
+    dxs = torch.empty(R, K, device=dev)
+    o.small_linear(dy.to(dev), [Ws[1].to(dev)], None, [dxs], act=2, aux=aux.to(dev), transpose_w=True)
+    sg = torch.sigmoid(aux.double())
+    close(dxs, (dy.double() @ Ws[1].double()) * sg * (1 + aux.double() * (1 - sg)), rtol=1e-5, what="dsilu")
+    dW = [torch.full((N, K), 0.5, device=dev) for _ in range(2)]
+    db = [torch.full((N,), 0.25, device=dev) for _ in range(2)]
+    xs = [torch.randn(R, K, generator=gen) for _ in range(2)]
+    dys = [torch.randn(R, N, generator=gen) for _ in range(2)]
+    o.small_dw([(dys[i].to(dev), xs[i].to(dev), dW[i], db[i]) for i in range(2)])
+    for i in range(2):
+        close(dW[i], 0.5 + dys[i].double().T @ xs[i].double(), rtol=1e-5, what="small_dw")
+        close(db[i], 0.25 + dys[i].double().sum(0), rtol=1e-5, what="small_db")
+
+
+def test_rows_mean_time_embed_kl_reduce():
+    o = ops()
+    gen = torch.Generator().manual_seed(41)
+    x = torch.randn(3, 37, 130, generator=gen)
+    for dt in (torch.float32, torch.bfloat16):
+        xd = x.to(dev, dt)
+        close(o.rows_mean(xd), xd.double().mean(1), rtol=1e-6, what=f"rows_mean {dt}")
+    t = torch.tensor([1, 7, 200, 55])
+    # sin/cos of t * f with t up to T = 200: a 1-ulp difference of f between the device expf and the CPU's exp
+    # moves the argument by up to 200 * 6e-8, hence the 3e-5 absolute tolerance
+    close(o.time_embed(t.to(dev), 512, 10000), O.time_embedding(t, 512), rtol=0, atol=3e-5, what="time_embed")
+    close(o.time_embed(t.to(dev), 129, 10000), O.time_embedding(t, 129), rtol=0, atol=3e-5, what="time_embed odd")
+    B, L = 5, 70
+    kl = torch.rand(B * L, generator=gen)
+    m = torch.rand(B, L, generator=gen) > 0.3
+    m[3] = False                                  # an all-pad row: per = 0 / (0 + eps)
+    loss, w = o.kl_reduce(kl.to(dev), m.reshape(-1).to(dev).view(torch.uint8), B, L)
+    v = m.double()
+    per = (kl.view(B, L).double() * v).sum(1) / (v.sum(1) + 1e-8)
+    close(loss, per.mean(), rtol=1e-6, what="kl_reduce loss")
+    close(w.view(B, L), v / (v.sum(1, keepdim=True) + 1e-8) / B, rtol=1e-6, what="kl_reduce w")
+    loss2, w2 = o.kl_reduce(kl.to(dev), None, B, L)
+    close(loss2, kl.double().mean(), rtol=1e-6, what="kl_reduce unmasked")
+    close(w2, torch.full((B * L,), 1.0 / (B * L)), rtol=1e-6, what="kl_reduce unmasked w")

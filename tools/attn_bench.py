@@ -46,12 +46,14 @@ def main():
         f = lambda: ops.attn_fwd(q, k, v, o, lse, B, H, Lq, Lk, key_keep=keep, gate=gate, table=table,  # noqa
                                  drop_p=p, seed=1, rng_stream=1, dbits=db)
         fl = 4.0 * B * H * Lq * Lk * 64
-        t2 = timeit(f)
-        os.environ["FDDM_ATTN_V1"] = "1"
-        t1 = timeit(f)
-        del os.environ["FDDM_ATTN_V1"]
-        print(f"fwd {name:44s} v2 {t2*1e3:8.1f} us {fl/t2/1e9:7.1f} TF/s | v1 {t1*1e3:8.1f} us {fl/t1/1e9:7.1f} TF/s",
-              flush=True)
+        res = []
+        for tag, env in (("v3", {}), ("v3/4w", {"FDDM_ATTN_NW": "4"}), ("v2", {"FDDM_ATTN_V2": "1"})):
+            os.environ.update(env)
+            t = timeit(f)
+            for k_ in env:
+                del os.environ[k_]
+            res.append(f"{tag} {t*1e3:7.1f} us {fl/t/1e9:6.1f} TF/s")
+        print(f"fwd {name:44s} " + " | ".join(res), flush=True)
         if not rel:
             do = torch.randn_like(o)
             dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
