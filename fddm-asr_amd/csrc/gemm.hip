@@ -643,6 +643,32 @@ static int dispatch_layout(int a_kc, int b_kc, int epi, int out_dtype, const Gem
   return dispatch_epi<T, TA, false, true>(epi, out_dtype, g, s, nz);
 }
 
+// f32 [M][N] sub-matrix (row stride ldc) := 0 — the split-K pre-zero. A kernel on the launch stream, not
+// hipMemset2DAsync: captured into a HIP graph, the memset node did not stay ordered before the accumulating
+// GEMM on replays (the frozen encoder's graph, fddm_hip/graphs.py, read partially zeroed outputs).
+__global__ void __launch_bounds__(256) zero2d_kernel(float* __restrict__ C, long ldc, long M, long N) {
+  const long n4 = N / 4, per_row = n4 + (N & 3);
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < M * per_row; i += (long)gridDim.x * 256) {
+    const long m = i / per_row, j = i - m * per_row;
+    float* row = C + m * ldc;
+    if (j < n4 && !(((uintptr_t)row) & 15)) {
+      *(float4*)(row + 4 * j) = make_float4(0.f, 0.f, 0.f, 0.f);
+    } else if (j < n4) {
+      row[4 * j] = 0.f; row[4 * j + 1] = 0.f; row[4 * j + 2] = 0.f; row[4 * j + 3] = 0.f;
+    } else {
+      row[4 * n4 + (j - n4)] = 0.f;
+    }
+  }
+}
+
+static hipError_t zero2d(float* C, long ldc, long M, long N, hipStream_t s) {
+  const long work = M * (N / 4 + (N & 3));
+  if (work <= 0) return hipSuccess;
+  const unsigned grid = (unsigned)std::min<long>((work + 255) / 256, 2048);
+  hipLaunchKernelGGL(zero2d_kernel, dim3(grid), dim3(256), 0, s, C, ldc, M, N);
+  return hipGetLastError();
+}
+
 }  // namespace fddm
 
 using namespace fddm;
@@ -698,7 +724,7 @@ FDDM_API int fddm_gemm(int dtype, int a_dtype, int a_kc, int b_kc, int epi, int 
   if (colsum) {
     if (a_kc || a_dtype != dtype) return (int)hipErrorInvalidValue;
     if (epi != EPI_ACC_F32) {  // colsum follows C: overwritten by STORE, accumulated by ACC
-      hipError_t e = hipMemsetAsync(colsum, 0, M * sizeof(float), (hipStream_t)hip_stream);
+      hipError_t e = zero2d(colsum, M, 1, M, (hipStream_t)hip_stream);
       if (e != hipSuccess) return (int)e;
     }
     g.colsum = colsum;
@@ -724,7 +750,7 @@ FDDM_API int fddm_gemm(int dtype, int a_dtype, int a_kc, int b_kc, int epi, int 
         nz128 = (int)((K + ks - 1) / ks);
         g.ksplit = ks;
         if (epi == EPI_STORE) {
-          hipError_t e = hipMemset2DAsync(C, ldc * sizeof(float), 0, N * sizeof(float), M, s);
+          hipError_t e = zero2d((float*)C, ldc, M, N, s);
           if (e != hipSuccess) return (int)e;
           epi = EPI_ACC_F32;
         }
@@ -749,7 +775,7 @@ FDDM_API int fddm_gemm(int dtype, int a_dtype, int a_kc, int b_kc, int epi, int 
       nz = (int)((K + ks - 1) / ks);
       g.ksplit = ks;
       if (epi == EPI_STORE) {
-        hipError_t e = hipMemset2DAsync(C, ldc * sizeof(float), 0, N * sizeof(float), M, s);
+        hipError_t e = zero2d((float*)C, ldc, M, N, s);
         if (e != hipSuccess) return (int)e;
         epi = EPI_ACC_F32;
       }

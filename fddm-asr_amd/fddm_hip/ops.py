@@ -32,8 +32,14 @@ def ptr(t):
     return 0 if t is None else t.data_ptr()
 
 
+_raw_stream = torch._C._cuda_getCurrentRawStream
+_cur_device = torch._C._cuda_getDevice
+
+
 def stream():
-    return torch.cuda.current_stream().cuda_stream
+    """The current HIP stream of the current device as a raw handle (the launch path's hottest host call:
+    torch.cuda.current_stream() builds a Stream object and resolves the device index through Python)."""
+    return _raw_stream(_cur_device())
 
 
 def _chk(cond, msg):

@@ -51,13 +51,17 @@ class AcousticEncoder(nn.Module):
         if lengths is not None:
             raise NotImplementedError("lengths-masked encoding is not on the train step (train.py:349)")
         with torch.no_grad():
-            h = self.backbone.forward_hidden(waveforms)                  # [B, S, hidden] compute dtype
-            B, S, E = h.shape
-            if self.use_proj:
-                cd = rt.compute_dtype()
-                feats = ops.linear(h.view(B * S, E), rt.wt(self.proj.weight), self.proj.bias.detach(),
-                                   out_dtype=cd).view(B, S, -1)
-            else:
-                feats = h
+            feats = self.project(self.backbone.forward_hidden(waveforms))
         pooled = feats.float().mean(dim=1) if self.pooling == "mean" else None
         return feats, None, pooled
+
+    @torch.no_grad()
+    def project(self, h: torch.Tensor) -> torch.Tensor:
+        """encoder.proj (acoustic_encoder.py:107) on the backbone's [B, S, hidden] output (identity if hidden ==
+        d_model)."""
+        if not self.use_proj:
+            return h
+        B, S, E = h.shape
+        cd = rt.compute_dtype()
+        return ops.linear(h.view(B * S, E), rt.wt(self.proj.weight), self.proj.bias.detach(),
+                          out_dtype=cd).view(B, S, -1)

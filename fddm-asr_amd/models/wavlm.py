@@ -91,10 +91,25 @@ class WavLMModel(nn.Module):
         self.encoder = enc
         self._prep_key = None
         self._prep = None
+        self._plist = None
+        self._gen = 0
 
     # ------------------------------------------------------------------ prepared (cast/permuted) weights
+    def _apply(self, fn, *a, **k):     # .to() / .cuda() / .half(): new storage -> re-prepare
+        self._gen += 1
+        self._plist = None
+        return super()._apply(fn, *a, **k)
+
+    def _load_from_state_dict(self, *a, **k):
+        self._gen += 1
+        return super()._load_from_state_dict(*a, **k)
+
     def _prepared(self, cd):
-        key = (cd,) + tuple((p.data_ptr(), p._version) for p in self.parameters())
+        # the encoder is frozen: its prepared (cast / permuted) weights are rebuilt when the module is moved or
+        # loaded (_gen) or a parameter is changed in place (the versions, summed over a cached parameter list)
+        if self._plist is None:
+            self._plist = list(self.parameters())
+        key = (cd, self._gen, sum(p._version for p in self._plist))
         if self._prep_key == key:
             return self._prep
         c = self.config
@@ -155,29 +170,53 @@ class WavLMModel(nn.Module):
             T = (T - k) // s + 1
         return T
 
+    # The forward in three stages (the conv-layer-1 launch on its own, so a HIP-graph replay of the other two keeps
+    # the benchmark's probe of that dominant launch an ordinary timed launch: fddm_hip/graphs.py)
     @torch.no_grad()
-    def forward_hidden(self, wave: torch.Tensor) -> torch.Tensor:
-        """last_hidden_state [B, S, E] in the compute dtype (eval mode, attention_mask=None)."""
+    def stage_conv0(self, wave: torch.Tensor) -> torch.Tensor:
+        """conv layer 0 + GroupNorm + GELU (HF:723-744) -> [B, T0, C] compute dtype."""
         c = self.config
         cd = rt.compute_dtype()
         P = self._prepared(cd)
         wave = wave.float().contiguous()
-        B, nsamp = wave.shape
-        # conv feature extractor (HF:747-782)
-        h = ops.conv0_gn_gelu(wave, P["w0"], P["gn"][0], P["gn"][1], cd, c.conv_dim[0], c.conv_kernel[0],
-                              c.conv_stride[0])
-        T = h.shape[1]
-        cin = c.conv_dim[0]
-        for i in range(1, len(c.conv_dim)):
-            k, s, co = c.conv_kernel[i], c.conv_stride[i], c.conv_dim[i]
-            Tout = (T - k) // s + 1
-            out = torch.empty(B, Tout, co, device=wave.device, dtype=cd)
-            with rt.probe(f"wavlm.conv{i}"):
-                ops.conv1d_gemm(h, P["conv"][i - 1], out, lda=cin, sAb=T * cin, Tin=T, Cg=cin, cstride=s, cpad=0,
-                                Bn=B, Tout=Tout, N=co, K=k * cin, gelu=True)
-            h, T, cin = out, Tout, co
+        return ops.conv0_gn_gelu(wave, P["w0"], P["gn"][0], P["gn"][1], cd, c.conv_dim[0], c.conv_kernel[0],
+                                 c.conv_stride[0])
+
+    def conv_out_shape(self, h):
+        c = self.config
+        B, T, _ = h.shape
+        return B, (T - c.conv_kernel[1]) // c.conv_stride[1] + 1, c.conv_dim[1]
+
+    @torch.no_grad()
+    def stage_conv1(self, h: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        """conv layer 1 + GELU as an implicit GEMM (HF:747-782), the step's largest MFMA launch."""
+        return self._conv(h, 1, out)
+
+    def _conv(self, h, i, out=None):
+        c = self.config
+        P = self._prepared(rt.compute_dtype())
+        B, T, cin = h.shape
+        k, s, co = c.conv_kernel[i], c.conv_stride[i], c.conv_dim[i]
+        Tout = (T - k) // s + 1
+        if out is None:
+            out = torch.empty(B, Tout, co, device=h.device, dtype=h.dtype)
+        with rt.probe(f"wavlm.conv{i}"):
+            ops.conv1d_gemm(h, P["conv"][i - 1], out, lda=cin, sAb=T * cin, Tin=T, Cg=cin, cstride=s, cpad=0, Bn=B,
+                            Tout=Tout, N=co, K=k * cin, gelu=True)
+        return out
+
+    @torch.no_grad()
+    def stage_rest(self, h: torch.Tensor) -> torch.Tensor:
+        """conv layers 2..6, feature projection, positional conv, 12 transformer layers -> [B, S, E]."""
+        c = self.config
+        cd = rt.compute_dtype()
+        P = self._prepared(cd)
+        for i in range(2, len(c.conv_dim)):
+            h = self._conv(h, i)
+        B, T, cin = h.shape
         S, E, H = T, c.hidden_size, c.num_attention_heads
         eps = c.layer_norm_eps
+        dev = h.device
         # feature projection (HF:93-105)
         h2 = h.view(B * S, cin)
         hn = torch.empty_like(h2)
@@ -187,7 +226,7 @@ class WavLMModel(nn.Module):
         G = c.num_conv_pos_embedding_groups
         Cg = E // G
         kp = c.num_conv_pos_embeddings
-        pos = torch.empty(B * S, E, device=wave.device, dtype=cd)
+        pos = torch.empty(B * S, E, device=dev, dtype=cd)
         if cd == torch.bfloat16 and Cg % 16 == 0 and Cg <= 64:
             ops.posconv_gelu(x, P["pos"][0], P["pos"][1], pos, B, S, E, G, kp)   # whole-window LDS kernel
         else:
@@ -200,7 +239,7 @@ class WavLMModel(nn.Module):
                                  c.max_bucket_distance)
         for Lp in P["layers"]:
             qkv = ops.linear(x, Lp["qkv"], Lp["bqkv"], out_dtype=cd)
-            o = torch.empty(B * S, E, device=wave.device, dtype=cd)
+            o = torch.empty(B * S, E, device=dev, dtype=cd)
             if cd == torch.bfloat16:
                 ops.attn_fwd_relgate(qkv, qkv[:, E:], qkv[:, 2 * E:], o, qkv[:, 3 * E:], Lp["gru"][2], table, B, H, S)
             else:
@@ -214,6 +253,11 @@ class WavLMModel(nn.Module):
             x = torch.empty_like(x1)
             ops.ln_fwd(x1, y, Lp["ln2"][0], Lp["ln2"][1], out_t=x, eps=eps)
         return x.view(B, S, E)
+
+    @torch.no_grad()
+    def forward_hidden(self, wave: torch.Tensor) -> torch.Tensor:
+        """last_hidden_state [B, S, E] in the compute dtype (eval mode, attention_mask=None)."""
+        return self.stage_rest(self.stage_conv1(self.stage_conv0(wave)))
 
     def forward(self, input_values, attention_mask=None, output_hidden_states=False, **kw):
         if attention_mask is not None:

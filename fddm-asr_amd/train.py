@@ -15,6 +15,7 @@ import argparse
 import logging
 import os
 import random
+import weakref
 from dataclasses import dataclass
 from datetime import datetime
 
@@ -26,6 +27,7 @@ from fddm_hip import dist as fdist
 from fddm_hip import functions as FN
 from fddm_hip import runtime as rt
 from fddm_hip._lib import lib as _fddm_lib
+from fddm_hip.graphs import GraphedEncoder
 from fddm_hip.optim import FusedAdamW
 from losses.fddm_losses import lfd_loss
 from models.acoustic_encoder import AcousticEncoder
@@ -120,6 +122,13 @@ def _encoded(encoder, loader, device, optimizer):
     # persistent encoder GEMMs on 3/4 of the CUs (measured: 192 of 256 beats 256, 224, 208, 176 and 160)
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
     enc_cus = int(os.environ.get("FDDM_ENC_CUS", ncu * 3 // 4))
+    # HIP-graph replay of the encoder forward (fddm_hip.graphs): the host launch path, not the GPU, bounded the step
+    graphs = None
+    if os.environ.get("FDDM_ENC_GRAPH", "1") != "0" and GraphedEncoder.supported(encoder):
+        graphs = _ENC_GRAPHS.get(encoder)
+        if graphs is None:
+            graphs = _ENC_GRAPHS[encoder] = GraphedEncoder(encoder)
+    nbatch = [0]
 
     def launch(batch):
         wave, x0 = batch
@@ -129,7 +138,11 @@ def _encoded(encoder, loader, device, optimizer):
         prev = _fddm_lib().fddm_gemm_persistent_cap(enc_cus)
         try:
             with torch.cuda.stream(side):
-                c, c_mask, _ = encoder(wave)
+                if graphs is not None:
+                    c, c_mask = graphs.run(wave, nbatch[0] % 2, enc_cus), None
+                else:
+                    c, c_mask, _ = encoder(wave)
+            nbatch[0] += 1
         finally:
             _fddm_lib().fddm_gemm_persistent_cap(prev)
         with torch.cuda.stream(side):
@@ -153,6 +166,7 @@ def _encoded(encoder, loader, device, optimizer):
 
 
 _ENC_STREAMS: dict = {}
+_ENC_GRAPHS = weakref.WeakKeyDictionary()     # encoder -> GraphedEncoder (released with the encoder)
 
 
 def _enc_stream(dev):

@@ -122,7 +122,7 @@ def _run(cfg_name, prec, monkeypatch):
     final = {("decoder." + n): p.detach().cpu() for n, p in dec.named_parameters()}
     for pre, m in (("s_proj.", sp), ("t_embed.", te), ("t_proj.", tp)):
         final.update({pre + n: p.detach().cpu() for n, p in m.named_parameters()})
-    got = dict(kl=[float(v) for v in rec["kl"]], lfd=float(rec["lfd"][0]), final=final, grads=step_grads)
+    got = dict(kl=[float(v.detach()) for v in rec["kl"]], lfd=float(rec["lfd"][0].detach()), final=final, grads=step_grads)
     del enc, dec, sp, te, tp, opt
     torch.cuda.empty_cache()
     # ---- CPU oracle: the same two steps
