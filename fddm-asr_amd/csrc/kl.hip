@@ -345,6 +345,187 @@ __global__ void __launch_bounds__(NT) kl4_kernel(const float* __restrict__ logit
   }
 }
 
+// Fused forward + gradient (the train step's KL): ONE read of the fp32 logits row yields kl_tok[row] and the
+// row's logits gradient w[row] * d kl_tok / d z (w = d loss / d kl_tok of the masked mean, computed here from the
+// utterance's mask row: mask / (count + 1e-8) / B, or 1 / (L B) without a mask — kl_reduce's weights). The
+// upstream scalar is applied afterwards by fddm_scale_if, which returns without touching memory when it is 1
+// (the train step: loss = kl + ...). 393 MB of HBM per step at V = 8000, B*L = 8192 (f32 in, bf16 out) instead of
+// 262 + 393 MB for the separate forward and backward passes.
+__device__ __forceinline__ float4 block_sum4(float a, float b, float c, float d, float* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o, 64);
+    b += __shfl_xor(b, o, 64);
+    c += __shfl_xor(c, o, 64);
+    d += __shfl_xor(d, o, 64);
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if (lane == 0) { red[4 * w] = a; red[4 * w + 1] = b; red[4 * w + 2] = c; red[4 * w + 3] = d; }
+  __syncthreads();
+  float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int i = 0; i < nw; ++i) { r.x += red[4 * i]; r.y += red[4 * i + 1]; r.z += red[4 * i + 2]; r.w += red[4 * i + 3]; }
+  return r;
+}
+
+template <int NV, typename OT, int NT>
+__global__ void __launch_bounds__(NT) kl4_fused_kernel(const float* __restrict__ logits, const long* __restrict__ xt_,
+                                                        const long* __restrict__ x0_, const long* __restrict__ t_,
+                                                        const float* __restrict__ betas,
+                                                        const unsigned char* __restrict__ mask,
+                                                        float* __restrict__ kl_tok, OT* __restrict__ dz, long L, long V,
+                                                        long B) {
+  __shared__ float red[2 * (NT / 64) + 4 * (NT / 64)];
+  const long row = blockIdx.x;
+  const int tid = threadIdx.x;
+  const float* z = logits + row * V;
+  const long V4 = V >> 2;
+  const long xt = xt_[row], x0 = x0_[row], b = row / L, tv = t_[b];
+  const float eps = 1e-8f;
+  const KlRow c = kl_consts(betas, tv, xt, x0, (float)V);
+  const float zxt = z[xt], zx0 = z[x0];
+
+  float v[NV][4];
+  float mt = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const long q = tid + (long)NT * i;
+    float4 f = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+    if (q < V4) f = *(const float4*)(z + 4 * q);
+    v[i][0] = f.x; v[i][1] = f.y; v[i][2] = f.z; v[i][3] = f.w;
+    mt = fmaxf(mt, fmaxf(fmaxf(f.x, f.y), fmaxf(f.z, f.w)));
+  }
+  float st_ = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[i][j] = (mt == -INFINITY) ? 0.f : __expf(v[i][j] - mt);
+      st_ += v[i][j];
+    }
+  const float2 ms = block_maxsum(mt, st_, red);
+  const float mx = ms.x, inv_s = 1.f / ms.y;
+  const float resc = (mt == -INFINITY) ? 0.f : __expf(mt - mx) * inv_s;
+  const float xhat_xt = __expf(zxt - mx) * inv_s;
+  const float xhat_x0 = __expf(zx0 - mx) * inv_s;
+  const float dp = c.b_t + c.a_t * xhat_xt;
+  const float inv_dp = 1.f / (dp + eps);
+  const float Qg = c.b_t * c.b_p * c.inv_dq;
+  const float LQg = __logf(Qg + eps);
+  auto special = [&](long k, float xh, float& P, float& Q, float& M) {
+    M = c.b_t + (k == xt ? c.a_t : 0.f);
+    Q = M * ((k == x0 ? c.a_p : 0.f) + c.b_p) * c.inv_dq;
+    P = M * (c.a_p * xh + c.b_p) * inv_dp;
+  };
+  const float pa = c.b_t * c.a_p * inv_dp, pb = c.b_t * c.b_p * inv_dp;
+  const long ks[2] = {xt, x0};
+  const float xs[2] = {xhat_xt, xhat_x0};
+  const int nsp = (xt == x0) ? 1 : 2;
+
+  // one row pass: the KL's generic log terms and the gradient's two sums; the mask count of this utterance rides
+  // in the same block reduction
+  float acc = 0.f, a1 = 0.f, a2 = 0.f, cnt = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const bool ok = tid + (long)NT * i < V4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float xh = v[i][j] * resc;
+      v[i][j] = xh;
+      const float P = fmaf(pa, xh, pb);
+      const float r = __builtin_amdgcn_rcpf(P + eps);
+      if (ok) {
+        acc += LQg - __logf(P + eps);
+        a1 += P * r;
+        a2 += xh * r;
+      }
+    }
+  }
+  if (mask)
+    for (long l = tid; l < L; l += NT) cnt += mask[b * L + l] ? 1.f : 0.f;
+  const float4 sums = block_sum4(acc, a1, a2, cnt, red + 2 * (NT / 64));
+  if (tid == 0) {
+    float kl = Qg * sums.x;
+    for (int j = 0; j < nsp; ++j) {
+      float P, Q, M;
+      special(ks[j], xs[j], P, Q, M);
+      kl += Q * (__logf(Q + eps) - __logf(P + eps)) - Qg * (LQg - __logf(fmaf(pa, xs[j], pb) + eps));
+    }
+    kl_tok[row] = kl;
+  }
+  const float gc = -Qg * c.b_t * c.a_p * inv_dp;
+  float s1 = Qg * sums.y, g0s = gc * sums.z;
+  for (int j = 0; j < nsp; ++j) {
+    float P, Q, M;
+    special(ks[j], xs[j], P, Q, M);
+    const float Pg = fmaf(pa, xs[j], pb);
+    s1 += Q * P / (P + eps) - Qg * Pg / (Pg + eps);
+    g0s += -Q * M * c.a_p / (P + eps) * inv_dp * xs[j] - gc * xs[j] / (Pg + eps);
+  }
+  const float gxt = c.a_t * s1 * inv_dp;
+  const float G = g0s + xhat_xt * gxt;
+  const float wr = mask ? ((mask[row] ? 1.f : 0.f) / (sums.w + eps) / (float)B) : 1.f / ((float)L * (float)B);
+  OT* out = dz + row * V;
+  const int qxt = (int)(xt >> 2), qx0 = (int)(x0 >> 2), iv4 = (int)V4;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int q = tid + NT * i;
+    if (q < iv4) {
+      float o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = wr * v[i][j] * (gc * __builtin_amdgcn_rcpf(fmaf(pa, v[i][j], pb) + eps) - G);
+      if (q == qxt || q == qx0) {
+        for (int j = 0; j < 4; ++j) {
+          const long k = 4L * q + j;
+          if (k == xt || k == x0) {
+            float P, Q, M;
+            special(k, v[i][j], P, Q, M);
+            const float g = -Q * M * c.a_p / (P + eps) * inv_dp + (k == xt ? gxt : 0.f);
+            o[j] = wr * v[i][j] * (g - G);
+          }
+        }
+      }
+      st4<OT>(out + 4 * q, o[0], o[1], o[2], o[3]);
+    }
+  }
+}
+
+// x *= g[0] unless g[0] == 1 (then no memory is touched): the upstream gradient of a fused forward+gradient pass
+template <typename T>
+__global__ void __launch_bounds__(256) scale_if_kernel(T* __restrict__ x, const float* __restrict__ g, long n) {
+  const float s = g[0];
+  if (s == 1.f) return;
+  const long n8 = n / 8;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
+    if constexpr (sizeof(T) == 2) {
+      uint4 u = ((uint4*)x)[i];
+      unsigned* w = (unsigned*)&u;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float lo = __uint_as_float(w[k] << 16) * s, hi = __uint_as_float(w[k] & 0xffff0000u) * s;
+        w[k] = pk_bf16(lo, hi);
+      }
+      ((uint4*)x)[i] = u;
+    } else {
+      float4* p = (float4*)x + 2 * i;
+      float4 a = p[0], c = p[1];
+      a.x *= s; a.y *= s; a.z *= s; a.w *= s;
+      c.x *= s; c.y *= s; c.z *= s; c.w *= s;
+      p[0] = a;
+      p[1] = c;
+    }
+  }
+  for (long i = 8 * n8 + blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    if constexpr (sizeof(T) == 2) {
+      unsigned short* h = (unsigned short*)x;
+      const float f = __uint_as_float(((unsigned)h[i]) << 16) * s;
+      h[i] = (unsigned short)(pk_bf16(f, 0.f) & 0xffffu);
+    } else {
+      x[i] *= s;
+    }
+  }
+}
+
 // softmax over rows of length V (fp32 in) -> T out
 template <int NPT, typename OT>
 __global__ void __launch_bounds__(256) softmax_rows_kernel(const float* __restrict__ x, OT* __restrict__ y, long V) {
@@ -520,4 +701,42 @@ FDDM_API int fddm_softmax_bwd_rows(const void* y, const void* dy, float* dz, int
   SMB_DISPATCH(32)
   SMB_DISPATCH(64)
   return (int)hipErrorInvalidValue;
+}
+
+#define KLF_DISPATCH(NV)                                                                                           \
+  if (V <= 2048L * NV) {                                                                                          \
+    if (dz_dtype == FDDM_BF16)                                                                                    \
+      hipLaunchKernelGGL((kl4_fused_kernel<NV, bf16_t, 512>), dim3((unsigned)N), dim3(512), 0, s, logits, xt, x0, \
+                         t, betas, mask, kl_tok, (bf16_t*)dz, L, V, N / L);                                       \
+    else                                                                                                          \
+      hipLaunchKernelGGL((kl4_fused_kernel<NV, float, 512>), dim3((unsigned)N), dim3(512), 0, s, logits, xt, x0,  \
+                         t, betas, mask, kl_tok, (float*)dz, L, V, N / L);                                        \
+    return (int)hipGetLastError();                                                                                \
+  }
+
+// kl_tok[N] and dz[N][V] = w * d kl_tok / d logits in one pass (w: the masked-mean weights of fddm_kl_reduce)
+FDDM_API int fddm_kl_fused(const float* logits, const long* xt, const long* x0, const long* t, const float* betas,
+                           const unsigned char* mask, float* kl_tok, void* dz, int dz_dtype, long N, long L, long V,
+                           void* hs) {
+  if (N <= 0) return 0;
+  if (L <= 0 || N % L || V % 4 || (((uintptr_t)logits) & 15) || (((uintptr_t)dz) & 15)) return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)hs;
+  KLF_DISPATCH(1)
+  KLF_DISPATCH(4)
+  KLF_DISPATCH(8)
+  KLF_DISPATCH(16)
+  return (int)hipErrorInvalidValue;
+}
+
+// x[n] *= g[0] on the device, skipped (no memory traffic) when g[0] == 1
+FDDM_API int fddm_scale_if(void* x, int dtype, const float* g, long n, void* hs) {
+  if (n <= 0) return 0;
+  if (((uintptr_t)x) & 15) return (int)hipErrorInvalidValue;
+  const long want = (n / 8 + 255) / 256 + 1;
+  const unsigned grid = (unsigned)(want < 4096 ? want : 4096);
+  if (dtype == FDDM_BF16)
+    hipLaunchKernelGGL(scale_if_kernel<bf16_t>, dim3(grid), dim3(256), 0, (hipStream_t)hs, (bf16_t*)x, g, n);
+  else
+    hipLaunchKernelGGL(scale_if_kernel<float>, dim3(grid), dim3(256), 0, (hipStream_t)hs, (float*)x, g, n);
+  return (int)hipGetLastError();
 }

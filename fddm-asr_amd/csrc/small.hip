@@ -178,10 +178,11 @@ __global__ void __launch_bounds__(1024) kl_reduce_kernel(const float* __restrict
     s = wave_sum(s);
     m = wave_sum(m);
     const float den = mask ? m + eps : (float)L;
-    for (long l = lane; l < L; l += 64) {
-      const float mv = mask ? (mask[b * L + l] ? 1.f : 0.f) : 1.f;
-      w[b * L + l] = mask ? mv / den / (float)B : 1.f / ((float)L * (float)B);
-    }
+    if (w)
+      for (long l = lane; l < L; l += 64) {
+        const float mv = mask ? (mask[b * L + l] ? 1.f : 0.f) : 1.f;
+        w[b * L + l] = mask ? mv / den / (float)B : 1.f / ((float)L * (float)B);
+      }
     if (lane == 0) per[b] = s / den;
   }
   __syncthreads();

@@ -405,34 +405,45 @@ class HeadFn(torch.autograd.Function):
 
 # -------------------------------------------------------------------------------------- KL term
 class KLFn(torch.autograd.Function):
-    """SchedulerAdapter.kl_term (train.py:190-255): fused closed-form KL; the exact gradient is
-    produced in backward by a second fused pass that reads the upstream scalar on the device."""
+    """SchedulerAdapter.kl_term (train.py:190-255): fused closed-form KL. With a gradient wanted, ONE pass over the
+    logits produces the per-token KL and its logits gradient (times the masked-mean weights); backward only applies
+    the upstream scalar on the device (ops.scale_if: nothing to do when it is 1, the train step's case)."""
 
     @staticmethod
     def forward(ctx, logits, xt, x0, t, mask_u8, betas):
         """mask_u8: x_mask as uint8 [B*L] (or None: plain mean over L, train.py:253)."""
         B, L, V = logits.shape
         l2 = logits.reshape(B * L, V)
-        kl_tok = ops.kl_fwd(l2, xt.reshape(-1).contiguous(), x0.reshape(-1).contiguous(), t.contiguous(), betas, L)
-        loss, w = ops.kl_reduce(kl_tok, mask_u8, B, L)       # masked mean over L, mean over B; w = dloss/dkl_tok
-        ctx.save_for_backward(l2, xt, x0, t, w, betas)
+        xf, x0f, tc = xt.reshape(-1).contiguous(), x0.reshape(-1).contiguous(), t.contiguous()
         ctx.shape = (B, L, V)
+        ctx.handover = None
+        if not ctx.needs_input_grad[0]:
+            kl_tok = ops.kl_fwd(l2, xf, x0f, tc, betas, L)
+            loss, _ = ops.kl_reduce(kl_tok, mask_u8, B, L, want_w=False)
+            return loss
+        # bf16 mode: the gradient goes to the live HeadFn that produced these logits, in bf16
+        ptr = l2.data_ptr()
+        ref = _head_outputs.get(ptr)
+        owner = ref() if ref is not None else None
+        bf = owner is not None and owner.data_ptr() == ptr and ptr not in _dlogits_bf16
+        kl_tok, dz = ops.kl_fused(l2.contiguous(), xf, x0f, tc, betas, mask_u8, L,
+                                  out_dtype=torch.bfloat16 if bf else F32)
+        loss, _ = ops.kl_reduce(kl_tok, mask_u8, B, L, want_w=False)
+        ctx.dz = dz
+        ctx.handover = ptr if bf else None
         return loss
 
     @staticmethod
     def backward(ctx, g):
-        l2, xt, x0, t, w, betas = ctx.saved_tensors
         B, L, V = ctx.shape
-        gs = g.reshape(1).to(F32).contiguous()
-        ptr = l2.data_ptr()
-        ref = _head_outputs.get(ptr)
-        owner = ref() if ref is not None else None
-        if owner is not None and owner.data_ptr() == ptr and ptr not in _dlogits_bf16:
-            # logits of a live bf16-mode HeadFn: hand it the gradient in bf16 (HeadFn.backward picks it up)
-            _dlogits_bf16[ptr] = ops.kl_bwd(l2, xt.reshape(-1).contiguous(), x0.reshape(-1).contiguous(),
-                                            t.contiguous(), betas, w, gs, L, out_dtype=torch.bfloat16)
-            return torch.zeros((), device=l2.device, dtype=F32).expand(B, L, V), None, None, None, None, None
-        dz = ops.kl_bwd(l2, xt.reshape(-1).contiguous(), x0.reshape(-1).contiguous(), t.contiguous(), betas, w, gs, L)
+        dz, ctx.dz = ctx.dz, None
+        ops.scale_if(dz, g.reshape(1).to(F32).contiguous())
+        if ctx.handover is not None:
+            ref = _head_outputs.get(ctx.handover)
+            if ref is not None and ref() is not None and ctx.handover not in _dlogits_bf16:
+                _dlogits_bf16[ctx.handover] = dz     # HeadFn.backward picks it up
+                return torch.zeros((), device=dz.device, dtype=F32).expand(B, L, V), None, None, None, None, None
+            dz = dz.float()
         return dz.view(B, L, V), None, None, None, None, None
 
 

@@ -324,6 +324,26 @@ def kl_bwd(logits2d, xt, x0, t, betas, w, gscale, L, out_dtype=torch.float32):
     return dz
 
 
+def kl_fused(logits2d, xt, x0, t, betas, mask_u8, L, out_dtype=torch.float32):
+    """(kl_tok [N] f32, dz [N, V]) in one pass: dz = w * d kl_tok / d logits with kl_reduce's weights w (from the
+    uint8 mask [N], or None = plain mean over L); the upstream gradient is applied later by scale_if."""
+    N, V = logits2d.shape
+    _chk(logits2d.dtype == torch.float32 and logits2d.is_contiguous() and N % L == 0, "kl_fused: f32 [B*L, V] rows")
+    _chk(mask_u8 is None or (mask_u8.numel() == N and mask_u8.dtype == torch.uint8), "kl_fused mask")
+    kl = torch.empty(N, device=logits2d.device, dtype=torch.float32)
+    dz = torch.empty(N, V, device=logits2d.device, dtype=out_dtype)
+    call("fddm_kl_fused", ptr(logits2d), ptr(xt), ptr(x0), ptr(t), ptr(betas), ptr(mask_u8), ptr(kl), ptr(dz),
+         code(dz), N, L, V, stream())
+    return kl, dz
+
+
+def scale_if(x, g):
+    """x *= g (a device scalar), in place; no memory traffic when g == 1."""
+    _chk(x.is_contiguous() and g.dtype == torch.float32 and g.numel() == 1, "scale_if operands")
+    call("fddm_scale_if", ptr(x), code(x), ptr(g), x.numel(), stream())
+    return x
+
+
 def softmax_rows(x2d, out_dtype):
     N, V = x2d.shape
     y = torch.empty(N, V, device=x2d.device, dtype=out_dtype)
@@ -465,12 +485,13 @@ def small_dw(jobs):
              _parr([j[3] for j in ch]), L(*[j[0].shape[1] for j in ch]), L(*[j[1].shape[1] for j in ch]), R, stream())
 
 
-def kl_reduce(kl_tok, mask_u8, B, L):
-    """Masked batch mean of the per-token KL (train.py:247-253) -> (loss f32 scalar, w [B*L] = d loss / d kl_tok)."""
+def kl_reduce(kl_tok, mask_u8, B, L, want_w=True):
+    """Masked batch mean of the per-token KL (train.py:247-253) -> (loss f32 scalar, w [B*L] = d loss / d kl_tok,
+    or None when not wanted)."""
     _chk(kl_tok.numel() == B * L and (mask_u8 is None or (mask_u8.numel() == B * L and mask_u8.dtype == torch.uint8)),
          "kl_reduce shapes")
     loss = torch.empty((), device=kl_tok.device, dtype=torch.float32)
-    w = torch.empty(B * L, device=kl_tok.device, dtype=torch.float32)
+    w = torch.empty(B * L, device=kl_tok.device, dtype=torch.float32) if want_w else None
     call("fddm_kl_reduce", ptr(kl_tok), ptr(mask_u8), ptr(w), ptr(loss), B, L, stream())
     return loss, w
 

@@ -136,6 +136,13 @@ int fddm_kl_fwd(const float* logits, const long* xt, const long* x0, const long*
 int fddm_kl_bwd(const float* logits, const long* xt, const long* x0, const long* t, const float* betas,
                 const float* w, const float* gscale, void* dz, int dz_dtype, long N, long L, long V,
                 void* hip_stream);
+/* the train step's form: kl_tok and dz = w * d kl_tok / d logits in one pass over the logits (w = the masked-mean
+ * weights of fddm_kl_reduce, from mask [N] uint8 or NULL = plain mean over L); the upstream scalar is applied by
+ * fddm_scale_if afterwards (no memory traffic when it is 1). */
+int fddm_kl_fused(const float* logits, const long* xt, const long* x0, const long* t, const float* betas,
+                  const unsigned char* mask, float* kl_tok, void* dz, int dz_dtype, long N, long L, long V,
+                  void* hip_stream);
+int fddm_scale_if(void* x, int dtype, const float* g, long n, void* hip_stream);
 
 /* ---- TextEmbedding softmax (models/projection.py:41-47) */
 int fddm_softmax_rows(const float* x, void* y, int out_dtype, long N, long V, void* hip_stream);

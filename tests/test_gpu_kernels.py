@@ -596,6 +596,41 @@ def test_kl_full_vocab_matches_oracle():
     assert err < 1e-4, f"kl grad V=8000 rel err {err:.2e}"
 
 
+def test_kl_fused_matches_oracle_and_scale_if():
+    """The train step's one-pass KL (kl_tok + w-weighted gradient, w from the mask in the kernel) vs the closed-form
+    oracle: loss within 1e-4, f32 gradient within 1e-4 of the max, bf16 gradient within bf16 rounding (2^-8
+    relative per element + 1e-4 of the max); unmasked (plain mean) too; scale_if applies g != 1, skips g == 1."""
+    o = ops()
+    K, Tn, B, L = 8000, 200, 4, 256
+    betas, _ = O.sched_tables(Tn)
+    logits = 3.0 * torch.randn(B, L, K, generator=g(73))
+    x0 = torch.randint(1, K, (B, L), generator=g(74))
+    xt = torch.randint(1, K, (B, L), generator=g(75))
+    xt[:, ::3] = x0[:, ::3]
+    t = torch.tensor([1, 2, 117, 200])
+    for masked in (True, False):
+        xm = torch.ones(B, L, dtype=torch.bool)
+        if masked:
+            xm[2, 200:] = False
+            xm[0, 17] = False
+        ref_loss, ref_dz = O.kl_term(logits, xt, x0, t, xm if masked else None, betas)
+        args = (logits.view(-1, K).to(dev), xt.reshape(-1).to(dev), x0.reshape(-1).to(dev), t.to(dev), betas.to(dev),
+                xm.reshape(-1).to(dev).view(torch.uint8) if masked else None, L)
+        for dt in (torch.float32, torch.bfloat16):
+            kl_tok, dz = o.kl_fused(*args, out_dtype=dt)
+            loss, _ = o.kl_reduce(kl_tok, args[5], B, L, want_w=False)
+            close(loss, ref_loss, rtol=1e-4, what=f"fused kl loss masked={masked}")
+            d = dz.float().view(B, L, K).cpu()
+            tol = 1e-4 * ref_dz.abs().max() + (2.0 ** -8 * ref_dz.abs() if dt == torch.bfloat16 else 0.0)
+            bad = ((d - ref_dz).abs() > tol).sum().item()
+            assert bad == 0, f"fused kl grad {dt} masked={masked}: {bad} elements off"
+            before = dz.clone()
+            o.scale_if(dz, torch.ones(1, device=dev))
+            assert torch.equal(dz, before)
+            o.scale_if(dz, torch.full((1,), -3.0, device=dev))
+            close(dz.float(), -3.0 * before.float(), rtol=1e-2 if dt == torch.bfloat16 else 1e-6, what="scale_if")
+
+
 def test_lfd_kernels_match_reference():
     from helpers import load, T
     from fddm_hip import runtime as rt
