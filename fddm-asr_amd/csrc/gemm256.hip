@@ -71,6 +71,9 @@ template <int N> __device__ __forceinline__ void vmcnt() {
 // rewritten (a wide store reads its data late: the builtin let hipcc overwrite them in the next instruction,
 // corrupting the last lanes' data)
 __device__ __forceinline__ void store16(const u32x4_t& d, const i32x4_t& srd, int voff, int soff) {
+#ifdef G256_NOSTORE  // timing diagnostic only (tools/g256_stamps.py): no output, so no MFMA survives either
+  if (soff == -1)
+#endif
   asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 1" ::"v"(d), "v"(voff), "s"(srd), "s"(soff)
                : "memory");
 }

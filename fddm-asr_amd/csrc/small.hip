@@ -11,19 +11,55 @@ namespace small {
 constexpr int MAXJ = 16;  // jobs per launch
 
 // ------------------------------------------------------------------------------------------ pooled mean
-// out[b][j] = mean_s x[b][s][j]; block = 64 columns x 4 S-slices (LDS reduction, fixed order)
+// out[b][j] = mean_s x[b][s][j]. Block = one utterance x 512 columns: 64 column groups of 8 (one 16-B load per
+// row) x 16 row slices, each thread's loads independent (unrolled by 4); the 16 slice sums combine in LDS in a
+// fixed order (deterministic).
 template <typename T>
-__global__ void __launch_bounds__(256) rows_mean_kernel(const T* __restrict__ x, float* __restrict__ out, long S,
-                                                        long d) {
-  __shared__ float part[4][64];
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const long b = blockIdx.y, j = (long)blockIdx.x * 64 + tx;
-  float acc = 0.f;
-  if (j < d)
-    for (long s = ty; s < S; s += 4) acc += ld<T>(x + (b * S + s) * d + j);
-  part[ty][tx] = acc;
+__global__ void __launch_bounds__(1024) rows_mean_kernel(const T* __restrict__ x, float* __restrict__ out, long S,
+                                                         long d) {
+  constexpr int E = 16 / sizeof(T);  // elements per 16-B load
+  __shared__ float part[16][64 * E + 4];
+  const int cg = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const long b = blockIdx.y, j0 = (long)blockIdx.x * 64 * E + cg * E;
+  float acc[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) acc[e] = 0.f;
+  if (j0 + E <= d && (d % E) == 0) {
+    const T* base = x + b * S * d + j0;
+    long s = sl;
+    for (; s + 48 < S; s += 64) {
+      uint4 u[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) u[q] = *(const uint4*)(base + (s + 16 * q) * d);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const T* v = (const T*)&u[q];
+#pragma unroll
+        for (int e = 0; e < E; ++e) acc[e] += ld<T>(v + e);
+      }
+    }
+    for (; s < S; s += 16) {
+      const uint4 u = *(const uint4*)(base + s * d);
+      const T* v = (const T*)&u;
+#pragma unroll
+      for (int e = 0; e < E; ++e) acc[e] += ld<T>(v + e);
+    }
+  } else {
+    for (int e = 0; e < E; ++e)
+      if (j0 + e < d)
+        for (long s = sl; s < S; s += 16) acc[e] += ld<T>(x + (b * S + s) * d + j0 + e);
+  }
+#pragma unroll
+  for (int e = 0; e < E; ++e) part[sl][cg * E + e] = acc[e];
   __syncthreads();
-  if (ty == 0 && j < d) out[b * d + j] = ((part[0][tx] + part[1][tx]) + (part[2][tx] + part[3][tx])) / (float)S;
+  for (int c = threadIdx.x; c < 64 * E; c += 1024) {
+    const long j = (long)blockIdx.x * 64 * E + c;
+    if (j >= d) continue;
+    float a = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) a += part[q][c];
+    out[b * d + j] = a / (float)S;
+  }
 }
 
 // ------------------------------------------------------------------------------------------ time embedding
@@ -57,57 +93,95 @@ struct LinJobs {
   float* out2[MAXJ];
 };
 
+// Block: 32 rows x 8 columns of one job, thread = (row, column) with the whole K; K in chunks of 128 staged in
+// LDS (in [32][128], W as [8][128]), the next chunk's global loads issued into registers before the current chunk's
+// FMAs (one exposed load latency per launch instead of one per chunk). Fixed summation order per output.
+constexpr int LKC = 128, LNC = 8;
 template <bool TW>
 __global__ void __launch_bounds__(256) linear_kernel(const float* __restrict__ in, long ldi, LinJobs J, long ldw,
                                                      long ldo, const float* __restrict__ aux, long R, long N, long K,
                                                      int act) {
-  // tile: 32 rows x 16 columns, K in chunks of 32; thread = column (t & 15) x rows 2*(t >> 4) .. +1
-  __shared__ float Is[32][33];
-  __shared__ float Ws[16][33];
-  const int tid = threadIdx.x, c = tid & 15, rg = tid >> 4;
-  const long n0 = (long)blockIdx.x * 16, r0 = (long)blockIdx.z * 32;
+  __shared__ float Is[32][LKC + 4];
+  __shared__ float Ws[LNC][LKC + 4];
+  const int tid = threadIdx.x, c = tid & (LNC - 1), rr = tid >> 3;
+  const long n0 = (long)blockIdx.x * LNC, r0 = (long)blockIdx.z * 32;
   const int j = blockIdx.y;
   const float* W = J.W[j];
-  float acc[2] = {0.f, 0.f};
-  for (long k0 = 0; k0 < K; k0 += 32) {
-    for (int e = tid; e < 32 * 32; e += 256) {
-      const int rr = e >> 5, kk = e & 31;
-      const long r = r0 + rr, k = k0 + kk;
-      Is[rr][kk] = (r < R && k < K) ? in[r * ldi + k] : 0.f;
-    }
-    for (int e = tid; e < 16 * 32; e += 256) {
-      int cc, kk;
-      if (TW) { kk = e >> 4; cc = e & 15; } else { cc = e >> 5; kk = e & 31; }
-      const long n = n0 + cc, k = k0 + kk;
-      Ws[cc][kk] = (n < N && k < K) ? (TW ? W[k * ldw + n] : W[n * ldw + k]) : 0.f;
-    }
-    __syncthreads();
-#pragma unroll 8
-    for (int kk = 0; kk < 32; ++kk) {
-      const float w = Ws[c][kk];
-      acc[0] = fmaf(Is[2 * rg][kk], w, acc[0]);
-      acc[1] = fmaf(Is[2 * rg + 1][kk], w, acc[1]);
-    }
-    __syncthreads();
-  }
-  const long n = n0 + c;
-  if (n >= N) return;
-  const float bias = J.b[j] ? J.b[j][n] : 0.f;
+  // per chunk each thread fetches 4 x 4 floats of `in` (rows ri, k 4*kq..) and 4 floats of W
+  float4 pin[4];
+  float pw[4];
+  auto fetch = [&](long k0) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const long r = r0 + 2 * rg + i;
-    if (r >= R) continue;
-    float v = acc[i] + bias;
-    if (act == 1) {
-      J.out[j][r * ldo + n] = v;
-      J.out2[j][r * ldo + n] = v / (1.f + expf(-v));
-    } else if (act == 2) {
-      const float x = aux[r * ldo + n];
-      const float sg = 1.f / (1.f + expf(-x));
-      J.out[j][r * ldo + n] = acc[i] * (sg * (1.f + x * (1.f - sg)));
-    } else {
-      J.out[j][r * ldo + n] = v;
+    for (int q = 0; q < 4; ++q) {
+      const int e = tid + 256 * q;          // 1024 float4 slots = 32 rows x 32 float4
+      const int ri = e >> 5, kq = e & 31;
+      const long r = r0 + ri, k = k0 + 4 * kq;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (r < R) {
+        const float* src = in + r * ldi + k;
+        if (k + 3 < K && ((((uintptr_t)src) & 15) == 0)) {
+          v = *(const float4*)src;
+        } else {
+          if (k < K) v.x = src[0];
+          if (k + 1 < K) v.y = src[1];
+          if (k + 2 < K) v.z = src[2];
+          if (k + 3 < K) v.w = src[3];
+        }
+      }
+      pin[q] = v;
     }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = tid + 256 * q;          // 1024 W elements = 8 columns x 128 k
+      int cc, kk;
+      if (TW) { kk = e >> 3; cc = e & 7; } else { cc = e >> 7; kk = e & 127; }
+      const long n = n0 + cc, k = k0 + kk;
+      pw[q] = (n < N && k < K) ? (TW ? W[k * ldw + n] : W[n * ldw + k]) : 0.f;
+    }
+  };
+  auto stash = [&]() {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = tid + 256 * q;
+      *(float4*)&Is[e >> 5][4 * (e & 31)] = pin[q];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = tid + 256 * q;
+      if (TW) Ws[e & 7][e >> 3] = pw[q];
+      else Ws[e >> 7][e & 127] = pw[q];
+    }
+  };
+  float acc = 0.f;
+  fetch(0);
+  for (long k0 = 0; k0 < K; k0 += LKC) {
+    __syncthreads();                        // the previous chunk's reads are done
+    stash();
+    __syncthreads();
+    if (k0 + LKC < K) fetch(k0 + LKC);
+#pragma unroll 8
+    for (int kk = 0; kk < LKC; kk += 4) {
+      const float4 a = *(const float4*)&Is[rr][kk];
+      const float4 w = *(const float4*)&Ws[c][kk];
+      acc = fmaf(a.x, w.x, acc);
+      acc = fmaf(a.y, w.y, acc);
+      acc = fmaf(a.z, w.z, acc);
+      acc = fmaf(a.w, w.w, acc);
+    }
+  }
+  const long n = n0 + c, r = r0 + rr;
+  if (n >= N || r >= R) return;
+  const float bias = J.b[j] ? J.b[j][n] : 0.f;
+  const float v = acc + bias;
+  if (act == 1) {
+    J.out[j][r * ldo + n] = v;
+    J.out2[j][r * ldo + n] = v / (1.f + expf(-v));
+  } else if (act == 2) {
+    const float x = aux[r * ldo + n];
+    const float sg = 1.f / (1.f + expf(-x));
+    J.out[j][r * ldo + n] = acc * (sg * (1.f + x * (1.f - sg)));
+  } else {
+    J.out[j][r * ldo + n] = v;
   }
 }
 
@@ -201,11 +275,13 @@ using namespace fddm::small;
 
 FDDM_API int fddm_rows_mean(int dtype, const void* x, float* out, long B, long S, long d, void* hs) {
   if (B <= 0 || d <= 0) return 0;
-  dim3 g((unsigned)((d + 63) / 64), (unsigned)B);
+  const long cols = dtype == FDDM_BF16 ? 512 : 256;  // columns per block: 64 groups x one 16-B load
+  dim3 g((unsigned)((d + cols - 1) / cols), (unsigned)B);
+  if (((uintptr_t)x) & 15) return (int)hipErrorInvalidValue;
   if (dtype == FDDM_BF16)
-    hipLaunchKernelGGL(rows_mean_kernel<bf16_t>, g, dim3(256), 0, (hipStream_t)hs, (const bf16_t*)x, out, S, d);
+    hipLaunchKernelGGL(rows_mean_kernel<bf16_t>, g, dim3(1024), 0, (hipStream_t)hs, (const bf16_t*)x, out, S, d);
   else
-    hipLaunchKernelGGL(rows_mean_kernel<float>, g, dim3(256), 0, (hipStream_t)hs, (const float*)x, out, S, d);
+    hipLaunchKernelGGL(rows_mean_kernel<float>, g, dim3(1024), 0, (hipStream_t)hs, (const float*)x, out, S, d);
   return (int)hipGetLastError();
 }
 
@@ -231,7 +307,7 @@ FDDM_API int fddm_small_linear(const float* in, long ldi, int njobs, const float
     if (act == 1 && !J.out2[j]) return (int)hipErrorInvalidValue;
   }
   if (act == 2 && !aux) return (int)hipErrorInvalidValue;
-  dim3 g((unsigned)((N + 15) / 16), (unsigned)njobs, (unsigned)((R + 31) / 32));
+  dim3 g((unsigned)((N + LNC - 1) / LNC), (unsigned)njobs, (unsigned)((R + 31) / 32));
   if (transpose_w)
     hipLaunchKernelGGL(linear_kernel<true>, g, dim3(256), 0, (hipStream_t)hs, in, ldi, J, ldw, ldo, aux, R, N, K, act);
   else
