@@ -586,6 +586,79 @@ __global__ void __launch_bounds__(256) softmax_bwd_kernel(const T* __restrict__ 
   }
 }
 
+// bf16 logits-gradient hand-over of the L_fd step (functions.TextEmbedFn / KLFn / HeadFn):
+// out = bf16( y * (dy - sum(y*dy)) + add ), y = softmax rows (bf16), dy (bf16), add = the KL's gradient (bf16).
+// 8 elements per 16-B load, NV loads per thread, one block per row (V % 8 == 0).
+template <int NV>
+__global__ void __launch_bounds__(256) softmax_bwd_add_kernel(const bf16_t* __restrict__ y, const bf16_t* __restrict__ dy,
+                                                              const bf16_t* __restrict__ add, bf16_t* __restrict__ out,
+                                                              long V) {
+  __shared__ float red[8];
+  const long row = blockIdx.x;
+  const int tid = threadIdx.x;
+  const long V8 = V >> 3;
+  uint4 yv[NV], dv[NV];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const long q = tid + 256L * i;
+    yv[i] = make_uint4(0u, 0u, 0u, 0u);
+    dv[i] = yv[i];
+    if (q < V8) {
+      yv[i] = ((const uint4*)(y + row * V))[q];
+      dv[i] = ((const uint4*)(dy + row * V))[q];
+    }
+    const unsigned* a = (const unsigned*)&yv[i];
+    const unsigned* b = (const unsigned*)&dv[i];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      s = fmaf(__uint_as_float(a[k] << 16), __uint_as_float(b[k] << 16), s);
+      s = fmaf(__uint_as_float(a[k] & 0xffff0000u), __uint_as_float(b[k] & 0xffff0000u), s);
+    }
+  }
+  s = block_sum(s, red);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const long q = tid + 256L * i;
+    if (q >= V8) continue;
+    const uint4 ad = ((const uint4*)(add + row * V))[q];
+    const unsigned* a = (const unsigned*)&yv[i];
+    const unsigned* b = (const unsigned*)&dv[i];
+    const unsigned* c = (const unsigned*)&ad;
+    uint4 o;
+    unsigned* ov = (unsigned*)&o;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float lo = __uint_as_float(a[k] << 16) * (__uint_as_float(b[k] << 16) - s) + __uint_as_float(c[k] << 16);
+      const float hi = __uint_as_float(a[k] & 0xffff0000u) * (__uint_as_float(b[k] & 0xffff0000u) - s) +
+                       __uint_as_float(c[k] & 0xffff0000u);
+      ov[k] = pk_bf16(lo, hi);
+    }
+    ((uint4*)(out + row * V))[q] = o;
+  }
+}
+
+// x += (g[0] - 1) * y (bf16), skipped without memory traffic when g[0] == 1: the KL's upstream scalar applied to
+// its share of a hand-over buffer that already holds x = text part + KL part
+__global__ void __launch_bounds__(256) axpy_if_kernel(bf16_t* __restrict__ x, const bf16_t* __restrict__ y,
+                                                      const float* __restrict__ g, long n8) {
+  const float c = g[0] - 1.f;
+  if (g[0] == 1.f) return;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
+    uint4 u = ((uint4*)x)[i];
+    const uint4 v = ((const uint4*)y)[i];
+    unsigned* a = (unsigned*)&u;
+    const unsigned* b = (const unsigned*)&v;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float lo = __uint_as_float(a[k] << 16) + c * __uint_as_float(b[k] << 16);
+      const float hi = __uint_as_float(a[k] & 0xffff0000u) + c * __uint_as_float(b[k] & 0xffff0000u);
+      a[k] = pk_bf16(lo, hi);
+    }
+    ((uint4*)x)[i] = u;
+  }
+}
+
 }  // namespace fddm
 
 using namespace fddm;
@@ -738,5 +811,37 @@ FDDM_API int fddm_scale_if(void* x, int dtype, const float* g, long n, void* hs)
     hipLaunchKernelGGL(scale_if_kernel<bf16_t>, dim3(grid), dim3(256), 0, (hipStream_t)hs, (bf16_t*)x, g, n);
   else
     hipLaunchKernelGGL(scale_if_kernel<float>, dim3(grid), dim3(256), 0, (hipStream_t)hs, (float*)x, g, n);
+  return (int)hipGetLastError();
+}
+
+// out (bf16) = y * (dy - rowsum(y*dy)) + add: y, dy, add, out bf16 [N][V], V % 8 == 0 (out may alias add)
+FDDM_API int fddm_softmax_bwd_add_bf16(const void* y, const void* dy, const void* add, void* out, long N, long V,
+                                       void* hs) {
+  if (N <= 0) return 0;
+  if (V % 8 || ((((uintptr_t)y) | ((uintptr_t)dy) | ((uintptr_t)add) | ((uintptr_t)out)) & 15))
+    return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)hs;
+#define SMBA(NV)                                                                                            \
+  if (V <= 2048L * NV) {                                                                                   \
+    hipLaunchKernelGGL(softmax_bwd_add_kernel<NV>, dim3((unsigned)N), dim3(256), 0, s, (const bf16_t*)y,   \
+                       (const bf16_t*)dy, (const bf16_t*)add, (bf16_t*)out, V);                           \
+    return (int)hipGetLastError();                                                                        \
+  }
+  SMBA(1)
+  SMBA(2)
+  SMBA(4)
+  SMBA(8)
+  SMBA(16)
+#undef SMBA
+  return (int)hipErrorInvalidValue;
+}
+
+// x += (g[0] - 1) * y over n bf16 elements (n % 8 == 0); no memory traffic when g[0] == 1
+FDDM_API int fddm_axpy_if_bf16(void* x, const void* y, const float* g, long n, void* hs) {
+  if (n <= 0) return 0;
+  if (n % 8 || ((((uintptr_t)x) | ((uintptr_t)y)) & 15)) return (int)hipErrorInvalidValue;
+  const long want = (n / 8 + 255) / 256;
+  const unsigned grid = (unsigned)(want < 4096 ? want : 4096);
+  hipLaunchKernelGGL(axpy_if_kernel, dim3(grid), dim3(256), 0, (hipStream_t)hs, (bf16_t*)x, (const bf16_t*)y, g, n / 8);
   return (int)hipGetLastError();
 }

@@ -354,11 +354,24 @@ class DecoderBlockFn(torch.autograd.Function):
 
 
 # --------------------------------------------------------------------------------------- head
-# bf16 mode: the KL backward writes its logits gradient straight in bf16 for the head backward (the head GEMMs
-# run on bf16 operands) instead of an fp32 [B*L, V] tensor plus a cast pass. The hand-over is keyed by the
-# address of a live HeadFn output; autograd sees a stride-0 zero gradient on that path.
+# bf16 mode: the logits gradient reaches the head backward in bf16 straight from the kernels that produce it, not
+# as fp32 [B*L, V] tensors that autograd sums and a cast pass converts. The hand-over is keyed by the address of a
+# live HeadFn output: KLFn leaves its gradient (computed in its forward, unscaled) in _kl_dz; on L_fd steps
+# TextEmbedFn.backward (which autograd runs first) writes softmax-backward + that KL part into one bf16 buffer
+# (_dlogits_bf16, flagged in _combined) and KLFn.backward then only applies its upstream scalar to its share (a
+# no-op when it is 1); without L_fd, KLFn.backward scales its own buffer and hands it over. Both return no
+# gradient to autograd, so HeadFn.backward (materialize_grads off) receives None and takes the buffer.
 _head_outputs: dict = {}     # data_ptr -> weakref to a HeadFn output (bf16 mode)
-_dlogits_bf16: dict = {}     # data_ptr -> bf16 gradient left by KLFn.backward
+_dlogits_bf16: dict = {}     # data_ptr -> bf16 logits gradient for HeadFn.backward
+_kl_dz: dict = {}            # data_ptr -> the KL's unscaled bf16 gradient (between KLFn forward and backward)
+_combined: set = set()       # data_ptrs whose _dlogits_bf16 buffer already holds text part + unscaled KL part
+
+
+def _drop_handover(ptr):
+    _head_outputs.pop(ptr, None)
+    _dlogits_bf16.pop(ptr, None)
+    _kl_dz.pop(ptr, None)
+    _combined.discard(ptr)
 
 
 class HeadFn(torch.autograd.Function):
@@ -371,22 +384,25 @@ class HeadFn(torch.autograd.Function):
         ctx.save_for_backward(xT, weight)
         ctx.bias = (bias,)
         ctx.out_ptr = logits.data_ptr()
+        ctx.set_materialize_grads(False)
         if xT.dtype == torch.bfloat16:
             for k in [k for k, r in _head_outputs.items() if r() is None]:   # outputs freed without a backward
-                _head_outputs.pop(k, None)
-                _dlogits_bf16.pop(k, None)
+                _drop_handover(k)
+            _drop_handover(ctx.out_ptr)
             _head_outputs[ctx.out_ptr] = weakref.ref(logits)
         return logits
 
     @staticmethod
     def backward(ctx, dlogits):
         xT, weight = ctx.saved_tensors
-        _head_outputs.pop(ctx.out_ptr, None)
-        dz16 = _dlogits_bf16.pop(ctx.out_ptr, None)
-        if dz16 is not None and all(st == 0 for st in dlogits.stride()):
-            dl = dz16                                     # the KL gradient alone, already bf16
+        dz16 = _dlogits_bf16.get(ctx.out_ptr)
+        _drop_handover(ctx.out_ptr)
+        if dz16 is not None and (dlogits is None or all(st == 0 for st in dlogits.stride())):
+            dl = dz16                                     # the handed-over gradient, already bf16
         elif dz16 is not None:
-            dl = (dlogits + dz16.view(dlogits.shape)).to(torch.bfloat16).contiguous()  # + L_fd's contribution
+            dl = (dlogits + dz16.view(dlogits.shape)).to(torch.bfloat16).contiguous()  # + another consumer's part
+        elif dlogits is None:
+            dl = torch.zeros(xT.shape[0], weight.shape[0], device=xT.device, dtype=xT.dtype)
         else:
             dl = dlogits.contiguous()
             if xT.dtype == torch.bfloat16 and dl.dtype == F32:
@@ -407,7 +423,8 @@ class HeadFn(torch.autograd.Function):
 class KLFn(torch.autograd.Function):
     """SchedulerAdapter.kl_term (train.py:190-255): fused closed-form KL. With a gradient wanted, ONE pass over the
     logits produces the per-token KL and its logits gradient (times the masked-mean weights); backward only applies
-    the upstream scalar on the device (ops.scale_if: nothing to do when it is 1, the train step's case)."""
+    the upstream scalar on the device (ops.scale_if / axpy_if_bf16: nothing to do when it is 1, the train step's
+    case). bf16 mode hands the gradient to the HeadFn that produced the logits (see the module notes above)."""
 
     @staticmethod
     def forward(ctx, logits, xt, x0, t, mask_u8, betas):
@@ -421,30 +438,35 @@ class KLFn(torch.autograd.Function):
             kl_tok = ops.kl_fwd(l2, xf, x0f, tc, betas, L)
             loss, _ = ops.kl_reduce(kl_tok, mask_u8, B, L, want_w=False)
             return loss
-        # bf16 mode: the gradient goes to the live HeadFn that produced these logits, in bf16
         ptr = l2.data_ptr()
         ref = _head_outputs.get(ptr)
         owner = ref() if ref is not None else None
-        bf = owner is not None and owner.data_ptr() == ptr and ptr not in _dlogits_bf16
+        bf = owner is not None and owner.data_ptr() == ptr and ptr not in _dlogits_bf16 and ptr not in _kl_dz
         kl_tok, dz = ops.kl_fused(l2.contiguous(), xf, x0f, tc, betas, mask_u8, L,
                                   out_dtype=torch.bfloat16 if bf else F32)
         loss, _ = ops.kl_reduce(kl_tok, mask_u8, B, L, want_w=False)
         ctx.dz = dz
-        ctx.handover = ptr if bf else None
+        if bf:
+            ctx.handover = ptr
+            _kl_dz[ptr] = dz
         return loss
 
     @staticmethod
     def backward(ctx, g):
         B, L, V = ctx.shape
         dz, ctx.dz = ctx.dz, None
-        ops.scale_if(dz, g.reshape(1).to(F32).contiguous())
-        if ctx.handover is not None:
-            ref = _head_outputs.get(ctx.handover)
-            if ref is not None and ref() is not None and ctx.handover not in _dlogits_bf16:
-                _dlogits_bf16[ctx.handover] = dz     # HeadFn.backward picks it up
-                return torch.zeros((), device=dz.device, dtype=F32).expand(B, L, V), None, None, None, None, None
-            dz = dz.float()
-        return dz.view(B, L, V), None, None, None, None, None
+        gs = g.reshape(1).to(F32).contiguous()
+        ptr = ctx.handover
+        if ptr is not None and _kl_dz.pop(ptr, None) is not None:
+            if ptr in _combined:                          # the text part already added our unscaled share
+                ops.axpy_if_bf16(_dlogits_bf16[ptr], dz, gs)
+                return None, None, None, None, None, None
+            ref = _head_outputs.get(ptr)
+            if ref is not None and ref() is not None and ptr not in _dlogits_bf16:
+                _dlogits_bf16[ptr] = ops.scale_if(dz, gs)
+                return None, None, None, None, None, None
+        ops.scale_if(dz, gs)
+        return dz.float().view(B, L, V), None, None, None, None, None
 
 
 # ------------------------------------------------------------------------------- TextEmbedding
@@ -461,6 +483,7 @@ class TextEmbedFn(torch.autograd.Function):
         z = ops.linear(xhat, rt.wt(weight), None, out_dtype=F32)
         ctx.save_for_backward(xhat, weight)
         ctx.shp = shp
+        ctx.lptr = l2.data_ptr()
         return z.view(*shp[:-1], weight.shape[0])
 
     @staticmethod
@@ -469,8 +492,16 @@ class TextEmbedFn(torch.autograd.Function):
         dz2 = dz.reshape(-1, weight.shape[0]).contiguous()
         cd = rt.compute_dtype()
         dxhat = ops.linear_dx(dz2, rt.wt(weight), out_dtype=cd)
-        dlogits = ops.softmax_bwd_rows(xhat, dxhat)
         dW = ops.linear_dw(_t(dz2), xhat)
+        ptr = ctx.lptr
+        kl = _kl_dz.get(ptr)
+        if (kl is not None and cd == torch.bfloat16 and ptr in _head_outputs and ptr not in _dlogits_bf16
+                and ptr not in _combined):
+            # bf16 hand-over: softmax backward + the KL's (unscaled) share in one bf16 buffer for HeadFn
+            _dlogits_bf16[ptr] = ops.softmax_bwd_add_bf16(xhat, dxhat, kl)
+            _combined.add(ptr)
+            return None, dW
+        dlogits = ops.softmax_bwd_rows(xhat, dxhat)
         return dlogits.view(ctx.shp), dW
 
 

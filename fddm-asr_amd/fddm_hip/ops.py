@@ -344,6 +344,25 @@ def scale_if(x, g):
     return x
 
 
+def softmax_bwd_add_bf16(y, dy, add, out=None):
+    """out = bf16(y * (dy - rowsum(y*dy)) + add), all bf16 [N, V] (out may be `add`)."""
+    N, V = y.shape
+    _chk(all(t.dtype == torch.bfloat16 and t.is_contiguous() and tuple(t.shape) == (N, V) for t in (y, dy, add)),
+         "softmax_bwd_add_bf16 operands")
+    if out is None:
+        out = torch.empty_like(y)
+    call("fddm_softmax_bwd_add_bf16", ptr(y), ptr(dy), ptr(add), ptr(out), N, V, stream())
+    return out
+
+
+def axpy_if_bf16(x, y, g):
+    """x += (g - 1) * y in place (bf16), no memory traffic when the device scalar g == 1."""
+    _chk(x.dtype == y.dtype == torch.bfloat16 and x.numel() == y.numel() and x.is_contiguous() and y.is_contiguous(),
+         "axpy_if_bf16 operands")
+    call("fddm_axpy_if_bf16", ptr(x), ptr(y), ptr(g), x.numel(), stream())
+    return x
+
+
 def softmax_rows(x2d, out_dtype):
     N, V = x2d.shape
     y = torch.empty(N, V, device=x2d.device, dtype=out_dtype)

@@ -143,6 +143,11 @@ int fddm_kl_fused(const float* logits, const long* xt, const long* x0, const lon
                   const unsigned char* mask, float* kl_tok, void* dz, int dz_dtype, long N, long L, long V,
                   void* hip_stream);
 int fddm_scale_if(void* x, int dtype, const float* g, long n, void* hip_stream);
+/* L_fd steps, bf16: the TextEmbedding softmax backward summed with the KL's gradient straight into the bf16
+ * logits gradient the head GEMMs read (out may alias add), and the KL's upstream scalar applied to its share. */
+int fddm_softmax_bwd_add_bf16(const void* y, const void* dy, const void* add, void* out, long N, long V,
+                              void* hip_stream);
+int fddm_axpy_if_bf16(void* x, const void* y, const float* g, long n, void* hip_stream);
 
 /* ---- TextEmbedding softmax (models/projection.py:41-47) */
 int fddm_softmax_rows(const float* x, void* y, int out_dtype, long N, long V, void* hip_stream);

@@ -682,6 +682,35 @@ def test_softmax_rows_and_bwd():
     close(dz, ref, rtol=1e-5, what="softmax bwd")
 
 
+@pytest.mark.parametrize("V", [8000, 1000, 24])
+def test_softmax_bwd_add_bf16_and_axpy_if(V):
+    """The bf16 hand-over kernels: y*(dy - rowsum(y*dy)) + add from bf16 operands (f32 arithmetic, one bf16
+    rounding of the result: within 2^-8 relative + 1e-3 of the row scale), in place over `add` too; axpy_if adds
+    (g-1)*y and leaves x untouched bit for bit when g == 1."""
+    o = ops()
+    bf = torch.bfloat16
+    N = 19
+    x = 3 * torch.randn(N, V, generator=g(76))
+    y = torch.softmax(x, -1).to(bf)
+    dy = torch.randn(N, V, generator=g(77)).to(bf)
+    add = (1e-3 * torch.randn(N, V, generator=g(78))).to(bf)
+    yd, dyd = y.double(), dy.double()
+    ref = yd * (dyd - (yd * dyd).sum(-1, keepdim=True)) + add.double()
+    out = o.softmax_bwd_add_bf16(y.to(dev), dy.to(dev), add.to(dev)).cpu().double()
+    tol = 2.0 ** -8 * ref.abs() + 1e-3 * ref.abs().amax(-1, keepdim=True)
+    assert ((out - ref).abs() <= tol).all()
+    a = add.to(dev)
+    o.softmax_bwd_add_bf16(y.to(dev), dy.to(dev), a, out=a)
+    assert torch.equal(a.cpu().double(), out)
+    xb = torch.randn(N * V, generator=g(79)).to(bf).to(dev)
+    yb = torch.randn(N * V, generator=g(80)).to(bf).to(dev)
+    before = xb.clone()
+    o.axpy_if_bf16(xb, yb, torch.ones(1, device=dev))
+    assert torch.equal(xb, before)
+    o.axpy_if_bf16(xb, yb, torch.full((1,), 3.0, device=dev))
+    close(xb.float(), before.float() + 2.0 * yb.float(), rtol=1e-2, atol=1e-2, what="axpy_if")
+
+
 def test_fused_adamw_nonfinite_guard_skips_whole_step():
     """A non-finite gradient norm skips the whole step on the device — parameters, moments and the step
     counters stay as they were (GradScaler.step's skip on the reference's GPU path, train.py:401-413) — and the
