@@ -831,3 +831,21 @@ def test_rows_mean_time_embed_kl_reduce():
     loss2, w2 = o.kl_reduce(kl.to(dev), None, B, L)
     close(loss2, kl.double().mean(), rtol=1e-6, what="kl_reduce unmasked")
     close(w2, torch.full((B * L,), 1.0 / (B * L)), rtol=1e-6, what="kl_reduce unmasked w")
+
+
+def test_conv0_gn_gelu_matches_reference():
+    """WavLM conv layer 0 + per-channel GroupNorm over time + GELU (HF modeling_wavlm.py:723-744) in bf16 (Gram-
+    matrix statistics, fp32 conv, packed-f32 GELU) vs a float64 torch reference within bf16 rounding (2^-8
+    relative + 2e-3 absolute)."""
+    o = ops()
+    B, nsamp, C, K, S = 3, 16000 + 7, 512, 10, 5
+    wave = torch.randn(B, nsamp, generator=g(81)) * 0.1
+    w = torch.randn(C, K, generator=g(82)) * 0.3
+    gamma = 1 + 0.1 * torch.randn(C, generator=g(83))
+    beta = 0.1 * torch.randn(C, generator=g(84))
+    out = o.conv0_gn_gelu(wave.to(dev), w.to(dev), gamma.to(dev), beta.to(dev), torch.bfloat16, C, K, S).float().cpu()
+    y = F.conv1d(wave.double()[:, None], w.double()[:, None], stride=S)            # [B, C, T]
+    y = F.group_norm(y, C, gamma.double(), beta.double(), eps=1e-5)
+    ref = F.gelu(y).transpose(1, 2)
+    assert ref.shape == out.shape
+    assert ((out.double() - ref).abs() <= 2.0 ** -8 * ref.abs() + 2e-3).all()
