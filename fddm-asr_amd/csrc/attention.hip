@@ -19,6 +19,19 @@
 namespace fddm {
 namespace attn {
 
+// XCD-aware block order: the hardware deals workgroups round-robin over the 8 XCDs (linear id L -> XCD L % 8);
+// remap so that each XCD receives a contiguous range of (bh, tile) work items — all tiles of one (batch, head) run
+// on one XCD and read that head's K / V (or Q / dO) through one L2 instead of up to 8 (bijective for any grid size).
+__device__ __forceinline__ void xcd_tile(int& bx, int& by) {
+  const int nx = gridDim.x, n = nx * gridDim.y;
+  const int L = blockIdx.x + blockIdx.y * nx;
+  const int x = L & 7, j = L >> 3, q = n >> 3, r = n & 7;
+  const int W = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + j;
+  by = W / nx;
+  bx = W - by * nx;
+}
+
+
 constexpr int DH = 64;
 
 template <typename T> struct Cfg;
@@ -223,8 +236,10 @@ __global__ void __launch_bounds__(256) fwd_kernel(AttnArgs a) {
   unsigned char* kimg = smem;
   unsigned char* vimg = smem + 64 * RB;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, i = lane & 15;
-  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
-  const int q = blockIdx.x * 64 + w * 16 + i;
+  int bxi, bh;
+  xcd_tile(bxi, bh);
+  const int b = bh / a.H, h = bh % a.H;
+  const int q = bxi * 64 + w * 16 + i;
   const bool qv = q < a.Lq;
   const T* Qb = (const T*)a.Q + (long)b * a.Lq * a.sq + h * DH;
   const T* Kb = (const T*)a.K + (long)b * a.Lk * a.sk + h * DH;
@@ -314,8 +329,10 @@ __global__ void __launch_bounds__(256, ATTN_FWD_WPS) fwd2_kernel(AttnArgs a) {
   __shared__ float tbuf[2][192];
   __shared__ __attribute__((aligned(16))) float mbuf[2][64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, i = lane & 15;
-  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
-  const int qbase = blockIdx.x * (64 * NG);
+  int bxi, bh;
+  xcd_tile(bxi, bh);
+  const int b = bh / a.H, h = bh % a.H;
+  const int qbase = bxi * (64 * NG);
   const bf16_t* Qb = (const bf16_t*)a.Q + (long)b * a.Lq * a.sq + h * DH;
   const bf16_t* Kb = (const bf16_t*)a.K + (long)b * a.Lk * a.sk + h * DH;
   const bf16_t* Vb = (const bf16_t*)a.V + (long)b * a.Lk * a.sv + h * DH;
@@ -565,8 +582,10 @@ __global__ void __launch_bounds__(64 * NW, 1) fwd3_kernel(AttnArgs a) {
   unsigned char* dtab = (unsigned char*)(mfull + LkP + (REL ? LkP + QW : 0));  // [3][4096] u16 (DROP)
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
             i = lane & 15;
-  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
-  const int qbase = blockIdx.x * QW;
+  int bxi, bh;
+  xcd_tile(bxi, bh);
+  const int b = bh / a.H, h = bh % a.H;
+  const int qbase = bxi * QW;
   const bf16_t* Qb = (const bf16_t*)a.Q + (long)b * a.Lq * a.sq + h * DH;
   const bf16_t* Kb = (const bf16_t*)a.K + (long)b * a.Lk * a.sk + h * DH;
   const bf16_t* Vb = (const bf16_t*)a.V + (long)b * a.Lk * a.sv + h * DH;
@@ -801,8 +820,10 @@ __global__ void __launch_bounds__(256) dq_kernel(AttnArgs a) {
   unsigned char* ktimg = smem + 64 * RB;  // K transposed reads (MC)
   unsigned char* vimg = smem + 128 * RB;  // V rows (KC)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, i = lane & 15;
-  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
-  const int q = blockIdx.x * 64 + w * 16 + i;
+  int bxi, bh;
+  xcd_tile(bxi, bh);
+  const int b = bh / a.H, h = bh % a.H;
+  const int q = bxi * 64 + w * 16 + i;
   const bool qv = q < a.Lq;
   const int qq = qv ? q : 0;
   const T* Qb = (const T*)a.Q + (long)b * a.Lq * a.sq + h * DH;
@@ -876,8 +897,10 @@ __global__ void __launch_bounds__(256) dkv_kernel(AttnArgs a) {
   float* lse_s = (float*)(smem + 256 * RB);
   float* del_s = lse_s + 64;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, i = lane & 15;
-  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
-  const int key = blockIdx.x * 64 + w * 16 + i;
+  int bxi, bh;
+  xcd_tile(bxi, bh);
+  const int b = bh / a.H, h = bh % a.H;
+  const int key = bxi * 64 + w * 16 + i;
   const bool kv = key < a.Lk;
   const bool kok = key_ok(a, b, kv ? key : 0) && kv;
   const T* Qb = (const T*)a.Q + (long)b * a.Lq * a.sq + h * DH;
@@ -983,8 +1006,10 @@ __global__ void __launch_bounds__(256, 2) dq2_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) unsigned char vc[2][64 * RB];
   __shared__ __attribute__((aligned(16))) float mbuf[2][64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, i = lane & 15;
-  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
-  const int qbase = blockIdx.x * 128;
+  int bxi, bh;
+  xcd_tile(bxi, bh);
+  const int b = bh / a.H, h = bh % a.H;
+  const int qbase = bxi * 128;
   const bf16_t* Qb = (const bf16_t*)a.Q + (long)b * a.Lq * a.sq + h * DH;
   const bf16_t* Ob = (const bf16_t*)a.O + (long)b * a.Lq * a.so + h * DH;
   const bf16_t* dOb = (const bf16_t*)a.dO + (long)b * a.Lq * a.sdo + h * DH;
@@ -1146,8 +1171,10 @@ __global__ void __launch_bounds__(256, (DM == 1 ? 1 : 2)) dkv2_kernel(AttnArgs a
   __shared__ float lse_s[2][64], del_s[2][64];
   __shared__ __attribute__((aligned(16))) uint64_t wb_s[2][2][64];  // [buf][key tile of the block][query]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, i = lane & 15;
-  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
-  const int kbase = blockIdx.x * 128;
+  int bxi, bh;
+  xcd_tile(bxi, bh);
+  const int b = bh / a.H, h = bh % a.H;
+  const int kbase = bxi * 128;
   const int ntk = (a.Lk + 63) / 64;
   const bf16_t* Qb = (const bf16_t*)a.Q + (long)b * a.Lq * a.sq + h * DH;
   const bf16_t* dOb = (const bf16_t*)a.dO + (long)b * a.Lq * a.sdo + h * DH;
@@ -1185,7 +1212,7 @@ __global__ void __launch_bounds__(256, (DM == 1 ? 1 : 2)) dkv2_kernel(AttnArgs a
       if (qq < a.Lq) lv = tid < 64 ? a.lse[(long)bh * a.Lq + qq] * 1.4426950408889634f : a.delta[(long)bh * a.Lq + qq];
     }
     if (DM == 2 && tid >= 128) {
-      const int qq = q0 + (tid & 63), kt = 2 * blockIdx.x + ((tid - 128) >> 6);
+      const int qq = q0 + (tid & 63), kt = 2 * bxi + ((tid - 128) >> 6);
       wv = (qq < a.Lq && kt < ntk) ? a.dbits[((long)bh * ntk + kt) * a.Lq + qq] : 0;
     }
   };

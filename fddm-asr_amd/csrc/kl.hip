@@ -8,6 +8,7 @@
 //                         one write). Closed form: SURVEY §8(a) "KL closed form".
 //  * fddm_softmax_rows / fddm_softmax_bwd_rows — TextEmbedding (models/projection.py:41-47).
 #include "common.h"
+#include <cstdlib>
 
 namespace fddm {
 
@@ -776,15 +777,15 @@ FDDM_API int fddm_softmax_bwd_rows(const void* y, const void* dy, float* dz, int
   return (int)hipErrorInvalidValue;
 }
 
-#define KLF_DISPATCH(NV)                                                                                           \
-  if (V <= 2048L * NV) {                                                                                          \
-    if (dz_dtype == FDDM_BF16)                                                                                    \
-      hipLaunchKernelGGL((kl4_fused_kernel<NV, bf16_t, 512>), dim3((unsigned)N), dim3(512), 0, s, logits, xt, x0, \
-                         t, betas, mask, kl_tok, (bf16_t*)dz, L, V, N / L);                                       \
-    else                                                                                                          \
-      hipLaunchKernelGGL((kl4_fused_kernel<NV, float, 512>), dim3((unsigned)N), dim3(512), 0, s, logits, xt, x0,  \
-                         t, betas, mask, kl_tok, (float*)dz, L, V, N / L);                                        \
-    return (int)hipGetLastError();                                                                                \
+#define KLF_LAUNCH(NV, NT)                                                                                        \
+  if (V <= 4L * NT * NV) {                                                                                       \
+    if (dz_dtype == FDDM_BF16)                                                                                   \
+      hipLaunchKernelGGL((kl4_fused_kernel<NV, bf16_t, NT>), dim3((unsigned)N), dim3(NT), 0, s, logits, xt, x0,  \
+                         t, betas, mask, kl_tok, (bf16_t*)dz, L, V, N / L);                                      \
+    else                                                                                                         \
+      hipLaunchKernelGGL((kl4_fused_kernel<NV, float, NT>), dim3((unsigned)N), dim3(NT), 0, s, logits, xt, x0,   \
+                         t, betas, mask, kl_tok, (float*)dz, L, V, N / L);                                       \
+    return (int)hipGetLastError();                                                                               \
   }
 
 // kl_tok[N] and dz[N][V] = w * d kl_tok / d logits in one pass (w: the masked-mean weights of fddm_kl_reduce)
@@ -794,10 +795,24 @@ FDDM_API int fddm_kl_fused(const float* logits, const long* xt, const long* x0, 
   if (N <= 0) return 0;
   if (L <= 0 || N % L || V % 4 || (((uintptr_t)logits) & 15) || (((uintptr_t)dz) & 15)) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)hs;
-  KLF_DISPATCH(1)
-  KLF_DISPATCH(4)
-  KLF_DISPATCH(8)
-  KLF_DISPATCH(16)
+  const char* nt_env = getenv("FDDM_KLF_NT");
+  const int nt = nt_env ? atoi(nt_env) : 256;
+  if (nt == 128) {
+    KLF_LAUNCH(4, 128)
+    KLF_LAUNCH(16, 128)
+  } else if (nt == 256) {
+    KLF_LAUNCH(2, 256)
+    KLF_LAUNCH(8, 256)
+    KLF_LAUNCH(16, 256)
+  } else if (nt == 1024) {
+    KLF_LAUNCH(1, 1024)
+    KLF_LAUNCH(2, 1024)
+    KLF_LAUNCH(4, 1024)
+  }
+  KLF_LAUNCH(1, 512)
+  KLF_LAUNCH(4, 512)
+  KLF_LAUNCH(8, 512)
+  KLF_LAUNCH(16, 512)
   return (int)hipErrorInvalidValue;
 }
 

@@ -15,7 +15,8 @@ from fddm_hip import graphs as G  # noqa: E402
 
 
 def main():
-    sys.argv = [sys.argv[0]] + sys.argv[1:]
+    dec_only = "--dec-only" in sys.argv
+    sys.argv = [a for a in sys.argv if a != "--dec-only"]
     args = bench.parse()
     dev = torch.device("cuda:0")
     T_, cfg, models, opt = bench.build(args, dev)
@@ -60,6 +61,16 @@ def main():
         mark("opt1")
         return out
     opt.clip_and_step = step
+    if dec_only:      # the decoder step alone on the whole chip: the condition precomputed (no encoder stream)
+        with torch.no_grad():
+            cs = [enc(b[0])[0].clone() for b in batches]
+
+        def fake_encoded(encoder, loader, device, optimizer):
+            for k, (wave, x0) in enumerate(loader):
+                mark("enc0")
+                mark("enc1")
+                yield cs[k % 4], None, x0
+        T_._encoded = fake_encoded
     gs = 4
     gs, _ = T_.train_one_epoch(enc, dec, sp, te, tp, sch, [batches[j % 4] for j in range(4)], opt, dev, cfg, gs, None,
                                0, False)
