@@ -60,7 +60,8 @@ class GraphedEncoder:
     def run(self, wave, slot: int, cap: int = 0):
         """The encoder's features for `wave` in slot `slot`'s static output buffer (valid until this slot is run
         again), on the current stream."""
-        key = (tuple(wave.shape), wave.dtype, str(wave.device), rt.precision(), int(cap))
+        key = (tuple(wave.shape), wave.dtype, str(wave.device), rt.precision(), int(cap),
+               int(getattr(self.enc.backbone, "conv_cus", 0)))   # grid sizes are part of the captured launches
         slots = self.cache.setdefault(key, [None] * self.nslots)
         s = slots[slot]
         if s is None:

@@ -195,6 +195,17 @@ class WavLMModel(nn.Module):
     def _conv(self, h, i, out=None):
         c = self.config
         P = self._prepared(rt.compute_dtype())
+        cap = getattr(self, "conv_cus", 0)   # persistent-GEMM workgroup cap for the conv layers (train._encoded)
+        if cap:
+            from fddm_hip._lib import lib
+            prev = lib().fddm_gemm_persistent_cap(cap)
+            try:
+                return self._conv_launch(h, i, out, c, P)
+            finally:
+                lib().fddm_gemm_persistent_cap(prev)
+        return self._conv_launch(h, i, out, c, P)
+
+    def _conv_launch(self, h, i, out, c, P):
         B, T, cin = h.shape
         k, s, co = c.conv_kernel[i], c.conv_stride[i], c.conv_dim[i]
         Tout = (T - k) // s + 1

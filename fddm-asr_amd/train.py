@@ -119,9 +119,16 @@ def _encoded(encoder, loader, device, optimizer):
         return
     main = torch.cuda.current_stream(dev)
     side = _enc_stream(dev)
-    # persistent encoder GEMMs on 3/4 of the CUs (measured: 192 of 256 beats 256, 224, 208, 176 and 160)
+    # persistent encoder GEMMs on 3/4 of the CUs (measured: 192 of 256 beats 256, 224, 208, 176 and 160), the conv
+    # feature extractor's on half (it runs beside the decoder forward; bench.py C2 step, tools/cap_sweep.sh: conv
+    # cap 128 -> 10.85-10.91 ms, 112 / 120 / 136 / 144 / 160 -> 11.0-11.06, 192 (= the rest) 11.02-11.11, 256
+    # 11.17, 64 12.4)
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
     enc_cus = int(os.environ.get("FDDM_ENC_CUS", ncu * 3 // 4))
+    conv_cus = int(os.environ.get("FDDM_ENC_CUS_CONV", ncu // 2))
+    bb = getattr(encoder, "backbone", None)
+    if bb is not None and hasattr(bb, "stage_rest"):
+        bb.conv_cus = conv_cus
     # HIP-graph replay of the encoder forward (fddm_hip.graphs): the host launch path, not the GPU, bounded the step
     graphs = None
     if os.environ.get("FDDM_ENC_GRAPH", "1") != "0" and GraphedEncoder.supported(encoder):

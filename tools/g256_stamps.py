@@ -19,6 +19,9 @@ dev = torch.device("cuda:0")
 A = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
 W = torch.randn(N, K, device=dev, dtype=torch.bfloat16) / 30
 o = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+cap = int(os.environ.get("G256_CAP", "0"))
+if cap:
+    _lib.lib().fddm_gemm_persistent_cap(cap)
 for _ in range(5):
     ops.gemm(A, W, o, M, N, K, lda=K, ldb=K, ldc=N, epi=EPI)
 torch.cuda.synchronize()
@@ -30,7 +33,7 @@ st = np.frombuffer(buf, dtype=np.uint64).reshape(256, NS).astype(np.int64)
 d = np.diff(st, axis=1)
 ok = (st[:, 1:] > 0) & (st[:, :-1] > 0)
 nk = K // 64
-print(f"M{M} N{N} K{K} epi{EPI} nk={nk}: median cycles per K-tile (column = K-tile index within the workgroup)")
+print(f"M{M} N{N} K{K} epi{EPI} nk={nk} cap={cap}: median cycles per K-tile (column = K-tile index within the workgroup)")
 med = [int(np.median(d[ok[:, j], j])) if ok[:, j].any() else -1 for j in range(NS - 1)]
 for j in range(0, NS - 1, 8):
     print(" ".join(f"{v:7d}" for v in med[j:j + 8]))
