@@ -410,7 +410,12 @@ __global__ void __launch_bounds__(256, ATTN_FWD_WPS) fwd2_kernel(AttnArgs a) {
   store(0);
   __syncthreads();
   const int ntiles = (a.Lk + 63) / 64;
-  for (int t = 0; t < ntiles; ++t) {
+  // lazy rescale (defer-max): a row's running max m moves only when a tile's max exceeds it by more than 8 in
+  // log2 units, decided per wave; otherwise p = 2^(x*sl2 - m*sl2) <= 2^8 and O, l keep their scale (no alpha
+  // exp, no O multiply on most tiles). The softmax result is unchanged; only rounding differs.
+  const float th_raw = 8.f / sl2;
+  auto tile = [&](const int t, auto mc) {
+    constexpr bool MT = decltype(mc)::value;  // this tile adds the 0/-inf mask row
     const int cur = t & 1, k0 = t * 64;
     if (t + 1 < ntiles) load(k0 + 64);
     const unsigned char* kimg = kbuf[cur];
@@ -434,7 +439,7 @@ __global__ void __launch_bounds__(256, ATTN_FWD_WPS) fwd2_kernel(AttnArgs a) {
     // compiled to an add plus a select per score on every tile. The dropout scale 1/(1-p) is applied to O once
     // at the end, not per kept probability.
     f32x2_t mrow[4][2];
-    if constexpr (MASK) {
+    if constexpr (MT) {
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb) {
         const float4 mv4 = *(const float4*)(&mbuf[cur][kb * 16 + 4 * g]);
@@ -457,7 +462,7 @@ __global__ void __launch_bounds__(256, ATTN_FWD_WPS) fwd2_kernel(AttnArgs a) {
             const int kl = kb * 16 + 4 * g + 2 * jj + toff;
             x = gr2 * f32x2_t{tbuf[cur][kl], tbuf[cur][kl + 1]} + x;
           }
-          if constexpr (MASK) x += mrow[kb][jj];
+          if constexpr (MT) x += mrow[kb][jj];
           p[gq][kb][2 * jj] = x.x;
           p[gq][kb][2 * jj + 1] = x.y;
         }
@@ -465,10 +470,17 @@ __global__ void __launch_bounds__(256, ATTN_FWD_WPS) fwd2_kernel(AttnArgs a) {
       }
       tmax = xmax16(tmax);
       tmax = xmax32(tmax);
-      const float mn = fmaxf(m[gq], tmax);
-      const float mref = (mn == -INFINITY) ? 0.f : mn;  // all-masked so far: exp2(-inf) = 0
+      if (__any(tmax > m[gq] + th_raw)) {  // wave-uniform: rescale O and l to the new running max
+        const float mn = fmaxf(m[gq], tmax);
+        const float mref = (mn == -INFINITY) ? 0.f : mn;
+        const float alpha = __builtin_amdgcn_exp2f((m[gq] - mref) * sl2);
+        l[gq] *= alpha;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) o[gq][d] *= alpha;
+        m[gq] = mn;
+      }
+      const float mref = (m[gq] == -INFINITY) ? 0.f : m[gq];  // all-masked so far: exp2(-inf) = 0
       const float nbias = -mref * sl2;
-      const float alpha = __builtin_amdgcn_exp2f((m[gq] - mref) * sl2);
       const f32x2_t sl2v = {sl2, sl2}, nb2 = {nbias, nbias};
       f32x2_t ls2 = {0.f, 0.f};
       uint64_t bits = 0;
@@ -504,10 +516,7 @@ __global__ void __launch_bounds__(256, ATTN_FWD_WPS) fwd2_kernel(AttnArgs a) {
           if (g == 0 && qv[gq]) a.dbits[((long)bh * ntiles + t) * a.Lq + q[gq]] = ((uint64_t)hi << 32) | lo;
         }
       }
-      l[gq] = l[gq] * alpha + ls;
-      m[gq] = mn;
-#pragma unroll
-      for (int d = 0; d < 4; ++d) o[gq][d] *= alpha;
+      l[gq] += ls;
     }
     // O^T += V^T P^T for both query groups (one tr-read A fragment, two MFMAs)
     {
@@ -539,6 +548,13 @@ __global__ void __launch_bounds__(256, ATTN_FWD_WPS) fwd2_kernel(AttnArgs a) {
       store(cur ^ 1);
       __syncthreads();
     }
+  };
+  // the mask row only where it can be non-zero: every tile with a key-padding mask, else only the ragged last one
+  if (MASK && a.key_keep != nullptr) {
+    for (int t = 0; t < ntiles; ++t) tile(t, std::integral_constant<bool, MASK>{});
+  } else {
+    for (int t = 0; t + 1 < ntiles; ++t) tile(t, std::false_type{});
+    tile(ntiles - 1, std::integral_constant<bool, MASK>{});
   }
 #pragma unroll
   for (int gq = 0; gq < NG; ++gq) {
@@ -666,7 +682,9 @@ __global__ void __launch_bounds__(64 * NW, 1) fwd3_kernel(AttnArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  for (int t = 0; t < ntiles; ++t) {
+  const float th_raw = 8.f / sl2;  // lazy rescale threshold (raw score units), as in fwd2_kernel
+  auto tile = [&](const int t, auto mc) {
+    constexpr bool MT = decltype(mc)::value;  // this tile adds the mask row
     const int k0 = t * 64;
     const unsigned char* kimg = kres + k0 * 128;
     const unsigned char* vimg = vres + k0 * 128;
@@ -683,7 +701,7 @@ __global__ void __launch_bounds__(64 * NW, 1) fwd3_kernel(AttnArgs a) {
       }
     }
     f32x2_t mrow[4][2];
-    if constexpr (MASK) {
+    if constexpr (MT) {
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb) {
         const float4 mv4 = *(const float4*)(&mfull[k0 + kb * 16 + 4 * g]);
@@ -706,7 +724,7 @@ __global__ void __launch_bounds__(64 * NW, 1) fwd3_kernel(AttnArgs a) {
             const int kl = kb * 16 + 4 * g + 2 * jj + toff;
             x = gr2 * f32x2_t{tfull[kl], tfull[kl + 1]} + x;
           }
-          if constexpr (MASK) x += mrow[kb][jj];
+          if constexpr (MT) x += mrow[kb][jj];
           p[gq][kb][2 * jj] = x.x;
           p[gq][kb][2 * jj + 1] = x.y;
         }
@@ -714,10 +732,17 @@ __global__ void __launch_bounds__(64 * NW, 1) fwd3_kernel(AttnArgs a) {
       }
       tmax = xmax16(tmax);
       tmax = xmax32(tmax);
-      const float mn = fmaxf(m[gq], tmax);
-      const float mref = (mn == -INFINITY) ? 0.f : mn;
+      if (__any(tmax > m[gq] + th_raw)) {
+        const float mn = fmaxf(m[gq], tmax);
+        const float mref = (mn == -INFINITY) ? 0.f : mn;
+        const float alpha = __builtin_amdgcn_exp2f((m[gq] - mref) * sl2);
+        l[gq] *= alpha;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) o[gq][d] *= alpha;
+        m[gq] = mn;
+      }
+      const float mref = (m[gq] == -INFINITY) ? 0.f : m[gq];
       const float nbias = -mref * sl2;
-      const float alpha = __builtin_amdgcn_exp2f((m[gq] - mref) * sl2);
       const f32x2_t sl2v = {sl2, sl2}, nb2 = {nbias, nbias};
       f32x2_t ls2 = {0.f, 0.f};
       uint64_t bits = 0;
@@ -759,10 +784,7 @@ __global__ void __launch_bounds__(64 * NW, 1) fwd3_kernel(AttnArgs a) {
           if (g == 0 && qv[gq]) a.dbits[((long)bh * ntiles + t) * a.Lq + q[gq]] = ((uint64_t)hi << 32) | lo;
         }
       }
-      l[gq] = l[gq] * alpha + ls;
-      m[gq] = mn;
-#pragma unroll
-      for (int d = 0; d < 4; ++d) o[gq][d] *= alpha;
+      l[gq] += ls;
     }
     {
       const int qq = i >> 2, pp = i & 3;
@@ -789,6 +811,12 @@ __global__ void __launch_bounds__(64 * NW, 1) fwd3_kernel(AttnArgs a) {
         }
       }
     }
+  };
+  if (MASK && a.key_keep != nullptr) {
+    for (int t = 0; t < ntiles; ++t) tile(t, std::integral_constant<bool, MASK>{});
+  } else {
+    for (int t = 0; t + 1 < ntiles; ++t) tile(t, std::false_type{});
+    tile(ntiles - 1, std::integral_constant<bool, MASK>{});
   }
 #pragma unroll
   for (int gq = 0; gq < NG; ++gq) {

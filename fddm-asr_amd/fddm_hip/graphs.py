@@ -56,10 +56,24 @@ class GraphedEncoder:
             out = self.enc.project(bb.stage_rest(h1))
         return SimpleNamespace(inp=inp, h0=h0, h1=h1, out=out, gA=gA, gC=gC)
 
+    def _weights_token(self):
+        """Identity of the weights the graphs read: the backbone's prepared (cast / permuted) weight set — rebuilt
+        when the module is moved, loaded or changed in place — and encoder.proj. A change drops every captured
+        graph (they would read freed or stale buffers) and the next run recaptures."""
+        enc = self.enc
+        P = enc.backbone._prepared(rt.compute_dtype())
+        proj = getattr(enc, "proj", None)
+        pw = getattr(proj, "weight", None) if getattr(enc, "use_proj", False) else None
+        return (id(P), None if pw is None else (pw.data_ptr(), pw._version)), P
+
     @torch.no_grad()
     def run(self, wave, slot: int, cap: int = 0):
         """The encoder's features for `wave` in slot `slot`'s static output buffer (valid until this slot is run
         again), on the current stream."""
+        tok, P = self._weights_token()
+        if tok != getattr(self, "_tok", None):
+            self.cache.clear()
+            self._tok, self._P = tok, P          # the captured launches read these buffers: keep them alive
         key = (tuple(wave.shape), wave.dtype, str(wave.device), rt.precision(), int(cap),
                int(getattr(self.enc.backbone, "conv_cus", 0)))   # grid sizes are part of the captured launches
         slots = self.cache.setdefault(key, [None] * self.nslots)

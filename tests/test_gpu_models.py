@@ -232,3 +232,60 @@ def test_bf16_kl_gradient_handover_matches_fp32_gradient_path(with_lfd):
     for n in grads[0]:
         close(grads[0][n], grads[1][n], rtol=2e-2, atol=1e-6, what=n)
     assert any(g.abs().max().item() > 0 for g in grads[0].values())
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("geom,d", [(SMALL_WAVLM, 128), ({}, 768), ({}, 512)])
+def test_graphed_encoder_slots_match_eager(prec, geom, d):
+    """train._encoded's HIP-graph replay of the frozen encoder (fddm_hip/graphs.py: two slots, a private memory pool
+    each) yields, for every batch, the eager forward's features — at the yield and still after main-stream work
+    that allocates and writes memory while the next batch is encoded on the side stream (a shared pool let slot 0's
+    replay overwrite slot 1's output; the split-K memset node raced the GEMM on replays). bf16: bit-identical;
+    fp32: within 1e-5 of the feature scale (split-K f32 atomics sum in launch order)."""
+    import train as T_
+    rt = _rt()
+
+    class Opt:
+        param_groups = [{"params": []}]
+
+    with rt.use_precision(prec):
+        enc = _encoder(geom, d)
+        gen = torch.Generator().manual_seed(3)
+        sec = 1 if geom else 4
+        loader = [(0.1 * torch.randn(2, 16000 * sec, generator=gen), torch.zeros(2, 8, dtype=torch.long))
+                  for _ in range(5)]
+        got = []
+        for c, _, _ in T_._encoded(enc, loader, dev, Opt()):
+            a = c.float().clone()
+            junk = [torch.randn(2048, 2048, device=dev) for _ in range(3)]
+            for _ in range(3):
+                junk[0] = junk[1] @ junk[2] + junk[0]
+            del junk
+            got.append((a, c.float().clone()))
+        torch.cuda.synchronize()
+        refs = [enc(w.to(dev))[0].float() for w, _ in loader]
+    for i, ((a, b), r) in enumerate(zip(got, refs)):
+        tol = 0.0 if prec == "bf16" else 1e-5 * float(r.abs().max())
+        assert float((a - r).abs().max()) <= tol, f"batch {i} at yield"
+        assert float((b - r).abs().max()) <= tol, f"batch {i} after main-stream work"
+
+
+def test_graphed_encoder_recaptures_after_weight_change():
+    """Changing a frozen encoder's parameters in place (or its projection) between replays: the graph runner sees
+    the re-prepared weights and recaptures, so replays follow the new weights (no stale or freed buffers)."""
+    from fddm_hip.graphs import GraphedEncoder
+    rt = _rt()
+    with rt.use_precision("bf16"):
+        enc = _encoder(SMALL_WAVLM, 96)
+        assert enc.use_proj
+        ge = GraphedEncoder(enc)
+        w = 0.1 * torch.randn(2, 16000, generator=torch.Generator().manual_seed(5)).to(dev)
+        first = ge.run(w, 0).float().clone()
+        with torch.no_grad():
+            enc.backbone.encoder.layers[0].feed_forward.output_dense.weight.mul_(1.5)
+            enc.proj.weight.add_(0.01)
+        again = ge.run(w, 0).float().clone()
+        ref = enc(w)[0].float()
+        torch.cuda.synchronize()
+    assert float((again - ref).abs().max()) == 0.0
+    assert float((again - first).abs().max()) > 0.0
