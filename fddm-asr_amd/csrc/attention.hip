@@ -813,7 +813,13 @@ __global__ void __launch_bounds__(64 * NW, 1) fwd3_kernel(AttnArgs a) {
     }
   };
   if (MASK && a.key_keep != nullptr) {
-    for (int t = 0; t < ntiles; ++t) tile(t, std::integral_constant<bool, MASK>{});
+    // key tiles whose 64 keys are all padding add exactly nothing (exp(-inf) = 0): skipped (wave-uniform flags;
+    // their dropout words are never read — dQ skips the same tiles and dK/dV zeroes masked keys)
+    unsigned tmask = 0;
+    for (int t = 0; t < ntiles; ++t)
+      if (__any(key_ok(a, b, 64 * t + lane))) tmask |= 1u << t;
+    for (int t = 0; t < ntiles; ++t)
+      if ((tmask >> t) & 1u) tile(t, std::integral_constant<bool, MASK>{});
   } else {
     for (int t = 0; t + 1 < ntiles; ++t) tile(t, std::false_type{});
     tile(ntiles - 1, std::integral_constant<bool, MASK>{});
@@ -1105,7 +1111,8 @@ __global__ void __launch_bounds__(256, 2) dq2_kernel(AttnArgs a) {
   store(0);
   __syncthreads();
   const int ntiles = (a.Lk + 63) / 64;
-  for (int t = 0; t < ntiles; ++t) {
+  auto tile = [&](const int t, auto mc) {
+    constexpr bool MT = decltype(mc)::value;  // this tile adds the mask row (see fwd2_kernel)
     const int cur = t & 1, k0 = t * 64;
     if (t + 1 < ntiles) load(k0 + 64);
     f32x4_t s[2][4], dp[2][4];
@@ -1123,7 +1130,7 @@ __global__ void __launch_bounds__(256, 2) dq2_kernel(AttnArgs a) {
       }
     }
     float mrow[4][4];
-    if constexpr (MASK) {
+    if constexpr (MT) {
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb) {
         const float4 m4 = *(const float4*)(&mbuf[cur][kb * 16 + 4 * g]);
@@ -1150,7 +1157,7 @@ __global__ void __launch_bounds__(256, 2) dq2_kernel(AttnArgs a) {
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj) {
           f32x2_t off = {-lse2[gq], -lse2[gq]};
-          if constexpr (MASK) off += f32x2_t{mrow[kb][2 * jj], mrow[kb][2 * jj + 1]};
+          if constexpr (MT) off += f32x2_t{mrow[kb][2 * jj], mrow[kb][2 * jj + 1]};
           const f32x2_t arg = f32x2_t{s[gq][kb][2 * jj], s[gq][kb][2 * jj + 1]} * sl2v + off;
           const f32x2_t pr = {__builtin_amdgcn_exp2f(arg.x), __builtin_amdgcn_exp2f(arg.y)};
           f32x2_t dpv = {dp[gq][kb][2 * jj], dp[gq][kb][2 * jj + 1]};
@@ -1171,6 +1178,22 @@ __global__ void __launch_bounds__(256, 2) dq2_kernel(AttnArgs a) {
       store(cur ^ 1);
       __syncthreads();
     }
+  };
+  if (MASK && a.key_keep != nullptr) {
+    unsigned tmask = 0;  // fully padded key tiles, skipped as in fwd3_kernel
+    for (int t = 0; t < ntiles; ++t)
+      if (__any(key_ok(a, b, 64 * t + lane))) tmask |= 1u << (t & 31);
+    for (int t = 0; t < ntiles; ++t) {
+      if (ntiles > 32 || ((tmask >> t) & 1u)) tile(t, std::integral_constant<bool, MASK>{});
+      else if (t + 1 < ntiles) {  // keep the tile pipeline: the next tile's loads, stores and barrier
+        if (t + 1 < ntiles) load((t + 1) * 64);
+        store((t & 1) ^ 1);
+        __syncthreads();
+      }
+    }
+  } else {
+    for (int t = 0; t + 1 < ntiles; ++t) tile(t, std::false_type{});
+    tile(ntiles - 1, std::integral_constant<bool, MASK>{});
   }
 #pragma unroll
   for (int gq = 0; gq < 2; ++gq) {
@@ -1265,7 +1288,8 @@ __global__ void __launch_bounds__(256, (DM == 1 ? 1 : 2)) dkv2_kernel(AttnArgs a
   load(0);
   store(0);
   __syncthreads();
-  const int ntiles = (a.Lq + 63) / 64;
+  // a block whose 128 keys are all padding: zero dK / dV (epilogue), no query loop
+  const int ntiles = __syncthreads_or(kok[0] || kok[1]) ? (a.Lq + 63) / 64 : 0;
   for (int t = 0; t < ntiles; ++t) {
     const int cur = t & 1, q0 = t * 64;
     if (t + 1 < ntiles) load(q0 + 64);
