@@ -150,6 +150,9 @@ __global__ void __launch_bounds__(512) gemm256_kernel(GemmArgs g) {
       }
   };
   auto issue = [&](int h, int buf, int v0, int v1, int so) {  // so: scalar byte offset
+#ifdef G256_NODMA  // timing diagnostic only: operand tiles never loaded (garbage results)
+    if (so != -12345) return;
+#endif
     lptr_t d = (lptr_t)(smem + buf * STAGE + h * HALF + wid * 2048);
     const __amdgpu_buffer_rsrc_t& r = h < 2 ? rA : rB;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, d, 16, v0, so, 0, 0);
@@ -290,6 +293,11 @@ __global__ void __launch_bounds__(512) gemm256_kernel(GemmArgs g) {
   const unsigned badr[2] = {lds0 + wc * 4096 + swz_kc(fr, fg), lds0 + wc * 4096 + swz_kc(fr, 4 + fg)};
   auto readA = [&](int buf, auto hc) {
     constexpr int h = decltype(hc)::value;
+#ifdef G256_NOREAD  // timing diagnostic only: no fragment reads (MFMAs on stale registers)
+    asm volatile("" : "+v"(af[0][0]), "+v"(af[1][0]), "+v"(af[2][0]), "+v"(af[3][0]), "+v"(af[0][1]), "+v"(af[1][1]),
+                 "+v"(af[2][1]), "+v"(af[3][1]));
+    if (buf >= 0) return;
+#endif
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const unsigned a = aadr[s] + buf * STAGE;
@@ -301,6 +309,10 @@ __global__ void __launch_bounds__(512) gemm256_kernel(GemmArgs g) {
   };
   auto readB = [&](int buf, auto hc, u32x4_t(&bf)[2][2]) {
     constexpr int h = decltype(hc)::value;
+#ifdef G256_NOREAD
+    asm volatile("" : "+v"(bf[0][0]), "+v"(bf[1][0]), "+v"(bf[0][1]), "+v"(bf[1][1]));
+    if (buf >= 0) return;
+#endif
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const unsigned a = badr[s] + buf * STAGE;
