@@ -149,14 +149,34 @@ __global__ void __launch_bounds__(512) gemm256_kernel(GemmArgs g) {
         v[h][i] = (b * (int)g.sAb + tt * (int)(g.geo.cstride * g.lda) + c * 8) * 2;
       }
   };
-  auto issue = [&](int h, int buf, int v0, int v1, int so) {  // so: scalar byte offset
+  // A half-tile is 2 LDS-DMA instructions per wave. In the K loop (split = true) the first is issued in the load
+  // segment and the second is left pending and issued between the MFMAs of the following compute segment (mma):
+  // the load segment — which bounds each barrier interval — carries one DMA issue instead of two.
+  int pd_v = 0, pd_so = 0;
+  lptr_t pd_d = nullptr;
+  bool pd_b = false;
+  auto issue = [&](int h, int buf, int v0, int v1, int so, bool split = false) {  // so: scalar byte offset
 #ifdef G256_NODMA  // timing diagnostic only: operand tiles never loaded (garbage results)
     if (so != -12345) return;
 #endif
     lptr_t d = (lptr_t)(smem + buf * STAGE + h * HALF + wid * 2048);
     const __amdgpu_buffer_rsrc_t& r = h < 2 ? rA : rB;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, d, 16, v0, so, 0, 0);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lptr_t)((unsigned char*)d + 1024), 16, v1, so, 0, 0);
+    if (split) {
+      pd_d = (lptr_t)((unsigned char*)d + 1024);
+      pd_v = v1;
+      pd_so = so;
+      pd_b = h >= 2;
+    } else {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lptr_t)((unsigned char*)d + 1024), 16, v1, so, 0, 0);
+    }
+  };
+  auto issue_pending = [&]() {
+#ifdef G256_NODMA
+    if (pd_so != -12345) return;
+#endif
+    if (pd_b) __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, pd_d, 16, pd_v, pd_so, 0, 0);
+    else __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, pd_d, 16, pd_v, pd_so, 0, 0);
   };
   const int nk = (int)(g.K / 64);
   const int cshift = CONV ? __builtin_ctz((unsigned)(g.geo.Cg / 64)) : 0;  // K-tiles per conv tap = 2^cshift
@@ -173,12 +193,12 @@ __global__ void __launch_bounds__(512) gemm256_kernel(GemmArgs g) {
     conv_rows(vcn, nm0);
   }
   // half h of K-tile kt of the tile at (m0, n0) [conv: lane offsets vc]
-  auto issueA = [&](int h, int buf, int kt, int m0, const int (&vc)[2][2]) {
-    if (CONV) issue(h, buf, vc[h][0], vc[h][1], koffA(kt));
-    else issue(h, buf, va[0], va[1], m0 * lda * 2 + h * 64 * lda * 2 + koffA(kt));
+  auto issueA = [&](int h, int buf, int kt, int m0, const int (&vc)[2][2], bool split = false) {
+    if (CONV) issue(h, buf, vc[h][0], vc[h][1], koffA(kt), split);
+    else issue(h, buf, va[0], va[1], m0 * lda * 2 + h * 64 * lda * 2 + koffA(kt), split);
   };
-  auto issueB = [&](int h, int buf, int kt, int n0) {
-    issue(h, buf, vb[0], vb[1], n0 * ldb * 2 + (h - 2) * 32 * ldb * 2 + kt * 128);
+  auto issueB = [&](int h, int buf, int kt, int n0, bool split = false) {
+    issue(h, buf, vb[0], vb[1], n0 * ldb * 2 + (h - 2) * 32 * ldb * 2 + kt * 128, split);
   };
 
   // ---------------------------------------------------------------- bias
@@ -327,7 +347,7 @@ __global__ void __launch_bounds__(512) gemm256_kernel(GemmArgs g) {
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i) {
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -335,6 +355,12 @@ __global__ void __launch_bounds__(512) gemm256_kernel(GemmArgs g) {
           acc[ib + i][jb + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
               __builtin_bit_cast(bf16x8_t, bf[j][s]), __builtin_bit_cast(bf16x8_t, af[i][s]), acc[ib + i][jb + j], 0, 0,
               0);
+      if (i == 1) {  // the load segment's second DMA instruction, behind 8 MFMAs
+        __builtin_amdgcn_sched_barrier(0);
+        issue_pending();
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
     __builtin_amdgcn_s_setprio(0);
     bar();
   };
@@ -394,28 +420,29 @@ __global__ void __launch_bounds__(512) gemm256_kernel(GemmArgs g) {
     // ---- phase 1: A rows 0..63 x B cols 0..31
     readA(bc, IC<HA0>{});
     load_bias(nn0, n1b);
-    issueB(HB1, bn, kt1, n1);
-    wait3(mode, IC<9>{}, IC<9>{}, IC<9 + 4 * SPQ>{});  // B1(T)
+    issueB(HB1, bn, kt1, n1, true);
+    // counts: VMEM instructions issued after the awaited half's second (pending) instruction
+    wait3(mode, IC<8>{}, IC<8>{}, IC<8 + 3 * SPQ>{});  // B1(T)
     if (EP) epi_quadrant(IC<0>{}, em0, en0, true);
     mma(0, 0, b0);
     // ---- phase 2: A rows 0..63 x B cols 32..63
     readB(bc, IC<HB1>{}, b1);
-    if (CONV) issueA(HA1, bn, kt1, m1, n1b ? vcn : vcc);
-    else issueA(HA1, bn, kt1, m1, vcc);
-    wait3(mode, IC<9>{}, IC<9 + SPQ>{}, IC<9 + 3 * SPQ>{});  // A1(T)
+    if (CONV) issueA(HA1, bn, kt1, m1, n1b ? vcn : vcc, true);
+    else issueA(HA1, bn, kt1, m1, vcc, true);
+    wait3(mode, IC<8>{}, IC<8 + SPQ>{}, IC<8 + 2 * SPQ>{});  // A1(T)
     if (EP) epi_quadrant(IC<1>{}, em0, en0, true);
     mma(0, 2, b1);
     // ---- phase 3: A rows 64..127 x B cols 0..31
     readA(bc, IC<HA1>{});
-    if (CONV) issueA(HA0, bc, kt2, m2, n2 ? vcn : vcc);
-    else issueA(HA0, bc, kt2, m2, vcc);
-    wait3(mode, IC<7>{}, IC<7 + 2 * SPQ>{}, IC<7 + SPQ>{});  // B0(T+1)
+    if (CONV) issueA(HA0, bc, kt2, m2, n2 ? vcn : vcc, true);
+    else issueA(HA0, bc, kt2, m2, vcc, true);
+    wait3(mode, IC<6>{}, IC<6 + 2 * SPQ>{}, IC<6>{});  // B0(T+1)
     if (EP) epi_quadrant(IC<2>{}, em0, en0, true);
     mma(4, 0, b0);
     // ---- phase 4: A rows 64..127 x B cols 32..63; B0 fragments of K-tile T+1
     readB(bn, IC<HB0>{}, b0);
-    issueB(HB0, bc, kt2, n2c);
-    wait3(mode, IC<11>{}, IC<11 + 3 * SPQ>{}, IC<11 + 2 * SPQ>{});  // A0(T+1)
+    issueB(HB0, bc, kt2, n2c, true);
+    wait3(mode, IC<10>{}, IC<10 + 3 * SPQ>{}, IC<10 + SPQ>{});  // A0(T+1)
     if (EP) epi_quadrant(IC<3>{}, em0, en0, true);
     mma(4, 2, b1);
   };
