@@ -41,6 +41,13 @@ typedef int i32x4_t __attribute__((ext_vector_type(4)));
 #ifndef G256_GM
 #define G256_GM 4
 #endif
+// Both LDS-DMA instructions of a half-tile are issued between the MFMAs of the compute segment that follows the
+// load segment which used to issue them (steady K-tile at the WavLM FF1 shape: 3256 cycles with both in the load
+// segment, 3080 with one deferred, 2972-2984 with both; tools/g256_stamps.py). -DG256_DEFER1 keeps one in the
+// load segment.
+#ifndef G256_DEFER1
+#define G256_DEFER2
+#endif
 constexpr int BM = 256, BN = 256, HALF = 16384, STAGE = 4 * HALF, LDS_BYTES = 2 * STAGE, GM = G256_GM;
 constexpr unsigned SRD_W3 = 0x00020000u;  // buffer resource word 3 (raw dword access) on gfx9xx
 enum { HA0 = 0, HA1 = 1, HB0 = 2, HB1 = 3 };
@@ -149,11 +156,15 @@ __global__ void __launch_bounds__(512) gemm256_kernel(GemmArgs g) {
         v[h][i] = (b * (int)g.sAb + tt * (int)(g.geo.cstride * g.lda) + c * 8) * 2;
       }
   };
-  // A half-tile is 2 LDS-DMA instructions per wave. In the K loop (split = true) the first is issued in the load
-  // segment and the second is left pending and issued between the MFMAs of the following compute segment (mma):
-  // the load segment — which bounds each barrier interval — carries one DMA issue instead of two.
+  // A half-tile is 2 LDS-DMA instructions per wave. In the K loop (split = true) they are left pending and issued
+  // between the MFMAs of the following compute segment (mma) — G256_DEFER1: only the second — so the load segment,
+  // which bounds each barrier interval (fragment reads + wait), carries no DMA issue.
   int pd_v = 0, pd_so = 0;
   lptr_t pd_d = nullptr;
+#ifdef G256_DEFER2
+  int pd0_v = 0;
+  lptr_t pd0_d = nullptr;
+#endif
   bool pd_b = false;
   auto issue = [&](int h, int buf, int v0, int v1, int so, bool split = false) {  // so: scalar byte offset
 #ifdef G256_NODMA  // timing diagnostic only: operand tiles never loaded (garbage results)
@@ -161,6 +172,12 @@ __global__ void __launch_bounds__(512) gemm256_kernel(GemmArgs g) {
 #endif
     lptr_t d = (lptr_t)(smem + buf * STAGE + h * HALF + wid * 2048);
     const __amdgpu_buffer_rsrc_t& r = h < 2 ? rA : rB;
+#ifdef G256_DEFER2
+    if (split) {
+      pd0_d = d;
+      pd0_v = v0;
+    } else
+#endif
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, d, 16, v0, so, 0, 0);
     if (split) {
       pd_d = (lptr_t)((unsigned char*)d + 1024);
@@ -355,7 +372,17 @@ __global__ void __launch_bounds__(512) gemm256_kernel(GemmArgs g) {
           acc[ib + i][jb + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
               __builtin_bit_cast(bf16x8_t, bf[j][s]), __builtin_bit_cast(bf16x8_t, af[i][s]), acc[ib + i][jb + j], 0, 0,
               0);
+#ifdef G256_DEFER2
+      if (i == 0) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (pd_b) __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, pd0_d, 16, pd0_v, pd_so, 0, 0);
+        else __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, pd0_d, 16, pd0_v, pd_so, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (i == 2) {
+#else
       if (i == 1) {  // the load segment's second DMA instruction, behind 8 MFMAs
+#endif
         __builtin_amdgcn_sched_barrier(0);
         issue_pending();
         __builtin_amdgcn_sched_barrier(0);
@@ -408,6 +435,11 @@ __global__ void __launch_bounds__(512) gemm256_kernel(GemmArgs g) {
     else if (mode == 1) vmcnt<decltype(nec)::value>();
     else vmcnt<decltype(npc)::value>();
   };
+#ifdef G256_DEFER2
+  constexpr int D2 = 1;  // both DMA instructions of a half deferred: one fewer issued before each wait
+#else
+  constexpr int D2 = 0;
+#endif
   auto ktile = [&](int T, int mode) {
     const bool EP = mode == 1;
     const int bc = T & 1, bn = bc ^ 1;
@@ -422,27 +454,27 @@ __global__ void __launch_bounds__(512) gemm256_kernel(GemmArgs g) {
     load_bias(nn0, n1b);
     issueB(HB1, bn, kt1, n1, true);
     // counts: VMEM instructions issued after the awaited half's second (pending) instruction
-    wait3(mode, IC<8>{}, IC<8>{}, IC<8 + 3 * SPQ>{});  // B1(T)
+    wait3(mode, IC<8 - D2>{}, IC<8 - D2>{}, IC<8 - D2 + 3 * SPQ>{});  // B1(T)
     if (EP) epi_quadrant(IC<0>{}, em0, en0, true);
     mma(0, 0, b0);
     // ---- phase 2: A rows 0..63 x B cols 32..63
     readB(bc, IC<HB1>{}, b1);
     if (CONV) issueA(HA1, bn, kt1, m1, n1b ? vcn : vcc, true);
     else issueA(HA1, bn, kt1, m1, vcc, true);
-    wait3(mode, IC<8>{}, IC<8 + SPQ>{}, IC<8 + 2 * SPQ>{});  // A1(T)
+    wait3(mode, IC<8 - D2>{}, IC<8 - D2 + SPQ>{}, IC<8 - D2 + 2 * SPQ>{});  // A1(T)
     if (EP) epi_quadrant(IC<1>{}, em0, en0, true);
     mma(0, 2, b1);
     // ---- phase 3: A rows 64..127 x B cols 0..31
     readA(bc, IC<HA1>{});
     if (CONV) issueA(HA0, bc, kt2, m2, n2 ? vcn : vcc, true);
     else issueA(HA0, bc, kt2, m2, vcc, true);
-    wait3(mode, IC<6>{}, IC<6 + 2 * SPQ>{}, IC<6>{});  // B0(T+1)
+    wait3(mode, IC<6 - D2>{}, IC<6 - D2 + 2 * SPQ>{}, IC<6 - D2>{});  // B0(T+1)
     if (EP) epi_quadrant(IC<2>{}, em0, en0, true);
     mma(4, 0, b0);
     // ---- phase 4: A rows 64..127 x B cols 32..63; B0 fragments of K-tile T+1
     readB(bn, IC<HB0>{}, b0);
     issueB(HB0, bc, kt2, n2c, true);
-    wait3(mode, IC<10>{}, IC<10 + 3 * SPQ>{}, IC<10 + SPQ>{});  // A0(T+1)
+    wait3(mode, IC<10 - D2>{}, IC<10 - D2 + 3 * SPQ>{}, IC<10 - D2 + SPQ>{});  // A0(T+1)
     if (EP) epi_quadrant(IC<3>{}, em0, en0, true);
     mma(4, 2, b1);
   };
