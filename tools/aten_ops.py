@@ -26,7 +26,7 @@ def main():
     with profile(activities=[ProfilerActivity.CPU], with_stack=True) as prof:
         gs, _ = T_.train_one_epoch(enc, dec, sp, te, tp, sch, batches, opt, dev, cfg, gs, None, 0, False)
         torch.cuda.synchronize()
-    want = ("aten::fill_", "aten::zero_", "aten::copy_", "aten::cat", "aten::stack", "aten::clone", "aten::add",
+    want = ("aten::fill_", "aten::zero_", "aten::copy_", "aten::zeros", "aten::zero_", "aten::copy_", "aten::cat", "aten::stack", "aten::clone", "aten::add",
             "aten::mul", "aten::sum", "aten::mean", "aten::index", "aten::ne", "aten::eq", "aten::to",
             "aten::contiguous", "aten::where", "aten::expand", "aten::zeros", "aten::ones", "aten::empty")
     cnt = Counter()
@@ -35,9 +35,12 @@ def main():
             continue
         src = "?"
         for fr in (ev.stack or []):
-            if "/repo/" in fr and "torch/" not in fr:
-                src = fr.split("/repo/")[-1]
+            if ("fddm" in fr or "bench" in fr or "train" in fr or "models" in fr) and "site-packages" not in fr \
+                    and "dist-packages" not in fr:
+                src = fr.split("/")[-1] if "/" in fr else fr
                 break
+        if src == "?" and ev.stack:
+            src = "|".join(f.split("/")[-1] for f in ev.stack[:3])
         cnt[(ev.name, src)] += 1
     for (name, src), n in sorted(cnt.items(), key=lambda kv: -kv[1]):
         print(f"{n / 4:6.1f}/step  {name:18s} {src}")
