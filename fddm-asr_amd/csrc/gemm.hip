@@ -718,6 +718,7 @@ FDDM_API int fddm_gemm(int dtype, int a_dtype, int a_kc, int b_kc, int epi, int 
   if (a_kc ? (K % ech || lda % ech || sAb % ech) : (M % ech || lda % ech)) return (int)hipErrorInvalidValue;
   if (b_kc ? (K % ech || ldb % ech) : (N % ech || ldb % ech)) return (int)hipErrorInvalidValue;
   if (((uintptr_t)A & 15) || ((uintptr_t)B & 15)) return (int)hipErrorInvalidValue;
+  if (!C || ((epi == EPI_GELU || epi == EPI_DGELU) && !C2)) return (int)hipErrorInvalidValue;  // second output
   if (!a_kc && Mi > 0 && Mi != M) return (int)hipErrorInvalidValue;
   if (Mi <= 0) Mi = 1L << 62;
   GemmArgs g{A, lda, Mi, sAb, B, ldb, C, ldc, C2, bias, alpha, M, N, K, seed, stream, 0u, 1.f, ConvGeo{1, 0, 0, 0}, 0, 0, 0, 0, K, nullptr};

@@ -5,7 +5,7 @@
 //
 // Persistent: one 512-thread workgroup per CU walks its tiles back to back through ONE continuous LDS-DMA
 // pipeline — the first K-tiles of tile i+1 are in flight while tile i finishes, and tile i's results are
-// stored from registers one quadrant per phase during tile i+1's first K-tile, so neither the prologue
+// stored from registers in phase 1 of tile i+1's first K-tile, so neither the prologue
 // latency nor the store drain is exposed per tile. Tile order: each XCD owns a contiguous range of a
 // grouped (4 M-rows x all N-tiles) ordering, so the ~32 tiles an XCD runs at once share A and B panels in
 // its L2.
@@ -18,14 +18,14 @@
 //   {0..31} / {32..63}). Every image is [128 rows][128 B] with the XOR chunk swizzle swz_kc (conflict-free
 //   ds_read_b128), filled by global_load_lds_dwordx4 (1 KB = 8 rows per wave instruction; the swizzle is
 //   applied to the SOURCE address).
-// K-tile = 4 phases; each phase = [epilogue quadrant of the previous tile (first K-tile only), fragment
+// K-tile = 4 phases; each phase = [the previous tile's epilogue (phase 1 of the first K-tile only), fragment
 // reads, one half-tile LDS-DMA, counted vmcnt] -> s_barrier -> 16 MFMAs (one 64x32 quadrant, K = 64) ->
 // s_barrier. The wave groups wr = 0 / 1 run one barrier apart: on every SIMD one wave issues MFMAs while its
 // partner reads LDS and issues DMA. A half-tile is re-staged >= 2 phases after its last read and read >= 4
 // phases after its DMA. Every vmcnt is exact: the wave counts each vector-memory instruction it issues
 // (DMA, bias loads, stores — all explicit, none compiler-generated) and waits for "issued since X".
 // The MFMAs compute C^T fragments (operands swapped) so a lane owns 4 consecutive columns of one row: the
-// epilogue writes 16-B buffer stores straight from the accumulators (bf16: lane pairs trade halves first).
+// epilogue writes 16-B buffer stores of whole 128-B lines from the accumulators after two lane exchanges.
 #include "gemm.h"
 #include <type_traits>
 
@@ -249,53 +249,88 @@ __global__ void __launch_bounds__(512) gemm256_kernel(GemmArgs g) {
   const i32x4_t rc = make_srd(g.C);
   const i32x4_t rc2 = make_srd(EPI == EPI_GELU ? g.C2 : g.C);
   constexpr int ESZ = (int)sizeof(OT);
-  // store instructions per quadrant: f32 8 (dwordx4 per block); bf16 4 per output (paired blocks)
-  constexpr int SPQ = sizeof(OT) == 4 ? 8 : (EPI == EPI_GELU ? 8 : 4);
-  const int vst = ((wr * 128 + fr) * ldc + wc * 64 + 4 * fg) * ESZ;
-  const int vst2 = vst + ((fg & 1) ? 12 * ESZ : 0);
+  // store instructions per half (4 row blocks x 64 columns): f32 16; bf16 8 per output
+  constexpr int SPH = sizeof(OT) == 4 ? 16 : (EPI == EPI_GELU ? 16 : 8);
+  // Every store instruction writes 8 whole rows x 128 B (full cache lines), and each group of 4 consecutive
+  // lanes 2 rows: a wave's 16 x 64 row block leaves in 2 (bf16) or 4 (f32) instructions, even rows in the
+  // first, odd rows in the second. Lane (fr, fg) writes row (fr & ~1) (+1 in the second register); fr & 1
+  // selects the column half (bf16: 32 of the wave's 64 columns, f32: 16 of a 32-column pair); cc = the 16-B
+  // chunk within it. Epilogue K-tile at the WavLM FF1 shape (tools/g256_stamps.py): 16 rows x 64 B per
+  // instruction and 4 rows per lane group, one quadrant per phase: 11.9k cycles; whole lines but 4 rows per
+  // lane group: 11.7k; whole lines, 2 rows per lane group, one half-tile per odd phase: 9.9k; the same with
+  // the whole tile in phase 1: 9.2k (steady K-tile 2956).
+  const int cc = sizeof(OT) == 4 ? 4 * fg : 4 * fg + ((fg & 1) ? 12 : 0);
+  const int vst = ((wr * 128 + (fr & ~1)) * ldc + wc * 64 + (fr & 1) * (sizeof(OT) == 4 ? 16 : 32) + cc) * ESZ;
+  const bool odd_r = fr & 1;
 
   u32x4_t af[4][2], b0[2][2], b1[2][2];
   f32x4_t acc[8][4];
 
-  // quadrant q of the finished tile at (em0, en0): blocks i in 4*(q>>1).., j in 2*(q&1)..; then (reseed)
-  // seed it with the bias of the tile that follows
-  // bf16: the two lanes 16 apart (fg, fg^1) trade packed halves (v_permlane16_swap, no LDS) so that each lane
-  // stores 8 consecutive
-  // columns (16 B) — one dwordx4 store per row block and column pair instead of two dwordx2 (store issue, not
-  // bandwidth, bounds the epilogue); odd-fg lanes write the second block of the pair
-  auto epi_quadrant = [&](auto qc, int em0, int en0, bool reseed) {
-    constexpr int q = decltype(qc)::value, ib = (q >> 1) * 4, jb = (q & 1) * 2;
-    f32x4_t bq[2];
-    if (reseed) bias_pair(jb, bq[0], bq[1]);
-    const bool odd = fg & 1;
-    auto emit = [&](const f32x4_t& a, const f32x4_t& b, const i32x4_t& r, int so) {
-      const u32x2_t pa = {pk_bf16(a[0], a[1]), pk_bf16(a[2], a[3])};
-      const u32x2_t pb = {pk_bf16(b[0], b[1]), pk_bf16(b[2], b[3])};
-      const u32x2_t x = odd ? pa : pb;
-      // v_permlane16_swap(x, x): odd 16-lane rows get x of lane-16 in [0], even rows x of lane+16 in [1]
-      const auto s0 = __builtin_amdgcn_permlane16_swap(x[0], x[0], false, false);
-      const auto s1 = __builtin_amdgcn_permlane16_swap(x[1], x[1], false, false);
-      const u32x2_t y = odd ? u32x2_t{s0[0], s1[0]} : u32x2_t{s0[1], s1[1]};
-      const u32x4_t d = odd ? u32x4_t{y[0], y[1], pb[0], pb[1]} : u32x4_t{pa[0], pa[1], y[0], y[1]};
-      store16(d, r, vst2, so);
-    };
+  // x0 / x1 hold row fr of column group 0 / 1; after the exchange (lane bit 0 <-> register) x0 holds the even
+  // and x1 the odd rows of the block, lane bit 0 selecting the column group. Lanes fr and fr ^ 1 trade through
+  // DPP quad_perm [1,0,3,2].
+  auto xchg1 = [&](u32x4_t& x0, u32x4_t& x1) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int so = ((em0 + (ib + i) * 16) * ldc + en0 + jb * 16) * ESZ;
+    for (int e = 0; e < 4; ++e) {
+      const unsigned y = odd_r ? x0[e] : x1[e];
+      const unsigned z = (unsigned)__builtin_amdgcn_mov_dpp((int)y, 0xb1, 0xf, 0xf, false);
+      x0[e] = odd_r ? z : x0[e];
+      x1[e] = odd_r ? x1[e] : z;
+    }
+  };
+  // bf16: the two lanes 16 apart (fg, fg^1) trade packed halves (v_permlane16_swap) so that each lane holds 8
+  // consecutive columns (16 B) of a 32-column pair; odd-fg lanes hold the second block of the pair
+  const bool odd = fg & 1;
+  auto chunk16 = [&](const f32x4_t& a, const f32x4_t& b) -> u32x4_t {
+    const u32x2_t pa = {pk_bf16(a[0], a[1]), pk_bf16(a[2], a[3])};
+    const u32x2_t pb = {pk_bf16(b[0], b[1]), pk_bf16(b[2], b[3])};
+    const u32x2_t x = odd ? pa : pb;
+    // v_permlane16_swap(x, x): odd 16-lane rows get x of lane-16 in [0], even rows x of lane+16 in [1]
+    const auto s0 = __builtin_amdgcn_permlane16_swap(x[0], x[0], false, false);
+    const auto s1 = __builtin_amdgcn_permlane16_swap(x[1], x[1], false, false);
+    const u32x2_t y = odd ? u32x2_t{s0[0], s1[0]} : u32x2_t{s0[1], s1[1]};
+    return odd ? u32x4_t{y[0], y[1], pb[0], pb[1]} : u32x4_t{pa[0], pa[1], y[0], y[1]};
+  };
+  // one bf16 row block (4 column blocks v) -> 2 whole-line stores
+  auto emit_bf16 = [&](const f32x4_t (&v)[4], const i32x4_t& r, int so) {
+    u32x4_t x0 = chunk16(v[0], v[1]), x1 = chunk16(v[2], v[3]);
+    xchg1(x0, x1);
+    store16(x0, r, vst, so);
+    store16(x1, r, vst, so + ldc * ESZ);
+  };
+
+  // half hh of the finished tile at (em0, en0): row blocks 4*hh .. 4*hh+3, all 4 column blocks; then (reseed)
+  // seed them with the bias of the tile that follows
+  auto epi_rows = [&](auto ibc, auto nc, int em0, int en0, bool reseed) {
+    constexpr int ib = decltype(ibc)::value, NR = decltype(nc)::value;
+    f32x4_t bq[4];
+    if (reseed) {
+      bias_pair(0, bq[0], bq[1]);
+      bias_pair(2, bq[2], bq[3]);
+    }
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int so = ((em0 + (ib + i) * 16) * ldc + en0) * ESZ;
       if constexpr (sizeof(OT) == 4) {
-        store16(__builtin_bit_cast(u32x4_t, acc[ib + i][jb]), rc, vst, so);
-        store16(__builtin_bit_cast(u32x4_t, acc[ib + i][jb + 1]), rc, vst, so + 16 * ESZ);
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          u32x4_t x0 = __builtin_bit_cast(u32x4_t, acc[ib + i][2 * p]);
+          u32x4_t x1 = __builtin_bit_cast(u32x4_t, acc[ib + i][2 * p + 1]);
+          xchg1(x0, x1);
+          store16(x0, rc, vst, so + 32 * p * ESZ);
+          store16(x1, rc, vst, so + (ldc + 32 * p) * ESZ);
+        }
       } else {
-        f32x4_t v[2] = {acc[ib + i][jb], acc[ib + i][jb + 1]};
+        f32x4_t v[4] = {acc[ib + i][0], acc[ib + i][1], acc[ib + i][2], acc[ib + i][3]};
         if constexpr (EPI == EPI_GELU) {
-          emit(v[0], v[1], rc, so);
+          emit_bf16(v, rc, so);
           const unsigned thr = g.thr16;
 #pragma unroll
-          for (int j = 0; j < 2; ++j) {
+          for (int j = 0; j < 4; ++j) {
             unsigned keep = 0xfu;
             if (thr) {  // 4 consecutive columns (N % 8 == 0): one hash
               const unsigned m = (unsigned)(em0 + wr * 128 + (ib + i) * 16 + fr);
-              const unsigned n = (unsigned)(en0 + wc * 64 + (jb + j) * 16 + 4 * fg);
+              const unsigned n = (unsigned)(en0 + wc * 64 + j * 16 + 4 * fg);
               keep = drop_keep4(g.seed, g.stream, ((uint64_t)m * (uint64_t)Nc + n) >> 2, thr);
             }
 #pragma unroll
@@ -304,20 +339,20 @@ __global__ void __launch_bounds__(512) gemm256_kernel(GemmArgs g) {
               v[j][e] = thr ? ((keep >> e) & 1u ? a * g.drop_scale : 0.f) : a;
             }
           }
-          emit(v[0], v[1], rc2, so);
+          emit_bf16(v, rc2, so);
         } else {
           if constexpr (EPI == EPI_GELU_ONLY) {
 #pragma unroll
-            for (int j = 0; j < 2; ++j)
+            for (int j = 0; j < 4; ++j)
 #pragma unroll
               for (int e = 0; e < 4; ++e) v[j][e] = gelu_f(v[j][e]);
           }
-          emit(v[0], v[1], rc, so);
+          emit_bf16(v, rc, so);
         }
       }
       if (reseed) {
-        acc[ib + i][jb] = bq[0];
-        acc[ib + i][jb + 1] = bq[1];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[ib + i][j] = bq[j];
       }
       __builtin_amdgcn_sched_barrier(0);  // one row block at a time: bounds the epilogue's live registers
     }
@@ -425,23 +460,22 @@ __global__ void __launch_bounds__(512) gemm256_kernel(GemmArgs g) {
   // One K-tile T (kt within tile ti). Issues, in order: phase 1 bias DMA (real slot on a tile's last K-tile),
   // B1(T+1); phase 2 A1(T+1); phase 3 A0(T+2); phase 4 B0(T+2) — K-tiles past the end re-read valid data.
   // Each phase then waits for the half its successor reads; the count of younger vector-memory instructions
-  // is exact and compile-time per mode: EP (kt 0 of tiles >= 1) stores the previous tile after each wait,
-  // POST (kt 1) still sees those stores in its windows. Requires nk >= 2.
+  // is exact and compile-time per mode: EP (kt 0 of tiles >= 1) stores the whole previous tile in phase 1,
+  // after its wait, so phases 2-4 of EP count those stores too; the stores precede the next K-tile's awaited
+  // halves, so no later count sees them. Requires nk >= 2.
   int em0 = 0, en0 = 0, kt = 0, ti = 0;
   const int NT = nmine * nk;
-  // mode: 0 steady, 1 EP, 2 POST (one body; only the s_waitcnt immediate depends on the mode)
-  auto wait3 = [&](int mode, auto n0c, auto nec, auto npc) {
-    if (mode == 0) vmcnt<decltype(n0c)::value>();
-    else if (mode == 1) vmcnt<decltype(nec)::value>();
-    else vmcnt<decltype(npc)::value>();
+  // one body for steady and EP K-tiles; only the s_waitcnt immediate depends on the mode
+  auto wait2 = [&](bool EP, auto n0c, auto nec) {
+    if (EP) vmcnt<decltype(nec)::value>();
+    else vmcnt<decltype(n0c)::value>();
   };
 #ifdef G256_DEFER2
   constexpr int D2 = 1;  // both DMA instructions of a half deferred: one fewer issued before each wait
 #else
   constexpr int D2 = 0;
 #endif
-  auto ktile = [&](int T, int mode) {
-    const bool EP = mode == 1;
+  auto ktile = [&](int T, bool EP) {
     const int bc = T & 1, bn = bc ^ 1;
     // K-tile T+1 is in the next tile iff LAST; T+2 iff kt >= nk-2
     const bool n1b = kt == nk - 1, n2 = kt >= nk - 2;
@@ -454,28 +488,25 @@ __global__ void __launch_bounds__(512) gemm256_kernel(GemmArgs g) {
     load_bias(nn0, n1b);
     issueB(HB1, bn, kt1, n1, true);
     // counts: VMEM instructions issued after the awaited half's second (pending) instruction
-    wait3(mode, IC<8 - D2>{}, IC<8 - D2>{}, IC<8 - D2 + 3 * SPQ>{});  // B1(T)
-    if (EP) epi_quadrant(IC<0>{}, em0, en0, true);
+    vmcnt<8 - D2>();  // B1(T)
+    if (EP) epi_rows(IC<0>{}, IC<8>{}, em0, en0, true);
     mma(0, 0, b0);
     // ---- phase 2: A rows 0..63 x B cols 32..63
     readB(bc, IC<HB1>{}, b1);
     if (CONV) issueA(HA1, bn, kt1, m1, n1b ? vcn : vcc, true);
     else issueA(HA1, bn, kt1, m1, vcc, true);
-    wait3(mode, IC<8 - D2>{}, IC<8 - D2 + SPQ>{}, IC<8 - D2 + 2 * SPQ>{});  // A1(T)
-    if (EP) epi_quadrant(IC<1>{}, em0, en0, true);
+    wait2(EP, IC<8 - D2>{}, IC<8 - D2 + 2 * SPH>{});  // A1(T)
     mma(0, 2, b1);
     // ---- phase 3: A rows 64..127 x B cols 0..31
     readA(bc, IC<HA1>{});
     if (CONV) issueA(HA0, bc, kt2, m2, n2 ? vcn : vcc, true);
     else issueA(HA0, bc, kt2, m2, vcc, true);
-    wait3(mode, IC<6 - D2>{}, IC<6 - D2 + 2 * SPQ>{}, IC<6 - D2>{});  // B0(T+1)
-    if (EP) epi_quadrant(IC<2>{}, em0, en0, true);
+    wait2(EP, IC<6 - D2>{}, IC<6 - D2 + 2 * SPH>{});  // B0(T+1)
     mma(4, 0, b0);
     // ---- phase 4: A rows 64..127 x B cols 32..63; B0 fragments of K-tile T+1
     readB(bn, IC<HB0>{}, b0);
     issueB(HB0, bc, kt2, n2c, true);
-    wait3(mode, IC<10 - D2>{}, IC<10 - D2 + 3 * SPQ>{}, IC<10 - D2 + SPQ>{});  // A0(T+1)
-    if (EP) epi_quadrant(IC<3>{}, em0, en0, true);
+    wait2(EP, IC<10 - D2>{}, IC<10 - D2 + 2 * SPH>{});  // A0(T+1)
     mma(4, 2, b1);
   };
   // after a tile's last K-tile: its results move to the epilogue slot, the workgroup's next tile becomes current
@@ -499,7 +530,7 @@ __global__ void __launch_bounds__(512) gemm256_kernel(GemmArgs g) {
 #ifdef G256_STAMPS
     if (tid == 0 && T < G256_STAMPS) g256_stamps[blockIdx.x * G256_STAMPS + T] = __builtin_amdgcn_s_memtime();
 #endif
-    ktile(T, later ? (kt == 0 ? 1 : kt == 1 ? 2 : 0) : 0);
+    ktile(T, later && kt == 0);
     if (kt == nk - 1) {
       next_tile();
       kt = 0;
@@ -509,10 +540,7 @@ __global__ void __launch_bounds__(512) gemm256_kernel(GemmArgs g) {
   }
   if (wr == 0) bar();
   // the last tile (its successor "tile" was a clamped re-read: nothing to seed)
-  epi_quadrant(IC<0>{}, em0, en0, false);
-  epi_quadrant(IC<1>{}, em0, en0, false);
-  epi_quadrant(IC<2>{}, em0, en0, false);
-  epi_quadrant(IC<3>{}, em0, en0, false);
+  epi_rows(IC<0>{}, IC<8>{}, em0, en0, false);
   vmcnt<0>();  // no LDS-DMA may land after the workgroup retires
 }
 
