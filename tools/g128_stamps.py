@@ -41,6 +41,11 @@ def main():
         w = torch.randn(K, N, device=dev, dtype=bf)
         o = torch.empty(M, N, device=dev)
         a = run(f"dX {M}x{N}x{K}", lambda: ops.linear_dx(dy, w, out=o), (M // 128) * (N // 128))
+        if os.environ.get("G128_DW"):  # weight gradient of the same shapes: dW[K, N] += dy^T x (MC x MC)
+            x = torch.randn(M, N, device=dev, dtype=bf)
+            dW = torch.zeros(K, N, device=dev)
+            a = run(f"dW {K}x{N} over {M} tokens", lambda: ops.linear_dw(dy, x, out=dW, accumulate=True),
+                    min(2048, (K // 128) * (N // 128) * 8))
         nk = K // 64
         if os.environ.get("G128_FINE"):
             f = a[:, 2:42].reshape(-1, 8, 5)
