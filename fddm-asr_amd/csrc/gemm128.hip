@@ -322,7 +322,11 @@ __device__ __forceinline__ void tile128(const GemmArgs& g, unsigned char* smem, 
         const float v = tl[r * 64 + ((((lane >> 2) ^ (r & 15)) << 2) | (lane & 3))] * alpha;
         if (nok && m >= mlo) {
           float* c = C + (long)m * ldc + n;
+#ifdef G128_ACC_PLAIN  // timing diagnostic only: split-K slices overwrite instead of adding (wrong results)
+          if (nz > 1) *c = v;
+#else
           if (nz > 1) atomicAdd(c, v);
+#endif
           else *c += v;
         }
       }

@@ -26,12 +26,19 @@ def main():
     with profile(activities=[ProfilerActivity.CPU], with_stack=True) as prof:
         gs, _ = T_.train_one_epoch(enc, dec, sp, te, tp, sch, batches, opt, dev, cfg, gs, None, 0, False)
         torch.cuda.synchronize()
-    want = ("aten::fill_", "aten::zero_", "aten::copy_", "aten::zeros", "aten::zero_", "aten::copy_", "aten::cat", "aten::stack", "aten::clone", "aten::add",
+    want = ("aten::fill_", "aten::zero_", "aten::copy_", "aten::zeros", "aten::cat", "aten::stack", "aten::clone", "aten::add",
             "aten::mul", "aten::sum", "aten::mean", "aten::index", "aten::ne", "aten::eq", "aten::to",
             "aten::contiguous", "aten::where", "aten::expand", "aten::zeros", "aten::ones", "aten::empty")
     cnt = Counter()
     for ev in prof.events():
         if ev.name not in want:
+            continue
+        if ev.name in ("aten::fill_", "aten::copy_") and os.environ.get("PARENTS"):
+            chain, p = [], ev.cpu_parent
+            while p is not None and len(chain) < 4:
+                chain.append(p.name[:60])
+                p = p.cpu_parent
+            cnt[(ev.name, " < ".join(chain) or "(top)")] += 1
             continue
         src = "?"
         for fr in (ev.stack or []):

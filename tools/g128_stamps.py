@@ -34,7 +34,45 @@ def run(name, fn, nblk):
     return a
 
 
+def grouped():
+    """one decoder block's weight-gradient group (tools/g128_bench.py shapes): per-block durations (cycles)"""
+    bf = torch.bfloat16
+    M, Me = 32 * 256, 32 * 499
+    shapes = [(M, 1536, 512), (M, 512, 512), (M, 512, 512), (M, 512, 512), (M, 2048, 512), (M, 512, 2048),
+              (Me, 1024, 512)]
+    jobs = [(torch.randn(m, a, device=dev, dtype=bf), torch.randn(m, b, device=dev, dtype=bf),
+             torch.zeros(a, b, device=dev), torch.zeros(a, device=dev)) for (m, a, b) in shapes]
+    for _ in range(3):
+        ops.linear_dw_grouped(jobs)
+    torch.cuda.synchronize()
+    buf = (ctypes.c_ulonglong * (2048 * NS))()
+    assert lib().fddm_gemm128_stamps(buf, ctypes.c_long(2048 * NS)) == 0
+    a = np.frombuffer(buf, dtype=np.uint64).reshape(2048, NS).astype(np.int64)
+    a = a[a[:, 0] > 0]
+    if os.environ.get("G128_FINE"):
+        f = a[:, 2:42].reshape(-1, 8, 5)
+        d = np.diff(f, axis=2)
+        nxt = f[:, 1:, 0] - f[:, :-1, 4]
+        ok = (d > 0).all(axis=(1, 2)) & (d < 100000).all(axis=(1, 2))
+        d, nxt = d[ok], nxt[ok]
+        print("grouped fine (median cycles over %d blocks): reads+lgkm %.0f | vmcnt %.0f | bar1 %.0f | mfma %.0f | "
+              "bar2 %.0f" % (ok.sum(), np.median(d[:, :, 0]), np.median(d[:, :, 1]), np.median(d[:, :, 2]),
+                             np.median(d[:, :, 3]), np.median(nxt)))
+        print("   vmcnt p90 %.0f, reads p90 %.0f" % (np.percentile(d[:, :, 1], 90), np.percentile(d[:, :, 0], 90)))
+        return
+    tot = a[:, NS - 1] - a[:, 0]
+    pro = a[:, 1] - a[:, 0]
+    epi = a[:, NS - 1] - a[:, NS - 2]
+    print(f"grouped dW: {len(a)} blocks stamped; block cycles med {np.median(tot):.0f} min {tot.min()} max {tot.max()}; "
+          f"prologue med {np.median(pro):.0f}; epilogue med {np.median(epi):.0f} p90 {np.percentile(epi, 90):.0f}")
+    d = np.diff(a[:, 2:NS - 4], axis=1)
+    d = d[(d > 0) & (d < 100000)]
+    print(f"   K-tile cycles: med {np.median(d):.0f} p10 {np.percentile(d, 10):.0f} p90 {np.percentile(d, 90):.0f}")
+
+
 def main():
+    if os.environ.get("G128_GROUPED"):
+        return grouped()
     bf = torch.bfloat16
     for (M, N, K) in [(8192, 512, 2048), (8192, 512, 512)]:
         dy = torch.randn(M, K, device=dev, dtype=bf)
