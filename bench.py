@@ -322,6 +322,8 @@ def main():
         ev = probes["wavlm.conv1"]
         kms = sum(a.elapsed_time(b) for a, b in ev) / max(1, len(ev))
         kflops = dominant_flops(args)
+        ncu = torch.cuda.get_device_properties(device).multi_processor_count
+        conv_cus = int(os.environ.get("FDDM_ENC_CUS_CONV", ncu // 2))
         traffic, traffic_src = pmc_traffic(args)
         peak = BF16_PEAK_TFLOPS if args.precision == "bf16" else F32_PEAK_TFLOPS
         achieved = kflops / (kms * 1e-3) / 1e12
@@ -345,8 +347,12 @@ def main():
                          "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
                          "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_unit": "B/launch",
                          "traffic_source": traffic_src, "avg_ms": round(kms, 4),
-                         "launches_timed": len(ev), "flops_per_launch": kflops},
-            "roofline_isolated": {"kernel": "same launch, encoder not overlapped with the decoder (untimed step)",
+                         "launches_timed": len(ev), "flops_per_launch": kflops,
+                         # inside the timed steps the conv feature extractor's persistent GEMMs are capped to this many
+                         # CUs (the decoder forward runs on the rest, train._encoded); frac_of_cus = achieved against
+                         # that share of the chip's peak
+                         "cus": conv_cus, "frac_of_cus": round(achieved / (peak * conv_cus / ncu), 4)},
+            "roofline_isolated": {"kernel": "same launch, encoder not overlapped with the decoder, whole chip (untimed step)",
                                   "achieved": round(iso, 1), "frac": round(iso / peak, 4), "avg_ms": round(iso_ms, 4)},
             "decoder_attention": decoder_attention(args, aprobes, peak),
             "step_mfma_frac": round(step_tflops / peak, 4),

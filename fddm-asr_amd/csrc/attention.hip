@@ -586,9 +586,12 @@ __global__ void __launch_bounds__(256, ATTN_FWD_WPS) fwd2_kernel(AttnArgs a) {
 // mask row (key padding, keys >= Lk) and, for WavLM, the relative-bias slice of the workgroup's whole query
 // range are staged once as well. NW waves x 2 query groups x 16 = 32*NW queries per workgroup; the per-tile
 // softmax / dropout / P.V code is that of fwd2_kernel.
-template <bool DROP, bool MASK, bool REL, int NW>
+// NG = 1 with NW = 16 (round 2 probe): 16 queries per wave, 16 waves per workgroup — 4 waves per SIMD instead of
+// 2 for the same LDS footprint, each K / V fragment feeding one MFMA instead of two.
+template <bool DROP, bool MASK, bool REL, int NW, int NG = 2>
 __global__ void __launch_bounds__(64 * NW, 1) fwd3_kernel(AttnArgs a) {
-  constexpr int NG = 2, QW = 32 * NW;
+  constexpr int QW = 16 * NG * NW;
+  static_assert(NW == 4 || NW == 8 || NW == 16, "fwd3 wave count");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem3[];
   const int ntiles = (a.Lk + 63) / 64, LkP = ntiles * 64;
   unsigned char* kres = smem3;                                  // [LkP][128 B] KC image
@@ -610,14 +613,27 @@ __global__ void __launch_bounds__(64 * NW, 1) fwd3_kernel(AttnArgs a) {
     typedef __attribute__((address_space(1))) const void* gp_t;
     typedef __attribute__((address_space(3))) void* lp_t;
     for (int t = 0; t < ntiles; ++t) {
-#pragma unroll
-      for (int u = 0; u < 8 / NW; ++u) {
-        const int R = 64 * t + 8 * (w + NW * u);
+      if constexpr (NW == 16) {  // waves 0-7: K rows 8w.., waves 8-15: V rows 8(w-8)..
+        const int R = 64 * t + 8 * (w & 7);
         const int r = R + (lane >> 3), pch = lane & 7;
         const int rr = min(r, a.Lk - 1);
-        const int ck = pch ^ ((r >> 1) & 7), cv = pch ^ (((r >> 1) & 3) << 1);
-        __builtin_amdgcn_global_load_lds((gp_t)(Kb + (long)rr * a.sk + ck * 8), (lp_t)(kres + R * 128), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds((gp_t)(Vb + (long)rr * a.sv + cv * 8), (lp_t)(vres + R * 128), 16, 0, 0);
+        if (w < 8) {
+          const int ck = pch ^ ((r >> 1) & 7);
+          __builtin_amdgcn_global_load_lds((gp_t)(Kb + (long)rr * a.sk + ck * 8), (lp_t)(kres + R * 128), 16, 0, 0);
+        } else {
+          const int cv = pch ^ (((r >> 1) & 3) << 1);
+          __builtin_amdgcn_global_load_lds((gp_t)(Vb + (long)rr * a.sv + cv * 8), (lp_t)(vres + R * 128), 16, 0, 0);
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < 8 / NW; ++u) {
+          const int R = 64 * t + 8 * (w + NW * u);
+          const int r = R + (lane >> 3), pch = lane & 7;
+          const int rr = min(r, a.Lk - 1);
+          const int ck = pch ^ ((r >> 1) & 7), cv = pch ^ (((r >> 1) & 3) << 1);
+          __builtin_amdgcn_global_load_lds((gp_t)(Kb + (long)rr * a.sk + ck * 8), (lp_t)(kres + R * 128), 16, 0, 0);
+          __builtin_amdgcn_global_load_lds((gp_t)(Vb + (long)rr * a.sv + cv * 8), (lp_t)(vres + R * 128), 16, 0, 0);
+        }
       }
     }
   }
@@ -1408,19 +1424,25 @@ static int run(int which, AttnArgs& a, hipStream_t s) {
 #undef FWD1
           return (int)hipGetLastError();
         }
-        // v3 (K/V resident in LDS) for Lk <= 512 unless FDDM_ATTN_V2 is set; 8 waves (256 queries) when that
-        // still leaves >= 2 workgroups per CU-round, else 4 (128 queries)
+        // v3 (K/V resident in LDS) for Lk <= 512 unless FDDM_ATTN_V2 is set
         if (a.Lk <= 512 && !rel && !getenv("FDDM_ATTN_V2")) {  // WavLM (rel): fwd2's 2 workgroups per CU measure faster
           const int LkP = (a.Lk + 63) / 64 * 64;
           const char* nw_env = getenv("FDDM_ATTN_NW");
-          const int nw = nw_env ? atoi(nw_env) : 8;
-          const int QW = 32 * nw;
+          // 16 waves x 16 queries (4 waves per SIMD) by default: tools/attn_bench.py, decoder self (kpm, dropout)
+          // 16.3 -> 15.2 us, cross 31.7 -> 30.0 us against 8 waves x 32 queries (same LDS footprint)
+          const int nw = nw_env ? atoi(nw_env) : 16;
+          const int QW = nw == 16 ? 16 * nw : 32 * nw;
           const size_t lds = (size_t)LkP * 256 + (size_t)LkP * 4 + (rel ? (size_t)(LkP + QW) * 4 : 0) +
                              (drop ? (size_t)3 * ATTN_R * 2 : 0);
           const bool mask3 = a.key_keep != nullptr || (a.Lk % 64) != 0;
           dim3 grid3((a.Lq + QW - 1) / QW, a.B * a.H);
 #define FWD3(D, M, R, W) hipLaunchKernelGGL((fwd3_kernel<D, M, R, W>), grid3, dim3(64 * W), lds, s, a)
-#define FWD3W(D, M, R) do { if (nw == 4) FWD3(D, M, R, 4); else FWD3(D, M, R, 8); } while (0)
+#define FWD3W(D, M, R)                                                                                 \
+  do {                                                                                                  \
+    if (nw == 4) FWD3(D, M, R, 4);                                                                      \
+    else if (nw == 16) hipLaunchKernelGGL((fwd3_kernel<D, M, R, 16, 1>), grid3, dim3(1024), lds, s, a); \
+    else FWD3(D, M, R, 8);                                                                              \
+  } while (0)
           if (rel) {
             if (mask3) FWD3W(false, true, true); else FWD3W(false, false, true);
           } else if (drop) {

@@ -111,6 +111,9 @@ def _encoded(encoder, loader, device, optimizer):
     frozen = not any(id(p) in opt_ids for p in encoder.parameters())
     dev = torch.device(device)
     if dev.type != "cuda" or not frozen or os.environ.get("FDDM_NO_ENC_PIPELINE"):
+        bb = getattr(encoder, "backbone", None)
+        if bb is not None and getattr(bb, "conv_cus", 0):
+            bb.conv_cus = 0                     # nothing runs beside it: the conv GEMMs get the whole chip
         for wave, x0 in loader:
             wave = wave.to(device, non_blocking=True)
             x0 = x0.to(device, non_blocking=True)

@@ -366,7 +366,8 @@ def _attn_ref(q, k, v, keep, p_drop, seed, stream, gate=None, table=None):
 @pytest.mark.parametrize("Lq,Lk,masked,p,bits", [(70, 70, True, 0.0, False), (64, 130, False, 0.1, False),
                                                  (33, 49, True, 0.1, False), (150, 200, True, 0.1, True),
                                                  (64, 130, False, 0.1, True), (40, 499, False, 0.1, True),
-                                                 (129, 257, True, 0.1, True)])
+                                                 (129, 257, True, 0.1, True), (96, 256, True, 0.1, True),
+                                                 (64, 499, False, 0.0, False)])
 def test_attention_fwd_bwd(dtype, Lq, Lk, masked, p, bits):
     """bits: the forward records the dropout keep bits and the backward reads them (bf16 path)."""
     o = ops()

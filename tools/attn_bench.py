@@ -47,7 +47,8 @@ def main():
                                  drop_p=p, seed=1, rng_stream=1, dbits=db)
         fl = 4.0 * B * H * Lq * Lk * 64
         res = []
-        for tag, env in (("v3", {}), ("v3/4w", {"FDDM_ATTN_NW": "4"}), ("v2", {"FDDM_ATTN_V2": "1"})):
+        for tag, env in (("v3/16w", {}), ("v3/4w", {"FDDM_ATTN_NW": "4"}), ("v3/8w", {"FDDM_ATTN_NW": "8"}),
+                         ("v2", {"FDDM_ATTN_V2": "1"})):
             os.environ.update(env)
             t = timeit(f)
             for k_ in env:
