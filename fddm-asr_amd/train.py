@@ -302,15 +302,13 @@ def build_models(cfg: Config, device):
 
 
 def _tokenizer(cfg, tok_path):
-    """SentencePiece when its .model is present (reference train.py:596-598), else the offline
-    vocab.json decoder (models.evaluate.VocabTokenizer)."""
-    if tok_path and os.path.exists(tok_path):
+    """SentencePiece (reference train.py:596-598): the .model, or the BPE model rebuilt from the .vocab next to it
+    (data_io.load_tokenizer); else the offline vocab.json decoder (models.evaluate.VocabTokenizer)."""
+    if tok_path:
         try:
-            import sentencepiece as spm
-            tok = spm.SentencePieceProcessor()
-            tok.load(tok_path)
-            return tok
-        except Exception:
+            from data_io import load_tokenizer
+            return load_tokenizer(tok_path)
+        except (FileNotFoundError, ImportError):
             pass
     from models.evaluate import VocabTokenizer
     vj = cfg.data.get("vocab_json") or os.path.join(os.path.dirname(tok_path or "."), "vocab.json")
@@ -384,7 +382,7 @@ def main():
         list(t_proj.parameters())
     optim = FusedAdamW(params, lr=cfg.optim["lr"], weight_decay=cfg.optim["weight_decay"])
 
-    from data_io import CVZhTWDataset  # real-data input path (librosa / sentencepiece)
+    from data_io import CVZhTWDataset  # real-data input path (WAV reader + SentencePiece)
     train_json = cfg.data.get("train_json", "data/processed/train.json")
     val_json = cfg.data.get("val_json", "data/processed/validation.json")    # reference train.py:555
     test_json = cfg.data.get("test_json", "data/processed/test.json")
