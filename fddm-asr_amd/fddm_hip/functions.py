@@ -239,7 +239,8 @@ class DecoderBlockFn(torch.autograd.Function):
                    drop_p=p, seed=seed, rng_stream=st + 2)
         # 2. cross-attention to the acoustic condition
         qc = ops.linear(x1T, W["ca"][:d], ca_b[:d], out_dtype=cd)
-        kvc = ops.linear(cT, W["ca"][d:], ca_b[d:], out_dtype=cd)
+        kvc = meta[10] if len(meta) > 10 and meta[10] is not None else \
+            ops.linear(cT, W["ca"][d:], ca_b[d:], out_dtype=cd)      # (precomputed for all blocks in one GEMM)
         oc = torch.empty(N, d, device=dev, dtype=cd)
         lsec = torch.empty(B * H, L, device=dev, dtype=F32)
         bits_c = ops.drop_bits(B, H, L, S, dev) if p > 0 else None

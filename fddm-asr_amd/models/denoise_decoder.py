@@ -12,6 +12,7 @@ produced (the encoder is frozen and its projection is never optimised, train.py:
 from __future__ import annotations
 
 import math
+import os
 from typing import Literal, Optional, Tuple
 
 import torch
@@ -20,6 +21,7 @@ import torch.nn.functional as F
 
 from fddm_hip import functions as FN
 from fddm_hip import runtime as rt
+from fddm_hip.ops import linear as ops_linear
 from fddm_hip.ops import rows_mean as ops_rows_mean
 
 
@@ -121,12 +123,12 @@ class DecoderBlock(nn.Module):
                 self.ff[3].weight, self.ff[3].bias, self.norm1.weight, self.norm1.bias, self.norm2.weight,
                 self.norm2.bias, self.norm3.weight, self.norm3.bias)
 
-    def run(self, x, xT, cT, key_keep, film, B, L, S, layer, seed, cos, sin):
+    def run(self, x, xT, cT, key_keep, film, B, L, S, layer, seed, cos, sin, kv=None):
         """film = (scale, shift, (dscale, dshift) accumulators or None) from DenoisingTransformerDecoder's
-        conditioning Function."""
+        conditioning Function; kv = this block's precomputed cross-attention K|V [B*S, 2d] (strided view) or None."""
         fscale, fshift, gfilm = film
         p = self.p if self.training else 0.0
-        meta = (B, L, S, self.nhead, layer, p, seed, cos, sin, gfilm)
+        meta = (B, L, S, self.nhead, layer, p, seed, cos, sin, gfilm, kv)
         return FN.DecoderBlockFn.apply(x, xT, cT, key_keep, fscale, fshift, meta, *self.block_params())
 
 
@@ -184,11 +186,27 @@ class DenoisingTransformerDecoder(nn.Module):
             cT = (c if c.dtype == cd else c.to(cd)).reshape(B * S, -1).contiguous()
         cos, sin = self.pos_emb(L, dev)
         seed = rt.next_seed()
+        kv_all = self._cross_kv(cT)
         for i, blk in enumerate(self.blocks):
             film = (films[2 * i], films[2 * i + 1], (gbuf[2 * i], gbuf[2 * i + 1]))
-            x, xT = blk.run(x, xT, cT, key_keep, film, B, L, S, i, seed, cos, sin)
+            kv = None if kv_all is None else kv_all[:, 2 * self.d_model * i: 2 * self.d_model * (i + 1)]
+            x, xT = blk.run(x, xT, cT, key_keep, film, B, L, S, i, seed, cos, sin, kv)
         logits = FN.HeadFn.apply(x, xT, self.head.weight, self.head.bias)           # (:286)
         return logits.view(B, L, -1)
+
+    @torch.no_grad()
+    def _cross_kv(self, cT):
+        """The cross-attention K|V projections of the acoustic condition for ALL blocks as one GEMM
+        ([B*S, d] x [NL*2d, d]^T): they depend only on the condition and the blocks' weights, not on the decoder
+        state, so NL launches of [B*S, 2d] (one 256^2-tile round each at C2) become one launch of NL x the work.
+        Block i attends to columns [2d*i, 2d*(i+1)) (row stride NL*2d); the K|V weight gradients stay in each
+        block's backward (cond carries no gradient)."""
+        if len(self.blocks) < 2 or os.environ.get("FDDM_CROSS_KV_FUSED", "1") == "0":
+            return None
+        d = self.d_model
+        w = torch.cat([rt.wt(blk.cross_attn.in_proj_weight)[d:] for blk in self.blocks])
+        b = torch.cat([blk.cross_attn.in_proj_bias.detach()[d:] for blk in self.blocks])
+        return ops_linear(cT, w, b, out_dtype=rt.compute_dtype())
 
     def grad_ready_order(self):
         """Parameters in the order backward finalises their gradients: head, the blocks from last to first (their

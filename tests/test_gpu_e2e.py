@@ -76,8 +76,10 @@ def test_sanity_forward_cer_matches_cpu_oracle(mode, graph, monkeypatch):
 
 def test_real_data_loader_trains(tmp_path, monkeypatch):
     """The real-data path (data_io.CVZhTWDataset: WAV clips + SentencePiece ids rebuilt from the reference's .vocab)
-    feeding train.train_one_epoch at C1 geometry: two steps from the DataLoader give the same KL values, bit for bit,
-    as the same two steps fed the expected (wav, ids) tensors directly, and the losses are finite."""
+    feeding train.train_one_epoch at C1 geometry: two steps from the DataLoader give the same KL values as the same two
+    steps fed the expected (wav, ids) tensors directly (1e-5: the encoder's split-K and the LayerNorm parameter
+    gradients accumulate with float atomics, so two identical runs agree to ~1e-7, not bit for bit), and the losses are
+    finite."""
     import gzip
     import json
 
@@ -149,4 +151,4 @@ def test_real_data_loader_trains(tmp_path, monkeypatch):
     got = run(torch.utils.data.DataLoader(ds, batch_size=2))
     want = run(direct)
     assert len(got) == 2 and all(np.isfinite(got))
-    assert got == want
+    np.testing.assert_allclose(got, want, rtol=1e-5)

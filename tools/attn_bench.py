@@ -29,11 +29,16 @@ def main():
     cases = [("WavLM self S=499 B32 H12 (relbias)", 32, 12, 499, 499, True, 0.0, False),
              ("decoder self L=256 B32 H8 (kpm, drop .1)", 32, 8, 256, 256, False, 0.1, True),
              ("decoder self L=256 B32 H8 (no drop)", 32, 8, 256, 256, False, 0.0, True),
-             ("decoder cross 256x499 B32 H8 (drop .1)", 32, 8, 256, 499, False, 0.1, False)]
+             ("decoder cross 256x499 B32 H8 (drop .1)", 32, 8, 256, 499, False, 0.1, False),
+             ("decoder cross, K|V in the 6-block buffer", 32, 8, 256, 499, False, 0.1, False)]
     for name, B, H, Lq, Lk, rel, p, kpm in cases:
         q = torch.randn(B * Lq, H * 64, device=dev, dtype=bf)
-        k = torch.randn(B * Lk, H * 64, device=dev, dtype=bf)
-        v = torch.randn(B * Lk, H * 64, device=dev, dtype=bf)
+        if "6-block" in name:     # block 2's K|V columns of the fused [B*S, 6 * 2d] projection (row stride 6144)
+            kv = torch.randn(B * Lk, 6 * 2 * H * 64, device=dev, dtype=bf)
+            k, v = kv[:, 2048:2560], kv[:, 2560:3072]
+        else:
+            k = torch.randn(B * Lk, H * 64, device=dev, dtype=bf)
+            v = torch.randn(B * Lk, H * 64, device=dev, dtype=bf)
         o = torch.empty(B * Lq, H * 64, device=dev, dtype=bf)
         lse = torch.empty(B * H, Lq, device=dev)
         gate = torch.rand(B * H, Lq, device=dev) if rel else None
@@ -57,7 +62,8 @@ def main():
         print(f"fwd {name:44s} " + " | ".join(res), flush=True)
         if not rel:
             do = torch.randn_like(o)
-            dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+            dq, dk, dv = torch.empty_like(q), torch.empty(B * Lk, H * 64, device=dev, dtype=bf), \
+                torch.empty(B * Lk, H * 64, device=dev, dtype=bf)
             g = lambda: ops.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, B, H, Lq, Lk, key_keep=keep, drop_p=p,  # noqa
                                      seed=1, rng_stream=1, dbits=db)
             tb = timeit(g)
