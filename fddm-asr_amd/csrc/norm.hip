@@ -55,26 +55,60 @@ __device__ __forceinline__ void st8(T* p, const float (&v)[8]) {
 
 constexpr int LN_MAXCH = 2;  // chunks of 8 per lane: d <= 1024
 
-template <typename XT, typename YT, typename OT>
+// wave-wide sum in the VALU: DPP within rows of 16 lanes (quad swaps, half-row and row mirrors), then the
+// gfx950 lane-swap instructions across rows — no LDS round trip (__shfl_xor is a ds_bpermute per step);
+// every lane receives the total
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float wave_sum_v(float v) {
+  v += dppf<0xB1>(v);   // quad_perm(1,0,3,2)
+  v += dppf<0x4E>(v);   // quad_perm(2,3,0,1)
+  v += dppf<0x141>(v);  // row_half_mirror
+  v += dppf<0x140>(v);  // row_mirror
+  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// One wave per row. Every load of the row (x, y, gamma, beta, FiLM scale / shift) is issued before the first use,
+// so a wave waits for one memory round trip, not three; the two row reductions run in the VALU (wave_sum_v).
+// HY: residual branch y present, HF: FiLM present (compile-time: a load under a runtime branch gets its own wait)
+template <typename XT, typename YT, typename OT, bool HY, bool HF>
 __global__ void __launch_bounds__(256) ln_fwd_kernel(LnFwdArgs a) {
   const int lane = threadIdx.x & 63;
-  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const long row = (long)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
   if (row >= a.N) return;
   const long d = a.d, nch = d / 8;
   const XT* x = (const XT*)a.x + row * d;
-  const YT* y = a.y ? (const YT*)a.y + row * d : nullptr;
-  float v[LN_MAXCH][8];
+  const YT* y = HY ? (const YT*)a.y + row * d : nullptr;
+  const long b = HF ? row / a.rows_per_batch : 0;
+  float v[LN_MAXCH][8], yv[LN_MAXCH][8], gm[LN_MAXCH][8], bt[LN_MAXCH][8], fs[LN_MAXCH][8], fh[LN_MAXCH][8];
+  // lanes past the row end load its last chunk again (no divergent branch around the loads: a load inside one
+  // would be waited for at the branch join) and contribute zeros
+#pragma unroll
+  for (int i = 0; i < LN_MAXCH; ++i) {
+    const long c0 = min(lane + 64L * i, nch - 1) * 8;
+    ld8<XT>(x + c0, v[i]);
+    if constexpr (HY) ld8<YT>(y + c0, yv[i]);
+    ld8<float>(a.gamma + c0, gm[i]);
+    ld8<float>(a.beta + c0, bt[i]);
+    if constexpr (HF) {
+      ld8<float>(a.fsc + b * d + c0, fs[i]);
+      ld8<float>(a.fsh + b * d + c0, fh[i]);
+    }
+  }
   float sum = 0.f;
 #pragma unroll
   for (int i = 0; i < LN_MAXCH; ++i) {
     const long ch = lane + 64L * i;
+    if (ch >= nch) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[i][e] = 0.f;
-    if (ch < nch) {
-      ld8<XT>(x + ch * 8, v[i]);
-      if (y) {
-        float yv[8];
-        ld8<YT>(y + ch * 8, yv);
+      for (int e = 0; e < 8; ++e) v[i][e] = 0.f;
+    } else {
+      if constexpr (HY) {
         unsigned keep = 0xffu;  // d % 8 == 0: two hashes per 8 elements
         if (a.thr16) {
           const uint64_t e4 = (uint64_t)(row * d + ch * 8) >> 2;
@@ -82,7 +116,7 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(LnFwdArgs a) {
         }
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const float t = yv[e];
+          const float t = yv[i][e];
           v[i][e] += a.thr16 ? ((keep >> e) & 1u ? t * a.drop_scale : 0.f) : t;
         }
       }
@@ -90,7 +124,7 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(LnFwdArgs a) {
       for (int e = 0; e < 8; ++e) sum += v[i][e];
     }
   }
-  const float mean = wave_sum(sum) / (float)d;
+  const float mean = wave_sum_v(sum) / (float)d;
   float sq = 0.f;
 #pragma unroll
   for (int i = 0; i < LN_MAXCH; ++i) {
@@ -103,26 +137,20 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(LnFwdArgs a) {
       }
     }
   }
-  const float var = wave_sum(sq) / (float)d;
+  const float var = wave_sum_v(sq) / (float)d;
   const float rstd = 1.f / sqrtf(var + a.eps);
-  const long b = a.fsc ? row / a.rows_per_batch : 0;
 #pragma unroll
   for (int i = 0; i < LN_MAXCH; ++i) {
     const long ch = lane + 64L * i;
     if (ch < nch) {
       const long c0 = ch * 8;
       if (a.save_s) st8<float>(a.save_s + row * d + c0, v[i]);
-      float o[8], gm[8], bt[8];
-      ld8<float>(a.gamma + c0, gm);
-      ld8<float>(a.beta + c0, bt);
+      float o[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = (v[i][e] - mean) * rstd * gm[e] + bt[e];
-      if (a.fsc) {
-        float fs[8], fh[8];
-        ld8<float>(a.fsc + b * d + c0, fs);
-        ld8<float>(a.fsh + b * d + c0, fh);
+      for (int e = 0; e < 8; ++e) o[e] = (v[i][e] - mean) * rstd * gm[i][e] + bt[i][e];
+      if constexpr (HF) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = o[e] * (1.f + fs[e]) + fh[e];
+        for (int e = 0; e < 8; ++e) o[e] = o[e] * (1.f + fs[i][e]) + fh[i][e];
       }
       if (a.out_f32) st8<float>(a.out_f32 + row * d + c0, o);
       if (a.out_t) st8<OT>((OT*)a.out_t + row * d + c0, o);
@@ -168,8 +196,8 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
       s2 += gx * x;
     }
   }
-  s1 = wave_sum(s1) / (float)d;
-  s2 = wave_sum(s2) / (float)d;
+  s1 = wave_sum_v(s1) / (float)d;
+  s2 = wave_sum_v(s2) / (float)d;
 #pragma unroll
   for (int i = 0; i < LN_MAXPL; ++i) {
     const long c = lane + 64L * i;
@@ -257,8 +285,8 @@ __global__ void __launch_bounds__(512) ln_bwd_fused_kernel(LnBwdArgs a) {
         }
       }
     }
-    s1 = wave_sum(s1) / (float)d;
-    s2 = wave_sum(s2) / (float)d;
+    s1 = wave_sum_v(s1) / (float)d;
+    s2 = wave_sum_v(s2) / (float)d;
 #pragma unroll
     for (int i = 0; i < CH; ++i) {
       const long ch = lane + 64L * i;
@@ -394,18 +422,28 @@ FDDM_API int fddm_ln_fwd(int x_dtype, int y_dtype, int out_dtype, const void* x,
     a.thr16 = (unsigned)llrintf(drop_p * 65536.f);
     a.drop_scale = 1.f / (1.f - drop_p);
   }
+  if ((film_scale == nullptr) != (film_shift == nullptr)) return (int)hipErrorInvalidValue;
   dim3 grid((unsigned)((N + 3) / 4));
   hipStream_t s = (hipStream_t)hs;
+  const bool hy = y != nullptr, hf = film_scale != nullptr;
+#define LNF(XT, YT, OT)                                                                                   \
+  do {                                                                                                    \
+    if (hy && hf) hipLaunchKernelGGL((ln_fwd_kernel<XT, YT, OT, true, true>), grid, dim3(256), 0, s, a);   \
+    else if (hy) hipLaunchKernelGGL((ln_fwd_kernel<XT, YT, OT, true, false>), grid, dim3(256), 0, s, a);   \
+    else if (hf) hipLaunchKernelGGL((ln_fwd_kernel<XT, YT, OT, false, true>), grid, dim3(256), 0, s, a);   \
+    else hipLaunchKernelGGL((ln_fwd_kernel<XT, YT, OT, false, false>), grid, dim3(256), 0, s, a);          \
+  } while (0)
   if (x_dtype == FDDM_F32 && y_dtype == FDDM_BF16 && out_dtype == FDDM_BF16)
-    hipLaunchKernelGGL((ln_fwd_kernel<float, bf16_t, bf16_t>), grid, dim3(256), 0, s, a);
+    LNF(float, bf16_t, bf16_t);
   else if (x_dtype == FDDM_F32 && y_dtype == FDDM_F32 && out_dtype == FDDM_F32)
-    hipLaunchKernelGGL((ln_fwd_kernel<float, float, float>), grid, dim3(256), 0, s, a);
+    LNF(float, float, float);
   else if (x_dtype == FDDM_BF16 && y_dtype == FDDM_BF16 && out_dtype == FDDM_BF16)
-    hipLaunchKernelGGL((ln_fwd_kernel<bf16_t, bf16_t, bf16_t>), grid, dim3(256), 0, s, a);
+    LNF(bf16_t, bf16_t, bf16_t);
   else if (x_dtype == FDDM_F32 && y_dtype == FDDM_F32 && out_dtype == FDDM_BF16)
-    hipLaunchKernelGGL((ln_fwd_kernel<float, float, bf16_t>), grid, dim3(256), 0, s, a);
+    LNF(float, float, bf16_t);
   else
     return (int)hipErrorInvalidValue;
+#undef LNF
   return (int)hipGetLastError();
 }
 
