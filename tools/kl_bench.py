@@ -39,6 +39,9 @@ def main():
         tk = timeit(lambda: ops.kl_fused(z, xt, x0, t, betas, None, L, out_dtype=torch.bfloat16))
         print(f"fused fwd+grad NT={nt}: {tk * 1e3:7.1f} us  {(N * V * 6) / tk / 1e6:7.0f} GB/s", flush=True)
     del os.environ["FDDM_KLF_NT"]
+    mask = (torch.rand(B, L, device=dev) > 0.2).to(torch.uint8)
+    tk = timeit(lambda: ops.kl_fused(z, xt, x0, t, betas, mask, L, out_dtype=torch.bfloat16))
+    print(f"fused fwd+grad NT=256 masked: {tk * 1e3:7.1f} us  {(N * V * 6) / tk / 1e6:7.0f} GB/s", flush=True)
     for mode in ("vector", "scalar"):
         if mode == "scalar":
             os.environ["FDDM_KL_SCALAR"] = "1"
