@@ -1225,6 +1225,160 @@ __global__ void __launch_bounds__(256, 2) dq2_kernel(AttnArgs a) {
   }
 }
 
+// dQ, v3 (round 2): the whole K / V range of one (b, h) resident in LDS for Lk <= 512 (LDS-DMA up front, as
+// fwd3_kernel), 16 waves x one 16-query group = 256 queries per workgroup (4 waves per SIMD). One K image in the
+// KC (row-read) layout serves both the S^T = K Q^T row reads and the dQ^T += K^T dS^T transposed reads
+// (ds_read_b64_tr_b16 addresses the 8-byte units through the same XOR swizzle), so K + V take 2 x Lk x 128 B
+// (128 KB at the decoder's cross-attention Lk = 499). DM: 0 no dropout, 2 the forward's recorded keep bits.
+__device__ __forceinline__ int kc_tr_off(int k, int u) {  // 8-byte unit u of row k in a KC image
+  return k * 128 + ((((u >> 1) ^ ((k >> 1) & 7)) << 4) | ((u & 1) << 3));
+}
+template <int DM, bool MASK>
+__global__ void __launch_bounds__(1024, 1) dq3_kernel(AttnArgs a) {
+  static_assert(DM == 0 || DM == 2, "dq3: no-dropout or recorded keep bits");
+  constexpr int NW = 16, QW = 16 * NW;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smq[];
+  const int ntiles = (a.Lk + 63) / 64, LkP = ntiles * 64;
+  unsigned char* kres = smq;               // [LkP][128 B] KC image
+  unsigned char* vres = smq + LkP * 128;   // [LkP][128 B] KC image
+  float* mfull = (float*)(smq + 2 * LkP * 128);
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
+            i = lane & 15;
+  int bxi, bh;
+  xcd_tile(bxi, bh);
+  const int b = bh / a.H, h = bh % a.H;
+  const bf16_t* Qb = (const bf16_t*)a.Q + (long)b * a.Lq * a.sq + h * DH;
+  const bf16_t* Ob = (const bf16_t*)a.O + (long)b * a.Lq * a.so + h * DH;
+  const bf16_t* dOb = (const bf16_t*)a.dO + (long)b * a.Lq * a.sdo + h * DH;
+  const bf16_t* Kb = (const bf16_t*)a.K + (long)b * a.Lk * a.sk + h * DH;
+  const bf16_t* Vb = (const bf16_t*)a.V + (long)b * a.Lk * a.sv + h * DH;
+  {
+    typedef __attribute__((address_space(1))) const void* gp_t;
+    typedef __attribute__((address_space(3))) void* lp_t;
+    for (int t = 0; t < ntiles; ++t) {  // waves 0-7: K rows 8w.., waves 8-15: V rows 8(w-8).. of every tile
+      const int R = 64 * t + 8 * (w & 7);
+      const int r = R + (lane >> 3), pch = lane & 7;
+      const int rr = min(r, a.Lk - 1);
+      const int ck = pch ^ ((r >> 1) & 7);
+      if (w < 8)
+        __builtin_amdgcn_global_load_lds((gp_t)(Kb + (long)rr * a.sk + ck * 8), (lp_t)(kres + R * 128), 16, 0, 0);
+      else
+        __builtin_amdgcn_global_load_lds((gp_t)(Vb + (long)rr * a.sv + ck * 8), (lp_t)(vres + R * 128), 16, 0, 0);
+    }
+  }
+  for (int k = tid; k < LkP; k += 64 * NW) mfull[k] = (MASK && !key_ok(a, b, k)) ? -INFINITY : 0.f;
+  const float sl2 = a.scale * 1.4426950408889634f;
+  const int q = bxi * QW + w * 16 + i;
+  const bool qv = q < a.Lq;
+  const int qq0 = qv ? q : 0;
+  uint4 qf[2], dof[2], of[2];
+  row_frags<bf16_t>(qf, Qb, a.sq, qq0, qv, lane);
+  row_frags<bf16_t>(dof, dOb, a.sdo, qq0, qv, lane);
+  row_frags<bf16_t>(of, Ob, a.so, qq0, qv, lane);
+  float dl = 0.f;
+#pragma unroll
+  for (int sb = 0; sb < 2; ++sb) {
+    const bf16_t* x = (const bf16_t*)&dof[sb];
+    const bf16_t* y = (const bf16_t*)&of[sb];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dl += bf2f(x[e]) * bf2f(y[e]);
+  }
+  dl = xsum16(dl);
+  dl = xsum32(dl);
+  const float delta = dl;
+  if (qv && g == 0) a.delta[(long)bh * a.Lq + q] = dl;
+  const float lse2 = qv ? a.lse[(long)bh * a.Lq + q] * 1.4426950408889634f : 0.f;
+  f32x4_t dq[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) dq[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const f32x2_t sl2v = {sl2, sl2}, dscv = {a.drop_scale, a.drop_scale}, ndl = {-delta, -delta};
+  auto tile = [&](const int t, auto mc) {
+    constexpr bool MT = decltype(mc)::value;
+    const int k0 = t * 64;
+    const unsigned char* kimg = kres + k0 * 128;
+    const unsigned char* vimg = vres + k0 * 128;
+    uint64_t wbits = 0;
+    if constexpr (DM == 2) wbits = qv ? a.dbits[((long)bh * ntiles + t) * a.Lq + q] : 0;
+    f32x4_t sc[4], dp[4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      sc[kb] = dp[kb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub) {
+        const uint4 ak = *(const uint4*)(kimg + kc_off(128, kb * 16 + i, sub * 4 + g));
+        const uint4 av = *(const uint4*)(vimg + kc_off(128, kb * 16 + i, sub * 4 + g));
+        mma<bf16_t>(sc[kb], ak, qf[sub]);
+        mma<bf16_t>(dp[kb], av, dof[sub]);
+      }
+    }
+    float ds[4][4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      unsigned keep = 0xF;
+      if constexpr (DM == 2) keep = (unsigned)(wbits >> (kb * 16 + 4 * g)) & 0xFu;
+      float4 m4 = make_float4(0.f, 0.f, 0.f, 0.f);
+      if constexpr (MT) m4 = *(const float4*)(&mfull[k0 + kb * 16 + 4 * g]);
+      const float mr[4] = {m4.x, m4.y, m4.z, m4.w};
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        f32x2_t off = {-lse2, -lse2};
+        if constexpr (MT) off += f32x2_t{mr[2 * jj], mr[2 * jj + 1]};
+        const f32x2_t arg = f32x2_t{sc[kb][2 * jj], sc[kb][2 * jj + 1]} * sl2v + off;
+        const f32x2_t pr = {__builtin_amdgcn_exp2f(arg.x), __builtin_amdgcn_exp2f(arg.y)};
+        f32x2_t dpv = {dp[kb][2 * jj], dp[kb][2 * jj + 1]};
+        if constexpr (DM == 2) {
+          dpv.x = __int_as_float(__float_as_int(dpv.x) & __builtin_amdgcn_sbfe((int)keep, 2 * jj, 1));
+          dpv.y = __int_as_float(__float_as_int(dpv.y) & __builtin_amdgcn_sbfe((int)keep, 2 * jj + 1, 1));
+          dpv = dpv * dscv + ndl;
+        } else {
+          dpv += ndl;
+        }
+        const f32x2_t d2 = pr * dpv;
+        ds[kb][2 * jj] = d2.x;
+        ds[kb][2 * jj + 1] = d2.y;
+      }
+    }
+    // dQ^T[d][q] += sum_k K[k][d] dS^T[k][q]: A = K^T fragments by transposed reads of the KC image
+    const int qq = i >> 2, pp = i & 3;
+    typedef __attribute__((address_space(3))) s16x4_t* lp;
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) {
+      uint4 bq;
+      bq.x = pk(ds[2 * ss][0], ds[2 * ss][1]);
+      bq.y = pk(ds[2 * ss][2], ds[2 * ss][3]);
+      bq.z = pk(ds[2 * ss + 1][0], ds[2 * ss + 1][1]);
+      bq.w = pk(ds[2 * ss + 1][2], ds[2 * ss + 1][3]);
+      const int k1 = 32 * ss + 4 * g + qq, k2 = k1 + 16;
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        const int u = db * 4 + pp;
+        const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(kimg + kc_tr_off(k1, u)));
+        const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(kimg + kc_tr_off(k2, u)));
+        mma<bf16_t>(dq[db], join_tr(lo, hi), bq);
+      }
+    }
+  };
+  if (MASK && a.key_keep != nullptr) {
+    for (int t = 0; t < ntiles; ++t)  // fully padded key tiles skipped (wave-uniform), as in fwd3_kernel
+      if (__any(key_ok(a, b, 64 * t + lane))) tile(t, std::integral_constant<bool, MASK>{});
+  } else {
+    for (int t = 0; t + 1 < ntiles; ++t) tile(t, std::false_type{});
+    tile(ntiles - 1, std::integral_constant<bool, MASK>{});
+  }
+  if (qv) {
+    bf16_t* dQb = (bf16_t*)a.dQ + ((long)b * a.Lq + q) * a.sdq + h * DH;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      uint2 u2;
+      u2.x = pk(dq[d][0] * a.scale, dq[d][1] * a.scale);
+      u2.y = pk(dq[d][2] * a.scale, dq[d][3] * a.scale);
+      *(uint2*)(dQb + d * 16 + 4 * g) = u2;
+    }
+  }
+}
+
 // dK, dV, key-owned: 128 keys per workgroup (two 16-key groups per wave), Q/dO tiles double-buffered
 // (row images for S, dP and transposed images for dV^T += dO^T P', dK^T += Q^T dS).
 template <int DM>
@@ -1403,6 +1557,174 @@ __global__ void __launch_bounds__(256, (DM == 1 ? 1 : 2)) dkv2_kernel(AttnArgs a
   }
 }
 
+// dK / dV, v3 (round 2): key-owned, the whole Q / dO range of one (b, h) resident in LDS for Lq <= 512 (LDS-DMA
+// up front) with the query rows' LSE, delta and — DM == 2 — the forward's keep words of this workgroup's key tiles;
+// 16 waves x one 16-key group = 256 keys per workgroup. Row reads of the KC images give S = Q K^T and dP = dO V^T;
+// transposed reads of the same images give dV^T += dO^T P' and dK^T += Q^T dS. DM: 0 no dropout, 2 recorded bits.
+template <int DM>
+__global__ void __launch_bounds__(1024, 1) dkv3_kernel(AttnArgs a) {
+  static_assert(DM == 0 || DM == 2, "dkv3: no-dropout or recorded keep bits");
+  constexpr bool DROP = DM != 0;
+  constexpr int NW = 16, KW = 16 * NW, KT = KW / 64;  // keys per workgroup, key tiles per workgroup
+  extern __shared__ __attribute__((aligned(16))) unsigned char smk[];
+  const int nq = (a.Lq + 63) / 64, LqP = nq * 64;
+  const int ntk = (a.Lk + 63) / 64;
+  unsigned char* qres = smk;                       // [LqP][128 B] KC image of Q
+  unsigned char* ores = smk + LqP * 128;           // [LqP][128 B] KC image of dO
+  float* lse_s = (float*)(smk + 2 * LqP * 128);    // [LqP] lse * log2(e)
+  float* del_s = lse_s + LqP;                      // [LqP] delta
+  uint64_t* wb_s = (uint64_t*)(del_s + LqP);       // [KT][LqP] keep words (DM == 2)
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
+            i = lane & 15;
+  int bxi, bh;
+  xcd_tile(bxi, bh);
+  const int b = bh / a.H, h = bh % a.H;
+  const bf16_t* Qb = (const bf16_t*)a.Q + (long)b * a.Lq * a.sq + h * DH;
+  const bf16_t* dOb = (const bf16_t*)a.dO + (long)b * a.Lq * a.sdo + h * DH;
+  const bf16_t* Kb = (const bf16_t*)a.K + (long)b * a.Lk * a.sk + h * DH;
+  const bf16_t* Vb = (const bf16_t*)a.V + (long)b * a.Lk * a.sv + h * DH;
+  {
+    typedef __attribute__((address_space(1))) const void* gp_t;
+    typedef __attribute__((address_space(3))) void* lp_t;
+    for (int t = 0; t < nq; ++t) {  // waves 0-7: Q rows 8w.., waves 8-15: dO rows 8(w-8).. of every query tile
+      const int R = 64 * t + 8 * (w & 7);
+      const int r = R + (lane >> 3), pch = lane & 7;
+      const int rr = min(r, a.Lq - 1);
+      const int ck = pch ^ ((r >> 1) & 7);
+      if (w < 8)
+        __builtin_amdgcn_global_load_lds((gp_t)(Qb + (long)rr * a.sq + ck * 8), (lp_t)(qres + R * 128), 16, 0, 0);
+      else
+        __builtin_amdgcn_global_load_lds((gp_t)(dOb + (long)rr * a.sdo + ck * 8), (lp_t)(ores + R * 128), 16, 0, 0);
+    }
+  }
+  // query rows past Lq (their Q / dO images repeat the last row) get lse = +inf: P = 0, so they add nothing
+  for (int j = tid; j < 2 * LqP; j += 64 * NW) {
+    const int qq = j < LqP ? j : j - LqP;
+    float v = j < LqP ? INFINITY : 0.f;
+    if (qq < a.Lq) v = j < LqP ? a.lse[(long)bh * a.Lq + qq] * 1.4426950408889634f : a.delta[(long)bh * a.Lq + qq];
+    (j < LqP ? lse_s : del_s)[qq] = v;
+  }
+  if constexpr (DM == 2) {
+    for (int j = tid; j < KT * LqP; j += 64 * NW) {
+      const int kt = bxi * KT + j / LqP, qq = j % LqP;
+      wb_s[j] = (qq < a.Lq && kt < ntk) ? a.dbits[((long)bh * ntk + kt) * a.Lq + qq] : 0;
+    }
+  }
+  const float sl2 = a.scale * 1.4426950408889634f;
+  const int key = bxi * KW + w * 16 + i;
+  const bool kvld = key < a.Lk;
+  const bool kok = kvld && key_ok(a, b, key);
+  uint4 kf[2], vf[2];
+  row_frags<bf16_t>(kf, Kb, a.sk, kvld ? key : 0, kvld, lane);
+  row_frags<bf16_t>(vf, Vb, a.sv, kvld ? key : 0, kvld, lane);
+  f32x4_t dk[4], dv[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) dk[d] = dv[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int kbit = (w & 3) * 16 + i;      // key bit within its 64-key tile; the tile is w >> 2 of the workgroup's
+  const int kts = w >> 2;
+  const f32x2_t sl2v = {sl2, sl2}, dscv = {a.drop_scale, a.drop_scale};
+  const int qq_ = i >> 2, pp = i & 3;
+  typedef __attribute__((address_space(3))) s16x4_t* lp;
+  if (__any(kok)) {  // a wave whose 16 keys are all padding writes zeros (epilogue), no query loop
+    for (int t = 0; t < nq; ++t) {
+      const int q0 = t * 64;
+      const unsigned char* qimg = qres + q0 * 128;
+      const unsigned char* oimg = ores + q0 * 128;
+      f32x4_t sc[4], dp[4];
+#pragma unroll
+      for (int qb = 0; qb < 4; ++qb) {
+        sc[qb] = dp[qb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub) {
+          const uint4 aq = *(const uint4*)(qimg + kc_off(128, qb * 16 + i, sub * 4 + g));
+          const uint4 ao = *(const uint4*)(oimg + kc_off(128, qb * 16 + i, sub * 4 + g));
+          mma<bf16_t>(sc[qb], aq, kf[sub]);
+          mma<bf16_t>(dp[qb], ao, vf[sub]);
+        }
+      }
+      float pd[4][4], ds[4][4];
+#pragma unroll
+      for (int qb = 0; qb < 4; ++qb) {
+        const float4 l4 = *(const float4*)(&lse_s[q0 + qb * 16 + 4 * g]);
+        const float4 d4 = *(const float4*)(&del_s[q0 + qb * 16 + 4 * g]);
+        const f32x2_t nl[2] = {f32x2_t{-l4.x, -l4.y}, f32x2_t{-l4.z, -l4.w}};
+        const f32x2_t nd[2] = {f32x2_t{-d4.x, -d4.y}, f32x2_t{-d4.z, -d4.w}};
+        unsigned wq[4] = {0, 0, 0, 0};  // the 32-bit half of each query's keep word holding this key's bit
+        if constexpr (DM == 2) {
+          const unsigned* src = (const unsigned*)&wb_s[kts * LqP + q0 + qb * 16 + 4 * g] + (kbit >> 5);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) wq[j] = src[2 * j];
+        }
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          const f32x2_t arg = f32x2_t{sc[qb][2 * jj], sc[qb][2 * jj + 1]} * sl2v + nl[jj];
+          const f32x2_t pr = {__builtin_amdgcn_exp2f(arg.x), __builtin_amdgcn_exp2f(arg.y)};
+          f32x2_t dpv = {dp[qb][2 * jj], dp[qb][2 * jj + 1]};
+          f32x2_t pdv = pr;
+          if constexpr (DROP) {
+            const int m0 = __builtin_amdgcn_sbfe((int)wq[2 * jj], kbit & 31, 1);
+            const int m1 = __builtin_amdgcn_sbfe((int)wq[2 * jj + 1], kbit & 31, 1);
+            pdv.x = __int_as_float(__float_as_int(pr.x) & m0);
+            pdv.y = __int_as_float(__float_as_int(pr.y) & m1);
+            dpv.x = __int_as_float(__float_as_int(dpv.x) & m0);
+            dpv.y = __int_as_float(__float_as_int(dpv.y) & m1);
+            dpv = dpv * dscv + nd[jj];
+          } else {
+            dpv += nd[jj];
+          }
+          const f32x2_t d2 = pr * dpv;
+          pd[qb][2 * jj] = pdv.x;
+          pd[qb][2 * jj + 1] = pdv.y;
+          ds[qb][2 * jj] = d2.x;
+          ds[qb][2 * jj + 1] = d2.y;
+        }
+      }
+      // dV^T[d][key] += sum_q dO[q][d] P'[q][key], dK^T[d][key] += sum_q Q[q][d] dS[q][key]: transposed reads
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        uint4 bp, bs;
+        bp.x = pk(pd[2 * ss][0], pd[2 * ss][1]);
+        bp.y = pk(pd[2 * ss][2], pd[2 * ss][3]);
+        bp.z = pk(pd[2 * ss + 1][0], pd[2 * ss + 1][1]);
+        bp.w = pk(pd[2 * ss + 1][2], pd[2 * ss + 1][3]);
+        bs.x = pk(ds[2 * ss][0], ds[2 * ss][1]);
+        bs.y = pk(ds[2 * ss][2], ds[2 * ss][3]);
+        bs.z = pk(ds[2 * ss + 1][0], ds[2 * ss + 1][1]);
+        bs.w = pk(ds[2 * ss + 1][2], ds[2 * ss + 1][3]);
+        const int k1 = 32 * ss + 4 * g + qq_, k2 = k1 + 16;
+#pragma unroll
+        for (int db = 0; db < 4; ++db) {
+          const int u = db * 4 + pp;
+          const s16x4_t olo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(oimg + kc_tr_off(k1, u)));
+          const s16x4_t ohi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(oimg + kc_tr_off(k2, u)));
+          const s16x4_t qlo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(qimg + kc_tr_off(k1, u)));
+          const s16x4_t qhi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(qimg + kc_tr_off(k2, u)));
+          mma<bf16_t>(dv[db], join_tr(olo, ohi), bp);
+          mma<bf16_t>(dk[db], join_tr(qlo, qhi), bs);
+        }
+      }
+    }
+  }
+  if (kvld) {
+    bf16_t* dKb = (bf16_t*)a.dK + ((long)b * a.Lk + key) * a.sdk + h * DH;
+    bf16_t* dVb = (bf16_t*)a.dV + ((long)b * a.Lk + key) * a.sdv + h * DH;
+    // masked key: zero gradient (its P was never zeroed); dV carries the dropout scale of P'
+    const float ksc = kok ? a.scale : 0.f, vsc = kok ? (DROP ? a.drop_scale : 1.f) : 0.f;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      uint2 uk, uv;
+      uk.x = pk(kok ? dk[d][0] * ksc : 0.f, kok ? dk[d][1] * ksc : 0.f);
+      uk.y = pk(kok ? dk[d][2] * ksc : 0.f, kok ? dk[d][3] * ksc : 0.f);
+      uv.x = pk(kok ? dv[d][0] * vsc : 0.f, kok ? dv[d][1] * vsc : 0.f);
+      uv.y = pk(kok ? dv[d][2] * vsc : 0.f, kok ? dv[d][3] * vsc : 0.f);
+      *(uint2*)(dKb + d * 16 + 4 * g) = uk;
+      *(uint2*)(dVb + d * 16 + 4 * g) = uv;
+    }
+  }
+}
+
 template <typename T>
 static int run(int which, AttnArgs& a, hipStream_t s) {
   constexpr int RB = Cfg<T>::RB;
@@ -1472,9 +1794,22 @@ static int run(int which, AttnArgs& a, hipStream_t s) {
   } else if (which == 1) {
     if constexpr (sizeof(T) == 2) {
       if (!getenv("FDDM_ATTN_V1")) {
-        dim3 grid((a.Lq + 127) / 128, a.B * a.H);
         const bool drop = a.thr16 != 0, mask = a.key_keep != nullptr || (a.Lk % 64) != 0;
         const int dm = drop ? (a.dbits ? 2 : 1) : 0;
+        // v3: K/V resident, 256 queries per workgroup, for Lk <= 256 (tools/attn_bench.py: decoder self-attention
+        // backward 38.6 -> 35.3 us with dkv3; at the cross-attention's Lk = 499 — 130 KB of LDS, one workgroup per
+        // CU — no faster than the streamed kernels, 64.0 vs 62.8 us); FDDM_ATTN_DQ2=1 keeps the streamed kernel
+        if (a.Lk <= 256 && dm != 1 && !getenv("FDDM_ATTN_DQ2")) {
+          const int LkP = (a.Lk + 63) / 64 * 64;
+          const size_t lds = (size_t)LkP * 256 + (size_t)LkP * 4;
+          dim3 g3((a.Lq + 255) / 256, a.B * a.H);
+#define DQ3(D, M) hipLaunchKernelGGL((dq3_kernel<D, M>), g3, dim3(1024), lds, s, a)
+          if (dm == 2) { if (mask) DQ3(2, true); else DQ3(2, false); }
+          else { if (mask) DQ3(0, true); else DQ3(0, false); }
+#undef DQ3
+          return (int)hipGetLastError();
+        }
+        dim3 grid((a.Lq + 127) / 128, a.B * a.H);
 #define DQ2(D, M) hipLaunchKernelGGL((dq2_kernel<D, M>), grid, dim3(256), 0, s, a)
         if (dm == 2) { if (mask) DQ2(2, true); else DQ2(2, false); }
         else if (dm == 1) { if (mask) DQ2(1, true); else DQ2(1, false); }
@@ -1488,6 +1823,16 @@ static int run(int which, AttnArgs& a, hipStream_t s) {
   } else {
     if constexpr (sizeof(T) == 2) {
       if (!getenv("FDDM_ATTN_V1")) {
+        // v3: Q/dO resident, 256 keys per workgroup, for Lq, Lk <= 256 (see dq3 above); FDDM_ATTN_DKV2=1 keeps the
+        // streamed kernel
+        if (a.Lq <= 256 && a.Lk <= 256 && (!a.thr16 || a.dbits) && !getenv("FDDM_ATTN_DKV2")) {
+          const int LqP = (a.Lq + 63) / 64 * 64;
+          const size_t lds = (size_t)LqP * 256 + (size_t)LqP * 8 + (a.thr16 ? (size_t)4 * LqP * 8 : 0);
+          dim3 g3((a.Lk + 255) / 256, a.B * a.H);
+          if (a.thr16) hipLaunchKernelGGL((dkv3_kernel<2>), g3, dim3(1024), lds, s, a);
+          else hipLaunchKernelGGL((dkv3_kernel<0>), g3, dim3(1024), lds, s, a);
+          return (int)hipGetLastError();
+        }
         dim3 grid((a.Lk + 127) / 128, a.B * a.H);
         if (a.thr16 && a.dbits) hipLaunchKernelGGL((dkv2_kernel<2>), grid, dim3(256), 0, s, a);
         else if (a.thr16) hipLaunchKernelGGL((dkv2_kernel<1>), grid, dim3(256), 0, s, a);

@@ -67,7 +67,15 @@ def main():
             g = lambda: ops.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, B, H, Lq, Lk, key_keep=keep, drop_p=p,  # noqa
                                      seed=1, rng_stream=1, dbits=db)
             tb = timeit(g)
-            print(f"bwd {name:44s}    {tb*1e3:8.1f} us {2.5*fl/tb/1e9:7.1f} TF/s", flush=True)
+            os.environ["FDDM_ATTN_DQ2"] = "1"
+            tq2 = timeit(g)
+            os.environ["FDDM_ATTN_DKV2"] = "1"
+            tb2 = timeit(g)
+            del os.environ["FDDM_ATTN_DQ2"]
+            tk2 = timeit(g)
+            del os.environ["FDDM_ATTN_DKV2"]
+            print(f"bwd {name:44s}    v3 {tb*1e3:6.1f} us {2.5*fl/tb/1e9:6.1f} TF/s | dq2+dkv3 {tq2*1e3:6.1f} | "
+                  f"dq3+dkv2 {tk2*1e3:6.1f} | v2 {tb2*1e3:6.1f} us", flush=True)
 
 
 if __name__ == "__main__":
