@@ -198,8 +198,15 @@ def decoder_attention(args, probes, peak):
         lk = L if "self" in name else S
         fl = (10 if name.endswith("bwd") else 4) * args.batch * args.heads * L * lk * dh
         tf = fl / (ms * 1e-3) / 1e12
-        out[name.split(".", 1)[1]] = {"avg_us": round(1e3 * ms, 1), "gflop_per_launch": round(fl / 1e9, 3),
-                                      "tflops": round(tf, 1), "frac": round(tf / peak, 4), "launches": len(ev)}
+        row = {"avg_us": round(1e3 * ms, 1), "gflop_per_launch": round(fl / 1e9, 3), "tflops": round(tf, 1),
+               "frac": round(tf / peak, 4), "launches": len(ev)}
+        rep = probes.get(name + "#replay") or []
+        if rep:   # the same launches replayed back to back on the step's tensors: kernel time without launch gaps
+            kms = sum(a.elapsed_time(b) / n for a, b, n in rep) / len(rep)
+            ktf = fl / (kms * 1e-3) / 1e12
+            row.update({"kernel_us": round(1e3 * kms, 1), "kernel_tflops": round(ktf, 1),
+                        "kernel_frac": round(ktf / peak, 4)})
+        out[name.split(".", 1)[1]] = row
     return out
 
 
@@ -310,7 +317,7 @@ def main():
     # on the whole chip ("roofline_isolated"; inside the timed steps it shares the GPU with the decoder)
     os.environ["FDDM_NO_ENC_PIPELINE"] = "1"
     try:
-        with rt.probing(["wavlm.conv1", *ATTN_PROBES]) as aprobes:
+        with rt.probing(["wavlm.conv1", *ATTN_PROBES], replays=5) as aprobes:
             T_.train_one_epoch(enc, dec, sp, te, tp, sch, loader_t[:1], opt, device, cfg, gs, None, 2, False)
         torch.cuda.synchronize()
     finally:

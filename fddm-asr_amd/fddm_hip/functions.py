@@ -226,9 +226,10 @@ class DecoderBlockFn(torch.autograd.Function):
         o = torch.empty(N, d, device=dev, dtype=cd)
         lse = torch.empty(B * H, L, device=dev, dtype=F32)
         bits_s = ops.drop_bits(B, H, L, L, dev) if p > 0 else None
-        with rt.probe("decoder.self_attn_fwd"):
-            ops.attn_fwd(qk, qk[:, d:], v, o, lse, B, H, L, L, key_keep=key_keep, drop_p=p, seed=seed,
-                         rng_stream=st + 1, dbits=bits_s)
+        fwd_s = lambda: ops.attn_fwd(qk, qk[:, d:], v, o, lse, B, H, L, L, key_keep=key_keep, drop_p=p,  # noqa: E731
+                                     seed=seed, rng_stream=st + 1, dbits=bits_s)
+        with rt.probe("decoder.self_attn_fwd", replay=fwd_s):
+            fwd_s()
         y = ops.linear(o, W["so"], so_b, out_dtype=cd)
         s1 = torch.empty(N, d, device=dev, dtype=F32)
         m1 = torch.empty(N, device=dev, dtype=F32)
@@ -244,9 +245,10 @@ class DecoderBlockFn(torch.autograd.Function):
         oc = torch.empty(N, d, device=dev, dtype=cd)
         lsec = torch.empty(B * H, L, device=dev, dtype=F32)
         bits_c = ops.drop_bits(B, H, L, S, dev) if p > 0 else None
-        with rt.probe("decoder.cross_attn_fwd"):
-            ops.attn_fwd(qc, kvc, kvc[:, d:], oc, lsec, B, H, L, S, drop_p=p, seed=seed, rng_stream=st + 3,
-                         dbits=bits_c)
+        fwd_c = lambda: ops.attn_fwd(qc, kvc, kvc[:, d:], oc, lsec, B, H, L, S, drop_p=p, seed=seed,  # noqa: E731
+                                     rng_stream=st + 3, dbits=bits_c)
+        with rt.probe("decoder.cross_attn_fwd", replay=fwd_c):
+            fwd_c()
         yc = ops.linear(oc, W["co"], co_b, out_dtype=cd)
         s2 = torch.empty(N, d, device=dev, dtype=F32)
         m2 = torch.empty(N, device=dev, dtype=F32)
@@ -326,9 +328,10 @@ class DecoderBlockFn(torch.autograd.Function):
         dqc = torch.empty(N, d, device=dev, dtype=cd)
         dkvc = torch.empty(B * S, 2 * d, device=dev, dtype=cd)
         bits_s, bits_c = ctx.bits
-        with rt.probe("decoder.cross_attn_bwd"):
-            ops.attn_bwd(qc, kvc, kvc[:, d:], oc, doc, lsec, dqc, dkvc, dkvc[:, d:], B, H, L, S, drop_p=p, seed=seed,
-                         rng_stream=st + 3, dbits=bits_c)
+        bwd_c = lambda: ops.attn_bwd(qc, kvc, kvc[:, d:], oc, doc, lsec, dqc, dkvc, dkvc[:, d:], B, H, L, S,  # noqa: E731
+                                     drop_p=p, seed=seed, rng_stream=st + 3, dbits=bits_c)
+        with rt.probe("decoder.cross_attn_bwd", replay=bwd_c):
+            bwd_c()
         dw_jobs += [(dqc, x1T, gca_w[:d], gca_b[:d]), (dkvc, cT, gca_w[d:], gca_b[d:])]
         ops.linear_dx(dqc, W["ca"][:d], out=dx1, accumulate=True)
         # LN1
@@ -341,9 +344,10 @@ class DecoderBlockFn(torch.autograd.Function):
         do = ops.linear_dx(dy, W["so"], out_dtype=cd)
         dqk = torch.empty(N, 2 * d, device=dev, dtype=cd)
         dv = torch.empty(N, d, device=dev, dtype=cd)
-        with rt.probe("decoder.self_attn_bwd"):
-            ops.attn_bwd(qk, qk[:, d:], v, o, do, lse, dqk, dqk[:, d:], dv, B, H, L, L, key_keep=key_keep, drop_p=p,
-                         seed=seed, rng_stream=st + 1, dbits=bits_s)
+        bwd_s = lambda: ops.attn_bwd(qk, qk[:, d:], v, o, do, lse, dqk, dqk[:, d:], dv, B, H, L, L,  # noqa: E731
+                                     key_keep=key_keep, drop_p=p, seed=seed, rng_stream=st + 1, dbits=bits_s)
+        with rt.probe("decoder.self_attn_bwd", replay=bwd_s):
+            bwd_s()
         dw_jobs += [(dqk, xr, gsa_w[: 2 * d], gsa_b[: 2 * d]), (dv, xT, gsa_w[2 * d:], gsa_b[2 * d:])]
         ops.linear_dx(dv, W["sa"][2 * d:], out=dx, accumulate=True)
         dxr = ops.linear_dx(dqk, W["sa"][: 2 * d])

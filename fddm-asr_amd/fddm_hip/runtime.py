@@ -280,12 +280,16 @@ def grad_slot(p: torch.Tensor):
 
 # ------------------------------------------------------------------------------ launch probes
 _probes: dict | None = None
+_replay_n = 0
 
 
 @contextlib.contextmanager
-def probe(name: str):
+def probe(name: str, replay=None):
     """HIP events around one launch site on the current stream, recorded only while
-    `probing([...names])` is active (bench.py times its dominant kernel inside the timed steps)."""
+    `probing([...names])` is active (bench.py times its dominant kernel inside the timed steps). With
+    `probing(..., replays=n)` and an idempotent `replay` callable (the same launch on the same tensors), the site is
+    also launched n more times back to back between a second event pair: the kernel's own duration without the
+    launch gap a lone event pair around one short kernel includes (key "<name>#replay", entries (start, end, n))."""
     if _probes is None or name not in _probes:
         yield
         return
@@ -295,15 +299,23 @@ def probe(name: str):
     yield
     e1.record(s)
     _probes[name].append((e0, e1))
+    if replay is not None and _replay_n > 0:
+        r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        r0.record(s)
+        for _ in range(_replay_n):
+            replay()
+        r1.record(s)
+        _probes.setdefault(name + "#replay", []).append((r0, r1, _replay_n))
 
 
 @contextlib.contextmanager
-def probing(names):
+def probing(names, replays=0):
     """Collect probe events for `names`; yields the dict name -> list of (start, end) events."""
-    global _probes
-    old = _probes
+    global _probes, _replay_n
+    old, old_n = _probes, _replay_n
     _probes = {n: [] for n in names}
+    _replay_n = replays
     try:
         yield _probes
     finally:
-        _probes = old
+        _probes, _replay_n = old, old_n

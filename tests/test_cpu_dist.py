@@ -29,7 +29,7 @@ def _worker(rank, world, port, q):
             g = torch.Generator().manual_seed(100 * rank + i)
             p.grad = torch.randn(p.shape, generator=g)
         fdist.allreduce_grads(params, bucket_bytes=64)
-        q.put((rank, [None if p.grad is None else p.grad.clone() for p in params]))
+        q.put((rank, [None if p.grad is None else p.grad.numpy().copy() for p in params]))   # by value: the worker may exit first
     finally:
         dist.destroy_process_group()
 
@@ -52,7 +52,7 @@ def test_allreduce_grads_gloo_world2():
             continue
         exp = sum(torch.randn(s, generator=torch.Generator().manual_seed(100 * r + i)) for r in range(world)) / world
         for r in range(world):
-            torch.testing.assert_close(got[r][i], exp, rtol=1e-6, atol=1e-6)
+            torch.testing.assert_close(torch.from_numpy(got[r][i]), exp, rtol=1e-6, atol=1e-6)
 
 
 def _overlap_worker(rank, world, port, q):
@@ -75,7 +75,7 @@ def _overlap_worker(rank, world, port, q):
                 rt.grads_ready([p])
                 inflight.append(len(red.works))
             fdist.allreduce_grads(params)
-            q.put((rank, step, [p.grad.clone() for p in order], max(inflight)))
+            q.put((rank, step, [p.grad.numpy().copy() for p in order], max(inflight)))   # by value
     finally:
         dist.destroy_process_group()
 
@@ -104,4 +104,4 @@ def test_overlap_reducer_gloo_world2():
             exp = sum(torch.randn(s, generator=torch.Generator().manual_seed(1000 * step + 100 * r + i))
                       for r in range(world)) / world
             for r in range(world):
-                torch.testing.assert_close(got[(r, step)][i], exp, rtol=1e-6, atol=1e-6)
+                torch.testing.assert_close(torch.from_numpy(got[(r, step)][i]), exp, rtol=1e-6, atol=1e-6)
