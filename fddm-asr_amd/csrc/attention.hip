@@ -1747,7 +1747,7 @@ static int run(int which, AttnArgs& a, hipStream_t s) {
           return (int)hipGetLastError();
         }
         // v3 (K/V resident in LDS) for Lk <= 512 unless FDDM_ATTN_V2 is set
-        if (a.Lk <= 512 && !rel && !getenv("FDDM_ATTN_V2")) {  // WavLM (rel): fwd2's 2 workgroups per CU measure faster
+        if (a.Lk <= 512 && (!rel || getenv("FDDM_ATTN_REL3")) && !getenv("FDDM_ATTN_V2")) {  // WavLM (rel): fwd2's 2 workgroups per CU measure faster
           const int LkP = (a.Lk + 63) / 64 * 64;
           const char* nw_env = getenv("FDDM_ATTN_NW");
           // 16 waves x 16 queries (4 waves per SIMD) by default: tools/attn_bench.py, decoder self (kpm, dropout)

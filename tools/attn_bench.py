@@ -52,8 +52,11 @@ def main():
                                  drop_p=p, seed=1, rng_stream=1, dbits=db)
         fl = 4.0 * B * H * Lq * Lk * 64
         res = []
-        for tag, env in (("v3/16w", {}), ("v3/4w", {"FDDM_ATTN_NW": "4"}), ("v3/8w", {"FDDM_ATTN_NW": "8"}),
-                         ("v2", {"FDDM_ATTN_V2": "1"})):
+        envs = (("v3/16w", {}), ("v3/4w", {"FDDM_ATTN_NW": "4"}), ("v3/8w", {"FDDM_ATTN_NW": "8"}),
+                ("v2", {"FDDM_ATTN_V2": "1"}))
+        if rel:   # the WavLM forward runs fwd2 by default; fwd3 (K/V resident) on request
+            envs = (("fwd2", {}), ("fwd3/16w", {"FDDM_ATTN_REL3": "1"}), ("fwd3/8w", {"FDDM_ATTN_REL3": "1", "FDDM_ATTN_NW": "8"}))
+        for tag, env in envs:
             os.environ.update(env)
             t = timeit(f)
             for k_ in env:
