@@ -75,7 +75,8 @@ class GraphedEncoder:
             self.cache.clear()
             self._tok, self._P = tok, P          # the captured launches read these buffers: keep them alive
         key = (tuple(wave.shape), wave.dtype, str(wave.device), rt.precision(), int(cap),
-               int(getattr(self.enc.backbone, "conv_cus", 0)))   # grid sizes are part of the captured launches
+               int(getattr(self.enc.backbone, "conv_cus", 0)),
+               int(getattr(self.enc.backbone, "conv_cus_rest", 0)))   # grid sizes are part of the captured launches
         slots = self.cache.setdefault(key, [None] * self.nslots)
         s = slots[slot]
         if s is None:

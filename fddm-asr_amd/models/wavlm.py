@@ -195,7 +195,8 @@ class WavLMModel(nn.Module):
     def _conv(self, h, i, out=None):
         c = self.config
         P = self._prepared(rt.compute_dtype())
-        cap = getattr(self, "conv_cus", 0)   # persistent-GEMM workgroup cap for the conv layers (train._encoded)
+        # persistent-GEMM workgroup cap for the conv layers (train._encoded); layers 2.. may take another
+        cap = getattr(self, "conv_cus", 0) if i == 1 else getattr(self, "conv_cus_rest", getattr(self, "conv_cus", 0))
         if cap:
             from fddm_hip._lib import lib
             prev = lib().fddm_gemm_persistent_cap(cap)

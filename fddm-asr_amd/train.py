@@ -113,7 +113,7 @@ def _encoded(encoder, loader, device, optimizer):
     if dev.type != "cuda" or not frozen or os.environ.get("FDDM_NO_ENC_PIPELINE"):
         bb = getattr(encoder, "backbone", None)
         if bb is not None and getattr(bb, "conv_cus", 0):
-            bb.conv_cus = 0                     # nothing runs beside it: the conv GEMMs get the whole chip
+            bb.conv_cus = bb.conv_cus_rest = 0  # nothing runs beside it: the conv GEMMs get the whole chip
         for wave, x0 in loader:
             wave = wave.to(device, non_blocking=True)
             x0 = x0.to(device, non_blocking=True)
@@ -132,6 +132,7 @@ def _encoded(encoder, loader, device, optimizer):
     bb = getattr(encoder, "backbone", None)
     if bb is not None and hasattr(bb, "stage_rest"):
         bb.conv_cus = conv_cus
+        bb.conv_cus_rest = int(os.environ.get("FDDM_ENC_CUS_CONV2", conv_cus))   # conv layers 2..6
     # HIP-graph replay of the encoder forward (fddm_hip.graphs): the host launch path, not the GPU, bounded the step
     graphs = None
     if os.environ.get("FDDM_ENC_GRAPH", "1") != "0" and GraphedEncoder.supported(encoder):
