@@ -341,11 +341,11 @@ __global__ void __launch_bounds__(512) gemm256_kernel(GemmArgs g) {
           }
           emit_bf16(v, rc2, so);
         } else {
-          if constexpr (EPI == EPI_GELU_ONLY) {
+          if constexpr (EPI == EPI_GELU_ONLY) {  // the frozen encoder's conv layers / FF1: bf16-output GELU
 #pragma unroll
             for (int j = 0; j < 4; ++j)
 #pragma unroll
-              for (int e = 0; e < 4; ++e) v[j][e] = gelu_f(v[j][e]);
+              for (int e = 0; e < 4; ++e) v[j][e] = gelu_bf16out(v[j][e]);
           }
           emit_bf16(v, rc, so);
         }

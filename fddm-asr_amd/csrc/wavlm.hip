@@ -141,7 +141,13 @@ __global__ void __launch_bounds__(256) conv0_apply_kernel(const float* __restric
       f2_t y = {0.f, 0.f};
 #pragma unroll
       for (int k = 0; k < K; ++k) y += wk[k] * xs[f * S + k];
-      const f2_t gv = gelu2(y * sc + sh);
+      f2_t gv;
+      if constexpr (sizeof(OT) == 2) {  // bf16 output: the bf16-output GELU (common.h)
+        const f2_t z = y * sc + sh;
+        gv = f2_t{gelu_bf16out(z.x), gelu_bf16out(z.y)};
+      } else {
+        gv = gelu2(y * sc + sh);
+      }
       if constexpr (sizeof(OT) == 2) {
         *(unsigned*)(o + (long)f * C) = pk_bf16(gv.x, gv.y);
       } else {

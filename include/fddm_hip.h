@@ -26,7 +26,9 @@ const char* fddm_error_string(int code);
 
 /* ---- GEMM (MFMA). C[m][n] = alpha * sum_k A(m,k) B(n,k) + bias[n], fused epilogue `epi`:
  *      0 store (out_dtype), 1 GELU (C = pre-activation, C2 = dropout(gelu)), 2 accumulate into f32 C,
- *      4 dGELU (C = acc * gelu'(C2) * dropout mask).  a_kc/b_kc: operand K-contiguous (1) or
+ *      3 GELU only (C = gelu(acc); bf16 output on the 256x256 kernel: the bf16-output GELU fit, |err| <= 2.6e-5 —
+ *      the frozen encoder's FF1 / conv layers), 4 dGELU (C = acc * gelu'(C2) * dropout mask).
+ *      a_kc/b_kc: operand K-contiguous (1) or
  *      M/N-contiguous (0).  A rows batched: A + (m/Mi)*sAb + (m%Mi)*lda (Mi <= 0: unbatched).
  *      colsum (optional, M/N-contiguous A only): colsum[m] = sum_k A(m,k) — the fused bias gradient of
  *      a weight-gradient GEMM dW = dY^T X (colsum = sum over tokens of dY); like C it is overwritten
