@@ -8,8 +8,94 @@ namespace fddm {
 //   out[i]   = x[2i]*cos[p][2i] - x[2i+1]*sin[p][2i+1]
 //   out[h+i] = x[2i]*sin[p][2i] + x[2i+1]*cos[p][2i+1]       (h = d/2, p = position)
 // cos/sin tables [L][d] are the reference's emb.cos()/emb.sin() (computed once on the host).
+// Vectorised (d % 8 == 0, N*d < 2^31): a thread owns i = 4q..4q+3 of one row — two float4 of x / cos / sin, 4
+// outputs to each half; 32-bit index arithmetic (the 64-bit divisions of a scalar kernel cost more than its bytes).
 template <typename OT>
-__global__ void rope_fwd_kernel(const float* __restrict__ x, const float* __restrict__ cs, const float* __restrict__ sn,
+__device__ __forceinline__ void st4v(OT* p, float a, float b, float c, float d_) {
+  if constexpr (sizeof(OT) == 2) {
+    uint2 u;
+    u.x = pk_bf16(a, b);
+    u.y = pk_bf16(c, d_);
+    *(uint2*)p = u;
+  } else {
+    *(float4*)p = make_float4(a, b, c, d_);
+  }
+}
+template <typename OT>
+__global__ void __launch_bounds__(256) rope_fwd_kernel(const float* __restrict__ x, const float* __restrict__ cs,
+                                                       const float* __restrict__ sn, OT* __restrict__ out, int N, int L,
+                                                       int d) {
+  const int h = d / 2, nq = h / 4;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= N * nq) return;
+  const int r = e / nq, q = e - r * nq, p = r % L;
+  const float* xr = x + (long)r * d + 8 * q;
+  const float4 xa = *(const float4*)xr, xb = *(const float4*)(xr + 4);
+  const float4 ca = *(const float4*)(cs + (long)p * d + 8 * q), cb = *(const float4*)(cs + (long)p * d + 8 * q + 4);
+  const float4 sa = *(const float4*)(sn + (long)p * d + 8 * q), sb = *(const float4*)(sn + (long)p * d + 8 * q + 4);
+  OT* o = out + (long)r * d;
+  st4v<OT>(o + 4 * q, xa.x * ca.x - xa.y * sa.y, xa.z * ca.z - xa.w * sa.w, xb.x * cb.x - xb.y * sb.y,
+           xb.z * cb.z - xb.w * sb.w);
+  st4v<OT>(o + h + 4 * q, xa.x * sa.x + xa.y * ca.y, xa.z * sa.z + xa.w * ca.w, xb.x * sb.x + xb.y * cb.y,
+           xb.z * sb.z + xb.w * cb.w);
+}
+
+// dx += RoPE^T(dy): a thread owns i = 4q..4q+3 of one row (dx elements 8q..8q+7)
+__global__ void __launch_bounds__(256) rope_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ cs,
+                                                       const float* __restrict__ sn, float* __restrict__ dx, int N,
+                                                       int L, int d) {
+  const int h = d / 2, nq = h / 4;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= N * nq) return;
+  const int r = e / nq, q = e - r * nq, p = r % L;
+  const float4 a = *(const float4*)(dy + (long)r * d + 4 * q), b = *(const float4*)(dy + (long)r * d + h + 4 * q);
+  const float4 ca = *(const float4*)(cs + (long)p * d + 8 * q), cb = *(const float4*)(cs + (long)p * d + 8 * q + 4);
+  const float4 sa = *(const float4*)(sn + (long)p * d + 8 * q), sb = *(const float4*)(sn + (long)p * d + 8 * q + 4);
+  float* xr = dx + (long)r * d + 8 * q;
+  float4 u = *(float4*)xr, v = *(float4*)(xr + 4);
+  u.x += a.x * ca.x + b.x * sa.x;
+  u.y += -a.x * sa.y + b.x * ca.y;
+  u.z += a.y * ca.z + b.y * sa.z;
+  u.w += -a.y * sa.w + b.y * ca.w;
+  v.x += a.z * cb.x + b.z * sb.x;
+  v.y += -a.z * sb.y + b.z * cb.y;
+  v.z += a.w * cb.z + b.w * sb.z;
+  v.w += -a.w * sb.w + b.w * cb.w;
+  *(float4*)xr = u;
+  *(float4*)(xr + 4) = v;
+}
+
+// x[r] = E[tok[r]] + tbias[r / L]   (models/denoise_decoder.py:254, 272-274): a thread owns 8 consecutive columns
+template <typename OT>
+__global__ void __launch_bounds__(256) embed_fwd_kernel(const long* __restrict__ tok, const float* __restrict__ E,
+                                                        const float* __restrict__ tbias, float* __restrict__ out,
+                                                        OT* __restrict__ out_t, int N, int L, int d) {
+  const int nc = d / 8;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= N * nc) return;
+  const int r = e / nc, c = 8 * (e - r * nc);
+  const float* src = E + tok[r] * (long)d + c;
+  float4 a = *(const float4*)src, b = *(const float4*)(src + 4);
+  if (tbias) {
+    const float* tb = tbias + (long)(r / L) * d + c;
+    const float4 ta = *(const float4*)tb, tb4 = *(const float4*)(tb + 4);
+    a.x += ta.x; a.y += ta.y; a.z += ta.z; a.w += ta.w;
+    b.x += tb4.x; b.y += tb4.y; b.z += tb4.z; b.w += tb4.w;
+  }
+  const long o = (long)r * d + c;
+  if (out) {
+    *(float4*)(out + o) = a;
+    *(float4*)(out + o + 4) = b;
+  }
+  if (out_t) {
+    st4v<OT>(out_t + o, a.x, a.y, a.z, a.w);
+    st4v<OT>(out_t + o + 4, b.x, b.y, b.z, b.w);
+  }
+}
+
+// Scalar forms (any d, unaligned tensors): one element per thread.
+template <typename OT>
+__global__ void rope_fwd_scalar(const float* __restrict__ x, const float* __restrict__ cs, const float* __restrict__ sn,
                                 OT* __restrict__ out, long N, long L, long d) {
   const long h = d / 2;
   const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -23,7 +109,7 @@ __global__ void rope_fwd_kernel(const float* __restrict__ x, const float* __rest
 }
 
 // dx += RoPE^T(dy)
-__global__ void rope_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ cs, const float* __restrict__ sn,
+__global__ void rope_bwd_scalar(const float* __restrict__ dy, const float* __restrict__ cs, const float* __restrict__ sn,
                                 float* __restrict__ dx, long N, long L, long d) {
   const long h = d / 2;
   const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -38,7 +124,7 @@ __global__ void rope_bwd_kernel(const float* __restrict__ dy, const float* __res
 
 // x[r] = E[tok[r]] + tbias[r / L]   (models/denoise_decoder.py:254, 272-274)
 template <typename OT>
-__global__ void embed_fwd_kernel(const long* __restrict__ tok, const float* __restrict__ E,
+__global__ void embed_fwd_scalar(const long* __restrict__ tok, const float* __restrict__ E,
                                  const float* __restrict__ tbias, float* __restrict__ out, OT* __restrict__ out_t, long N,
                                  long L, long d) {
   const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -152,15 +238,33 @@ using namespace fddm;
 
 static inline dim3 g1(long n, int bs = 256) { return dim3((unsigned)((n + bs - 1) / bs)); }
 
+// the vectorised kernels: d % 8 == 0, 32-bit element indices, 16-B aligned tensors (null pointers allowed)
+static bool vec_ok(long d, long N, std::initializer_list<const void*> ps) {
+  if (d % 8 || N * d >= (1L << 31)) return false;
+  for (const void* p : ps)
+    if (((uintptr_t)p) & 15) return false;
+  return true;
+}
+
 FDDM_API int fddm_rope_fwd(int out_dtype, const float* x, const float* cs, const float* sn, void* out, long N, long L,
                            long d, void* hs) {
   if (N <= 0) return 0;
   if (d % 2) return (int)hipErrorInvalidValue;
   const long n = N * (d / 2);
+  if (vec_ok(d, N, {x, cs, sn, out})) {
+    const long nv = N * (d / 8);
+    if (out_dtype == FDDM_BF16)
+      hipLaunchKernelGGL((rope_fwd_kernel<bf16_t>), g1(nv), dim3(256), 0, (hipStream_t)hs, x, cs, sn, (bf16_t*)out,
+                         (int)N, (int)L, (int)d);
+    else
+      hipLaunchKernelGGL((rope_fwd_kernel<float>), g1(nv), dim3(256), 0, (hipStream_t)hs, x, cs, sn, (float*)out,
+                         (int)N, (int)L, (int)d);
+    return (int)hipGetLastError();
+  }
   if (out_dtype == FDDM_BF16)
-    hipLaunchKernelGGL((rope_fwd_kernel<bf16_t>), g1(n), dim3(256), 0, (hipStream_t)hs, x, cs, sn, (bf16_t*)out, N, L, d);
+    hipLaunchKernelGGL((rope_fwd_scalar<bf16_t>), g1(n), dim3(256), 0, (hipStream_t)hs, x, cs, sn, (bf16_t*)out, N, L, d);
   else
-    hipLaunchKernelGGL((rope_fwd_kernel<float>), g1(n), dim3(256), 0, (hipStream_t)hs, x, cs, sn, (float*)out, N, L, d);
+    hipLaunchKernelGGL((rope_fwd_scalar<float>), g1(n), dim3(256), 0, (hipStream_t)hs, x, cs, sn, (float*)out, N, L, d);
   return (int)hipGetLastError();
 }
 
@@ -168,18 +272,31 @@ FDDM_API int fddm_rope_bwd(const float* dy, const float* cs, const float* sn, fl
                            void* hs) {
   if (N <= 0) return 0;
   const long n = N * (d / 2);
-  hipLaunchKernelGGL(rope_bwd_kernel, g1(n), dim3(256), 0, (hipStream_t)hs, dy, cs, sn, dx, N, L, d);
+  if (vec_ok(d, N, {dy, cs, sn, dx}))
+    hipLaunchKernelGGL(rope_bwd_kernel, g1(N * (d / 8)), dim3(256), 0, (hipStream_t)hs, dy, cs, sn, dx, (int)N, (int)L,
+                       (int)d);
+  else
+    hipLaunchKernelGGL(rope_bwd_scalar, g1(n), dim3(256), 0, (hipStream_t)hs, dy, cs, sn, dx, N, L, d);
   return (int)hipGetLastError();
 }
 
 FDDM_API int fddm_embed_fwd(int out_dtype, const long* tok, const float* E, const float* tbias, float* out, void* out_t,
                             long N, long L, long d, void* hs) {
   if (N <= 0) return 0;
+  if (vec_ok(d, N, {E, tbias, out, out_t})) {
+    if (out_dtype == FDDM_BF16)
+      hipLaunchKernelGGL((embed_fwd_kernel<bf16_t>), g1(N * (d / 8)), dim3(256), 0, (hipStream_t)hs, tok, E, tbias, out,
+                         (bf16_t*)out_t, (int)N, (int)L, (int)d);
+    else
+      hipLaunchKernelGGL((embed_fwd_kernel<float>), g1(N * (d / 8)), dim3(256), 0, (hipStream_t)hs, tok, E, tbias, out,
+                         (float*)out_t, (int)N, (int)L, (int)d);
+    return (int)hipGetLastError();
+  }
   if (out_dtype == FDDM_BF16)
-    hipLaunchKernelGGL((embed_fwd_kernel<bf16_t>), g1(N * d), dim3(256), 0, (hipStream_t)hs, tok, E, tbias, out,
+    hipLaunchKernelGGL((embed_fwd_scalar<bf16_t>), g1(N * d), dim3(256), 0, (hipStream_t)hs, tok, E, tbias, out,
                        (bf16_t*)out_t, N, L, d);
   else
-    hipLaunchKernelGGL((embed_fwd_kernel<float>), g1(N * d), dim3(256), 0, (hipStream_t)hs, tok, E, tbias, out,
+    hipLaunchKernelGGL((embed_fwd_scalar<float>), g1(N * d), dim3(256), 0, (hipStream_t)hs, tok, E, tbias, out,
                        (float*)out_t, N, L, d);
   return (int)hipGetLastError();
 }

@@ -509,9 +509,11 @@ def test_layernorm_fwd_bwd(film, L):
         close(dfh, fhr.grad, rtol=1e-4, what="dfilm shift")
 
 
-def test_rope_and_embedding():
+@pytest.mark.parametrize("d", [128, 6])
+def test_rope_and_embedding(d):
+    """d = 128: the vectorised kernels (8 columns per thread); d = 6: the scalar forms."""
     o = ops()
-    B, L, d, V = 2, 9, 128, 50
+    B, L, V = 2, 9, 50
     inv = O.rope_inv_freq(d)
     cos, sin = O.rope_cos_sin(L, inv)
     x = torch.randn(B * L, d, generator=g(50))

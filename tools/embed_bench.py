@@ -1,5 +1,5 @@
-"""Micro-benchmark: token-embedding backward (dE scatter-add + time-bias sums) at the C2 shapes
-(8192 tokens, d 512, V 8000, L 256), HIP-event timing."""
+"""Micro-benchmark of the decoder's small HBM kernels at the C2 shapes (8192 tokens, d 512, V 8000, L 256):
+token-embedding forward / backward, RoPE forward / backward. HIP-event timing."""
 import os
 import sys
 
@@ -17,16 +17,27 @@ def main():
     dx = torch.randn(B * L, d, device=dev)
     dE = torch.zeros(V, d, device=dev)
     dtb = torch.zeros(B, d, device=dev)
-    f = lambda: ops.embed_bwd(tok, dx, dE, dtb, L, 0)  # noqa: E731
-    for _ in range(5):
-        f()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(50):
-        f()
-    e.record()
-    torch.cuda.synchronize()
-    print(f"embed_bwd {s.elapsed_time(e) / 50 * 1e3:7.1f} us", flush=True)
+    E = torch.randn(V, d, device=dev)
+    tb = torch.randn(B, d, device=dev)
+    x = torch.empty(B * L, d, device=dev)
+    xt = torch.empty(B * L, d, device=dev, dtype=torch.bfloat16)
+    cos, sin = torch.randn(L, d, device=dev), torch.randn(L, d, device=dev)
+    xr = torch.empty(B * L, d, device=dev, dtype=torch.bfloat16)
+    dxr = torch.zeros(B * L, d, device=dev)
+    cases = [("embed_bwd", lambda: ops.embed_bwd(tok, dx, dE, dtb, L, 0)),
+             ("embed_fwd", lambda: ops.embed_fwd(tok, E, tb, x, xt, L)),
+             ("rope_fwd", lambda: ops.rope_fwd(dx, cos, sin, xr, L)),
+             ("rope_bwd", lambda: ops.rope_bwd(dx, cos, sin, dxr, L))]
+    for name, f in cases:
+        for _ in range(5):
+            f()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(50):
+            f()
+        e.record()
+        torch.cuda.synchronize()
+        print(f"{name} {s.elapsed_time(e) / 50 * 1e3:7.1f} us", flush=True)
 
 
 if __name__ == "__main__":
