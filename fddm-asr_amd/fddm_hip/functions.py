@@ -496,8 +496,9 @@ class TextEmbedFn(torch.autograd.Function):
         xhat, weight = ctx.saved_tensors
         dz2 = dz.reshape(-1, weight.shape[0]).contiguous()
         cd = rt.compute_dtype()
-        dxhat = ops.linear_dx(dz2, rt.wt(weight), out_dtype=cd)
-        dW = ops.linear_dw(_t(dz2), xhat)
+        dzt = _t(dz2)       # compute-dtype operand: the f32-A form fell back to the register-staged GEMM (121 us)
+        dxhat = ops.linear_dx(dzt, rt.wt(weight), out_dtype=cd)
+        dW = ops.linear_dw(dzt, xhat)
         ptr = ctx.lptr
         kl = _kl_dz.get(ptr)
         if (kl is not None and cd == torch.bfloat16 and ptr in _head_outputs and ptr not in _dlogits_bf16
