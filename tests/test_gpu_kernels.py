@@ -808,6 +808,14 @@ def test_small_linear_and_dw_match_torch():
     for i in range(2):
         close(dW[i], 0.5 + dys[i].double().T @ xs[i].double(), rtol=1e-5, what="small_dw")
         close(db[i], 0.25 + dys[i].double().sum(0), rtol=1e-5, what="small_db")
+    # 45 rows (two row chunks of the kernel), K a multiple of 4 and not
+    for K2 in (96, 98):
+        R2 = 45
+        x2, dy2 = torch.randn(R2, K2, generator=gen), torch.randn(R2, N, generator=gen)
+        dW2, db2 = torch.zeros(N, K2, device=dev), torch.zeros(N, device=dev)
+        o.small_dw([(dy2.to(dev), x2.to(dev), dW2, db2)])
+        close(dW2, dy2.double().T @ x2.double(), rtol=1e-5, what=f"small_dw K={K2}")
+        close(db2, dy2.double().sum(0), rtol=1e-5, what=f"small_db K={K2}")
 
 
 def test_rows_mean_time_embed_kl_reduce():

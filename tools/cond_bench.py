@@ -38,6 +38,7 @@ def main():
 
 
 def run(dev, B, d, NL):
+    import os
     x = torch.randn(B, d, device=dev)
     Ws = [torch.randn(d, d, device=dev) / 23 for _ in range(2 * NL)]
     bs = [torch.randn(d, device=dev) for _ in range(2 * NL)]
