@@ -896,6 +896,7 @@ static void g128_balance(int n, const long* tiles, const long* ktiles, int* nz, 
 
 static int g128_ncu() {
   static int ncu = 0;
+  if (ncu == 0) ncu = (int)env_long("FDDM_G128_NCU", 0);  // scheduling slots the split choice assumes (probe)
   if (ncu == 0) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
