@@ -9,11 +9,15 @@ step, clip + AdamW. Inputs are resident in HBM before the timed region. The froz
 runs on a second HIP stream beside step i's decoder (train._encoded); every timed batch is encoded exactly
 once inside the timed region (the first one without overlap).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c4|c5]
   N>1: one rank per GPU over RCCL, per-GPU batch fixed ("weak"). Under torch.distributed.run (WORLD_SIZE set)
   the ranks come from the launcher; `python bench.py --gpus N` alone starts that launcher itself (a child
   process, before this process touches the GPU) and exits with its status. The world size the process group
   reports must equal N.
+  --config c4: BASELINE configs[3] per GPU (12-layer d768 H12 decoder, seq 512, 16 utterances per GPU).
+  --config c5: BASELINE configs[4], jumpy-sampler inference (B=64 x 10 s, T_infer 20, r 5, exact, greedy, seq 256,
+  HIP-graph replay of the encoder and of the whole denoise loop): one "step" = encode + sample one batch; the line
+  reports utterances/s and the RTF (replicas only across GPUs: inference exchanges nothing).
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -41,21 +45,36 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=4)
-    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--config", choices=sorted(PRESETS), default="c2",
+                    help="BASELINE.json workload: c2 = configs[1] (default), c4 = configs[3] per GPU, c5 = configs[4]")
+    ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--seconds", type=float, default=10.0)
-    ap.add_argument("--seq-len", type=int, default=256)
-    ap.add_argument("--layers", type=int, default=6)
-    ap.add_argument("--d-model", type=int, default=512)
-    ap.add_argument("--heads", type=int, default=8)
+    ap.add_argument("--seq-len", type=int, default=None)
+    ap.add_argument("--layers", type=int, default=None)
+    ap.add_argument("--d-model", type=int, default=None)
+    ap.add_argument("--heads", type=int, default=None)
     ap.add_argument("--precision", default="bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=4)
     ap.add_argument("--cpu-batch", type=int, default=4)
     ap.add_argument("--lfd-sync", action="store_true",
                     help="DP: L_fd / w_t statistics over the global batch (lfd.sync_batch_stats)")
+    ap.add_argument("--checksum", action="store_true",
+                    help="report every rank's parameter checksum after the run (DP replicas must agree bit for bit)")
     ap.add_argument("--dry-run", action="store_true",
                     help="initialise the process group, report the launch shape, do no GPU work")
-    return ap.parse_args()
+    return apply_preset(ap.parse_args())
+
+
+# BASELINE.json workloads: (batch per GPU, seq_len, decoder layers, d_model, heads); explicit flags override
+PRESETS = {"c2": (32, 256, 6, 512, 8), "c4": (16, 512, 12, 768, 12), "c5": (64, 256, 6, 512, 8)}
+
+
+def apply_preset(args):
+    for k, v in zip(("batch", "seq_len", "layers", "d_model", "heads"), PRESETS[args.config]):
+        if getattr(args, k) is None:
+            setattr(args, k, v)
+    return args
 
 
 def _free_port() -> int:
@@ -94,13 +113,28 @@ def gflop_per_utt(args, S=None):
                                                                        2.0 * S * 64 * 8 * 12)
     if d != E:
         enc += 2.0 * S * E * d
-    blk = (2.0 * L * d * 3 * d + 4.0 * L * L * d + 2.0 * L * d * d + 2.0 * L * d * d + 2.0 * S * d * 2 * d +
-           4.0 * L * S * d + 2.0 * L * d * d + 4.0 * d * d + 4.0 * L * d * FF)
-    fwd = NL * blk + 2.0 * L * d * V + 2.0 * (4 * d * d * 2 + d * d)
+    fwd = decoder_fwd_gflop(args, S) * 1e9
     bwd = 2.0 * fwd - NL * (2.0 * S * d * 2 * d + 4.0 * d * d)
     lfd_f = 2.0 * L * V * P + 2.0 * L * P * P + 2.0 * S * d * P + 2.0 * L * P * P
     lfd_b = 2 * 2.0 * L * V * P + 2 * 2.0 * L * P * P + 2.0 * S * d * P + 2 * 2.0 * L * P * P
+    if getattr(args, "config", "c2") == "c5":     # inference: encoder + one decoder forward per jump
+        return (enc + n_jumps(args) * fwd) / 1e9
     return (enc + fwd + bwd + (lfd_f + lfd_b) / 4) / 1e9
+
+
+def decoder_fwd_gflop(args, S):
+    """Decoder forward GFLOP per utterance (SURVEY §8(d) accounting)."""
+    d, NL, L, V, FF = args.d_model, args.layers, args.seq_len, 8000, 2048
+    blk = (2.0 * L * d * 3 * d + 4.0 * L * L * d + 2.0 * L * d * d + 2.0 * L * d * d + 2.0 * S * d * 2 * d +
+           4.0 * L * S * d + 2.0 * L * d * d + 4.0 * d * d + 4.0 * L * d * FF)
+    return (NL * blk + 2.0 * L * d * V + 2.0 * (4 * d * d * 2 + d * d)) / 1e9
+
+
+T_INFER, JUMP_R = 20, 5      # C5: inference.T_infer / r (BASELINE configs[4])
+
+
+def n_jumps(args):
+    return -(-T_INFER // JUMP_R)
 
 
 def build(args, device):
@@ -159,6 +193,8 @@ def dominant_flops(args):
 
 def config_tag(args):
     geom = (args.layers, args.d_model, args.heads, args.seq_len, args.seconds)
+    if args.config == "c5":
+        return "C5 (BASELINE configs[4])" if geom == (6, 512, 8, 256, 10.0) and args.batch == 64 else "custom C5"
     if geom == (6, 512, 8, 256, 10.0) and args.batch == 32:
         return "fddm_zhTW_base C2"
     if geom == (12, 768, 12, 512, 10.0) and args.batch == 16:
@@ -210,6 +246,23 @@ def decoder_attention(args, probes, peak):
     return out
 
 
+def param_checksums(models, world):
+    """(sum of the raw fp32 bit patterns, float64 sum) of every trainable parameter, gathered from all ranks."""
+    enc, dec, sp, te, tp, sch = models
+    bits, tot = 0, 0.0
+    for m in (dec, sp, te, tp):
+        for p in m.parameters():
+            x = p.detach().float().contiguous()
+            bits += int(x.view(torch.int32).to(torch.int64).sum())
+            tot += float(x.double().sum())
+    mine = [bits, tot]
+    if world == 1:
+        return [mine]
+    out = [None] * world
+    dist.all_gather_object(out, mine)
+    return out
+
+
 def cpu_baseline(args, models):
     """The CPU oracle (plain torch fp32 restatement of the reference step) timed on the host cores on a
     bounded sample: 2 utterances of the same geometry, `cpu_steps` steps (kind "port")."""
@@ -245,6 +298,117 @@ def cpu_baseline(args, models):
             "sample": f"oracle train step (CPU fp32 restatement), {args.cpu_steps} steps x {Bc} utt x "
                       f"{args.seconds:g} s, same geometry as the GPU line, global steps 4..{3 + args.cpu_steps} "
                       f"(L_fd on 1 in 4); {dt:.1f} s wall"}
+
+
+def c5_sampler(models, device):
+    from sampler.jumpy_sampler import DiffusionJumpySampler
+    enc, dec, sp, te, tp, sch = models
+    enc.eval()
+    dec.eval()
+    return DiffusionJumpySampler(sch.sch, dec, K=8000, T_train=200, T_infer=T_INFER, r=JUMP_R, greedy=True,
+                                 posterior_mode="map", sampling_mode="exact", device=device)
+
+
+def c5_cpu_baseline(args, models, smp):
+    """The CPU oracle's C5 pipeline (WavLM restatement + decoder forward per jump + the reference's exact posterior
+    argmax, oracle.jump_argmax) timed on the host cores on a bounded sample: 2 utterances of the same geometry."""
+    from oracle import fddm_oracle as O
+    ncores = min(16, len(os.sched_getaffinity(0)))
+    torch.set_num_threads(ncores)
+    enc, dec, *_ = models
+    enc_sd = {k: v.detach().float().cpu() for k, v in enc.state_dict().items()}
+    sd = {k: v.detach().float().cpu() for k, v in dec.state_dict().items()}
+    geom = O.wavlm_geometry()
+    betas, ab = O.sched_tables(200)
+    Bc = 2
+    g = torch.Generator().manual_seed(0)
+    wave = 0.1 * torch.randn(Bc, int(16000 * args.seconds), generator=g)
+    xT = torch.randint(0, 8000, (Bc, args.seq_len), generator=g)
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        c = O.acoustic_encoder(enc_sd, wave, geom, args.d_model)
+        O.jumpy_sample(lambda x, tv: O.decoder_forward(sd, x, tv, c, None, H=args.heads, num_layers=args.layers),
+                       xT, T_INFER, JUMP_R, betas.numpy(), ab.numpy(), 8000, 200, mode="exact")
+    dt = time.perf_counter() - t0
+    return {"value": round(Bc / dt, 4), "unit": "utterances/s", "rtf": round(dt / (Bc * args.seconds), 5),
+            "cores": torch.get_num_threads(), "kind": "port", "affinity_cpus": len(os.sched_getaffinity(0)),
+            "sample": f"oracle C5 pipeline (CPU fp32 restatement: encoder + {n_jumps(args)} decoder forwards + exact "
+                      f"posterior argmax), {Bc} utt x {args.seconds:g} s; {dt:.1f} s wall"}
+
+
+def run_c5(args, device, world, rank):
+    """C5: jumpy-sampler inference throughput. Per step: the frozen encoder over one resident batch (HIP-graph replay,
+    conv layer 1 eager between the two graphs as in training) and the whole T_infer / r denoise loop replayed from one
+    HIP graph (decoder forward + the fused posterior-argmax jump kernel per jump)."""
+    from fddm_hip import runtime as rt
+    from fddm_hip.graphs import GraphedEncoder
+    T_, cfg, models, _ = build(args, device)
+    enc = models[0]
+    smp = c5_sampler(models, device)
+    bb = enc.backbone
+    bb.conv_cus = bb.conv_cus_rest = 0       # nothing runs beside the encoder here: whole chip
+    ge = GraphedEncoder(enc) if GraphedEncoder.supported(enc) else None
+    waves = [w for w, _ in synthetic_batches(args, device, 2, 3000 + rank)]
+
+    def step(i):
+        with torch.no_grad():
+            w = waves[i % 2]
+            c = ge.run(w, i % 2) if ge is not None else enc(w)[0]
+            x0, _ = smp.sample(c, seq_len=args.seq_len, graph=True, return_probs=False)
+        return x0
+
+    for i in range(max(1, args.warmup)):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    t0 = time.perf_counter()
+    ev[0].record()
+    with rt.probing(["wavlm.conv1"]) as probes:
+        for i in range(args.steps):
+            step(i)
+    ev[1].record()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        tt = torch.tensor([el], device=device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    utt = args.batch * args.steps * world
+    value = utt / el
+    if rank == 0:
+        pev = probes["wavlm.conv1"]
+        kms = sum(a.elapsed_time(b) for a, b in pev) / max(1, len(pev))
+        kflops = dominant_flops(args)
+        achieved = kflops / (kms * 1e-3) / 1e12
+        peak = BF16_PEAK_TFLOPS if args.precision == "bf16" else F32_PEAK_TFLOPS
+        gpu_utt = gflop_per_utt(args)
+        cpu = None if (args.no_cpu_baseline or world > 1) else c5_cpu_baseline(args, models, smp)
+        out = {
+            "metric": "jumpy-sampler inference utterances/sec (C5: 10 s @16 kHz, T_infer 20, r 5, exact, greedy, "
+                      "seq_len 256)",
+            "value": round(value, 2), "unit": "utterances/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(1000.0 * el / args.steps, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
+            "rtf": round(el / args.steps / (args.batch * args.seconds), 8),
+            "data": "synthetic (random-init WavLM-base + decoder, random audio)",
+            "config": {"workload": workload_name(args) + f", jumpy sampler T_infer {T_INFER} r {JUMP_R} exact greedy, "
+                                                         "HIP-graph encoder + denoise loop",
+                       "global_batch": args.batch * world, "seq_len": args.seq_len, "audio_seconds": args.seconds,
+                       "parallelism": f"replicas{world}"},
+            "roofline": {"bound": "mfma", "kernel": "WavLM conv layer 1 implicit GEMM (gemm256_kernel: persistent "
+                                                    "256x256, GELU)", "achieved": round(achieved, 1), "peak": peak,
+                         "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
+                         "avg_ms": round(kms, 4), "launches_timed": len(pev), "flops_per_launch": kflops},
+            "step_mfma_frac": round(value / world * gpu_utt / 1e3 / peak, 4),
+            "gflop_per_utt": round(gpu_utt, 2),
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def main():
@@ -287,6 +451,8 @@ def main():
         return
     device = torch.device("cuda", local)
     torch.manual_seed(1337 + rank)
+    if args.config == "c5":
+        return run_c5(args, device, world, rank)
     T_, cfg, models, opt = build(args, device)
     if args.lfd_sync:
         cfg.lfd["sync_batch_stats"] = True
@@ -325,6 +491,7 @@ def main():
     utt = args.batch * args.steps * world
     value = utt / el
     ms_step = 1000.0 * el / args.steps
+    checks = param_checksums(models, world) if args.checksum else None
     if rank == 0:
         ev = probes["wavlm.conv1"]
         kms = sum(a.elapsed_time(b) for a, b in ev) / max(1, len(ev))
@@ -369,6 +536,8 @@ def main():
             "avg_loss": round(avg_loss, 4),
             "cpu_baseline": cpu,
         }
+        if checks is not None:
+            out["param_checksums"] = checks
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

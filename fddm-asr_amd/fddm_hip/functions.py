@@ -447,9 +447,18 @@ class KLFn(torch.autograd.Function):
         ref = _head_outputs.get(ptr)
         owner = ref() if ref is not None else None
         bf = owner is not None and owner.data_ptr() == ptr and ptr not in _dlogits_bf16 and ptr not in _kl_dz
-        kl_tok, dz = ops.kl_fused(l2.contiguous(), xf, x0f, tc, betas, mask_u8, L,
-                                  out_dtype=torch.bfloat16 if bf else F32)
-        loss, _ = ops.kl_reduce(kl_tok, mask_u8, B, L, want_w=False)
+        l2 = l2.contiguous()
+        odt = torch.bfloat16 if bf else F32
+        if V % 4 == 0 and V <= ops.KL_FUSED_MAX_V and l2.data_ptr() % 16 == 0:
+            kl_tok, dz = ops.kl_fused(l2, xf, x0f, tc, betas, mask_u8, L, out_dtype=odt)
+            loss, _ = ops.kl_reduce(kl_tok, mask_u8, B, L, want_w=False)
+        else:
+            # vocabularies the one-pass kernel is not built for (V % 4 != 0, V > 32768, unaligned rows): the
+            # two-pass form — per-token KL, the masked-mean weights, then the weighted gradient
+            kl_tok = ops.kl_fwd(l2, xf, x0f, tc, betas, L)
+            loss, w = ops.kl_reduce(kl_tok, mask_u8, B, L, want_w=True)
+            one = torch.ones(1, device=l2.device, dtype=F32)
+            dz = ops.kl_bwd(l2, xf, x0f, tc, betas, w, one, L, out_dtype=odt)
         ctx.dz = dz
         if bf:
             ctx.handover = ptr
@@ -502,7 +511,7 @@ class TextEmbedFn(torch.autograd.Function):
         ptr = ctx.lptr
         kl = _kl_dz.get(ptr)
         if (kl is not None and cd == torch.bfloat16 and ptr in _head_outputs and ptr not in _dlogits_bf16
-                and ptr not in _combined):
+                and ptr not in _combined and xhat.shape[-1] % 8 == 0):     # fddm_softmax_bwd_add_bf16: V % 8 == 0
             # bf16 hand-over: softmax backward + the KL's (unscaled) share in one bf16 buffer for HeadFn
             _dlogits_bf16[ptr] = ops.softmax_bwd_add_bf16(xhat, dxhat, kl)
             _combined.add(ptr)

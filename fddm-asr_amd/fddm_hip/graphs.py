@@ -47,24 +47,29 @@ class GraphedEncoder:
         h0 = bb.stage_conv0(inp)
         h1 = bb.stage_conv1(h0)
         self.enc.project(bb.stage_rest(h1))
-        gA = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(gA):
-            h0 = bb.stage_conv0(inp)
-        h1 = torch.empty(bb.conv_out_shape(h0), device=h0.device, dtype=h0.dtype)
-        gC = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(gC, pool=gA.pool()):      # this slot's pool only (see the module docstring)
-            out = self.enc.project(bb.stage_rest(h1))
-        return SimpleNamespace(inp=inp, h0=h0, h1=h1, out=out, gA=gA, gC=gC)
+        # the runtime-cached tensors the captured launches read (the relative-bias table, the bf16 encoder.proj
+        # weight, ...) are held by the slot, so rt.clear_cache() cannot free memory a replay reads
+        with rt.retaining() as keep:
+            gA = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gA):
+                h0 = bb.stage_conv0(inp)
+            h1 = torch.empty(bb.conv_out_shape(h0), device=h0.device, dtype=h0.dtype)
+            gC = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gC, pool=gA.pool()):      # this slot's pool only (see the module docstring)
+                out = self.enc.project(bb.stage_rest(h1))
+        return SimpleNamespace(inp=inp, h0=h0, h1=h1, out=out, gA=gA, gC=gC, keep=keep)
 
     def _weights_token(self):
         """Identity of the weights the graphs read: the backbone's prepared (cast / permuted) weight set — rebuilt
-        when the module is moved, loaded or changed in place — and encoder.proj. A change drops every captured
-        graph (they would read freed or stale buffers) and the next run recaptures."""
+        when the module is moved, loaded or changed in place — encoder.proj, and the runtime cache epoch. A change
+        drops every captured graph (they would read freed or stale buffers) and the next run recaptures."""
         enc = self.enc
         P = enc.backbone._prepared(rt.compute_dtype())
         proj = getattr(enc, "proj", None)
         pw = getattr(proj, "weight", None) if getattr(enc, "use_proj", False) else None
-        return (id(P), None if pw is None else (pw.data_ptr(), pw._version)), P
+        # rt.cache_epoch(): a clear_cache() (load_checkpoint calls it) drops every capture, so the next run recaptures
+        # against freshly built tables instead of replaying stale ones
+        return (id(P), None if pw is None else (pw.data_ptr(), pw._version), rt.cache_epoch()), P
 
     @torch.no_grad()
     def run(self, wave, slot: int, cap: int = 0):

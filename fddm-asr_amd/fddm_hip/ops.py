@@ -48,12 +48,59 @@ def _chk(cond, msg):
 
 
 # ------------------------------------------------------------------------------------------ GEMM
+def _layout_ok(A, B, M, N, K, a_kc, b_kc, lda, ldb):
+    """fddm_gemm's layout preconditions (csrc/gemm.hip): 16-B chunks of every operand row never straddle a row end
+    (the contiguous dimension of each operand and its leading dimension are multiples of 8 bf16 / 4 f32 elements)
+    and both operand base addresses are 16-B aligned."""
+    ech = 8 if B.dtype == torch.bfloat16 else 4
+    ok = (K % ech == 0 if a_kc else M % ech == 0) and lda % ech == 0
+    ok = ok and (K % ech == 0 if b_kc else N % ech == 0) and ldb % ech == 0
+    return ok and A.data_ptr() % 16 == 0 and B.data_ptr() % 16 == 0
+
+
+def _gemm_padded(A, B, C, M, N, K, a_kc, b_kc, lda, ldb, ldc, epi, bias, alpha, colsum):
+    """A GEMM whose operands miss the kernels' layout preconditions (a vocabulary or width that is not a multiple of
+    8, e.g. the head / TextEmbedding GEMMs at V % 8 != 0): the operands are copied into zero-padded buffers (M, N,
+    K rounded up to 8; the zero tail adds nothing to any dot product), the padded GEMM runs, and the M x N block is
+    copied back. STORE / ACCUMULATE epilogues with bias and the fused column sum only."""
+    _chk(epi in (EPI_STORE, EPI_ACC), "ragged GEMM: only store / accumulate epilogues have a padded form")
+    p8 = lambda n: (n + 7) // 8 * 8   # noqa: E731
+    Mp, Np, Kp = p8(M), p8(N), p8(K)
+    a = torch.as_strided(A, (M, K) if a_kc else (K, M), (lda, 1))
+    b = torch.as_strided(B, (N, K) if b_kc else (K, N), (ldb, 1))
+    Ap = torch.zeros((Mp, Kp) if a_kc else (Kp, Mp), device=A.device, dtype=A.dtype)
+    Bp = torch.zeros((Np, Kp) if b_kc else (Kp, Np), device=B.device, dtype=B.dtype)
+    Ap[: a.shape[0], : a.shape[1]] = a
+    Bp[: b.shape[0], : b.shape[1]] = b
+    c = torch.as_strided(C, (M, N), (ldc, 1))
+    Cp = torch.zeros(Mp, Np, device=C.device, dtype=C.dtype)
+    if epi == EPI_ACC:
+        Cp[:M, :N] = c
+    bp = None
+    if bias is not None:
+        bp = torch.zeros(Np, device=bias.device, dtype=bias.dtype)
+        bp[:N] = bias[:N]
+    cs = None
+    if colsum is not None:
+        cs = torch.zeros(Mp, device=colsum.device, dtype=colsum.dtype)
+        if epi == EPI_ACC:
+            cs[:M] = colsum[:M]
+    gemm(Ap, Bp, Cp, Mp, Np, Kp, a_kc=a_kc, b_kc=b_kc, lda=Ap.shape[1], ldb=Bp.shape[1], ldc=Np, epi=epi, bias=bp,
+         alpha=alpha, colsum=cs)
+    c.copy_(Cp[:M, :N])
+    if colsum is not None:
+        colsum[:M].copy_(cs[:M])
+    return C
+
+
 def gemm(A, B, C, M, N, K, *, a_kc=True, b_kc=True, lda, ldb, ldc, epi=EPI_STORE, bias=None, alpha=1.0,
          C2=None, Mi=0, sAb=0, drop_p=0.0, seed=0, rng_stream=0, colsum=None):
     """C[m][n] = alpha * sum_k A(m,k) B(n,k) (+bias, epilogue). Compute dtype = B.dtype."""
     _chk(B.dtype in (torch.float32, torch.bfloat16), "B dtype")
     if M == 0 or N == 0:
         return C
+    if Mi == 0 and sAb == 0 and not _layout_ok(A, B, M, N, K, a_kc, b_kc, lda, ldb):
+        return _gemm_padded(A, B, C, M, N, K, a_kc, b_kc, lda, ldb, ldc, epi, bias, alpha, colsum)
     call("fddm_gemm", code(B), code(A), int(a_kc), int(b_kc), epi, code(C), ptr(A), lda, Mi, sAb, ptr(B), ldb,
          ptr(C), ldc, ptr(C2), ptr(bias), float(alpha), M, N, K, seed, rng_stream, float(drop_p), ptr(colsum),
          stream())
@@ -322,6 +369,9 @@ def kl_bwd(logits2d, xt, x0, t, betas, w, gscale, L, out_dtype=torch.float32):
     call("fddm_kl_bwd", ptr(logits2d), ptr(xt), ptr(x0), ptr(t), ptr(betas), ptr(w), ptr(gscale), ptr(dz),
          code(dz), N, L, V, stream())
     return dz
+
+
+KL_FUSED_MAX_V = 32768      # fddm_kl_fused: 512 threads x 16 float4 per row
 
 
 def kl_fused(logits2d, xt, x0, t, betas, mask_u8, L, out_dtype=torch.float32):

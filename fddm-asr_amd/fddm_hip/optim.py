@@ -144,13 +144,13 @@ class FusedAdamW(torch.optim.Optimizer):
         for group, plist, tab in groups:
             call("fddm_grad_sumsq", tab["ct"].data_ptr(), tab["cs"].data_ptr(), tab["numel"].data_ptr(),
                  tab["g"].data_ptr(), tab["n"], total.data_ptr(), stream())
-        for group, plist, tab in groups:
+        for gi, (group, plist, tab) in enumerate(groups):
             b1, b2 = group["betas"]
             call("fddm_adamw", tab["ct"].data_ptr(), tab["cs"].data_ptr(), tab["numel"].data_ptr(), tab["p"].data_ptr(),
                  tab["g"].data_ptr(), tab["m"].data_ptr(), tab["v"].data_ptr(), tab["b"].data_ptr(), tab["s"].data_ptr(),
                  tab["nt"], tab["n"], total.data_ptr(), float(max_norm or 0.0), float(group["lr"]),
                  float(group["lr"] * group["weight_decay"]), float(b1), float(b2), float(group["eps"]),
-                 self._skipped.data_ptr(), stream())
+                 self._skipped.data_ptr() if gi == 0 else 0, stream())   # a skipped step counts once
         self.last_total_sq = total
         return total.sqrt()
 

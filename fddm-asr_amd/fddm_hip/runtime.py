@@ -64,6 +64,33 @@ def _entry(p, tensor) -> _Entry:
 
 _wcache: dict = {}
 _wcache_gen = 0          # bumped whenever an entry is created, replaced or dropped (optimizer tables check it)
+_cache_epoch = 0         # bumped by clear_cache() only: captured HIP graphs key their validity on it
+_retained = None         # list collecting every cached tensor handed out while `retaining()` is active
+
+
+def cache_epoch() -> int:
+    return _cache_epoch
+
+
+@contextlib.contextmanager
+def retaining():
+    """Collect strong references to every cached weight copy / table served inside the block. A HIP graph captured
+    inside reads these buffers by address on every replay, so its owner keeps the list alive (fddm_hip.graphs):
+    a later clear_cache() then cannot free memory the graph still reads."""
+    global _retained
+    old, _retained = _retained, []
+    try:
+        yield _retained
+    finally:
+        if old is not None:
+            old.extend(_retained)
+        _retained = old
+
+
+def _retain(t):
+    if _retained is not None:
+        _retained.append(t)
+    return t
 
 
 def wcache_generation() -> int:
@@ -88,7 +115,7 @@ def wt(p: torch.Tensor, dtype=None, transform=None, key=None) -> torch.Tensor:
     k = (id(p), dtype, key)
     e = _wcache.get(k)
     if e is not None and e.valid_for(p):
-        return e.tensor
+        return _retain(e.tensor)
     with torch.no_grad():
         src = transform(p.detach()) if transform is not None else p.detach()
         src = src.contiguous()
@@ -96,7 +123,7 @@ def wt(p: torch.Tensor, dtype=None, transform=None, key=None) -> torch.Tensor:
     global _wcache_gen
     _wcache[k] = _entry(p, out)
     _wcache_gen += 1
-    return out
+    return _retain(out)
 
 
 def wt_refresh_from(p: torch.Tensor, bf16_copy: torch.Tensor) -> None:
@@ -116,9 +143,10 @@ def wt_bf16_buffer(p: torch.Tensor) -> torch.Tensor:
 
 
 def clear_cache():
-    global _wcache_gen
+    global _wcache_gen, _cache_epoch
     _wcache.clear()
     _wcache_gen += 1
+    _cache_epoch += 1
     _tables.clear()
 
 
@@ -162,11 +190,11 @@ def _table_get(k, owner):
     """Cached derived table of `owner` under key k — only while that very tensor is alive (its id is reused
     once it is freed, so the key alone could hand a new model the old one's table)."""
     v = _tables.get(k)
-    return v[1] if v is not None and v[0]() is owner else None
+    return _retain(v[1]) if v is not None and v[0]() is owner else None
 
 
 def _table_put(k, owner, t):
-    _tables[k] = (weakref.ref(owner), t)
+    _tables[k] = (weakref.ref(owner), _retain(t))
 
 
 def rope_tables(L: int, inv_freq: torch.Tensor, device):

@@ -219,6 +219,18 @@ def mha(q_in, k_in, v_in, W, bias, Wo, bo, H, key_keep=None, drop_p=0.0, drop=No
     return F.linear(o, Wo, bo)
 
 
+_MASKS: dict = {}      # (kind, args) -> keep mask: the contract's masks are pure functions of their arguments
+
+
+def _memo_mask(key, make):
+    m = _MASKS.get(key)
+    if m is None:
+        if len(_MASKS) >= 96:
+            _MASKS.clear()
+        m = _MASKS[key] = make()
+    return m
+
+
 class _Dropper:
     """Deterministic dropout per site following the RNG contract (seed, stream = base + site)."""
 
@@ -229,7 +241,8 @@ class _Dropper:
         self.site += 1
         if self.p <= 0:
             return x
-        keep = dropout_keep(self.seed, self.site, x.numel(), self.p).view(x.shape)
+        keep = _memo_mask(("e", self.seed, self.site, x.numel(), self.p),
+                          lambda: dropout_keep(self.seed, self.site, x.numel(), self.p)).view(x.shape)
         return x * keep.float() * (1.0 / (1.0 - self.p))
 
     def attn(self, p: torch.Tensor) -> torch.Tensor:
@@ -238,7 +251,8 @@ class _Dropper:
         if self.p <= 0:
             return p
         B, H, Lq, Lk = p.shape
-        keep = attn_dropout_keep(self.seed, self.site, B, H, Lq, Lk, self.p)
+        keep = _memo_mask(("a", self.seed, self.site, B, H, Lq, Lk, self.p),
+                          lambda: attn_dropout_keep(self.seed, self.site, B, H, Lq, Lk, self.p))
         return p * keep.to(p.dtype) * (1.0 / (1.0 - self.p))
 
 
@@ -268,8 +282,9 @@ def decoder_block(sd, pre, x, cond, x_mask, cos, sin, H, drop: Optional[_Dropper
 
 
 def decoder_forward(sd: Dict[str, torch.Tensor], xt, t, cond, x_mask, H: int, num_layers: int, pad_id: int = 0,
-                    dropout: float = 0.0, seed: int = 0):
-    """DenoisingTransformerDecoder.forward — models/denoise_decoder.py:242-287."""
+                    dropout: float = 0.0, seed: int = 0, taps: Optional[list] = None):
+    """DenoisingTransformerDecoder.forward — models/denoise_decoder.py:242-287. `taps` (a list, optional) receives
+    each block's output x (with retain_grad() when it requires grad), for per-block error budgets in tests."""
     d = sd["tok_emb.weight"].shape[1]
     L = xt.shape[1]
     x = F.embedding(xt, sd["tok_emb.weight"], padding_idx=pad_id)            # :254
@@ -284,6 +299,10 @@ def decoder_forward(sd: Dict[str, torch.Tensor], xt, t, cond, x_mask, H: int, nu
     drop = _Dropper(dropout, seed) if dropout > 0 else None
     for i in range(num_layers):
         x = decoder_block(sd, f"blocks.{i}.", x, cond, x_mask, cos, sin, H, drop)
+        if taps is not None:
+            if x.requires_grad:
+                x.retain_grad()
+            taps.append(x)
     return F.linear(x, sd["head.weight"], sd["head.bias"])                    # :286
 
 
@@ -449,18 +468,25 @@ def clip_grads(grads: Dict[str, Optional[torch.Tensor]], max_norm: float = 5.0):
 
 
 def oracle_train_step(params: Dict[str, torch.Tensor], enc_sd, enc_geom, wave, x0, t, xt, cfg: dict,
-                      optim: OracleAdamW, global_step: int, betas, alpha_bar):
+                      optim: OracleAdamW, global_step: int, betas, alpha_bar, c: Optional[torch.Tensor] = None,
+                      dropout: float = 0.0, seed: int = 0, taps: Optional[list] = None):
     """One teacher-forced step of train_one_epoch (train.py:342-423). `params` holds the trainable
     tensors under the names decoder.*, s_proj.*, t_embed.*, t_proj.* and is updated in place.
     cfg keys: d_model, nhead, num_layers, pad_id, n_step_fd, tau, lambda_offdiag.
-    Returns dict(kl, lfd, loss, c, logits)."""
+    Optional: `c` replaces the encoder output (the step from a given acoustic condition, e.g. the GPU's own, to
+    separate the encoder's rounding from the decoder's); `dropout` / `seed` run the decoder's dropout sites under the
+    RNG contract (decoder_forward); `taps` collects the block outputs (their .grad after backward).
+    Returns dict(kl, lfd, loss, c, logits, dlogits, grads)."""
     d = cfg["d_model"]
-    with torch.no_grad():
-        c = acoustic_encoder(enc_sd, wave, enc_geom, d)                     # train.py:349
+    if c is None:
+        with torch.no_grad():
+            c = acoustic_encoder(enc_sd, wave, enc_geom, d)                 # train.py:349
     leaves = {n: p.detach().clone().requires_grad_(True) for n, p in params.items()}
     dec_sd = {n[len("decoder."):]: p for n, p in leaves.items() if n.startswith("decoder.")}
     x_mask = x0 != cfg["pad_id"]
-    logits = decoder_forward(dec_sd, xt, t, c, x_mask, cfg["nhead"], cfg["num_layers"], cfg["pad_id"])
+    logits = decoder_forward(dec_sd, xt, t, c, x_mask, cfg["nhead"], cfg["num_layers"], cfg["pad_id"],
+                             dropout=dropout, seed=seed, taps=taps)
+    logits.retain_grad()
     B, L, V = logits.shape
     # KL (train.py:190-255) by its direct formula, differentiated by autograd
     eps = 1e-8
@@ -496,7 +522,7 @@ def oracle_train_step(params: Dict[str, torch.Tensor], enc_sd, enc_geom, wave, x
     clip_grads(grads, 5.0)
     optim.step(params, grads)
     return dict(kl=float(kl.detach()), lfd=None if lfd_v is None else float(lfd_v.detach()), loss=float(loss.detach()), c=c,
-                logits=logits.detach(), grads=raw)
+                logits=logits.detach(), dlogits=logits.grad, grads=raw)
 
 
 # ------------------------------------------------------------------------------------------------

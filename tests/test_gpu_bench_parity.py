@@ -1,0 +1,218 @@
+"""Parity of the benchmark's own path (bench.py at C2, BASELINE.json configs[1]) at the benchmark's batch.
+
+`bench.build()` builds the models exactly as the timed run does: WavLM-base encoder (random init) + 6-layer
+d_model 512 / 8 heads / ff 2048 decoder, V = 8000, T = 200, dropout 0.1, bf16, fused AdamW. Two teacher-forced
+steps of `train.train_one_epoch` (global steps 3 and 4: a KL step and an L_fd step, reference train.py:340-443) run
+on B = 32 utterances of 10 s audio, so every launch takes the benchmark's kernel choice — gemm256 for the decoder's
+FF1 (GELU + dropout epilogue), the vocabulary head and the fused cross-attention K|V GEMM, persistent encoder GEMMs
+on their CU caps under HIP-graph replay on the side stream (both graph slots), the decoder attention kernels at
+their benchmark grids. The tests in tests/test_gpu_step_configs.py run the same geometry at B = 2, where those
+GEMMs fall to gemm128.
+
+The CPU oracle (oracle/fddm_oracle.py: oracle_train_step, decoder dropout under the RNG contract) is run twice per
+step's evidence:
+* the encoder: 2 utterances of each batch (one per graph slot) through O.acoustic_encoder against the GPU's
+  B = 32 output;
+* the decoder step: from the GPU's own bf16 acoustic condition c (upcast to fp32), so the encoder's rounding is
+  removed and what remains is the decoder forward / KL / L_fd / backward error of the bf16 path. The per-stage
+  errors (logits, dlogits, each block's dX, every parameter gradient) are printed as the error budget and the
+  tolerances below are set from them (about 2x the measured worst).
+"""
+from types import SimpleNamespace
+
+import pytest
+import torch
+
+from oracle import fddm_oracle as O
+
+pytestmark = pytest.mark.gpu
+dev = torch.device("cuda:0")
+
+SEED = 4242                 # the decoder's dropout seed (rt.next_seed pinned: the oracle replays the same masks)
+NOISE_ONLY = ("s_proj.proj.net.0.bias", "t_proj.proj.net.0.bias")   # d/dbias of a batch-standardised input is 0
+
+
+def rel(a, b):
+    """Norm-wise relative error ||a - b|| / ||b||."""
+    a, b = a.double(), b.double()
+    return float((a - b).norm() / b.norm().clamp_min(1e-300))
+
+
+def _args():
+    return SimpleNamespace(batch=32, seconds=10.0, seq_len=256, layers=6, d_model=512, heads=8, precision="bf16")
+
+
+@pytest.fixture(scope="module")
+def bench_run():
+    import bench
+    import train as T_
+    from fddm_hip import functions as FN
+    from fddm_hip import runtime as rt
+    from models.denoise_decoder import DecoderBlock
+
+    args = _args()
+    B, L, V, Tn = args.batch, args.seq_len, 8000, 200
+    old_prec = rt.precision()
+    torch.manual_seed(1337)
+    T_, cfg, models, opt = bench.build(args, dev)
+    enc, dec, sp, te, tp, sch = models
+    named = [("decoder." + n, p) for n, p in dec.named_parameters()]
+    for pre, m in (("s_proj.", sp), ("t_embed.", te), ("t_proj.", tp)):
+        named += [(pre + n, p) for n, p in m.named_parameters()]
+    init = {n: p.detach().float().cpu().clone() for n, p in named}
+    enc_sd = {k: v.detach().float().cpu() for k, v in enc.state_dict().items()}
+    batches = bench.synthetic_batches(args, dev, 2, 77)
+    g = torch.Generator().manual_seed(9)
+    ts = [torch.randint(1, Tn + 1, (B,), generator=g) for _ in range(2)]
+    ts[0][:3] = torch.tensor([1, 2, Tn])          # t = 1 (beta_{t-1} = 0 rule), t = 2 and t = T
+    _, ab = O.sched_tables(Tn)
+    betas, _ = O.sched_tables(Tn)
+    x0s = [b[1].cpu() for b in batches]
+    xts = [O.sample_xt(x0, t, V, ab, seed=60 + i) for i, (x0, t) in enumerate(zip(x0s, ts))]
+
+    rec = {"c": [], "logits": [], "kl": [], "lfd": [], "grads": [], "dlogits": [], "dx": {}}
+    step = [-1]
+    xq = iter([x.to(dev) for x in xts])
+    tq = iter([t.to(dev) for t in ts])
+
+    class TF(type(sch)):
+        def sample_q(self, x0, t):
+            return next(xq)
+
+        def kl_term(self, *a, **k):
+            v = super().kl_term(*a, **k)
+            rec["kl"].append(v)
+            return v
+
+    sch_tf = TF(sch.sch)
+    fwd = dec.forward
+
+    def dec_forward(xt, t, cond, *a, **k):
+        step[0] += 1
+        rec["c"].append(cond.detach().float().cpu())
+        out = fwd(xt, t, cond, *a, **k)
+        rec["logits"].append(out.detach().float().cpu())
+        return out
+
+    run_blk = DecoderBlock.run
+
+    def run_tap(self, x, xT, cT, key_keep, film, B_, L_, S_, layer, *a, **k):
+        x3, x3T = run_blk(self, x, xT, cT, key_keep, film, B_, L_, S_, layer, *a, **k)
+        key = (step[0], layer)
+        x3.register_hook(lambda gr: rec["dx"].__setitem__(key, gr.detach().float().cpu()))
+        return x3, x3T
+
+    head_bwd = FN.HeadFn.backward
+
+    def head_backward(ctx, dlogits):
+        dz16 = FN._dlogits_bf16.get(ctx.out_ptr)
+        eff = None if dz16 is None else dz16.float()
+        if dlogits is not None and not all(s_ == 0 for s_ in dlogits.stride()):
+            eff = dlogits.float() if eff is None else eff + dlogits.float().reshape(eff.shape)
+        rec["dlogits"].append(None if eff is None else eff.cpu())
+        return head_bwd(ctx, dlogits)
+
+    inner = opt.clip_and_step
+
+    def snap(*a, **k):
+        rec["grads"].append({n: (None if p.grad is None else p.grad.detach().float().cpu().clone()) for n, p in named})
+        return inner(*a, **k)
+
+    orig_lfd = T_.lfd_loss
+
+    def lfd_rec(*a, **k):
+        v = orig_lfd(*a, **k)
+        rec["lfd"].append(v)
+        return v
+
+    with pytest.MonkeyPatch.context() as mp:
+        mp.setattr(rt, "next_seed", lambda: SEED)
+        mp.setattr(dec, "forward", dec_forward)
+        mp.setattr(DecoderBlock, "run", run_tap)
+        mp.setattr(FN.HeadFn, "backward", staticmethod(head_backward))
+        mp.setattr(opt, "clip_and_step", snap)
+        mp.setattr(T_, "lfd_loss", lfd_rec)
+        gs, _ = T_.train_one_epoch(enc, dec, sp, te, tp, sch_tf, batches, opt, dev, cfg, 3, None, 1, False,
+                                   draw_t=lambda B_: next(tq))
+        torch.cuda.synchronize()
+    assert gs == 5 and len(rec["kl"]) == 2 and len(rec["lfd"]) == 1 and len(rec["grads"]) == 2
+    rec["kl"] = [float(v.detach()) for v in rec["kl"]]
+    rec["lfd"] = float(rec["lfd"][0].detach())
+    waves2 = [b[0][[0, B - 1]].cpu() for b in batches]      # 2 utterances per batch for the encoder check
+    del enc, dec, sp, te, tp, opt, models, batches
+    rt.set_precision(old_prec)
+    torch.cuda.empty_cache()
+
+    # ---- CPU oracle: the encoder on 2 utterances of each batch, the two steps from the GPU's condition
+    torch.set_num_threads(min(16, torch.get_num_threads()))
+    geom = O.wavlm_geometry()
+    c_ref2 = [O.acoustic_encoder(enc_sd, w, geom, args.d_model) for w in waves2]
+    params = {k: v.clone() for k, v in init.items()}
+    ocfg = dict(d_model=args.d_model, nhead=args.heads, num_layers=args.layers, pad_id=0, n_step_fd=4, tau=1.0,
+                lambda_offdiag=5e-3)
+    oopt = O.OracleAdamW()
+    ref = []
+    for i in range(2):
+        taps = []
+        r = O.oracle_train_step(params, None, None, None, x0s[i], ts[i], xts[i], ocfg, oopt, 3 + i, betas, ab,
+                                c=rec["c"][i], dropout=0.1, seed=SEED, taps=taps)
+        r["dx"] = [x.grad.detach().clone() for x in taps]
+        r.pop("c")
+        ref.append(r)
+    assert ref[0]["lfd"] is None and ref[1]["lfd"] is not None
+    return SimpleNamespace(rec=rec, ref=ref, c_ref2=c_ref2, args=args)
+
+
+def test_bench_encoder_output_matches_oracle(bench_run):
+    """The graph-replayed, CU-capped B = 32 encoder output (both slots) vs the fp32 oracle on 2 utterances each:
+    the bf16 WavLM's end-to-end error (24 bf16 GEMM layers, minimax-fit GELU on the frozen encoder's conv / FF1
+    epilogues, common.h:gelu_bf16out)."""
+    R = bench_run
+    for i in range(2):
+        c = R.rec["c"][i][[0, R.args.batch - 1]]
+        e = rel(c, R.c_ref2[i])
+        mx = float((c - R.c_ref2[i]).abs().max() / R.c_ref2[i].abs().max())
+        print(f"encoder batch {i}: rel-L2 {e:.3e}, max/max {mx:.3e}")
+        assert e < 3e-2 and mx < 5e-2, f"encoder batch {i}: rel {e:.3e} max {mx:.3e}"
+
+
+def test_bench_step_values_match_oracle(bench_run):
+    """KL (both steps) and L_fd at B = 32 from the same condition: the bf16 decoder's loss values."""
+    R = bench_run
+    for i in range(2):
+        e = abs(R.rec["kl"][i] - R.ref[i]["kl"]) / abs(R.ref[i]["kl"])
+        print(f"KL step {i}: {R.rec['kl'][i]:.6f} vs {R.ref[i]['kl']:.6f} (rel {e:.2e})")
+        assert e < 5e-3
+    e = abs(R.rec["lfd"] - R.ref[1]["lfd"]) / abs(R.ref[1]["lfd"])
+    print(f"L_fd: {R.rec['lfd']:.6f} vs {R.ref[1]['lfd']:.6f} (rel {e:.2e})")
+    assert e < 1e-2
+
+
+def test_bench_step_error_budget(bench_run):
+    """Per-stage error of the bf16 step at the benchmark's batch, encoder rounding removed: logits, the logits
+    gradient the head GEMMs consume, each block's output gradient dX (hooks on the block outputs, backward order),
+    then every parameter gradient as clip_grad_norm_ sees it (norm-wise, floor 1e-3 of the global norm; same None
+    pattern) and the global gradient norm."""
+    R = bench_run
+    for i in range(2):
+        el = rel(R.rec["logits"][i], R.ref[i]["logits"])
+        ed = rel(R.rec["dlogits"][i].view_as(R.ref[i]["dlogits"]), R.ref[i]["dlogits"])
+        dxs = [rel(R.rec["dx"][(i, k)], R.ref[i]["dx"][k]) for k in range(R.args.layers)]
+        print(f"step {i}: logits {el:.3e}  dlogits {ed:.3e}  dX per block " + " ".join(f"{v:.3e}" for v in dxs))
+        assert el < 1e-2 and ed < 2e-2 and max(dxs) < 3e-2, (el, ed, dxs)
+        g, r = R.rec["grads"][i], R.ref[i]["grads"]
+        assert g.keys() == r.keys()
+        assert {n for n in g if g[n] is None} == {n for n in r if r[n] is None}, f"step {i}: None grads"
+        G = sum(float((v.double() ** 2).sum()) for v in r.values() if v is not None) ** 0.5
+        Gg = sum(float((v.double() ** 2).sum()) for v in g.values() if v is not None) ** 0.5
+        ratios = {}
+        for n in g:
+            if g[n] is None or n in NOISE_ONLY:
+                continue
+            err = float((g[n].double() - r[n].double()).norm())
+            ratios[n] = err / max(float(r[n].double().norm()), 1e-3 * G)
+        worst = sorted(ratios.items(), key=lambda kv: -kv[1])[:8]
+        print(f"step {i}: global grad norm {Gg:.6e} vs {G:.6e}; worst grad rel err " +
+              ", ".join(f"{n} {v:.2e}" for n, v in worst))
+        assert abs(Gg - G) <= 1e-2 * G
+        assert worst[0][1] <= 3e-2, worst

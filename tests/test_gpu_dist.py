@@ -215,3 +215,138 @@ def test_dp_train_step_global_batch_lfd_matches_full_batch():
             assert abs(da - db) <= 5e-3 * db + 1e-12, f"rank {r} {n}: update {da:.4e} vs {db:.4e}"
             if "in_proj_bias" not in n:
                 assert ((a - p.double()).abs() > 4e-6).float().mean().item() < 0.02, f"rank {r} {n}"
+
+
+# ------------------------------------------------------- the N > 1 benchmark path and the C2 geometry under DP
+def test_bench_two_ranks_run_real_c2_steps():
+    """`bench.py --gpus 2` at C2 (not a dry run): two ranks (gloo, both on this box's GPU; the 8-GPU node runs the
+    same code over RCCL, one GPU per rank) run warm-up and timed train steps with the overlapped gradient
+    all-reduce, the HIP-graph encoder on its side stream and the CU caps; the line reports n_gpus 2 / dp2 and a
+    finite loss, and both replicas end with bit-identical parameters (BASELINE configs[2])."""
+    import json
+    import math
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, FDDM_DIST_BACKEND="gloo", FDDM_DIST_TIMEOUT_S="300")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "3", "--warmup", "1",
+                        "--no-cpu-baseline", "--checksum"], cwd=root, env=env, capture_output=True, text=True,
+                       timeout=900)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    print(json.dumps({k: out[k] for k in ("value", "ms_per_step", "n_gpus", "avg_loss", "param_checksums")}))
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 64
+    assert math.isfinite(out["avg_loss"]) and out["value"] > 0
+    cs = out["param_checksums"]
+    assert len(cs) == 2 and cs[0] == cs[1], cs
+
+
+def _c2_dp_grads(rank, world):
+    """Two teacher-forced train_one_epoch steps (global steps 3: KL, 4: L_fd with global-batch statistics) at the C2
+    decoder geometry (6 layers, d_model 512, 8 heads, ff 2048, L 256, V 8000) over WavLM-base on 10 s audio, encoder
+    graph-replayed on its side stream with the CU caps, on this rank's rows (all 4 when world == 1); returns the
+    gradients clip_grad_norm_ sees at each step (after the DP average)."""
+    import train as T_
+    from fddm.sched.diffusion_scheduler import DiscreteDiffusionScheduler
+    from fddm_hip import runtime as rt
+    from fddm_hip.optim import FusedAdamW
+    from helpers import _step_params
+    from models.projection import SpeechProjector, TextEmbedding, TextProjector
+    from test_gpu_models import _encoder, make_decoder
+    dev = torch.device("cuda:0")
+    V_, d_, H_, NL_, FF_, L_, T_n = 8000, 512, 8, 6, 2048, 256, 200
+    g = torch.Generator().manual_seed(33)
+    data = []
+    for i in range(2):
+        wave = 0.1 * torch.randn(4, 160000, generator=g)
+        x0 = torch.randint(1, V_, (4, L_), generator=g)
+        x0[1, 200:] = 0
+        x0[3, 150:] = 0
+        xt = torch.randint(1, V_, (4, L_), generator=g)
+        t = torch.tensor([1, 50, 120, 200]) if i == 0 else torch.tensor([7, 2, 199, 64])
+        data.append((wave, x0, xt, t))
+    sl = slice(None) if world == 1 else slice(2 * rank, 2 * rank + 2)
+    data = [tuple(v[sl] for v in b) for b in data]
+    with rt.use_precision("fp32"):
+        enc = _encoder({}, d_)
+        dec = make_decoder(V_, d_, H_, NL_, FF_)
+        params = _step_params(V_, d_, NL_, FF_, H_)
+        sp, te, tp = SpeechProjector(d_, 256), TextEmbedding(V_, 256), TextProjector(256, 256)
+        for pre, m in (("s_proj.", sp), ("t_embed.", te), ("t_proj.", tp)):
+            m.load_state_dict({n: params[pre + n] for n, _ in m.named_parameters()})
+            m.to(dev)
+        named = [("decoder." + n, p) for n, p in dec.named_parameters()]
+        for pre, m in (("s_proj.", sp), ("t_embed.", te), ("t_proj.", tp)):
+            named += [(pre + n, p) for n, p in m.named_parameters()]
+        xq = iter([b[2].to(dev) for b in data])
+        tq = iter([b[3].to(dev) for b in data])
+
+        class TF(T_.SchedulerAdapter):
+            def sample_q(self, x0, t):
+                return next(xq)
+
+        opt = FusedAdamW([p for _, p in named], lr=2e-4, weight_decay=0.01)
+        grads = []
+        inner = opt.clip_and_step
+
+        def snap(*a, **k):
+            grads.append({n: (None if p.grad is None else p.grad.detach().cpu().clone()) for n, p in named})
+            return inner(*a, **k)
+
+        opt.clip_and_step = snap
+        cfg = T_.Config(seed=1, data={"pad_id": 0}, model={}, diffusion={"T": T_n}, inference={}, optim={},
+                        lfd={"n_step_fd": 4, "tau": 1.0, "lambda_offdiag": 5e-3, "sync_batch_stats": True},
+                        log={"log_every": 1000})
+        sch = TF(DiscreteDiffusionScheduler(K=V_, T=T_n, device=dev))
+        from train import GraphedEncoder
+        assert GraphedEncoder.supported(enc)
+        T_.train_one_epoch(enc, dec, sp, te, tp, sch, [(b[0], b[1]) for b in data], opt, dev, cfg, 3, None, 1, False,
+                           draw_t=lambda B: next(tq))
+        torch.cuda.synchronize()
+    return grads
+
+
+def _c2_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import datetime
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=300))
+    try:
+        grads = _c2_dp_grads(rank, world)
+        q.put((rank, [{n: (None if v is None else v.numpy()) for n, v in gr.items()} for gr in grads]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_c2_geometry_matches_full_batch():
+    """The overlapped all-reduce at the C2 decoder geometry, beside the graph-replayed, CU-capped encoder stream:
+    two ranks x 2 utterances give, at both steps (KL, then L_fd with global-batch statistics), the gradients of one
+    process on all 4 utterances (fp32 parity mode, norm-wise 1e-4; same None pattern)."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_c2_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(world):
+        r, gr = q.get(timeout=400)
+        got[r] = gr
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = _c2_dp_grads(0, 1)
+    for i in range(2):
+        G = sum(float((v.double() ** 2).sum()) for v in ref[i].values() if v is not None) ** 0.5
+        for r in range(world):
+            assert {n for n, v in got[r][i].items() if v is None} == {n for n, v in ref[i].items() if v is None}
+            worst = 0.0
+            for n, v in ref[i].items():
+                if v is None or n in NOISE_ONLY:
+                    continue
+                e = float((torch.from_numpy(got[r][i][n]).double() - v.double()).norm())
+                worst = max(worst, e / max(float(v.double().norm()), 1e-3 * G))
+            print(f"step {i} rank {r}: worst grad rel err {worst:.2e}")
+            assert worst < 1e-4

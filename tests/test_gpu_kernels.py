@@ -747,6 +747,24 @@ def test_fused_adamw_nonfinite_guard_skips_whole_step():
     assert all(float(opt.state[p]["step"]) == 2.0 for p in dps)
 
 
+def test_fused_adamw_skip_counts_once_over_groups():
+    """With several parameter groups a skipped (non-finite) step is counted once, not once per group's launch
+    (ADVICE r2), and no group is updated."""
+    from fddm_hip.optim import FusedAdamW
+    from fddm_hip import runtime as rt
+    with rt.use_precision("fp32"):
+        ps = [torch.nn.Parameter(torch.randn(40, 7, device=dev)) for _ in range(3)]
+        opt = FusedAdamW([{"params": [ps[0]]}, {"params": [ps[1]], "lr": 1e-3}, {"params": [ps[2]]}], lr=2e-4)
+        before = [p.detach().clone() for p in ps]
+        for p in ps:
+            p.grad = torch.randn(40, 7, device=dev)
+        ps[1].grad[0, 0] = float("inf")
+        opt.clip_and_step(max_norm=5.0)
+        torch.cuda.synchronize()
+        assert int(opt.skipped_steps()[0]) == 1
+        assert all(torch.equal(p.detach(), b) for p, b in zip(ps, before))
+
+
 def test_fused_adamw_follows_replaced_bf16_copies():
     """The optimizer writes each weight's bf16 copy for the next forward; when the runtime cache replaces that
     copy (clear_cache after a checkpoint load, an in-place change of the parameter), the optimizer's device

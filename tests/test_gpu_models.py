@@ -289,3 +289,102 @@ def test_graphed_encoder_recaptures_after_weight_change():
         torch.cuda.synchronize()
     assert float((again - ref).abs().max()) == 0.0
     assert float((again - first).abs().max()) > 0.0
+
+
+def test_graphed_encoder_survives_clear_cache():
+    """rt.clear_cache() (load_checkpoint calls it) drops the runtime's cached relative-bias table and bf16 encoder.proj
+    weight that a captured encoder graph reads by address: the graph runner holds those buffers for its
+    captures and recaptures on the next run, so a replay after the clear equals the eager forward."""
+    from fddm_hip.graphs import GraphedEncoder
+    rt = _rt()
+    with rt.use_precision("bf16"):
+        enc = _encoder(SMALL_WAVLM, 96)
+        assert enc.use_proj
+        ge = GraphedEncoder(enc)
+        w = 0.1 * torch.randn(2, 16000, generator=torch.Generator().manual_seed(6)).to(dev)
+        first = ge.run(w, 1).float().clone()
+        slot = ge.cache[next(iter(ge.cache))][1]
+        assert len(slot.keep) >= 2, "the capture must hold the cached tensors it reads"
+        rt.clear_cache()
+        junk = [torch.randn(1024, 1024, device=dev) for _ in range(8)]     # reuse the freed cache memory
+        for j in junk:
+            j.mul_(3.0)
+        again = ge.run(w, 1).float().clone()
+        ref = enc(w)[0].float()
+        torch.cuda.synchronize()
+    assert float((again - ref).abs().max()) == 0.0
+    assert float((first - ref).abs().max()) == 0.0
+
+
+@pytest.mark.parametrize("prec,tol", [("fp32", 1e-4), ("bf16", 3e-2)])
+def test_train_step_odd_vocab_matches_oracle(prec, tol, monkeypatch):
+    """A vocabulary the one-pass KL kernel is not built for (V = 997: V % 4 != 0) and the bf16 softmax-backward
+    hand-over skips (V % 8 != 0): two teacher-forced train_one_epoch steps (a KL step and an L_fd step) take the
+    two-pass KL and the f32 softmax backward, and match oracle_train_step from the same condition."""
+    import torch.nn as nn
+
+    import train as T_
+    from fddm.sched.diffusion_scheduler import DiscreteDiffusionScheduler
+    from fddm_hip.optim import FusedAdamW
+    from models.projection import SpeechProjector, TextEmbedding, TextProjector
+    rt = _rt()
+    V, d, H, NL, FF, B, L, S, Tn = 997, 128, 2, 2, 256, 3, 24, 30, 20
+
+    class Identity(nn.Module):      # the "encoder": the loader hands the acoustic condition itself
+        def forward(self, c):
+            return c, None, None
+
+    gen = torch.Generator().manual_seed(12)
+    conds = [torch.randn(B, S, d, generator=gen) for _ in range(2)]
+    x0s = [torch.randint(1, V, (B, L), generator=gen) for _ in range(2)]
+    x0s[0][1, 17:] = 0
+    ts = [torch.tensor([1, 9, 20]), torch.tensor([4, 2, 13])]
+    betas, ab = O.sched_tables(Tn)
+    xts = [O.sample_xt(x0, t, V, ab, seed=5 + i) for i, (x0, t) in enumerate(zip(x0s, ts))]
+    params = _step_params(V, d, NL, FF, H)
+    rec = {"kl": [], "lfd": []}
+    with rt.use_precision(prec):
+        dec = make_decoder(V, d, H, NL, FF)
+        sp, te, tp = SpeechProjector(d, 256), TextEmbedding(V, 256), TextProjector(256, 256)
+        for pre, m in (("s_proj.", sp), ("t_embed.", te), ("t_proj.", tp)):
+            m.load_state_dict({n: params[pre + n] for n, _ in m.named_parameters()})
+            m.to(dev)
+        xq = iter([x.to(dev) for x in xts])
+        tq = iter([t.to(dev) for t in ts])
+
+        class TF(T_.SchedulerAdapter):
+            def sample_q(self, x0, t):
+                return next(xq)
+
+            def kl_term(self, *a, **k):
+                v = super().kl_term(*a, **k)
+                rec["kl"].append(float(v.detach()))
+                return v
+
+        orig = T_.lfd_loss
+
+        def rl(*a, **k):
+            v = orig(*a, **k)
+            rec["lfd"].append(float(v.detach()))
+            return v
+
+        monkeypatch.setattr(T_, "lfd_loss", rl)
+        trainable = list(dec.parameters()) + list(sp.parameters()) + list(te.parameters()) + list(tp.parameters())
+        opt = FusedAdamW(trainable, lr=2e-4, weight_decay=0.01)
+        cfg = T_.Config(seed=1, data={"pad_id": 0}, model={}, diffusion={"T": Tn}, inference={}, optim={},
+                        lfd={"n_step_fd": 4, "tau": 1.0, "lambda_offdiag": 5e-3}, log={"log_every": 1000})
+        loader = list(zip(conds, x0s))
+        T_.train_one_epoch(Identity(), dec, sp, te, tp, TF(DiscreteDiffusionScheduler(K=V, T=Tn, device=dev)), loader,
+                           opt, dev, cfg, 3, None, 1, False, draw_t=lambda B_: next(tq))
+        torch.cuda.synchronize()
+    ocfg = dict(d_model=d, nhead=H, num_layers=NL, pad_id=0, n_step_fd=4, tau=1.0, lambda_offdiag=5e-3)
+    oopt = O.OracleAdamW()
+    ref = [O.oracle_train_step(params, None, None, None, x0s[i], ts[i], xts[i], ocfg, oopt, 3 + i, betas, ab,
+                               c=conds[i]) for i in range(2)]
+    close(torch.tensor(rec["kl"]), torch.tensor([r["kl"] for r in ref]), rtol=tol, what=f"{prec} odd-V KL")
+    close(torch.tensor(rec["lfd"]), torch.tensor([ref[1]["lfd"]]), rtol=tol, what=f"{prec} odd-V L_fd")
+    final = {("decoder." + n): p.detach().cpu() for n, p in dec.named_parameters()}
+    for pre, m in (("s_proj.", sp), ("t_embed.", te), ("t_proj.", tp)):
+        final.update({pre + n: p.detach().cpu() for n, p in m.named_parameters()})
+    for n in ("decoder.head.weight", "decoder.blocks.0.ff.0.weight", "t_embed.proj.weight"):
+        close(final[n], params[n], rtol=1e-4 if prec == "fp32" else 2e-3, what=f"{prec} odd-V {n}")
