@@ -38,6 +38,7 @@ import torch.distributed as dist  # noqa: E402
 
 BF16_PEAK_TFLOPS = 2500.0       # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 F32_PEAK_TFLOPS = 157.3
+HBM_PEAK_TBS = 8.0
 
 
 def parse():
@@ -169,18 +170,39 @@ def synthetic_batches(args, device, n, seed):
     return out
 
 
+CONV1_SOURCES = ("gemm256.hip", "gemm.hip", "gemm.h", "lds_dma.h", "common.h")
+
+
+def conv1_src_sha() -> str:
+    """Hash of the kernel sources the dominant launch (conv layer 1 on gemm256) is compiled from: a committed PMC
+    traffic figure is only valid for the kernel build it was measured on."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in CONV1_SOURCES:
+        with open(os.path.join(ROOT, "fddm-asr_amd", "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def pmc_traffic(args):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary
-    (profiles/*_pmc_conv1.json, written by tools/pmc_traffic.py for this workload), else None."""
+    (profiles/rNN_pmc_conv1.json, written by tools/pmc_traffic.py for this workload) — only a file measured on the
+    current kernel sources (`kernel_src_sha`); otherwise (None, the reason)."""
     import glob
+    sha = conv1_src_sha()
+    stale = None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_conv1.json")), reverse=True):
         try:
             d = json.load(open(path))
         except Exception:
             continue
-        if d.get("batch") == args.batch and d.get("traffic_bytes"):
-            return float(d["traffic_bytes"]), os.path.basename(path)
-    return None, None
+        if d.get("batch") != args.batch or not d.get("traffic_bytes"):
+            continue
+        if d.get("kernel_src_sha") != sha:
+            stale = stale or f"stale: {os.path.basename(path)} was measured on other kernel sources"
+            continue
+        return float(d["traffic_bytes"]), os.path.basename(path)
+    return None, stale
 
 
 def dominant_flops(args):
@@ -232,10 +254,20 @@ def decoder_attention(args, probes, peak):
             continue
         ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
         lk = L if "self" in name else S
-        fl = (10 if name.endswith("bwd") else 4) * args.batch * args.heads * L * lk * dh
+        bwd = name.endswith("bwd")
+        fl = (10 if bwd else 4) * args.batch * args.heads * L * lk * dh
         tf = fl / (ms * 1e-3) / 1e12
+        # algorithmic HBM bytes (bf16 tensors): fwd reads Q, K, V and writes O; bwd reads Q, K, V, O, dO and writes
+        # dQ, dK, dV (the per-row LSE / delta and the dropout keep words are < 2 % and left out)
+        q_b, kv_b = 2.0 * args.batch * L * args.d_model, 2.0 * args.batch * lk * args.d_model
+        byts = (4 * q_b + 4 * kv_b) if bwd else (2 * q_b + 2 * kv_b)
+        hbm_us = byts / (HBM_PEAK_TBS * 1e12) * 1e6
+        mfma_us = fl / (peak * 1e12) * 1e6
         row = {"avg_us": round(1e3 * ms, 1), "gflop_per_launch": round(fl / 1e9, 3), "tflops": round(tf, 1),
-               "frac": round(tf / peak, 4), "launches": len(ev)}
+               "frac": round(tf / peak, 4), "launches": len(ev), "hbm_mb_per_launch": round(byts / 1e6, 1),
+               "hbm_floor_us": round(hbm_us, 2), "mfma_floor_us": round(mfma_us, 2),
+               # the best MFMA fraction a launch could reach when it must also move its bytes at HBM peak
+               "attainable_frac": round(mfma_us / max(hbm_us, mfma_us), 4)}
         rep = probes.get(name + "#replay") or []
         if rep:   # the same launches replayed back to back on the step's tensors: kernel time without launch gaps
             kms = sum(a.elapsed_time(b) / n for a, b, n in rep) / len(rep)
@@ -450,7 +482,7 @@ def main():
             dist.destroy_process_group()
         return
     device = torch.device("cuda", local)
-    torch.manual_seed(1337 + rank)
+    torch.manual_seed(1337)         # one model init on every rank (train_one_epoch also broadcasts rank 0's weights)
     if args.config == "c5":
         return run_c5(args, device, world, rank)
     T_, cfg, models, opt = build(args, device)

@@ -87,6 +87,34 @@ def global_mean(x: torch.Tensor, group=None) -> torch.Tensor:
 
 
 @torch.no_grad()
+def broadcast_params(tensors, src: int = 0, bucket_bytes: int = BUCKET_BYTES) -> None:
+    """Make every rank's copy of `tensors` (parameters / buffers) equal to rank `src`'s, in flat buckets per dtype
+    (what DistributedDataParallel's constructor does): replicas that start from different random inits would
+    otherwise drift apart under the averaged gradients. The copies back go through Tensor.copy_ so each tensor's
+    version counter moves and every cached low-precision / permuted copy of it is rebuilt."""
+    if world() <= 1:
+        return
+    by_dtype = {}
+    for t in tensors:
+        by_dtype.setdefault((t.dtype, t.device), []).append(t)
+    for (dt, dev), ts in by_dtype.items():
+        bucket, size = [], 0
+        for t in ts + [None]:
+            if t is not None:
+                bucket.append(t)
+                size += t.numel() * t.element_size()
+            if bucket and (t is None or size >= bucket_bytes):
+                flat = torch.cat([x.detach().reshape(-1) for x in bucket])
+                dist.broadcast(flat, src=src)
+                off = 0
+                for x in bucket:
+                    n = x.numel()
+                    x.copy_(flat[off:off + n].view_as(x))
+                    off += n
+                bucket, size = [], 0
+
+
+@torch.no_grad()
 def allreduce_grads(params, bucket_bytes: int = BUCKET_BYTES) -> None:
     W = world()
     if W <= 1:

@@ -213,6 +213,12 @@ def train_one_epoch(encoder, decoder, s_proj, t_embed, t_proj, scheduler, loader
         if all(id(p) in opt_ids for p in dparams):
             order = decoder.grad_ready_order() if hasattr(decoder, "grad_ready_order") else None
             optimizer.use_grad_arena(dparams, order)
+    if fdist.world() > 1 and not getattr(optimizer, "_fddm_replicas_synced", False):
+        # DP replicas start from rank 0's weights (DDP's constructor broadcast): the trainable parameters and the
+        # frozen encoder's parameters / buffers (a random-init encoder differs per rank otherwise)
+        fdist.broadcast_params(trainable + list(encoder.parameters()) + list(encoder.buffers()) +
+                               [b for m in (decoder, s_proj, t_embed, t_proj) for b in m.buffers()])
+        optimizer._fddm_replicas_synced = True
     arena = getattr(optimizer, "arena", None)
     if arena is not None and fdist.world() > 1 and arena.reducer is None:
         fdist.OverlapReducer(arena)     # gradient all-reduce overlapped with backward

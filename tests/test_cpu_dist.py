@@ -105,3 +105,42 @@ def test_overlap_reducer_gloo_world2():
                       for r in range(world)) / world
             for r in range(world):
                 torch.testing.assert_close(torch.from_numpy(got[(r, step)][i]), exp, rtol=1e-6, atol=1e-6)
+
+
+def _bcast_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from fddm_hip import dist as fdist
+        torch.manual_seed(10 + rank)                 # different inits per rank
+        ts = [torch.nn.Parameter(torch.randn(5, 3)), torch.nn.Parameter(torch.randn(9)), torch.randint(0, 9, (4,))]
+        v0 = ts[0]._version
+        fdist.broadcast_params(ts, bucket_bytes=32)  # tiny buckets: several flushes, mixed dtypes
+        q.put((rank, [t.detach().numpy().copy() for t in ts], ts[0]._version > v0))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_broadcast_params_gloo_world2():
+    """DP replicas start from rank 0's weights (fddm_hip.dist.broadcast_params, called once by train_one_epoch):
+    every rank ends with rank 0's values, per dtype, across bucket boundaries, and the in-place copy moves the
+    version counters (so cached bf16 / permuted weight copies are rebuilt)."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_bcast_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(world):
+        r, vals, bumped = q.get(timeout=120)
+        got[r] = (vals, bumped)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    torch.manual_seed(10)
+    ref = [torch.randn(5, 3), torch.randn(9), torch.randint(0, 9, (4,))]
+    for r in range(world):
+        assert got[r][1]
+        for a, b in zip(got[r][0], ref):
+            assert torch.equal(torch.from_numpy(a), b)

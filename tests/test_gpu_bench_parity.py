@@ -182,10 +182,10 @@ def test_bench_step_values_match_oracle(bench_run):
     for i in range(2):
         e = abs(R.rec["kl"][i] - R.ref[i]["kl"]) / abs(R.ref[i]["kl"])
         print(f"KL step {i}: {R.rec['kl'][i]:.6f} vs {R.ref[i]['kl']:.6f} (rel {e:.2e})")
-        assert e < 5e-3
+        assert e < 2e-4          # measured 7e-7 / 9e-6
     e = abs(R.rec["lfd"] - R.ref[1]["lfd"]) / abs(R.ref[1]["lfd"])
     print(f"L_fd: {R.rec['lfd']:.6f} vs {R.ref[1]['lfd']:.6f} (rel {e:.2e})")
-    assert e < 1e-2
+    assert e < 1e-3
 
 
 def test_bench_step_error_budget(bench_run):
@@ -197,9 +197,10 @@ def test_bench_step_error_budget(bench_run):
     for i in range(2):
         el = rel(R.rec["logits"][i], R.ref[i]["logits"])
         ed = rel(R.rec["dlogits"][i].view_as(R.ref[i]["dlogits"]), R.ref[i]["dlogits"])
-        dxs = [rel(R.rec["dx"][(i, k)], R.ref[i]["dx"][k]) for k in range(R.args.layers)]
+        dxs = [rel(R.rec["dx"][(i, k)].view_as(R.ref[i]["dx"][k]), R.ref[i]["dx"][k]) for k in range(R.args.layers)]
         print(f"step {i}: logits {el:.3e}  dlogits {ed:.3e}  dX per block " + " ".join(f"{v:.3e}" for v in dxs))
-        assert el < 1e-2 and ed < 2e-2 and max(dxs) < 3e-2, (el, ed, dxs)
+        # measured (both steps): logits <= 4.0e-3, dlogits <= 2.2e-3, dX <= 3.8e-3
+        assert el < 1e-2 and ed < 5e-3 and max(dxs) < 1e-2, (el, ed, dxs)
         g, r = R.rec["grads"][i], R.ref[i]["grads"]
         assert g.keys() == r.keys()
         assert {n for n in g if g[n] is None} == {n for n in r if r[n] is None}, f"step {i}: None grads"
@@ -214,5 +215,6 @@ def test_bench_step_error_budget(bench_run):
         worst = sorted(ratios.items(), key=lambda kv: -kv[1])[:8]
         print(f"step {i}: global grad norm {Gg:.6e} vs {G:.6e}; worst grad rel err " +
               ", ".join(f"{n} {v:.2e}" for n, v in worst))
-        assert abs(Gg - G) <= 1e-2 * G
-        assert worst[0][1] <= 3e-2, worst
+        # measured: global norm 2e-4 / 8.5e-3; worst parameter 5.4e-3 (KL step), 1.4e-2 (L_fd step: projectors)
+        assert abs(Gg - G) <= 2e-2 * G
+        assert worst[0][1] <= (1.2e-2, 3e-2)[i], worst

@@ -19,10 +19,10 @@ rounding noise). After the two AdamW steps the per-parameter update norms are co
 fp32 (parity) mode: KL and L_fd within 1e-4 relative, gradients rtol 1e-4 on the KL step and 3e-4 on the L_fd
 step (measured worst 1.2e-4 at C4: the B = 2 batch-dim standardisation of L_fd, 1/sqrt(var + eps) per column,
 scales up summation-order differences), global gradient norm 1e-5, update norms within 5e-3.
-bf16 mode (the benchmark's precision): KL within 2e-2 relative, L_fd within 3e-2, gradients rtol 5e-2 on the KL
-step and 1.5e-1 on the L_fd step, global gradient norm within 2e-2 (measured worst 3.6e-2 / 1.2e-1: bf16
-operands carry 8 mantissa bits and the comparison is end to end — the bf16 WavLM output the decoder and the
-speech projector consume already differs from the fp32 oracle's by ~1e-2, tests/test_gpu_models.py). Update
+bf16 mode (the benchmark's precision): the encoder output against the oracle's WavLM (2.5e-2), then the step against
+the oracle run from the GPU's own condition (the decoder path's error alone: KL 5e-3, L_fd 1e-2, gradients 1.5e-2 on
+the KL step and 4e-2 on the L_fd step — B = 2 makes the batch standardisation of L_fd an amplifier, each column is
+scaled by 2 / |z_1 - z_2| — global gradient norm 1e-2; see test_train_step_bf16_matches_oracle). Update
 norms are not compared in bf16: AdamW's first steps are ~lr * sign(g), so elements whose gradient is at the
 rounding-noise level (directions with an analytically zero gradient, e.g. the mean-key direction of the K
 projection) move by O(lr) in a direction the noise picks. Elementwise parameter values are not compared at these
@@ -57,7 +57,7 @@ def _inputs(L, V, Tn, B=2, seconds=10.0):
     return waves, x0s, ts
 
 
-def _run(cfg_name, prec, monkeypatch):
+def _run(cfg_name, prec, monkeypatch, oracle_c_from_gpu=False):
     import train as T_
     from fddm.sched.diffusion_scheduler import DiscreteDiffusionScheduler
     from fddm_hip import runtime as rt
@@ -98,6 +98,14 @@ def _run(cfg_name, prec, monkeypatch):
             return v
 
         monkeypatch.setattr(T_, "lfd_loss", rl)
+        conds = []
+        fwd = dec.forward
+
+        def dec_forward(xt, t, cond, *a, **k):      # the acoustic condition the decoder consumed
+            conds.append(cond.detach().float().cpu())
+            return fwd(xt, t, cond, *a, **k)
+
+        monkeypatch.setattr(dec, "forward", dec_forward)
         named = [("decoder." + n, p) for n, p in dec.named_parameters()]
         for pre, m in (("s_proj.", sp), ("t_embed.", te), ("t_proj.", tp)):
             named += [(pre + n, p) for n, p in m.named_parameters()]
@@ -122,7 +130,8 @@ def _run(cfg_name, prec, monkeypatch):
     final = {("decoder." + n): p.detach().cpu() for n, p in dec.named_parameters()}
     for pre, m in (("s_proj.", sp), ("t_embed.", te), ("t_proj.", tp)):
         final.update({pre + n: p.detach().cpu() for n, p in m.named_parameters()})
-    got = dict(kl=[float(v.detach()) for v in rec["kl"]], lfd=float(rec["lfd"][0].detach()), final=final, grads=step_grads)
+    got = dict(kl=[float(v.detach()) for v in rec["kl"]], lfd=float(rec["lfd"][0].detach()), final=final, grads=step_grads,
+               c=conds)
     del enc, dec, sp, te, tp, opt
     torch.cuda.empty_cache()
     # ---- CPU oracle: the same two steps
@@ -133,7 +142,13 @@ def _run(cfg_name, prec, monkeypatch):
     ref = []
     for i in range(2):
         ref.append(O.oracle_train_step(params, enc_sd, O.wavlm_geometry(), waves[i], x0s[i], ts[i], xts[i], ocfg,
-                                       oopt, 3 + i, betas, ab))
+                                       oopt, 3 + i, betas, ab, c=got["c"][i] if oracle_c_from_gpu else None))
+    if oracle_c_from_gpu:       # the encoder on its own: the GPU's condition vs the oracle's WavLM
+        for i in range(2):
+            cr = O.acoustic_encoder(enc_sd, waves[i], O.wavlm_geometry(), d)
+            e = float((got["c"][i].double() - cr.double()).norm() / cr.double().norm())
+            print(f"{cfg_name} {prec} encoder output step {i}: rel-L2 {e:.3e}")
+            assert e < 2.5e-2
     assert ref[0]["lfd"] is None and ref[1]["lfd"] is not None
     if cfg_name == "C4":
         assert ref[1]["c"].shape[1] < L, "C4 must take the S < L repeat branch"
@@ -187,8 +202,14 @@ def test_train_step_fp32_matches_oracle(cfg_name, monkeypatch):
 
 @pytest.mark.parametrize("cfg_name", ["C2", "C4"])
 def test_train_step_bf16_matches_oracle(cfg_name, monkeypatch):
-    got, ref, init, ref_params = _run(cfg_name, "bf16", monkeypatch)
+    """bf16 error budget, measured (tests/test_gpu_bench_parity.py prints the per-stage split at B = 32): the bf16
+    WavLM's output differs from the fp32 oracle's by ~1.0e-2 (rel-L2) and that condition feeds every block's
+    cross-attention and FiLM — it was the ~3e-2 uniform gradient error of this test when the oracle ran its own
+    encoder. So the encoder is checked on its own (2.5e-2) and the decoder step against the oracle run from the
+    GPU's condition: the rest of the bf16 path (decoder fwd, KL, L_fd, backward) measured <= 6.4e-3 (KL step) and
+    1.4e-2 (L_fd step, projector weights) at B = 32."""
+    got, ref, init, ref_params = _run(cfg_name, "bf16", monkeypatch, oracle_c_from_gpu=True)
     for i in range(2):
-        close(got["kl"][i], ref[i]["kl"], rtol=2e-2, what=f"{cfg_name} bf16 KL step {i}")
-    close(got["lfd"], ref[1]["lfd"], rtol=3e-2, what=f"{cfg_name} bf16 L_fd")
-    _check_grads(got, ref, (5e-2, 1.5e-1), 2e-2, f"{cfg_name} bf16")
+        close(got["kl"][i], ref[i]["kl"], rtol=5e-3, what=f"{cfg_name} bf16 KL step {i}")
+    close(got["lfd"], ref[1]["lfd"], rtol=1e-2, what=f"{cfg_name} bf16 L_fd")
+    _check_grads(got, ref, (1.5e-2, 4e-2), 1e-2, f"{cfg_name} bf16")

@@ -10,8 +10,12 @@ kernel's grid is one workgroup per CU for all of them); it is the dispatch of th
 """
 import csv
 import json
+import os
 import sys
 from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import conv1_src_sha  # noqa: E402
 
 
 def load(path, counter):
@@ -45,7 +49,9 @@ def main():
     fpath, wpath, sub, out = sys.argv[1:5]
     f, nf, g1 = pick(load(fpath, "FETCH_SIZE"), sub, "FETCH_SIZE")
     w, nw, g2 = pick(load(wpath, "WRITE_SIZE"), sub, "WRITE_SIZE")
-    res = {"batch": int(sys.argv[5]) if len(sys.argv) > 5 else None, "kernel_substring": sub, "grid": g1, "launches": [nf, nw], "fetch_size_kb": f, "write_size_kb": w}
+    res = {"batch": int(sys.argv[5]) if len(sys.argv) > 5 else None, "kernel_substring": sub, "grid": g1,
+           "launches": [nf, nw], "fetch_size_kb": f, "write_size_kb": w, "kernel_src_sha": conv1_src_sha(),
+           "recipe": "bash tools/pmc_conv1.sh <out.json> (two rocprofv3 --pmc passes over bench.py --steps 2)"}
     if f is not None and w is not None:
         res["traffic_bytes"] = (2.0 * f + w) * 1024.0
     json.dump(res, open(out, "w"), indent=1)
