@@ -502,6 +502,7 @@ def main():
     t0 = time.perf_counter()
     with rt.probing(["wavlm.conv1"]) as probes:   # HIP events around the dominant launch, on its stream
         gs, avg_loss = T_.train_one_epoch(enc, dec, sp, te, tp, sch, loader_t, opt, device, cfg, gs, None, 1, False)
+    host_s = T_.LAST_ENQUEUE_DONE - t0     # host enqueue time of the K steps (before the epoch's closing loss read)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     if world > 1:
@@ -563,6 +564,7 @@ def main():
             "decoder_attention": decoder_attention(args, aprobes, peak),
             "step_mfma_frac": round(step_tflops / peak, 4),
             "step_tflops": round(step_tflops, 1),
+            "host_ms_per_step": round(1000.0 * host_s / args.steps, 3),
             "gflop_per_utt": round(gpu_utt, 2),
             "lfd_batch_stats": "global" if (args.lfd_sync and world > 1) else "local",
             "avg_loss": round(avg_loss, 4),

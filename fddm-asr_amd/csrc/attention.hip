@@ -196,6 +196,33 @@ __device__ __forceinline__ bool key_ok(const AttnArgs& a, int b, int key) {
   return key < a.Lk && (a.key_keep == nullptr || a.key_keep[(long)b * a.Lk + key]);
 }
 
+// Diagnostic build only (-DATTN_STAMPS, tools/attn_stamps.py): s_memtime stamps of wave 0 of every workgroup at the
+// phase boundaries of the v3 kernels (slot 0 entry, 1 loads issued, 2 data landed + barrier, 3.. after each key /
+// query tile, 12 stores issued, 13 exit), s_memrealtime at entry / exit (slots 14, 15) for the clock. The stamps go
+// to a buffer of their own; in the real build no stamp executes.
+#ifdef ATTN_STAMPS
+__device__ unsigned long long attn_stamps[8192 * 16];
+#define ASTAMP(k)                                                                              \
+  do {                                                                                         \
+    __builtin_amdgcn_sched_barrier(0);                                                         \
+    unsigned long long t_;                                                                     \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                  \
+    __builtin_amdgcn_sched_barrier(0);                                                         \
+    const int bl_ = blockIdx.x + blockIdx.y * gridDim.x;                                       \
+    if (threadIdx.x == 0 && bl_ < 8192) attn_stamps[bl_ * 16 + (k)] = t_;                       \
+  } while (0)
+#define ARTIME(k)                                                                              \
+  do {                                                                                         \
+    const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                            \
+    __builtin_amdgcn_s_waitcnt(0xC07F);                                                        \
+    const int bl_ = blockIdx.x + blockIdx.y * gridDim.x;                                       \
+    if (threadIdx.x == 0 && bl_ < 8192) attn_stamps[bl_ * 16 + (k)] = t_;                       \
+  } while (0)
+#else
+#define ASTAMP(k)
+#define ARTIME(k)
+#endif
+
 // Attention-probability dropout: RNG contract v2 (oracle/fddm_oracle.py: attn_dropout_keep). Per (b, h) three
 // tables of R = 4096 16-bit words, T_tau[j] = bits 16*(j&3).. of mix64(seed, stream, TAB0 + (bh*3 + tau)*1024 +
 // (j>>2)); per query row r = bh*Lq + q three offsets o_tau = (mix64(seed, stream, OFF0 + r) >> 16*tau) & 0xFFC;
@@ -599,6 +626,8 @@ __global__ void __launch_bounds__(64 * NW, 1) fwd3_kernel(AttnArgs a) {
   float* mfull = (float*)(smem3 + 2 * LkP * 128);               // [LkP] 0 / -inf
   float* tfull = mfull + LkP;                                   // [LkP + QW] relative-bias slice (REL)
   unsigned char* dtab = (unsigned char*)(mfull + LkP + (REL ? LkP + QW : 0));  // [3][4096] u16 (DROP)
+  ARTIME(14);
+  ASTAMP(0);
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
             i = lane & 15;
   int bxi, bh;
@@ -695,8 +724,10 @@ __global__ void __launch_bounds__(64 * NW, 1) fwd3_kernel(AttnArgs a) {
 #pragma unroll
     for (int d = 0; d < 4; ++d) o[gq][d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   }
+  ASTAMP(1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  ASTAMP(2);
 
   const float th_raw = 8.f / sl2;  // lazy rescale threshold (raw score units), as in fwd2_kernel
   auto tile = [&](const int t, auto mc) {
@@ -827,6 +858,7 @@ __global__ void __launch_bounds__(64 * NW, 1) fwd3_kernel(AttnArgs a) {
         }
       }
     }
+    ASTAMP(3 + (t < 8 ? t : 8));
   };
   if (MASK && a.key_keep != nullptr) {
     // key tiles whose 64 keys are all padding add exactly nothing (exp(-inf) = 0): skipped (wave-uniform flags;
@@ -858,6 +890,12 @@ __global__ void __launch_bounds__(64 * NW, 1) fwd3_kernel(AttnArgs a) {
     if (a.lse && g == 0)
       a.lse[(long)bh * a.Lq + q[gq]] = (lt > 0.f) ? (m[gq] * sl2 + __log2f(lt)) * 0.69314718055994531f : NAN;
   }
+  ASTAMP(12);
+#ifdef ATTN_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  ASTAMP(13);
+  ARTIME(15);
 }
 
 // ------------------------------------------------------------------------------------------- dQ
@@ -1242,6 +1280,8 @@ __global__ void __launch_bounds__(1024, 1) dq3_kernel(AttnArgs a) {
   unsigned char* kres = smq;               // [LkP][128 B] KC image
   unsigned char* vres = smq + LkP * 128;   // [LkP][128 B] KC image
   float* mfull = (float*)(smq + 2 * LkP * 128);
+  ARTIME(14);
+  ASTAMP(0);
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
             i = lane & 15;
   int bxi, bh;
@@ -1291,8 +1331,10 @@ __global__ void __launch_bounds__(1024, 1) dq3_kernel(AttnArgs a) {
   f32x4_t dq[4];
 #pragma unroll
   for (int d = 0; d < 4; ++d) dq[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  ASTAMP(1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  ASTAMP(2);
   const f32x2_t sl2v = {sl2, sl2}, dscv = {a.drop_scale, a.drop_scale}, ndl = {-delta, -delta};
   auto tile = [&](const int t, auto mc) {
     constexpr bool MT = decltype(mc)::value;
@@ -1359,6 +1401,7 @@ __global__ void __launch_bounds__(1024, 1) dq3_kernel(AttnArgs a) {
         mma<bf16_t>(dq[db], join_tr(lo, hi), bq);
       }
     }
+    ASTAMP(3 + (t < 8 ? t : 8));
   };
   if (MASK && a.key_keep != nullptr) {
     for (int t = 0; t < ntiles; ++t)  // fully padded key tiles skipped (wave-uniform), as in fwd3_kernel
@@ -1377,6 +1420,12 @@ __global__ void __launch_bounds__(1024, 1) dq3_kernel(AttnArgs a) {
       *(uint2*)(dQb + d * 16 + 4 * g) = u2;
     }
   }
+  ASTAMP(12);
+#ifdef ATTN_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  ASTAMP(13);
+  ARTIME(15);
 }
 
 // dK, dV, key-owned: 128 keys per workgroup (two 16-key groups per wave), Q/dO tiles double-buffered
@@ -1574,6 +1623,8 @@ __global__ void __launch_bounds__(1024, 1) dkv3_kernel(AttnArgs a) {
   float* lse_s = (float*)(smk + 2 * LqP * 128);    // [LqP] lse * log2(e)
   float* del_s = lse_s + LqP;                      // [LqP] delta
   uint64_t* wb_s = (uint64_t*)(del_s + LqP);       // [KT][LqP] keep words (DM == 2)
+  ARTIME(14);
+  ASTAMP(0);
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
             i = lane & 15;
   int bxi, bh;
@@ -1620,8 +1671,10 @@ __global__ void __launch_bounds__(1024, 1) dkv3_kernel(AttnArgs a) {
   f32x4_t dk[4], dv[4];
 #pragma unroll
   for (int d = 0; d < 4; ++d) dk[d] = dv[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  ASTAMP(1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  ASTAMP(2);
   const int kbit = (w & 3) * 16 + i;      // key bit within its 64-key tile; the tile is w >> 2 of the workgroup's
   const int kts = w >> 2;
   const f32x2_t sl2v = {sl2, sl2}, dscv = {a.drop_scale, a.drop_scale};
@@ -1705,6 +1758,7 @@ __global__ void __launch_bounds__(1024, 1) dkv3_kernel(AttnArgs a) {
           mma<bf16_t>(dk[db], join_tr(qlo, qhi), bs);
         }
       }
+      ASTAMP(3 + (t < 8 ? t : 8));
     }
   }
   if (kvld) {
@@ -1723,6 +1777,12 @@ __global__ void __launch_bounds__(1024, 1) dkv3_kernel(AttnArgs a) {
       *(uint2*)(dVb + d * 16 + 4 * g) = uv;
     }
   }
+  ASTAMP(12);
+#ifdef ATTN_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  ASTAMP(13);
+  ARTIME(15);
 }
 
 template <typename T>
@@ -1872,6 +1932,17 @@ static int attn_dispatch(int which, int dtype, AttnArgs& a, float drop_p, void* 
   if (dtype == FDDM_F32) return run<float>(which, a, (hipStream_t)hs);
   return (int)hipErrorInvalidValue;
 }
+
+#ifdef ATTN_STAMPS
+FDDM_API int fddm_attn_stamps(unsigned long long* host, long n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(fddm::attn::attn_stamps), n * sizeof(unsigned long long), 0,
+                                  hipMemcpyDeviceToHost);
+}
+FDDM_API int fddm_attn_stamps_clear() {
+  static unsigned long long z[8192 * 16];
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(fddm::attn::attn_stamps), z, sizeof(z), 0, hipMemcpyHostToDevice);
+}
+#endif
 
 // Forward. Q/K/V/O: element (b, pos, h, d) at base + (b*L + pos)*stride + h*64 + d.
 FDDM_API int fddm_attn_fwd(int dtype, const void* Q, long sq, const void* K, long sk, const void* V, long sv, void* O,

@@ -15,6 +15,7 @@ import argparse
 import logging
 import os
 import random
+import time
 import weakref
 from dataclasses import dataclass
 from datetime import datetime
@@ -176,6 +177,7 @@ def _encoded(encoder, loader, device, optimizer):
         yield c, c_mask, x0
 
 
+LAST_ENQUEUE_DONE = 0.0
 _ENC_STREAMS: dict = {}
 _ENC_GRAPHS = weakref.WeakKeyDictionary()     # encoder -> GraphedEncoder (released with the encoder)
 
@@ -273,6 +275,8 @@ def train_one_epoch(encoder, decoder, s_proj, t_embed, t_proj, scheduler, loader
                 post["lfd"] = f"{float(loss_fd):.3f}"
             pbar.set_postfix(post)
         global_step += 1
+    global LAST_ENQUEUE_DONE
+    LAST_ENQUEUE_DONE = time.perf_counter()     # host finished enqueueing the epoch (bench.py: host-bound check)
     avg = float(loss_sum) / max(1, nsteps)
     if print_epoch_summary:
         logging.info(f"[Summary] Epoch {epoch} Avg Train Loss: {avg:.4f}")
