@@ -1785,6 +1785,313 @@ __global__ void __launch_bounds__(1024, 1) dkv3_kernel(AttnArgs a) {
   ARTIME(15);
 }
 
+// dQ, dK, dV of one (b, h) in ONE workgroup when Lq == Lk <= 256 (the decoder's self-attention; round 3): dq3 and
+// dkv3 fused. The K, V, Q and dO rows are staged into four KC images once (LDS-DMA, 128 KB at L = 256) with the LSE
+// rows, the forward's keep words and the key mask; delta = rowsum(dO * O) is formed in registers and shared through
+// LDS. Phase 1 is dq3's query-owned loop (S^T = K Q^T, dP^T = V dO^T, dQ^T += K^T dS^T), phase 2 dkv3's key-owned
+// loop on the same images (S = Q K^T, dP = dO V^T, dV^T += dO^T P', dK^T += Q^T dS). Against the two launches it
+// saves the second kernel's load of Q / dO / K / V (the stamps put ~40 % of each kernel's cycles in its load phase)
+// and one launch. DM: 0 no dropout, 2 the forward's recorded keep bits.
+template <int DM, bool MASK>
+__global__ void __launch_bounds__(1024, 1) bwd3s_kernel(AttnArgs a) {
+  static_assert(DM == 0 || DM == 2, "bwd3s: no-dropout or recorded keep bits");
+  constexpr bool DROP = DM != 0;
+  constexpr int NW = 16;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smb[];
+  const int nt = (a.Lk + 63) / 64, LP = nt * 64;     // Lq == Lk
+  unsigned char* kres = smb;                        // [LP][128 B] KC images of K, V, Q, dO
+  unsigned char* vres = smb + LP * 128;
+  unsigned char* qres = smb + 2 * LP * 128;
+  unsigned char* ores = smb + 3 * LP * 128;
+  float* mfull = (float*)(smb + 4 * LP * 128);      // [LP] key mask 0 / -inf
+  float* lse_s = mfull + LP;                        // [LP] lse * log2(e), +inf past Lq
+  float* del_s = lse_s + LP;                        // [LP] delta
+  uint64_t* wb_s = (uint64_t*)(del_s + LP);         // [nt][LP] keep words (DM == 2)
+  ARTIME(14);
+  ASTAMP(0);
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
+            i = lane & 15;
+  int bxi, bh;
+  xcd_tile(bxi, bh);
+  const int b = bh / a.H, h = bh % a.H;
+  const bf16_t* Qb = (const bf16_t*)a.Q + (long)b * a.Lq * a.sq + h * DH;
+  const bf16_t* Ob = (const bf16_t*)a.O + (long)b * a.Lq * a.so + h * DH;
+  const bf16_t* dOb = (const bf16_t*)a.dO + (long)b * a.Lq * a.sdo + h * DH;
+  const bf16_t* Kb = (const bf16_t*)a.K + (long)b * a.Lk * a.sk + h * DH;
+  const bf16_t* Vb = (const bf16_t*)a.V + (long)b * a.Lk * a.sv + h * DH;
+  // ---- ordinary loads first (one vmcnt(0) behind the LDS-DMA covers all of them)
+  const int q = w * 16 + i;                        // phase 1: this lane's query; phase 2: this lane's key (same index)
+  const bool qv = q < a.Lq;
+  const int qq0 = qv ? q : 0;
+  uint4 qf[2], dof[2], of[2];
+  row_frags<bf16_t>(qf, Qb, a.sq, qq0, qv, lane);
+  row_frags<bf16_t>(dof, dOb, a.sdo, qq0, qv, lane);
+  row_frags<bf16_t>(of, Ob, a.so, qq0, qv, lane);
+  bool kk_ok = true;
+  float lraw = INFINITY;
+  if (tid < LP) {
+    kk_ok = !MASK || key_ok(a, b, tid);
+    if (tid < a.Lq) lraw = a.lse[(long)bh * a.Lq + tid];
+  }
+  uint64_t wv = 0;
+  if constexpr (DM == 2) {
+    const int kt = tid / LP, q2 = tid % LP;          // nt * LP <= 1024 words, one per thread
+    if (tid < nt * LP && q2 < a.Lq) wv = a.dbits[((long)bh * nt + kt) * a.Lq + q2];
+  }
+  // ---- LDS-DMA of the four images, tile order (waves 0-7: K and Q rows 8w.., waves 8-15: V and dO rows 8(w-8)..)
+  {
+    typedef __attribute__((address_space(1))) const void* gp_t;
+    typedef __attribute__((address_space(3))) void* lp_t;
+    for (int t = 0; t < nt; ++t) {
+      const int R = 64 * t + 8 * (w & 7);
+      const int r = R + (lane >> 3), pch = lane & 7;
+      const int ck = pch ^ ((r >> 1) & 7);
+      const int rk = min(r, a.Lk - 1), rq = min(r, a.Lq - 1);
+      if (w < 8) {
+        __builtin_amdgcn_global_load_lds((gp_t)(Kb + (long)rk * a.sk + ck * 8), (lp_t)(kres + R * 128), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((gp_t)(Qb + (long)rq * a.sq + ck * 8), (lp_t)(qres + R * 128), 16, 0, 0);
+      } else {
+        __builtin_amdgcn_global_load_lds((gp_t)(Vb + (long)rk * a.sv + ck * 8), (lp_t)(vres + R * 128), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((gp_t)(dOb + (long)rq * a.sdo + ck * 8), (lp_t)(ores + R * 128), 16, 0, 0);
+      }
+    }
+  }
+  const float sl2 = a.scale * 1.4426950408889634f;
+  float dl = 0.f;
+#pragma unroll
+  for (int sb = 0; sb < 2; ++sb) {
+    const bf16_t* x = (const bf16_t*)&dof[sb];
+    const bf16_t* y = (const bf16_t*)&of[sb];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dl += bf2f(x[e]) * bf2f(y[e]);
+  }
+  dl = xsum16(dl);
+  dl = xsum32(dl);
+  const float delta = dl;
+  const float lse2 = qv ? a.lse[(long)bh * a.Lq + q] * 1.4426950408889634f : 0.f;
+  if (tid < LP) {
+    mfull[tid] = kk_ok ? 0.f : -INFINITY;
+    lse_s[tid] = lraw * 1.4426950408889634f;
+  }
+  if (g == 0 && q < LP) del_s[q] = qv ? delta : 0.f;
+  if constexpr (DM == 2)
+    if (tid < nt * LP) wb_s[tid] = wv;
+  ASTAMP(1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  ASTAMP(2);
+  const f32x2_t sl2v = {sl2, sl2}, dscv = {a.drop_scale, a.drop_scale};
+  typedef __attribute__((address_space(3))) s16x4_t* lp;
+  // ================================================================ phase 1: dQ (query-owned, dq3's tile body)
+  {
+    f32x4_t dq[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) dq[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    const f32x2_t ndl = {-delta, -delta};
+    auto tile = [&](const int t, auto mc) {
+      constexpr bool MT = decltype(mc)::value;
+      const int k0 = t * 64;
+      const unsigned char* kimg = kres + k0 * 128;
+      const unsigned char* vimg = vres + k0 * 128;
+      uint64_t wbits = 0;
+      if constexpr (DM == 2) wbits = qv ? wb_s[t * LP + q] : 0;
+      f32x4_t sc[4], dp[4];
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        sc[kb] = dp[kb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub) {
+          const uint4 ak = *(const uint4*)(kimg + kc_off(128, kb * 16 + i, sub * 4 + g));
+          const uint4 av = *(const uint4*)(vimg + kc_off(128, kb * 16 + i, sub * 4 + g));
+          mma<bf16_t>(sc[kb], ak, qf[sub]);
+          mma<bf16_t>(dp[kb], av, dof[sub]);
+        }
+      }
+      float ds[4][4];
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        unsigned keep = 0xF;
+        if constexpr (DM == 2) keep = (unsigned)(wbits >> (kb * 16 + 4 * g)) & 0xFu;
+        float4 m4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        if constexpr (MT) m4 = *(const float4*)(&mfull[k0 + kb * 16 + 4 * g]);
+        const float mr[4] = {m4.x, m4.y, m4.z, m4.w};
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          f32x2_t off = {-lse2, -lse2};
+          if constexpr (MT) off += f32x2_t{mr[2 * jj], mr[2 * jj + 1]};
+          const f32x2_t arg = f32x2_t{sc[kb][2 * jj], sc[kb][2 * jj + 1]} * sl2v + off;
+          const f32x2_t pr = {__builtin_amdgcn_exp2f(arg.x), __builtin_amdgcn_exp2f(arg.y)};
+          f32x2_t dpv = {dp[kb][2 * jj], dp[kb][2 * jj + 1]};
+          if constexpr (DM == 2) {
+            dpv.x = __int_as_float(__float_as_int(dpv.x) & __builtin_amdgcn_sbfe((int)keep, 2 * jj, 1));
+            dpv.y = __int_as_float(__float_as_int(dpv.y) & __builtin_amdgcn_sbfe((int)keep, 2 * jj + 1, 1));
+            dpv = dpv * dscv + ndl;
+          } else {
+            dpv += ndl;
+          }
+          const f32x2_t d2 = pr * dpv;
+          ds[kb][2 * jj] = d2.x;
+          ds[kb][2 * jj + 1] = d2.y;
+        }
+      }
+      const int qq = i >> 2, pp = i & 3;
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        uint4 bq;
+        bq.x = pk(ds[2 * ss][0], ds[2 * ss][1]);
+        bq.y = pk(ds[2 * ss][2], ds[2 * ss][3]);
+        bq.z = pk(ds[2 * ss + 1][0], ds[2 * ss + 1][1]);
+        bq.w = pk(ds[2 * ss + 1][2], ds[2 * ss + 1][3]);
+        const int k1 = 32 * ss + 4 * g + qq, k2 = k1 + 16;
+#pragma unroll
+        for (int db = 0; db < 4; ++db) {
+          const int u = db * 4 + pp;
+          const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(kimg + kc_tr_off(k1, u)));
+          const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(kimg + kc_tr_off(k2, u)));
+          mma<bf16_t>(dq[db], join_tr(lo, hi), bq);
+        }
+      }
+      ASTAMP(3 + (t < 4 ? t : 4));
+    };
+    if (MASK && a.key_keep != nullptr) {
+      for (int t = 0; t < nt; ++t)  // fully padded key tiles skipped (wave-uniform), as in fwd3_kernel
+        if (__any(mfull[64 * t + lane] == 0.f)) tile(t, std::integral_constant<bool, MASK>{});
+    } else {
+      for (int t = 0; t + 1 < nt; ++t) tile(t, std::false_type{});
+      tile(nt - 1, std::integral_constant<bool, MASK>{});
+    }
+    if (qv) {
+      bf16_t* dQb = (bf16_t*)a.dQ + ((long)b * a.Lq + q) * a.sdq + h * DH;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        uint2 u2;
+        u2.x = pk(dq[d][0] * a.scale, dq[d][1] * a.scale);
+        u2.y = pk(dq[d][2] * a.scale, dq[d][3] * a.scale);
+        *(uint2*)(dQb + d * 16 + 4 * g) = u2;
+      }
+    }
+  }
+  // ================================================================ phase 2: dK, dV (key-owned, dkv3's tile body)
+  {
+    const int key = q;
+    const bool kvld = key < a.Lk;
+    const bool kok = kvld && mfull[min(key, LP - 1)] == 0.f;
+    uint4 kf[2], vf[2];
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {   // the key's own rows from the K / V images
+      kf[sub] = *(const uint4*)(kres + kc_off(128, min(key, LP - 1), sub * 4 + g));
+      vf[sub] = *(const uint4*)(vres + kc_off(128, min(key, LP - 1), sub * 4 + g));
+    }
+    f32x4_t dk[4], dv[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) dk[d] = dv[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    const int kbit = (w & 3) * 16 + i;     // key bit within its 64-key tile w >> 2
+    const int kts = w >> 2;
+    const int qq_ = i >> 2, pp = i & 3;
+    if (__any(kok)) {
+      for (int t = 0; t < nt; ++t) {
+        const int q0 = t * 64;
+        const unsigned char* qimg = qres + q0 * 128;
+        const unsigned char* oimg = ores + q0 * 128;
+        f32x4_t sc[4], dp[4];
+#pragma unroll
+        for (int qb = 0; qb < 4; ++qb) {
+          sc[qb] = dp[qb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int sub = 0; sub < 2; ++sub) {
+            const uint4 aq = *(const uint4*)(qimg + kc_off(128, qb * 16 + i, sub * 4 + g));
+            const uint4 ao = *(const uint4*)(oimg + kc_off(128, qb * 16 + i, sub * 4 + g));
+            mma<bf16_t>(sc[qb], aq, kf[sub]);
+            mma<bf16_t>(dp[qb], ao, vf[sub]);
+          }
+        }
+        float pd[4][4], ds[4][4];
+#pragma unroll
+        for (int qb = 0; qb < 4; ++qb) {
+          const float4 l4 = *(const float4*)(&lse_s[q0 + qb * 16 + 4 * g]);
+          const float4 d4 = *(const float4*)(&del_s[q0 + qb * 16 + 4 * g]);
+          const f32x2_t nl[2] = {f32x2_t{-l4.x, -l4.y}, f32x2_t{-l4.z, -l4.w}};
+          const f32x2_t nd[2] = {f32x2_t{-d4.x, -d4.y}, f32x2_t{-d4.z, -d4.w}};
+          unsigned wq[4] = {0, 0, 0, 0};
+          if constexpr (DM == 2) {
+            const unsigned* src = (const unsigned*)&wb_s[kts * LP + q0 + qb * 16 + 4 * g] + (kbit >> 5);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) wq[j] = src[2 * j];
+          }
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) {
+            const f32x2_t arg = f32x2_t{sc[qb][2 * jj], sc[qb][2 * jj + 1]} * sl2v + nl[jj];
+            const f32x2_t pr = {__builtin_amdgcn_exp2f(arg.x), __builtin_amdgcn_exp2f(arg.y)};
+            f32x2_t dpv = {dp[qb][2 * jj], dp[qb][2 * jj + 1]};
+            f32x2_t pdv = pr;
+            if constexpr (DROP) {
+              const int m0 = __builtin_amdgcn_sbfe((int)wq[2 * jj], kbit & 31, 1);
+              const int m1 = __builtin_amdgcn_sbfe((int)wq[2 * jj + 1], kbit & 31, 1);
+              pdv.x = __int_as_float(__float_as_int(pr.x) & m0);
+              pdv.y = __int_as_float(__float_as_int(pr.y) & m1);
+              dpv.x = __int_as_float(__float_as_int(dpv.x) & m0);
+              dpv.y = __int_as_float(__float_as_int(dpv.y) & m1);
+              dpv = dpv * dscv + nd[jj];
+            } else {
+              dpv += nd[jj];
+            }
+            const f32x2_t d2 = pr * dpv;
+            pd[qb][2 * jj] = pdv.x;
+            pd[qb][2 * jj + 1] = pdv.y;
+            ds[qb][2 * jj] = d2.x;
+            ds[qb][2 * jj + 1] = d2.y;
+          }
+        }
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          uint4 bp, bs;
+          bp.x = pk(pd[2 * ss][0], pd[2 * ss][1]);
+          bp.y = pk(pd[2 * ss][2], pd[2 * ss][3]);
+          bp.z = pk(pd[2 * ss + 1][0], pd[2 * ss + 1][1]);
+          bp.w = pk(pd[2 * ss + 1][2], pd[2 * ss + 1][3]);
+          bs.x = pk(ds[2 * ss][0], ds[2 * ss][1]);
+          bs.y = pk(ds[2 * ss][2], ds[2 * ss][3]);
+          bs.z = pk(ds[2 * ss + 1][0], ds[2 * ss + 1][1]);
+          bs.w = pk(ds[2 * ss + 1][2], ds[2 * ss + 1][3]);
+          const int k1 = 32 * ss + 4 * g + qq_, k2 = k1 + 16;
+#pragma unroll
+          for (int db = 0; db < 4; ++db) {
+            const int u = db * 4 + pp;
+            const s16x4_t olo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(oimg + kc_tr_off(k1, u)));
+            const s16x4_t ohi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(oimg + kc_tr_off(k2, u)));
+            const s16x4_t qlo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(qimg + kc_tr_off(k1, u)));
+            const s16x4_t qhi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(qimg + kc_tr_off(k2, u)));
+            mma<bf16_t>(dv[db], join_tr(olo, ohi), bp);
+            mma<bf16_t>(dk[db], join_tr(qlo, qhi), bs);
+          }
+        }
+        ASTAMP(7 + (t < 4 ? t : 4));
+      }
+    }
+    if (kvld) {
+      bf16_t* dKb = (bf16_t*)a.dK + ((long)b * a.Lk + key) * a.sdk + h * DH;
+      bf16_t* dVb = (bf16_t*)a.dV + ((long)b * a.Lk + key) * a.sdv + h * DH;
+      const float ksc = kok ? a.scale : 0.f, vsc = kok ? (DROP ? a.drop_scale : 1.f) : 0.f;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        uint2 uk, uv;
+        uk.x = pk(kok ? dk[d][0] * ksc : 0.f, kok ? dk[d][1] * ksc : 0.f);
+        uk.y = pk(kok ? dk[d][2] * ksc : 0.f, kok ? dk[d][3] * ksc : 0.f);
+        uv.x = pk(kok ? dv[d][0] * vsc : 0.f, kok ? dv[d][1] * vsc : 0.f);
+        uv.y = pk(kok ? dv[d][2] * vsc : 0.f, kok ? dv[d][3] * vsc : 0.f);
+        *(uint2*)(dKb + d * 16 + 4 * g) = uk;
+        *(uint2*)(dVb + d * 16 + 4 * g) = uv;
+      }
+    }
+  }
+  ASTAMP(12);
+#ifdef ATTN_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  ASTAMP(13);
+  ARTIME(15);
+}
+
 template <typename T>
 static int run(int which, AttnArgs& a, hipStream_t s) {
   constexpr int RB = Cfg<T>::RB;
@@ -1880,6 +2187,19 @@ static int run(int which, AttnArgs& a, hipStream_t s) {
     }
     dim3 grid((a.Lq + 63) / 64, a.B * a.H);
     hipLaunchKernelGGL(dq_kernel<T>, grid, dim3(256), 192 * RB, s, a);
+  } else if (which == 3) {
+    if constexpr (sizeof(T) == 2) {
+      const bool drop = a.thr16 != 0, mask = a.key_keep != nullptr || (a.Lk % 64) != 0;
+      const int LP = (a.Lk + 63) / 64 * 64;
+      const size_t lds = (size_t)LP * 512 + (size_t)LP * 12 + (drop ? (size_t)(LP / 64) * LP * 8 : 0);
+      dim3 g3(1, a.B * a.H);
+#define BW3(D, M) hipLaunchKernelGGL((bwd3s_kernel<D, M>), g3, dim3(1024), lds, s, a)
+      if (drop) { if (mask) BW3(2, true); else BW3(2, false); }
+      else { if (mask) BW3(0, true); else BW3(0, false); }
+#undef BW3
+      return (int)hipGetLastError();
+    }
+    return (int)hipErrorInvalidValue;
   } else {
     if constexpr (sizeof(T) == 2) {
       if (!getenv("FDDM_ATTN_V1")) {
@@ -1986,6 +2306,10 @@ FDDM_API int fddm_attn_bwd(int dtype, const void* Q, long sq, const void* K, lon
   a.sq = sq; a.sk = sk; a.sv = sv; a.so = so; a.sdo = sdo; a.sdq = sdq; a.sdk = sdk; a.sdv = sdv;
   a.key_keep = key_keep;
   a.B = B; a.H = H; a.Lq = Lq; a.Lk = Lk; a.scale = scale; a.seed = seed; a.stream = stream;
+  // self-attention shapes (Lq == Lk <= 256, bf16, no rehashed dropout): dQ, dK and dV in one fused launch
+  if (dtype == FDDM_BF16 && Lq == Lk && Lk <= 256 && (drop_p <= 0.f || drop_bits) && !getenv("FDDM_ATTN_BWD_SPLIT") &&
+      !getenv("FDDM_ATTN_V1"))
+    return attn_dispatch(3, dtype, a, drop_p, hs);
   int e = attn_dispatch(1, dtype, a, drop_p, hs);
   if (e) return e;
   return attn_dispatch(2, dtype, a, drop_p, hs);

@@ -52,6 +52,7 @@ __global__ void __launch_bounds__(256) sumsq_kernel(MTTable t, float* total) {
   if (threadIdx.x == 0) atomicAdd(total, v);
 }
 
+template <bool ZG>
 __global__ void __launch_bounds__(256) adamw_kernel(MTTable t, const float* total, float max_norm, float lr, float lr_wd,
                                                     float b1, float b2, float eps) {
   const long ci = blockIdx.x;
@@ -59,7 +60,13 @@ __global__ void __launch_bounds__(256) adamw_kernel(MTTable t, const float* tota
   const long n = min(MT_CHUNK, t.numel[ti] - s0);
   float coef = 1.f;
   if (total) {
-    if (!isfinite(total[0])) return;  // non-finite gradients: skip the step (GradScaler semantics)
+    if (!isfinite(total[0])) {  // non-finite gradients: skip the step (GradScaler semantics)
+      if constexpr (ZG) {       // ... but still leave the gradients zeroed for the next step
+        float* gz = (float*)t.g[ti] + s0;
+        for (long i = threadIdx.x; i < n; i += 256) gz[i] = 0.f;
+      }
+      return;
+    }
     if (max_norm > 0.f) {
       coef = max_norm / (sqrtf(total[0]) + 1e-6f);
       coef = fminf(coef, 1.f);
@@ -70,7 +77,7 @@ __global__ void __launch_bounds__(256) adamw_kernel(MTTable t, const float* tota
   const float ss = (float)((double)lr / (1.0 - pow((double)b1, stp)));
   const float bc2s = (float)sqrt(1.0 - pow((double)b2, stp));
   float* p = t.p[ti] + s0;
-  const float* g = t.g[ti] + s0;
+  float* g = (float*)t.g[ti] + s0;
   float* m = t.m[ti] + s0;
   float* v = t.v[ti] + s0;
   bf16_t* pb = t.pbf[ti] ? t.pbf[ti] + s0 : nullptr;
@@ -103,6 +110,7 @@ __global__ void __launch_bounds__(256) adamw_kernel(MTTable t, const float* tota
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const long j = j0 + 256 * u;
+        if constexpr (ZG) ((float4*)g)[j] = make_float4(0.f, 0.f, 0.f, 0.f);
         upd(gg[u].x, pp[u].x, mm[u].x, vv[u].x);
         upd(gg[u].y, pp[u].y, mm[u].y, vv[u].y);
         upd(gg[u].z, pp[u].z, mm[u].z, vv[u].z);
@@ -115,6 +123,7 @@ __global__ void __launch_bounds__(256) adamw_kernel(MTTable t, const float* tota
     }
     for (long j = j0; j < n4; j += 256) {
       const float4 gg = ((const float4*)g)[j];
+      if constexpr (ZG) ((float4*)g)[j] = make_float4(0.f, 0.f, 0.f, 0.f);
       float4 pp = ((float4*)p)[j], mm = ((float4*)m)[j], vv = ((float4*)v)[j];
       upd(gg.x, pp.x, mm.x, vv.x);
       upd(gg.y, pp.y, mm.y, vv.y);
@@ -130,6 +139,7 @@ __global__ void __launch_bounds__(256) adamw_kernel(MTTable t, const float* tota
   for (long i = i0 + threadIdx.x; i < n; i += 256) {
     float pp = p[i], mm = m[i], vv = v[i];
     upd(g[i], pp, mm, vv);
+    if constexpr (ZG) g[i] = 0.f;
     p[i] = pp;
     m[i] = mm;
     v[i] = vv;
@@ -161,11 +171,15 @@ FDDM_API int fddm_grad_sumsq(const long* chunk_tensor, const long* chunk_start, 
 FDDM_API int fddm_adamw(const long* chunk_tensor, const long* chunk_start, const long* numel, float* const* p,
                         const float* const* g, float* const* m, float* const* v, bf16_t* const* pbf, float* const* step,
                         long ntensors, long nchunks, const float* total, float max_norm, float lr, float lr_wd, float b1,
-                        float b2, float eps, int* skipped, void* hs) {
+                        float b2, float eps, int* skipped, int zero_g, void* hs) {
   if (nchunks <= 0) return 0;
   MTTable t{chunk_tensor, chunk_start, numel, p, g, m, v, pbf, step};
-  hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)nchunks), dim3(256), 0, (hipStream_t)hs, t, total, max_norm, lr, lr_wd,
-                     b1, b2, eps);
+  if (zero_g)
+    hipLaunchKernelGGL(adamw_kernel<true>, dim3((unsigned)nchunks), dim3(256), 0, (hipStream_t)hs, t, total, max_norm, lr,
+                       lr_wd, b1, b2, eps);
+  else
+    hipLaunchKernelGGL(adamw_kernel<false>, dim3((unsigned)nchunks), dim3(256), 0, (hipStream_t)hs, t, total, max_norm,
+                       lr, lr_wd, b1, b2, eps);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(adamw_step_kernel, dim3(1), dim3(256), 0, (hipStream_t)hs, step, ntensors, total, skipped);

@@ -36,6 +36,8 @@ class FusedAdamW(torch.optim.Optimizer):
     def zero_grad(self, set_to_none: bool = True):
         if self.arena is None:
             return super().zero_grad(set_to_none)
+        clean = self.arena.clean
+        self.arena.clean = False
         inside = set(id(p) for p in self.arena.params)
         for group in self.param_groups:
             for p in group["params"]:
@@ -44,7 +46,10 @@ class FusedAdamW(torch.optim.Optimizer):
                         p.grad = None
                     else:
                         p.grad.zero_()
-        self.arena.zero_()
+        if clean:           # the last clip_and_step(zero_grads=True) left the arena zeroed in its own pass
+            self.arena.attach()
+        else:
+            self.arena.zero_()
 
     @staticmethod
     def _bufs_live(plist, bufs) -> bool:
@@ -121,9 +126,10 @@ class FusedAdamW(torch.optim.Optimizer):
         return self._skipped
 
     @torch.no_grad()
-    def clip_and_step(self, max_norm: float | None = None):
+    def clip_and_step(self, max_norm: float | None = None, zero_grads: bool = False):
         """clip_grad_norm_(all params with grads, max_norm) followed by AdamW.step(); returns the
-        (device) total gradient norm."""
+        (device) total gradient norm. zero_grads: the step also zeroes every gradient it reads (the train loop's
+        next zero_grad then has no arena fill to do; .grad reads as zero after the call)."""
         groups = []
         for group in self.param_groups:
             plist = [p for p in group["params"] if p.grad is not None]
@@ -150,7 +156,9 @@ class FusedAdamW(torch.optim.Optimizer):
                  tab["g"].data_ptr(), tab["m"].data_ptr(), tab["v"].data_ptr(), tab["b"].data_ptr(), tab["s"].data_ptr(),
                  tab["nt"], tab["n"], total.data_ptr(), float(max_norm or 0.0), float(group["lr"]),
                  float(group["lr"] * group["weight_decay"]), float(b1), float(b2), float(group["eps"]),
-                 self._skipped.data_ptr() if gi == 0 else 0, stream())   # a skipped step counts once
+                 self._skipped.data_ptr() if gi == 0 else 0, int(bool(zero_grads)), stream())   # skip counted once
+        if zero_grads and self.arena is not None:
+            self.arena.clean = all(p.grad is not None for p in self.arena.params)   # every arena slot was in a table
         self.last_total_sq = total
         return total.sqrt()
 

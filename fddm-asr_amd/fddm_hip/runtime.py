@@ -269,6 +269,7 @@ class GradArena:
         self.slot = {id(p): i for i, p in enumerate(self.params)}
         self.on_ready = None     # set by dist.OverlapReducer (DP runs): called by grads_ready()
         self.reducer = None
+        self.clean = False       # True while the flat buffer is known to be zero (FusedAdamW zero_grads)
         self.views = []
         for p, o in zip(self.params, offs):
             v = self.flat[o:o + p.numel()].view_as(p)

@@ -367,7 +367,8 @@ def _attn_ref(q, k, v, keep, p_drop, seed, stream, gate=None, table=None):
                                                  (33, 49, True, 0.1, False), (150, 200, True, 0.1, True),
                                                  (64, 130, False, 0.1, True), (40, 499, False, 0.1, True),
                                                  (129, 257, True, 0.1, True), (96, 256, True, 0.1, True),
-                                                 (64, 499, False, 0.0, False)])
+                                                 (64, 499, False, 0.0, False), (256, 256, False, 0.1, True),
+                                                 (200, 200, True, 0.1, True), (32, 32, False, 0.0, False)])
 def test_attention_fwd_bwd(dtype, Lq, Lk, masked, p, bits):
     """bits: the forward records the dropout keep bits and the backward reads them (bf16 path)."""
     o = ops()
@@ -404,6 +405,37 @@ def test_attention_fwd_bwd(dtype, Lq, Lk, masked, p, bits):
     close(dq.float(), back(qr.grad), rtol=3 * tol, what="dq")
     close(dk.float(), back(kr.grad), rtol=3 * tol, what="dk")
     close(dv.float(), back(vr.grad), rtol=3 * tol, what="dv")
+
+
+@pytest.mark.parametrize("L,masked,p", [(256, False, 0.1), (200, True, 0.1), (70, True, 0.0), (32, False, 0.1)])
+def test_attention_fused_self_bwd_equals_split(L, masked, p, monkeypatch):
+    """Self-attention shapes (Lq == Lk <= 256, bf16) take the fused one-launch backward (bwd3s_kernel); it runs the
+    same arithmetic as the dQ and dK/dV kernels (FDDM_ATTN_BWD_SPLIT=1), so the gradients are bit-identical."""
+    o = ops()
+    B, H = 3, 8
+    D = H * 64
+    x = [torch.randn(B * L, D, generator=g(40 + j)).to(dev, torch.bfloat16) for j in range(4)]
+    qd, kd, vd, dod = x
+    kk = None
+    if masked:
+        kk = torch.ones(B, L, dtype=torch.uint8, device=dev)
+        kk[2, L - 37:] = 0
+    od = torch.empty(B * L, D, device=dev, dtype=torch.bfloat16)
+    lse = torch.empty(B * H, L, device=dev)
+    db = o.drop_bits(B, H, L, L, dev) if p > 0 else None
+    o.attn_fwd(qd, kd, vd, od, lse, B, H, L, L, key_keep=kk, drop_p=p, seed=11, rng_stream=3, dbits=db)
+    outs = []
+    for split in (False, True):
+        if split:
+            monkeypatch.setenv("FDDM_ATTN_BWD_SPLIT", "1")
+        dq, dk, dv = (torch.full_like(qd, float("nan")) for _ in range(3))
+        o.attn_bwd(qd, kd, vd, od, dod, lse, dq, dk, dv, B, H, L, L, key_keep=kk, drop_p=p, seed=11, rng_stream=3,
+                   dbits=db)
+        torch.cuda.synchronize()
+        outs.append((dq, dk, dv))
+    for name, a, b in zip(("dq", "dk", "dv"), *outs):
+        assert torch.isfinite(a.float()).all(), name
+        assert torch.equal(a, b), f"{name}: fused self-attention backward differs from the split kernels"
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
@@ -745,6 +777,41 @@ def test_fused_adamw_nonfinite_guard_skips_whole_step():
     for i, p in enumerate(dps):
         close(p, ref[str(i)], rtol=1e-5, atol=1e-7, what=f"guarded adamw p{i}")
     assert all(float(opt.state[p]["step"]) == 2.0 for p in dps)
+
+
+@pytest.mark.parametrize("finite", [True, False])
+def test_fused_adamw_zero_grads_in_step(finite):
+    """clip_and_step(zero_grads=True) (the train loop's form: the grad arena's zero fill folded into AdamW's read of it)
+    updates parameters and moments exactly as the plain step and leaves every gradient zero — also when the non-finite
+    guard skips the update — so the next zero_grad skips the arena fill."""
+    from fddm_hip.optim import FusedAdamW
+    from fddm_hip import runtime as rt
+    torch.manual_seed(4)
+    shapes = [(257, 33), (33,), (1000,)]
+    init = [torch.randn(*s_) for s_ in shapes]
+    grads = [10 * torch.randn(*s_) for s_ in shapes]
+    if not finite:
+        grads[0][5, 7] = float("nan")
+    out = []
+    with rt.use_precision("fp32"):
+        for zg in (False, True):
+            ps = [torch.nn.Parameter(x.clone().to(dev)) for x in init]
+            opt = FusedAdamW(ps, lr=2e-4, weight_decay=0.01)
+            arena = opt.use_grad_arena(ps)
+            opt.zero_grad()
+            for p_, g_ in zip(ps, grads):
+                p_.grad.copy_(g_.to(dev))
+            opt.clip_and_step(max_norm=5.0, zero_grads=zg)
+            torch.cuda.synchronize()
+            out.append([p_.detach().cpu().clone() for p_ in ps])
+            if zg:
+                assert arena.clean and float(arena.flat.abs().max()) == 0.0
+                opt.zero_grad()
+                assert not arena.clean and all(p_.grad.data_ptr() == v.data_ptr() for p_, v in zip(ps, arena.views))
+            else:
+                assert float(arena.flat.abs().max()) > 0 or not finite
+    for a_, b_ in zip(*out):
+        assert torch.equal(a_, b_)
 
 
 def test_fused_adamw_skip_counts_once_over_groups():
