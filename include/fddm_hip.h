@@ -95,6 +95,8 @@ int fddm_attn_fwd(int dtype, const void* Q, long sq, const void* K, long sk, con
 int fddm_attn_fwd_relgate(const void* Q, long sq, const void* K, long sk, const void* V, long sv, void* O, long so,
                           const void* graw, long sgr, const float* gconst, const float* table, int B, int H, int Lq,
                           int Lk, float scale, void* hip_stream);
+/* Backward: dQ, dK, dV (bf16 self-attention shapes Lq == Lk <= 256 with recorded or no dropout: one fused launch,
+ * delta_ws unused; otherwise a query-owned dQ launch that writes delta_ws [B*H][Lq] and a key-owned dK/dV launch). */
 int fddm_attn_bwd(int dtype, const void* Q, long sq, const void* K, long sk, const void* V, long sv, const void* O,
                   long so, const void* dO, long sdo, const float* lse, void* dQ, long sdq, void* dK, long sdk,
                   void* dV, long sdv, float* delta_ws, const unsigned char* key_keep, int B, int H, int Lq, int Lk,

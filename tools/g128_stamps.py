@@ -34,6 +34,10 @@ def run(name, fn, nblk):
     return a
 
 
+def t0s(a):
+    return a[:, 0].min()
+
+
 def grouped():
     """one decoder block's weight-gradient group (tools/g128_bench.py shapes): per-block durations (cycles)"""
     bf = torch.bfloat16
@@ -74,6 +78,19 @@ def main():
     if os.environ.get("G128_GROUPED"):
         return grouped()
     bf = torch.bfloat16
+    if os.environ.get("G128_FWD"):  # forward-type NT GEMMs with a bf16 STORE epilogue (V / out / cross-Q projections)
+        for (M, N, K) in [(8192, 512, 512), (8192, 512, 64), (8192, 2048, 64)]:
+            x = torch.randn(M, K, device=dev, dtype=bf)
+            w = torch.randn(N, K, device=dev, dtype=bf)
+            o = torch.empty(M, N, device=dev, dtype=bf)
+            a = run(f"fwd {M}x{N}x{K}", lambda: ops.linear(x, w, out=o), (M // 128) * (N // 128))
+            kt = min(K // 64, NS - 4)
+            d = np.diff(a[:, 1:2 + kt], axis=1)
+            print("   per-K-tile cycles (median over blocks):", " ".join(f"{int(x)}" for x in np.median(d, axis=0)))
+            e = a[:, NS - 1] - t0s(a)
+            print("   end time per round of 256 blocks (median):",
+                  " ".join(f"{int(np.median(e[r:r + 256]))}" for r in range(0, len(a), 256)))
+        return
     for (M, N, K) in [(8192, 512, 2048), (8192, 512, 512)]:
         dy = torch.randn(M, K, device=dev, dtype=bf)
         w = torch.randn(K, N, device=dev, dtype=bf)

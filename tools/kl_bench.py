@@ -34,7 +34,7 @@ def main():
     t = torch.randint(1, 201, (B,), device=dev)
     betas = O.sched_tables(200)[0].to(dev)
     w = torch.full((N,), 1.0 / N, device=dev)
-    for nt in ("128", "256", "512"):
+    for nt in ("128", "256", "512", "1024"):
         os.environ["FDDM_KLF_NT"] = nt
         tk = timeit(lambda: ops.kl_fused(z, xt, x0, t, betas, None, L, out_dtype=torch.bfloat16))
         print(f"fused fwd+grad NT={nt}: {tk * 1e3:7.1f} us  {(N * V * 6) / tk / 1e6:7.0f} GB/s", flush=True)
