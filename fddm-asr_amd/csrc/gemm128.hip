@@ -210,12 +210,11 @@ __device__ __forceinline__ void tile128(const GemmArgs& g, unsigned char* smem, 
   //   read phase of K-tile t: fragments (t) | DMA K-tile t+NST-1 into the stage of t-1 (read by both groups
   //   before the last barrier) | lgkmcnt(0) | vmcnt: own share of t+1 landed | barrier
   //   MFMA phase: 16 MFMAs | barrier
+  // (Issuing the 4 DMA instructions between the MFMAs instead of in the read phase — gemm256's placement — measured
+  // slower here: grouped weight gradients 115 -> 129 us; fine stamps: read phase 532 -> 448 cycles, MFMA phase
+  // 376 -> 516. The read phase is bound by its 16 transposed reads and their latency, not by the DMA issue.)
   u32x4_t fa[4], fb[4];
-#ifdef G128_DEFER
-  constexpr int AHEAD = NST - 2;  // fragment reads retire after the barrier: a stage is refilled one K-tile later
-#else
   constexpr int AHEAD = NST - 1;
-#endif
 #pragma unroll
   for (int u = 0; u < AHEAD; ++u) issue(min(u, nk - 1), u);
   vmcnt<(AHEAD - 1) * DPW>();
@@ -228,28 +227,16 @@ __device__ __forceinline__ void tile128(const GemmArgs& g, unsigned char* smem, 
 #endif
     FSTAMP(t, 0);
     read_set(t % NST, fa, fb);
-#ifdef G128_NODMA
-    if (t < 2)
-#endif
     issue(min(t + AHEAD, nk - 1), (t + AHEAD) % NST);
-#ifndef G128_DEFER
     lgkmcnt0();
     __builtin_amdgcn_sched_barrier(0);
     if (kv < 64 && t == nk - 1) mask_set(fa, fb);
-#endif
     FSTAMP(t, 1);
     vmcnt<(AHEAD - 1) * DPW>();
     FSTAMP(t, 2);
     bar();
-#ifdef G128_DEFER
-    lgkmcnt0();
-    __builtin_amdgcn_sched_barrier(0);
-    if (kv < 64 && t == nk - 1) mask_set(fa, fb);
-#endif
     FSTAMP(t, 3);
-#ifndef G128_NOMFMA
     mma(fa, fb);
-#endif
     FSTAMP(t, 4);
     bar();
   }
@@ -317,17 +304,27 @@ __device__ __forceinline__ void tile128(const GemmArgs& g, unsigned char* smem, 
       const int mlo = by * BM;
       const bool nok = n >= bx * BN;
       float* C = (float*)g.C;
-      for (int r = 0; r < 32; ++r) {
-        const int m = mw + 32 * G + r;
-        const float v = tl[r * 64 + ((((lane >> 2) ^ (r & 15)) << 2) | (lane & 3))] * alpha;
-        if (nok && m >= mlo) {
-          float* c = C + (long)m * ldc + n;
-#ifdef G128_ACC_PLAIN  // timing diagnostic only: split-K slices overwrite instead of adding (wrong results)
-          if (nz > 1) *c = v;
-#else
-          if (nz > 1) atomicAdd(c, v);
-#endif
-          else *c += v;
+      if (nz > 1) {
+        for (int r = 0; r < 32; ++r) {
+          const int m = mw + 32 * G + r;
+          const float v = tl[r * 64 + ((((lane >> 2) ^ (r & 15)) << 2) | (lane & 3))] * alpha;
+          if (nok && m >= mlo) atomicAdd(C + (long)m * ldc + n, v);
+        }
+      } else {
+        // read-modify-write, 8 rows' loads in flight before their adds (a load behind each store was one memory
+        // round trip per row: epilogue p90 25.8k cycles in the grouped weight gradients)
+        float* crow = C + (long)(mw + 32 * G) * ldc + n;
+#pragma unroll 1
+        for (int r0 = 0; r0 < 32; r0 += 8) {
+          float old[8];
+#pragma unroll
+          for (int r = 0; r < 8; ++r) old[r] = (nok && mw + 32 * G + r0 + r >= mlo) ? crow[(r0 + r) * ldc] : 0.f;
+#pragma unroll
+          for (int r = 0; r < 8; ++r) {
+            const int rr = r0 + r;
+            const float v = tl[rr * 64 + ((((lane >> 2) ^ (rr & 15)) << 2) | (lane & 3))] * alpha;
+            if (nok && mw + 32 * G + rr >= mlo) crow[rr * ldc] = old[r] + v;
+          }
         }
       }
     } else {

@@ -250,6 +250,28 @@ def test_gemm128_grouped_weight_grads(monkeypatch):
         close(db, rb, rtol=1e-4, what=f"db job{i}")
 
 
+def test_grouped_weight_grads_ragged_tiles(monkeypatch):
+    """Grouped weight gradients: ragged rows and columns (shifted last tiles, overlap added once), ragged token
+    counts, a split-K problem among read-modify-write ones (the batched read-modify-write epilogue), strided
+    destinations, fused bias gradients."""
+    o = ops()
+    monkeypatch.delenv("FDDM_GEMM_PATH", raising=False)
+    gen = torch.Generator(device=dev).manual_seed(29)
+    specs = [(1000, 200, 320), (8192, 1536, 512), (3992, 136, 264), (15968, 256, 512), (2048, 384, 768)]
+    jobs, refs = [], []
+    for K, M, N in specs:
+        dy = torch.randn(K, M, device=dev, generator=gen).bfloat16()
+        x = torch.randn(K, N, device=dev, generator=gen).bfloat16()
+        dW = torch.randn(M, N + 24, device=dev, generator=gen)[:, 8:8 + N]
+        db = torch.randn(M, device=dev, generator=gen)
+        refs.append((dW.double() + dy.double().T @ x.double(), db.double() + dy.double().sum(0)))
+        jobs.append((dy, x, dW, db))
+    o.linear_dw_grouped(jobs)
+    for i, ((dy, x, dW, db), (rw, rb)) in enumerate(zip(jobs, refs)):
+        close(dW, rw, rtol=1e-4, what=f"dW job{i}")
+        close(db, rb, rtol=1e-4, what=f"db job{i}")
+
+
 def test_gemm256_dropout_gelu_matches_small_path(monkeypatch):
     """EPI_GELU with dropout: the 256x256 epilogue draws the same keep mask (counter-based hash of m*N+n)."""
     o = ops()
