@@ -604,6 +604,288 @@ __global__ void __launch_bounds__(256, ATTN_FWD_WPS) fwd2_kernel(AttnArgs a) {
   }
 }
 
+// inline-asm loads for the streamed kernels (hipcc does not track them; the kernels wait explicitly): a 1-KB
+// LDS-DMA piece (16 B per lane into lds + 16 * lane; lds wave-uniform), and a register pin
+typedef unsigned u32x4v_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void dma16_asm(const void* src, const unsigned char* lds) {
+  typedef __attribute__((address_space(3))) const void* lcp_t;
+  const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lcp_t)(const void*)lds);
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(la) : "memory", "m0");
+}
+__device__ __forceinline__ void pin16(uint4& x) {
+  u32x4v_t v = __builtin_bit_cast(u32x4v_t, x);
+  asm volatile("" : "+v"(v));
+  x = __builtin_bit_cast(uint4, v);
+}
+
+// ------------------------------------------------------------------------- fwd (bf16, WavLM, streamed ring)
+// WavLM's gated relative-position attention (no dropout): fwd2's work split (4 waves x 2 query groups x 16 = 128
+// queries per workgroup) and tile body, with the K / V tiles streamed through an NST-stage LDS ring by LDS-DMA
+// (NST - 1 tiles in flight) instead of register staging (global loads, LDS writes and their address arithmetic per
+// tile, and a __syncthreads fence that drained the next tile's loads); the smaller LDS footprint lets three
+// workgroups share a CU (fwd2: two). The
+// bias slice of the workgroup's query range and the key mask row are staged once (fwd3's layout). The DMA is
+// inline asm (dma16_asm): hipcc does not track it, so it inserts no stream-draining wait before the tile's LDS
+// reads; each tile waits for its own pieces with a counted vmcnt (every wave issues exactly 4 DMA instructions per
+// tile — past the end the last tile is re-read into a free stage — and no other vector-memory instruction in the
+// loop), then a barrier; the stage of tile t-1 is refilled after it. WavLM attention 56.5 -> 52 us at C2.
+template <bool MASK, int NST = 2, int NG = 2>
+__global__ void __launch_bounds__(256, NG == 1 ? 4 : 2) fwd5_kernel(AttnArgs a) {
+  constexpr int QW = 64 * NG, TB = 64 * 128, RB = 128;
+  constexpr bool DROP = false, REL = true;
+  extern __shared__ __attribute__((aligned(16))) unsigned char sm5[];
+  const int ntiles = (a.Lk + 63) / 64, LkP = ntiles * 64;
+  unsigned char* kst = sm5;                      // [NST][64 rows][128 B] K, KC image
+  unsigned char* vst = sm5 + NST * TB;           // [NST][64 rows][128 B] V, tr-read image
+  float* mfull = (float*)(sm5 + 2 * NST * TB);   // [LkP] 0 / -inf
+  float* tfull = mfull + LkP;                    // [LkP + QW] relative-bias slice
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
+            i = lane & 15;
+  int bxi, bh;
+  xcd_tile(bxi, bh);
+  const int b = bh / a.H, h = bh % a.H;
+  const int qbase = bxi * QW;
+  const bf16_t* Qb = (const bf16_t*)a.Q + (long)b * a.Lq * a.sq + h * DH;
+  const bf16_t* Kb = (const bf16_t*)a.K + (long)b * a.Lk * a.sk + h * DH;
+  const bf16_t* Vb = (const bf16_t*)a.V + (long)b * a.Lk * a.sv + h * DH;
+  // ---- ordinary loads first; hipcc waits for them before the stream starts (the asm below pins the registers)
+  int q[NG];
+  bool qv[NG];
+  uint4 qf[NG][2];
+  float gate[NG];
+#pragma unroll
+  for (int gq = 0; gq < NG; ++gq) {
+    q[gq] = qbase + w * (16 * NG) + gq * 16 + i;
+    qv[gq] = q[gq] < a.Lq;
+    row_frags<bf16_t>(qf[gq], Qb, a.sq, qv[gq] ? q[gq] : 0, qv[gq], lane);
+    gate[gq] = (a.gate && qv[gq]) ? a.gate[(long)bh * a.Lq + q[gq]] : 0.f;
+    if (a.graw && qv[gq]) {
+      // gate from the 8 pre-activations the Q|K|V projection appended (HF modeling_wavlm.py:177-186)
+      const uint4 u = *(const uint4*)((const bf16_t*)a.graw + ((long)b * a.Lq + q[gq]) * a.sgr + h * 8);
+      const float ra = bf2f((bf16_t)(u.x & 0xffff)) + bf2f((bf16_t)(u.x >> 16)) + bf2f((bf16_t)(u.y & 0xffff)) +
+                       bf2f((bf16_t)(u.y >> 16));
+      const float rb = bf2f((bf16_t)(u.z & 0xffff)) + bf2f((bf16_t)(u.z >> 16)) + bf2f((bf16_t)(u.w & 0xffff)) +
+                       bf2f((bf16_t)(u.w >> 16));
+      const float ga = 1.f / (1.f + __expf(-ra)), gb = 1.f / (1.f + __expf(-rb));
+      gate[gq] = ga * (gb * a.gconst[h] - 1.f) + 2.f;
+    }
+  }
+  for (int k = tid; k < LkP; k += 256) mfull[k] = (MASK && !key_ok(a, b, k)) ? -INFINITY : 0.f;
+  {
+    const float* tabh = a.table + (long)h * (2 * a.Lk - 1);
+    const long off0 = (long)(a.Lk - 1) - (qbase + QW - 1);  // tfull[j] = table[h][off0 + j]
+    for (int j = tid; j < LkP + QW; j += 256) {
+      const long ti = off0 + j;
+      tfull[j] = (ti >= 0 && ti < 2L * a.Lk - 1) ? tabh[ti] : 0.f;
+    }
+  }
+#pragma unroll
+  for (int gq = 0; gq < NG; ++gq) {
+    pin16(qf[gq][0]);
+    pin16(qf[gq][1]);
+    asm volatile("" : "+v"(gate[gq]));
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  // ---- K / V stream: wave w fills rows 16w .. 16w+15 of a tile (2 K + 2 V instructions; XOR swizzles on the
+  // per-lane source addresses, as fwd3_kernel)
+  auto fill = [&](int tt, int st) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int R = 16 * w + 8 * u;
+      const int r = 64 * tt + R + (lane >> 3), pch = lane & 7;
+      const int rr = min(r, a.Lk - 1);
+      const int ck = pch ^ ((r >> 1) & 7), cv = pch ^ (((r >> 1) & 3) << 1);
+      dma16_asm(Kb + (long)rr * a.sk + ck * 8, kst + st * TB + R * 128);
+      dma16_asm(Vb + (long)rr * a.sv + cv * 8, vst + st * TB + R * 128);
+    }
+  };
+#pragma unroll
+  for (int u = 0; u < NST - 1; ++u) fill(min(u, ntiles - 1), u);
+
+  const float sl2 = a.scale * 1.4426950408889634f;  // running max m is kept in log2 units
+  float graw[NG];  // bias multiplier in raw score units (gate / scale)
+#pragma unroll
+  for (int gq = 0; gq < NG; ++gq) graw[gq] = gate[gq] / a.scale;
+  float m[NG], l[NG];
+  f32x4_t o[NG][4];
+#pragma unroll
+  for (int gq = 0; gq < NG; ++gq) {
+    m[gq] = -INFINITY;
+    l[gq] = 0.f;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) o[gq][d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  }
+  const float th_raw = 8.f / sl2;  // lazy rescale threshold, as in fwd2_kernel
+  auto tile = [&](const int t, auto mc) {
+    constexpr bool MT = decltype(mc)::value;  // this tile adds the 0/-inf mask row
+    const int k0 = t * 64;
+    const unsigned char* kimg = kst + (t % NST) * TB;
+    const unsigned char* vimg = vst + (t % NST) * TB;
+    f32x4_t s[NG][4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+#pragma unroll
+      for (int gq = 0; gq < NG; ++gq) s[gq][kb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub) {
+        const uint4 af = *(const uint4*)(kimg + kc_off(RB, kb * 16 + i, sub * 4 + g));
+#pragma unroll
+        for (int gq = 0; gq < NG; ++gq) mma<bf16_t>(s[gq][kb], af, qf[gq][sub]);
+      }
+    }
+    // softmax. Scores stay in raw units x = s (+ (gate/scale)*bias) (+ the tile's 0/-inf mask row); the running
+    // max m is in raw units and p = 2^(x*sl2 - m*sl2) is one FMA + v_exp_f32 per score. Score pairs are carried
+    // as float2 so the bias FMA, the mask add, the exponent FMA and the row sum issue as packed v_pk_* f32
+    // instructions. MASK kernels add the mask row on every tile (0 where keys are valid): a per-tile condition
+    // compiled to an add plus a select per score on every tile. The dropout scale 1/(1-p) is applied to O once
+    // at the end, not per kept probability.
+    f32x2_t mrow[4][2];
+    if constexpr (MT) {
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        const float4 mv4 = *(const float4*)(&mfull[k0 + kb * 16 + 4 * g]);
+        mrow[kb][0] = f32x2_t{mv4.x, mv4.y};
+        mrow[kb][1] = f32x2_t{mv4.z, mv4.w};
+      }
+    }
+    float p[NG][4][4];
+#pragma unroll
+    for (int gq = 0; gq < NG; ++gq) {
+      float tmax = -INFINITY;
+      const int toff = (QW - 1) - (q[gq] - qbase) + k0;
+      const f32x2_t gr2 = {graw[gq], graw[gq]};
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          f32x2_t x = {s[gq][kb][2 * jj], s[gq][kb][2 * jj + 1]};
+          if constexpr (REL) {
+            const int kl = kb * 16 + 4 * g + 2 * jj + toff;
+            x = gr2 * f32x2_t{tfull[kl], tfull[kl + 1]} + x;
+          }
+          if constexpr (MT) x += mrow[kb][jj];
+          p[gq][kb][2 * jj] = x.x;
+          p[gq][kb][2 * jj + 1] = x.y;
+        }
+        tmax = fmaxf(tmax, fmaxf(fmaxf(p[gq][kb][0], p[gq][kb][1]), fmaxf(p[gq][kb][2], p[gq][kb][3])));
+      }
+      tmax = xmax16(tmax);
+      tmax = xmax32(tmax);
+      if (__any(tmax > m[gq] + th_raw)) {  // wave-uniform: rescale O and l to the new running max
+        const float mn = fmaxf(m[gq], tmax);
+        const float mref = (mn == -INFINITY) ? 0.f : mn;
+        const float alpha = __builtin_amdgcn_exp2f((m[gq] - mref) * sl2);
+        l[gq] *= alpha;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) o[gq][d] *= alpha;
+        m[gq] = mn;
+      }
+      const float mref = (m[gq] == -INFINITY) ? 0.f : m[gq];  // all-masked so far: exp2(-inf) = 0
+      const float nbias = -mref * sl2;
+      const f32x2_t sl2v = {sl2, sl2}, nb2 = {nbias, nbias};
+      f32x2_t ls2 = {0.f, 0.f};
+      uint64_t bits = 0;
+      // dropout keep bits of the lane's 4 keys per block (generic contract form; fwd3 stages the tables in LDS)
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        unsigned keep = 0xF;
+        if constexpr (DROP) {
+          keep = attn_keep4(a, bh, q[gq], k0 + kb * 16 + 4 * g);
+          bits |= (uint64_t)keep << (kb * 16 + 4 * g);
+        }
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          const f32x2_t arg = f32x2_t{p[gq][kb][2 * jj], p[gq][kb][2 * jj + 1]} * sl2v + nb2;
+          f32x2_t e = {__builtin_amdgcn_exp2f(arg.x), __builtin_amdgcn_exp2f(arg.y)};
+          ls2 += e;
+          if constexpr (DROP) {
+            e.x = ((keep >> (2 * jj)) & 1u) ? e.x : 0.f;
+            e.y = ((keep >> (2 * jj + 1)) & 1u) ? e.y : 0.f;
+          }
+          p[gq][kb][2 * jj] = e.x;
+          p[gq][kb][2 * jj + 1] = e.y;
+        }
+      }
+      const float ls = ls2.x + ls2.y;
+      if constexpr (DROP) {
+        if (a.dbits) {  // the 4 lanes of a query hold disjoint key nibbles: OR them into the tile's 64-bit word
+          unsigned lo = (unsigned)bits, hi = (unsigned)(bits >> 32);
+          lo = xor16(lo);
+          hi = xor16(hi);
+          lo = xor32(lo);
+          hi = xor32(hi);
+          if (g == 0 && qv[gq]) a.dbits[((long)bh * ntiles + t) * a.Lq + q[gq]] = ((uint64_t)hi << 32) | lo;
+        }
+      }
+      l[gq] += ls;
+    }
+    // O^T += V^T P^T for both query groups (one tr-read A fragment, two MFMAs)
+    {
+      const int qq = i >> 2, pp = i & 3;
+      typedef __attribute__((address_space(3))) s16x4_t* lp;
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        uint4 bq[NG];
+#pragma unroll
+        for (int gq = 0; gq < NG; ++gq) {
+          bq[gq].x = pk(p[gq][2 * ss][0], p[gq][2 * ss][1]);
+          bq[gq].y = pk(p[gq][2 * ss][2], p[gq][2 * ss][3]);
+          bq[gq].z = pk(p[gq][2 * ss + 1][0], p[gq][2 * ss + 1][1]);
+          bq[gq].w = pk(p[gq][2 * ss + 1][2], p[gq][2 * ss + 1][3]);
+        }
+        const int k1 = 32 * ss + 4 * g + qq, k2 = k1 + 16;
+#pragma unroll
+        for (int db = 0; db < 4; ++db) {
+          const int u = db * 4 + pp;
+          const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(vimg + k1 * 128 + ((u ^ hatt(k1)) << 3)));
+          const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(vimg + k2 * 128 + ((u ^ hatt(k2)) << 3)));
+          const uint4 af = join_tr(lo, hi);
+#pragma unroll
+          for (int gq = 0; gq < NG; ++gq) mma<bf16_t>(o[gq][db], af, bq[gq]);
+        }
+      }
+    }
+  };
+  auto arrive = [&](int t) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (NST - 2)) : "memory");  // own pieces of tile t landed
+    __builtin_amdgcn_s_barrier();
+    fill(min(t + NST - 1, ntiles - 1), (t + NST - 1) % NST);  // into the stage of tile t - 1
+  };
+  // the mask row only where it can be non-zero: every tile with a key-padding mask, else only the ragged last one
+  if (MASK && a.key_keep != nullptr) {
+    for (int t = 0; t < ntiles; ++t) {
+      arrive(t);
+      tile(t, std::integral_constant<bool, MASK>{});
+    }
+  } else {
+    for (int t = 0; t + 1 < ntiles; ++t) {
+      arrive(t);
+      tile(t, std::false_type{});
+    }
+    arrive(ntiles - 1);
+    tile(ntiles - 1, std::integral_constant<bool, MASK>{});
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may land after the workgroup retires
+#pragma unroll
+  for (int gq = 0; gq < NG; ++gq) {
+    float lt = l[gq];
+    lt = xsum16(lt);
+    lt = xsum32(lt);
+    if (!qv[gq]) continue;
+    const float inv = (lt > 0.f) ? 1.f / lt : NAN;  // fully masked row -> NaN like softmax(all -inf)
+    bf16_t* Ob = (bf16_t*)a.Out + ((long)b * a.Lq + q[gq]) * a.so + h * DH;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      uint2 u2;
+      u2.x = pk(o[gq][d][0] * inv, o[gq][d][1] * inv);
+      u2.y = pk(o[gq][d][2] * inv, o[gq][d][3] * inv);
+      *(uint2*)(Ob + d * 16 + 4 * g) = u2;
+    }
+    if (a.lse && g == 0)
+      a.lse[(long)bh * a.Lq + q[gq]] = (lt > 0.f) ? (m[gq] * sl2 + __log2f(lt)) * 0.69314718055994531f : NAN;
+  }
+}
+
 // ------------------------------------------------------------------------------- fwd (bf16, v3)
 // K/V resident in LDS: for Lk <= 512 the whole key range of one (b, h) fits (2 x Lk_pad x 128 B <= 128 KB), so
 // the workgroup streams every K and V row into LDS once, by LDS-DMA issued up front in tile order (8 rows of
@@ -2144,6 +2426,31 @@ static int run(int which, AttnArgs& a, hipStream_t s) {
           return (int)hipGetLastError();
         }
         dim3 grid((a.Lq + 127) / 128, a.B * a.H);
+        // WavLM: the streamed-ring forward (fwd5_kernel); FDDM_ATTN_FWD5=0 keeps fwd2
+        if (rel && !drop && (!getenv("FDDM_ATTN_FWD5") || atoi(getenv("FDDM_ATTN_FWD5")) != 0)) {
+          const int LkP = (a.Lk + 63) / 64 * 64;
+          // ring depth 2 (one tile ahead; 37 KB of LDS, three workgroups per CU by registers): tools/attn_bench.py at
+          // the C2 shape 51.7-52.0 us; 3 stages 53.5, 4 stages (two workgroups per CU) 58.6-59.3, 64-query workgroups
+          // (4 waves per SIMD) 55.3 / 62.4 / 69.0 with 2 / 3 / 4 stages; fwd2 56.4-57.0 (FDDM_ATTN_FWD5=0).
+          // FDDM_ATTN_NST=3|4 and FDDM_ATTN_NG5=1 are probes
+          const int nst = getenv("FDDM_ATTN_NST") ? atoi(getenv("FDDM_ATTN_NST")) : 2;
+          const int ng5 = getenv("FDDM_ATTN_NG5") ? atoi(getenv("FDDM_ATTN_NG5")) : 2;
+          const int qw5 = 64 * ng5;
+          const size_t lds5 = (size_t)2 * nst * 64 * 128 + (size_t)LkP * 4 + (size_t)(LkP + qw5) * 4;
+          dim3 grid5((a.Lq + qw5 - 1) / qw5, a.B * a.H);
+#define FWD5(N, G)                                                                                          \
+  do {                                                                                                       \
+    if (mask) hipLaunchKernelGGL((fwd5_kernel<true, N, G>), grid5, dim3(256), lds5, s, a);                   \
+    else hipLaunchKernelGGL((fwd5_kernel<false, N, G>), grid5, dim3(256), lds5, s, a);                       \
+  } while (0)
+          if (ng5 == 1) {
+            if (nst == 2) FWD5(2, 1); else if (nst == 4) FWD5(4, 1); else FWD5(3, 1);
+          } else {
+            if (nst == 2) FWD5(2, 2); else if (nst == 4) FWD5(4, 2); else FWD5(3, 2);
+          }
+#undef FWD5
+          return (int)hipGetLastError();
+        }
 #define FWD2(D, M, R) hipLaunchKernelGGL((fwd2_kernel<D, M, R>), grid, dim3(256), 0, s, a)
         if (rel) {
           if (drop) { if (mask) FWD2(true, true, true); else FWD2(true, false, true); }
