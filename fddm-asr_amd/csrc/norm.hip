@@ -76,7 +76,8 @@ __device__ __forceinline__ float wave_sum_v(float v) {
 // One wave per row. Every load of the row (x, y, gamma, beta, FiLM scale / shift) is issued before the first use,
 // so a wave waits for one memory round trip, not three; the two row reductions run in the VALU (wave_sum_v).
 // HY: residual branch y present, HF: FiLM present (compile-time: a load under a runtime branch gets its own wait)
-template <typename XT, typename YT, typename OT, bool HY, bool HF>
+// CH chunks of 8 per lane: 1 for d <= 512 (the decoder), 2 for d <= 1024 (WavLM 768)
+template <typename XT, typename YT, typename OT, bool HY, bool HF, int CH>
 __global__ void __launch_bounds__(256) ln_fwd_kernel(LnFwdArgs a) {
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
@@ -85,11 +86,11 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(LnFwdArgs a) {
   const XT* x = (const XT*)a.x + row * d;
   const YT* y = HY ? (const YT*)a.y + row * d : nullptr;
   const long b = HF ? row / a.rows_per_batch : 0;
-  float v[LN_MAXCH][8], yv[LN_MAXCH][8], gm[LN_MAXCH][8], bt[LN_MAXCH][8], fs[LN_MAXCH][8], fh[LN_MAXCH][8];
+  float v[CH][8], yv[CH][8], gm[CH][8], bt[CH][8], fs[CH][8], fh[CH][8];
   // lanes past the row end load its last chunk again (no divergent branch around the loads: a load inside one
   // would be waited for at the branch join) and contribute zeros
 #pragma unroll
-  for (int i = 0; i < LN_MAXCH; ++i) {
+  for (int i = 0; i < CH; ++i) {
     const long c0 = min(lane + 64L * i, nch - 1) * 8;
     ld8<XT>(x + c0, v[i]);
     if constexpr (HY) ld8<YT>(y + c0, yv[i]);
@@ -102,7 +103,7 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(LnFwdArgs a) {
   }
   float sum = 0.f;
 #pragma unroll
-  for (int i = 0; i < LN_MAXCH; ++i) {
+  for (int i = 0; i < CH; ++i) {
     const long ch = lane + 64L * i;
     if (ch >= nch) {
 #pragma unroll
@@ -127,7 +128,7 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(LnFwdArgs a) {
   const float mean = wave_sum_v(sum) / (float)d;
   float sq = 0.f;
 #pragma unroll
-  for (int i = 0; i < LN_MAXCH; ++i) {
+  for (int i = 0; i < CH; ++i) {
     const long ch = lane + 64L * i;
     if (ch < nch) {
 #pragma unroll
@@ -140,7 +141,7 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(LnFwdArgs a) {
   const float var = wave_sum_v(sq) / (float)d;
   const float rstd = 1.f / sqrtf(var + a.eps);
 #pragma unroll
-  for (int i = 0; i < LN_MAXCH; ++i) {
+  for (int i = 0; i < CH; ++i) {
     const long ch = lane + 64L * i;
     if (ch < nch) {
       const long c0 = ch * 8;
@@ -426,12 +427,20 @@ FDDM_API int fddm_ln_fwd(int x_dtype, int y_dtype, int out_dtype, const void* x,
   dim3 grid((unsigned)((N + 3) / 4));
   hipStream_t s = (hipStream_t)hs;
   const bool hy = y != nullptr, hf = film_scale != nullptr;
-#define LNF(XT, YT, OT)                                                                                   \
-  do {                                                                                                    \
-    if (hy && hf) hipLaunchKernelGGL((ln_fwd_kernel<XT, YT, OT, true, true>), grid, dim3(256), 0, s, a);   \
-    else if (hy) hipLaunchKernelGGL((ln_fwd_kernel<XT, YT, OT, true, false>), grid, dim3(256), 0, s, a);   \
-    else if (hf) hipLaunchKernelGGL((ln_fwd_kernel<XT, YT, OT, false, true>), grid, dim3(256), 0, s, a);   \
-    else hipLaunchKernelGGL((ln_fwd_kernel<XT, YT, OT, false, false>), grid, dim3(256), 0, s, a);          \
+  // one chunk of 8 per lane when d <= 512: the two-chunk form re-loaded every lane's last chunk (x, y, gamma, beta,
+  // FiLM) for the decoder's d = 512 rows
+  const bool ch1 = d <= 512;
+#define LNF2(XT, YT, OT, C)                                                                                    \
+  do {                                                                                                         \
+    if (hy && hf) hipLaunchKernelGGL((ln_fwd_kernel<XT, YT, OT, true, true, C>), grid, dim3(256), 0, s, a);     \
+    else if (hy) hipLaunchKernelGGL((ln_fwd_kernel<XT, YT, OT, true, false, C>), grid, dim3(256), 0, s, a);     \
+    else if (hf) hipLaunchKernelGGL((ln_fwd_kernel<XT, YT, OT, false, true, C>), grid, dim3(256), 0, s, a);     \
+    else hipLaunchKernelGGL((ln_fwd_kernel<XT, YT, OT, false, false, C>), grid, dim3(256), 0, s, a);            \
+  } while (0)
+#define LNF(XT, YT, OT)                \
+  do {                                 \
+    if (ch1) LNF2(XT, YT, OT, 1);      \
+    else LNF2(XT, YT, OT, 2);          \
   } while (0)
   if (x_dtype == FDDM_F32 && y_dtype == FDDM_BF16 && out_dtype == FDDM_BF16)
     LNF(float, bf16_t, bf16_t);
@@ -444,6 +453,7 @@ FDDM_API int fddm_ln_fwd(int x_dtype, int y_dtype, int out_dtype, const void* x,
   else
     return (int)hipErrorInvalidValue;
 #undef LNF
+#undef LNF2
   return (int)hipGetLastError();
 }
 
