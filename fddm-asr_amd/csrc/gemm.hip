@@ -688,11 +688,18 @@ static int gemm_path() {
 static bool big_enabled() { return gemm_path() != 2 && gemm_path() != 4; }
 static bool g256_enabled() { return gemm_path() == 0 || gemm_path() == 3; }
 static bool g128_enabled() { return gemm_path() == 0 || gemm_path() == 4; }
-// the persistent 256x256 kernel wins from about half a round of tiles up (measured at the train step's shapes:
-// 189 tiles of 15968x768x3072 still beat the 256x128 kernel by 1.3x; 64 tiles of 8192x512x512 lose)
+// the persistent 256x256 kernel from a quarter round of tiles up: alone on the chip 64 tiles of 8192x512x512 lose
+// to the 128x128 kernel, but beside the encoder's persistent GEMMs (half or a quarter of the CUs free) one round of
+// 64 tiles beats two rounds of 256: the decoder's d-wide forward GEMMs (out-proj, cross Q / out, V, FF2) — C4
+// (d 768: 96 tiles) 17.79-17.87 -> 17.36-17.37 ms/step, C2 (64 tiles) 9.89 -> 9.87 ms average of 6 alternating rounds
+// (threshold 128 before; FDDM_G256_MIN_TILES, read once, is the probe)
 static bool prefer_256(long M, long N) {
   if (gemm_path() == 3) return true;
-  return gemm256_tiles(M, N) >= 128;
+  static const long min_tiles = []() {
+    const char* v = getenv("FDDM_G256_MIN_TILES");
+    return v ? atol(v) : 64L;
+  }();
+  return gemm256_tiles(M, N) >= min_tiles;
 }
 static long env_long(const char* name, long dflt) {
   const char* v = getenv(name);
