@@ -158,6 +158,98 @@ __global__ void __launch_bounds__(256) conv0_apply_kernel(const float* __restric
   }
 }
 
+// bf16 output: the conv and the GroupNorm affine on the matrix cores. Per utterance b the affine folds into the
+// weights, z = (sc w) . x + sh; v = sc w and sh are split into bf16 parts v = hi + lo (to ~2^-16 relative), and one
+// v_mfma_f32_16x16x32_bf16 over K = 32 forms z = v_hi.x_hi + v_hi.x_lo + v_lo.x_hi + sh_hi + sh_lo for 16 channels
+// x 16 frames (the dropped v_lo.x_lo term is ~2^-17 relative: f32-level accuracy, unlike a plain bf16 conv).
+// Frame rows [x_hi(10) x_lo(10) x_hi(10) 1 1] are staged once per block in LDS (64 B per frame, one ds_read_b128
+// per lane), channel rows [v_hi v_hi v_lo sh_hi sh_lo] stay in registers. Only GELU + convert remain on the VALU
+// (~11 VALU instructions per output; the recompute kernel spent 5 more on the conv; VALU-bound either way,
+// SQ_ACTIVE_INST_VALU ~70 % of the SIMD cycles). Wave = 64 channels as 4 MFMA tiles; row 4g + r of tile j is
+// channel 32(j/2) + 8g + 4(j%2) + r, so lane (frame f, g) holds channels 8g..8g+7 and 32+8g..32+8g+7 of frame f.
+constexpr int C0M_FRAMES = 512;  // frames per block: the per-block setup (weights, affine, LDS rows) amortised
+__device__ __forceinline__ int c0m_part(int k) { return k >= 20 ? 2 : (k >= 10 ? 1 : 0); }
+
+__global__ void __launch_bounds__(512) conv0_mfma_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                         const float* __restrict__ scsh, bf16_t* __restrict__ out,
+                                                         long nsamp, long T0, int C, int S) {
+  constexpr int K = 10;
+  __shared__ __attribute__((aligned(16))) bf16_t xr[C0M_FRAMES * 32];
+  const long b = blockIdx.y;
+  const long t0 = (long)blockIdx.x * C0M_FRAMES;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (int e = tid; e < C0M_FRAMES * 32; e += 512) {
+    const int f = e >> 5, k = e & 31;
+    float v = k >= 3 * K ? 1.f : 0.f;
+    int part = 0;
+    if (k < 3 * K && t0 + f < T0) {
+      part = c0m_part(k);
+      v = x[b * nsamp + (t0 + f) * S + (k - K * part)];
+    }
+    const bf16_t hi = f2bf(v);
+    xr[e] = part == 1 ? f2bf(v - bf2f(hi)) : hi;
+  }
+  const int fr = lane & 15, g = lane >> 4;
+  const int cb = blockIdx.z * 512 + wv * 64;
+  bf16x8_t wa[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = cb + 32 * (j >> 1) + 8 * (fr >> 2) + 4 * (j & 1) + (fr & 3);
+    const float sc = scsh[2 * (b * C + c)], sh = scsh[2 * (b * C + c) + 1];
+    const bf16_t shh = f2bf(sh);
+    bf16_t u[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int k = 8 * g + q;
+      bf16_t r;
+      if (k < 3 * K) {
+        const int part = c0m_part(k);
+        const float wk = sc * w[c * K + (k - K * part)];
+        const bf16_t hi = f2bf(wk);
+        r = part == 2 ? f2bf(wk - bf2f(hi)) : hi;
+      } else {
+        r = k == 3 * K ? shh : f2bf(sh - bf2f(shh));
+      }
+      u[q] = r;
+    }
+    wa[j] = __builtin_bit_cast(bf16x8_t, u);
+  }
+  __syncthreads();
+  const f32x4_t zero = {0.f, 0.f, 0.f, 0.f};
+  const bool hi8 = fr >= 8;
+  const long tend = min(T0 - t0, (long)C0M_FRAMES);
+  bf16_t* ob = out + (b * T0 + t0 + (fr & 7)) * C + cb + (hi8 ? 32 : 0) + 8 * g;
+  for (int f0 = 0; f0 < tend; f0 += 16) {
+    const bf16x8_t xb = *(const bf16x8_t*)(xr + (f0 + fr) * 32 + 8 * g);
+    f32x4_t acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[j], xb, zero, 0, 0, 0);
+    // acc[j][r] = channel 32(j/2) + 8g + 4(j%2) + r of frame f0 + fr
+    unsigned pk[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; r += 2) pk[2 * j + r / 2] = pk_bf16(gelu_bf16out(acc[j][r]), gelu_bf16out(acc[j][r + 1]));
+    // whole 128-B lines per store: lanes f and f ^ 8 (DPP row_ror:8) trade a 16-B chunk so that the first store
+    // writes frames 0..7 of the tile and the second frames 8..15, each frame's 64 channels by its 8 lanes
+    uint4 a, c;
+    {
+      unsigned y[4], z[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        y[e] = hi8 ? pk[e] : pk[4 + e];
+        z[e] = (unsigned)__builtin_amdgcn_mov_dpp((int)y[e], 0x128, 0xf, 0xf, false);
+      }
+      a = hi8 ? make_uint4(z[0], z[1], z[2], z[3]) : make_uint4(pk[0], pk[1], pk[2], pk[3]);
+      c = hi8 ? make_uint4(pk[4], pk[5], pk[6], pk[7]) : make_uint4(z[0], z[1], z[2], z[3]);
+    }
+    const int fa = f0 + (fr & 7);
+    bf16_t* o = ob + (long)f0 * C;
+    if (fa < tend) *(uint4*)o = a;
+    if (fa + 8 < tend) *(uint4*)(o + 8 * C) = c;
+  }
+}
+
 // one thread per (token, head): 64-element slice in 16-B loads, W (8 x 64) broadcast from LDS
 template <typename T>
 __global__ void __launch_bounds__(256) wavlm_gate_kernel(const T* __restrict__ x, const float* __restrict__ W,
@@ -209,6 +301,12 @@ FDDM_API int fddm_conv0_gn_gelu(int out_dtype, const float* x, const float* w, c
   float* scsh = (float*)(ws + B * (K + K * K));
   hipLaunchKernelGGL(conv0_gn_affine_kernel, dim3((unsigned)((B * C + 255) / 256)), dim3(256), 0, s, ws, w, gamma, beta,
                      scsh, B, T0, C, K, eps);
+  static const bool valu = getenv("FDDM_CONV0_VALU") != nullptr;  // A/B probe: the VALU recompute kernel
+  if (out_dtype == FDDM_BF16 && C % 512 == 0 && !valu) {
+    dim3 gm((unsigned)((T0 + C0M_FRAMES - 1) / C0M_FRAMES), (unsigned)B, (unsigned)(C / 512));
+    hipLaunchKernelGGL(conv0_mfma_kernel, gm, dim3(512), 0, s, x, w, scsh, (bf16_t*)out, nsamp, T0, C, S);
+    return (int)hipGetLastError();
+  }
   dim3 grid((unsigned)((T0 + C0_FRAMES - 1) / C0_FRAMES), (unsigned)B);
   const size_t lds = ((C0_FRAMES - 1) * S + K) * sizeof(float);
   if (out_dtype == FDDM_BF16)
