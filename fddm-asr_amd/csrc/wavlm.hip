@@ -16,11 +16,15 @@ constexpr int C0_MAXK = 16;
 // GroupNorm statistics without materialising y: per utterance the K sums S1[k] = sum_t x[S t + k] and
 // the K x K Gram G[k][k'] = sum_t x[S t + k] x[S t + k'] (fp64) give, per channel c,
 //   sum_t y = w_c . S1      sum_t y^2 = w_c^T G w_c.
-// ws layout per utterance: [K] S1 then [K*K] G, fp64, zeroed by the caller.
-constexpr int C0_GRAM_FRAMES = 4096;
+// Each block of C0_GRAM_FRAMES frames stores its partial [S1 (K), upper triangle of G (K(K+1)/2)] with plain stores
+// (ws: [B][nb][NQ]); the affine kernel sums the nb partials of its utterance in a fixed order (deterministic, and
+// no zero-fill: the double atomics of 8 blocks per utterance made the statistics ~33 us).
+constexpr int C0_GRAM_FRAMES = 4096;  // 1024 per block measured slower (50 vs 29 us)
+template <int K> constexpr int c0_nq() { return K + K * (K + 1) / 2; }
 template <int K>
-__global__ void __launch_bounds__(256) conv0_gram_kernel(const float* __restrict__ x, double* __restrict__ ws, long nsamp,
-                                                         long T0, int S) {
+__global__ void __launch_bounds__(256) conv0_gram_kernel(const float* __restrict__ x, double* __restrict__ part,
+                                                         long nsamp, long T0, int S) {
+  constexpr int NQ = c0_nq<K>();
   const long b = blockIdx.y;
   const long f0 = (long)blockIdx.x * C0_GRAM_FRAMES;
   const long f1 = min(T0, f0 + C0_GRAM_FRAMES);
@@ -29,6 +33,7 @@ __global__ void __launch_bounds__(256) conv0_gram_kernel(const float* __restrict
   for (int k = 0; k < K; ++k) s1[k] = 0.0;
 #pragma unroll
   for (int k = 0; k < K * (K + 1) / 2; ++k) g[k] = 0.0;
+#pragma unroll 4
   for (long f = f0 + threadIdx.x; f < f1; f += 256) {
     float xv[K];
 #pragma unroll
@@ -41,62 +46,57 @@ __global__ void __launch_bounds__(256) conv0_gram_kernel(const float* __restrict
       for (int j = k; j < K; ++j) g[q++] += (double)xv[k] * (double)xv[j];
     }
   }
-  // reduce over the block in LDS, one atomic per value
-  __shared__ double red[K + K * (K + 1) / 2][4];
+  __shared__ double red[NQ][4];
   const int w = threadIdx.x >> 6;
 #pragma unroll
-  for (int k = 0; k < K; ++k) {
-    double v = s1[k];
+  for (int q = 0; q < NQ; ++q) {
+    double v = q < K ? s1[q] : g[q - K];
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    if ((threadIdx.x & 63) == 0) red[k][w] = v;
-  }
-#pragma unroll
-  for (int q = 0; q < K * (K + 1) / 2; ++q) {
-    double v = g[q];
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    if ((threadIdx.x & 63) == 0) red[K + q][w] = v;
+    if ((threadIdx.x & 63) == 0) red[q][w] = v;
   }
   __syncthreads();
-  double* out = ws + b * (K + K * K);
-  if (threadIdx.x < K) {
-    const int k = threadIdx.x;
-    atomicAdd(out + k, red[k][0] + red[k][1] + red[k][2] + red[k][3]);
-  }
-  if (threadIdx.x < K * (K + 1) / 2) {
-    int q = threadIdx.x, k = 0;
-    while (q >= K - k) { q -= K - k; ++k; }
-    const int j = k + q;
-    const int qi = threadIdx.x;
-    const double t = red[K + qi][0] + red[K + qi][1] + red[K + qi][2] + red[K + qi][3];
-    atomicAdd(out + K + k * K + j, t);
-    if (j != k) atomicAdd(out + K + j * K + k, t);
+  if (threadIdx.x < NQ) {
+    const int q = threadIdx.x;
+    part[(b * gridDim.x + blockIdx.x) * NQ + q] = (red[q][0] + red[q][1]) + (red[q][2] + red[q][3]);
   }
 }
 
-// per (b, c): mean/var from (S1, G) -> fused GroupNorm affine  sc = gamma*rstd, sh = beta - mean*sc
-__global__ void conv0_gn_affine_kernel(const double* __restrict__ ws, const float* __restrict__ w,
-                                       const float* __restrict__ gamma, const float* __restrict__ beta,
-                                       float* __restrict__ scsh, long B, long T0, int C, int K, float eps) {
-  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= B * C) return;
-  const long b = e / C;
-  const int c = (int)(e % C);
-  const double* s1 = ws + b * (K + K * K);
-  const double* G = s1 + K;
-  double m = 0.0, q = 0.0;
-  for (int k = 0; k < K; ++k) {
-    const double wk = w[c * K + k];
-    m += wk * s1[k];
-    double r = 0.0;
-    for (int j = 0; j < K; ++j) r += G[k * K + j] * (double)w[c * K + j];
-    q += wk * r;
+// per (b, c): mean/var from (S1, G) -> fused GroupNorm affine  sc = gamma*rstd, sh = beta - mean*sc; one block
+// per utterance sums its nb partials once into LDS
+template <int K>
+__global__ void __launch_bounds__(512) conv0_gn_affine_kernel(const double* __restrict__ part, int nb,
+                                                              const float* __restrict__ w, const float* __restrict__ gamma,
+                                                              const float* __restrict__ beta, float* __restrict__ scsh,
+                                                              long T0, int C, float eps) {
+  constexpr int NQ = c0_nq<K>();
+  __shared__ double tot[NQ];
+  const long b = blockIdx.x;
+  if (threadIdx.x < NQ) {
+    double t = 0.0;
+    for (int i = 0; i < nb; ++i) t += part[(b * nb + i) * NQ + threadIdx.x];
+    tot[threadIdx.x] = t;
   }
-  m /= (double)T0;
-  const double var = fmax(q / (double)T0 - m * m, 0.0);
-  const float rstd = (float)(1.0 / sqrt(var + (double)eps));
-  const float sc = rstd * gamma[c];
-  scsh[2 * e] = sc;
-  scsh[2 * e + 1] = beta[c] - (float)m * sc;
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    double wk[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) wk[k] = (double)w[c * K + k];
+    double m = 0.0, q = 0.0;
+    int i = K;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      m += wk[k] * tot[k];
+      q += wk[k] * wk[k] * tot[i++];
+#pragma unroll
+      for (int j = k + 1; j < K; ++j) q += 2.0 * wk[k] * wk[j] * tot[i++];
+    }
+    m /= (double)T0;
+    const double var = fmax(q / (double)T0 - m * m, 0.0);
+    const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+    const float sc = rstd * gamma[c];
+    scsh[2 * (b * C + c)] = sc;
+    scsh[2 * (b * C + c) + 1] = beta[c] - (float)m * sc;
+  }
 }
 
 // recompute y, normalise, GELU; thread owns channel pair (2c, 2c+1) -> 4-B stores, 1 KB per wave row.
@@ -295,12 +295,12 @@ FDDM_API int fddm_conv0_gn_gelu(int out_dtype, const float* x, const float* w, c
   if (B <= 0 || T0 <= 0) return 0;
   if (K > C0_MAXK || C % 2) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)hs;
-  dim3 gg((unsigned)((T0 + C0_GRAM_FRAMES - 1) / C0_GRAM_FRAMES), (unsigned)B);
   if (K != 10) return (int)hipErrorInvalidValue;  // WavLM conv layer 0 (kernel 10, stride 5)
-  hipLaunchKernelGGL(conv0_gram_kernel<10>, gg, dim3(256), 0, s, x, ws, nsamp, T0, S);
-  float* scsh = (float*)(ws + B * (K + K * K));
-  hipLaunchKernelGGL(conv0_gn_affine_kernel, dim3((unsigned)((B * C + 255) / 256)), dim3(256), 0, s, ws, w, gamma, beta,
-                     scsh, B, T0, C, K, eps);
+  const int nb = (int)((T0 + C0_GRAM_FRAMES - 1) / C0_GRAM_FRAMES);
+  hipLaunchKernelGGL(conv0_gram_kernel<10>, dim3((unsigned)nb, (unsigned)B), dim3(256), 0, s, x, ws, nsamp, T0, S);
+  float* scsh = (float*)(ws + B * nb * c0_nq<10>());
+  hipLaunchKernelGGL(conv0_gn_affine_kernel<10>, dim3((unsigned)B), dim3(512), 0, s, ws, nb, w, gamma, beta, scsh, T0, C,
+                     eps);
   static const bool valu = getenv("FDDM_CONV0_VALU") != nullptr;  // A/B probe: the VALU recompute kernel
   if (out_dtype == FDDM_BF16 && C % 512 == 0 && !valu) {
     dim3 gm((unsigned)((T0 + C0M_FRAMES - 1) / C0M_FRAMES), (unsigned)B, (unsigned)(C / 512));

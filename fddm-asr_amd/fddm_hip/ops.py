@@ -202,7 +202,8 @@ def posconv_gelu(x, W, bias, out, B, S, E, G, kp):
 def conv0_gn_gelu(wave, w, gamma, beta, out_dtype, C, K, S, eps=1e-5):
     B, nsamp = wave.shape
     T0 = (nsamp - K) // S + 1
-    ws = torch.zeros(B * (K + K * K) + B * C, device=wave.device, dtype=torch.float64)
+    nb = (T0 + 4095) // 4096  # statistics blocks per utterance (wavlm.hip C0_GRAM_FRAMES)
+    ws = torch.empty(B * nb * (K + K * (K + 1) // 2) + B * C, device=wave.device, dtype=torch.float64)
     out = torch.empty(B, T0, C, device=wave.device, dtype=out_dtype)
     call("fddm_conv0_gn_gelu", code(out), ptr(wave), ptr(w), ptr(gamma), ptr(beta), ptr(ws), ptr(out), B, nsamp, T0,
          C, K, S, float(eps), stream())

@@ -69,8 +69,9 @@ int fddm_conv1d_gemm(int dtype, int epi, const void* x, long lda, long sAb, long
 int fddm_posconv_gelu(const void* x, const void* W, const float* bias, void* out, long B, long S, long E, int G,
                       int kp, void* hip_stream);
 
-/* ---- conv layer 0 + GroupNorm + GELU. HF modeling_wavlm.py:723-744. ws: zeroed f64 scratch of
- *      B*(K + K*K) + B*C doubles (per-utterance Gram statistics, then the GroupNorm affine). */
+/* ---- conv layer 0 + GroupNorm + GELU. HF modeling_wavlm.py:723-744. ws: f64 scratch (need not be zeroed) of
+ *      B*nb*(K + K*(K+1)/2) + B*C doubles, nb = ceil(T0 / 4096) (per-block Gram statistics, then the GroupNorm
+ *      affine). */
 int fddm_conv0_gn_gelu(int out_dtype, const float* x, const float* w, const float* gamma, const float* beta,
                        double* ws, void* out, long B, long nsamp, long T0, int C, int K, int S, float eps,
                        void* hip_stream);
