@@ -563,6 +563,29 @@ def test_layernorm_fwd_bwd(film, L):
         close(dfh, fhr.grad, rtol=1e-4, what="dfilm shift")
 
 
+@pytest.mark.parametrize("N,d", [(1001, 768), (37, 200), (64, 1024)])
+def test_ln_fwd_bf16_post_ln_rows(N, d):
+    """The frozen encoder's post-LN (bf16 x + bf16 residual -> bf16, one row per wave, 2 chunks of 8 per lane):
+    ragged row counts (N % 4 != 0), d with fewer chunks than lanes (200) and the largest d (1024), against a float64
+    layer_norm of the same bf16 inputs within the bf16 output rounding (2^-8 relative + 1e-3)."""
+    o = ops()
+    bf = torch.bfloat16
+    x = torch.randn(N, d, generator=g(47)).to(bf)
+    y = (0.5 * torch.randn(N, d, generator=g(48)) + 0.3).to(bf)
+    gm = 1 + 0.1 * torch.randn(d, generator=g(42))
+    bt = 0.1 * torch.randn(d, generator=g(43))
+    ref = F.layer_norm(x.double() + y.double(), (d,), gm.double(), bt.double(), 1e-5)
+    out = torch.empty(N, d, device=dev, dtype=bf)
+    mean = torch.empty(N, device=dev)
+    rstd = torch.empty(N, device=dev)
+    o.ln_fwd(x.to(dev), y.to(dev), gm.to(dev), bt.to(dev), out_t=out, mean=mean, rstd=rstd, eps=1e-5)
+    err = (out.double().cpu() - ref).abs()
+    assert (err <= 2.0 ** -8 * ref.abs() + 1e-3).all(), float(err.max())
+    s = x.double() + y.double()
+    close(mean, s.mean(1), rtol=1e-5, what="mean")
+    close(rstd, 1 / torch.sqrt(s.var(1, unbiased=False) + 1e-5), rtol=1e-4, what="rstd")
+
+
 @pytest.mark.parametrize("d", [128, 6])
 def test_rope_and_embedding(d):
     """d = 128: the vectorised kernels (8 columns per thread); d = 6: the scalar forms."""
