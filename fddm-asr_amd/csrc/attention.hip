@@ -2473,7 +2473,8 @@ static int run(int which, AttnArgs& a, hipStream_t s) {
         // v3: K/V resident, 256 queries per workgroup, for Lk <= 256 (tools/attn_bench.py: decoder self-attention
         // backward 38.6 -> 35.3 us with dkv3; at the cross-attention's Lk = 499 — 130 KB of LDS, one workgroup per
         // CU — no faster than the streamed kernels, 64.0 vs 62.8 us); FDDM_ATTN_DQ2=1 keeps the streamed kernel
-        if (a.Lk <= 256 && dm != 1 && !getenv("FDDM_ATTN_DQ2")) {
+        static const int v3max = getenv("FDDM_ATTN_V3_MAX") ? atoi(getenv("FDDM_ATTN_V3_MAX")) : 256;
+        if (a.Lk <= v3max && a.Lk <= 512 && dm != 1 && !getenv("FDDM_ATTN_DQ2")) {
           const int LkP = (a.Lk + 63) / 64 * 64;
           const size_t lds = (size_t)LkP * 256 + (size_t)LkP * 4;
           dim3 g3((a.Lq + 255) / 256, a.B * a.H);
@@ -2512,7 +2513,8 @@ static int run(int which, AttnArgs& a, hipStream_t s) {
       if (!getenv("FDDM_ATTN_V1")) {
         // v3: Q/dO resident, 256 keys per workgroup, for Lq, Lk <= 256 (see dq3 above); FDDM_ATTN_DKV2=1 keeps the
         // streamed kernel
-        if (a.Lq <= 256 && a.Lk <= 256 && (!a.thr16 || a.dbits) && !getenv("FDDM_ATTN_DKV2")) {
+        static const int v3max = getenv("FDDM_ATTN_V3_MAX") ? atoi(getenv("FDDM_ATTN_V3_MAX")) : 256;
+        if (a.Lq <= v3max && a.Lk <= v3max && a.Lq <= 512 && (!a.thr16 || a.dbits) && !getenv("FDDM_ATTN_DKV2")) {
           const int LqP = (a.Lq + 63) / 64 * 64;
           const size_t lds = (size_t)LqP * 256 + (size_t)LqP * 8 + (a.thr16 ? (size_t)4 * LqP * 8 : 0);
           dim3 g3((a.Lk + 255) / 256, a.B * a.H);

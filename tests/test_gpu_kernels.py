@@ -390,7 +390,8 @@ def _attn_ref(q, k, v, keep, p_drop, seed, stream, gate=None, table=None):
                                                  (64, 130, False, 0.1, True), (40, 499, False, 0.1, True),
                                                  (129, 257, True, 0.1, True), (96, 256, True, 0.1, True),
                                                  (64, 499, False, 0.0, False), (256, 256, False, 0.1, True),
-                                                 (200, 200, True, 0.1, True), (32, 32, False, 0.0, False)])
+                                                 (200, 200, True, 0.1, True), (32, 32, False, 0.0, False),
+                                                 (512, 512, True, 0.1, True), (300, 499, False, 0.1, True)])
 def test_attention_fwd_bwd(dtype, Lq, Lk, masked, p, bits):
     """bits: the forward records the dropout keep bits and the backward reads them (bf16 path)."""
     o = ops()
