@@ -28,8 +28,8 @@ struct MTTable {
 
 constexpr long MT_CHUNK = 65536;
 
-__global__ void __launch_bounds__(256) sumsq_kernel(MTTable t, float* total) {
-  __shared__ float red[4];
+__global__ void __launch_bounds__(1024) sumsq_kernel(MTTable t, float* total) {
+  __shared__ float red[16];
   const long ci = blockIdx.x;
   const long ti = t.chunk_tensor[ci], s0 = t.chunk_start[ci];
   const long n = min(MT_CHUNK, t.numel[ti] - s0);
@@ -38,7 +38,23 @@ __global__ void __launch_bounds__(256) sumsq_kernel(MTTable t, float* total) {
   long i = 0;
   if ((((uintptr_t)g) & 15) == 0) {  // 16-B loads, 4 independent accumulators
     const long n4 = n / 4;
-    for (long j = threadIdx.x; j < n4; j += 256) {
+    // 1024 threads, U iterations' loads issued before any accumulation: 32 KB in flight per block instead of 4 KB (the
+    // 256-thread one-load loop was latency-bound: 158.7 MB in 55 us, 2.9 TB/s; tools/probe/sumsq.py)
+    constexpr int U = 8;
+    long j = threadIdx.x;
+    for (; j + 1024 * (U - 1) < n4; j += 1024 * U) {
+      float4 x[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) x[u] = ((const float4*)g)[j + 1024 * u];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        acc[0] += x[u].x * x[u].x;
+        acc[1] += x[u].y * x[u].y;
+        acc[2] += x[u].z * x[u].z;
+        acc[3] += x[u].w * x[u].w;
+      }
+    }
+    for (; j < n4; j += 1024) {
       const float4 x = ((const float4*)g)[j];
       acc[0] += x.x * x.x;
       acc[1] += x.y * x.y;
@@ -47,7 +63,7 @@ __global__ void __launch_bounds__(256) sumsq_kernel(MTTable t, float* total) {
     }
     i = n4 * 4;
   }
-  for (long j = i + threadIdx.x; j < n; j += 256) acc[0] += g[j] * g[j];
+  for (long j = i + threadIdx.x; j < n; j += 1024) acc[0] += g[j] * g[j];
   float v = block_sum((acc[0] + acc[1]) + (acc[2] + acc[3]), red);
   if (threadIdx.x == 0) atomicAdd(total, v);
 }
@@ -164,7 +180,7 @@ FDDM_API int fddm_grad_sumsq(const long* chunk_tensor, const long* chunk_start, 
                              long nchunks, float* total, void* hs) {
   if (nchunks <= 0) return 0;
   MTTable t{chunk_tensor, chunk_start, numel, nullptr, g, nullptr, nullptr, nullptr, nullptr};
-  hipLaunchKernelGGL(sumsq_kernel, dim3((unsigned)nchunks), dim3(256), 0, (hipStream_t)hs, t, total);
+  hipLaunchKernelGGL(sumsq_kernel, dim3((unsigned)nchunks), dim3(1024), 0, (hipStream_t)hs, t, total);
   return (int)hipGetLastError();
 }
 
