@@ -85,6 +85,25 @@ def _free_port() -> int:
         return s_.getsockname()[1]
 
 
+def visible_gpus() -> int:
+    """GPUs this process could use, counted without initialising HIP (the parent of `--gpus N` only launches the
+    ranks): the KFD topology's GPU nodes (simd_count > 0), restricted by HIP/ROCR/CUDA_VISIBLE_DEVICES."""
+    import glob
+    n = 0
+    for f in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties"):
+        try:
+            props = dict(line.split() for line in open(f) if len(line.split()) == 2)
+        except OSError:
+            continue
+        if int(props.get("simd_count", "0")) > 0:
+            n += 1
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip() != ""]))
+    return n
+
+
 def launch_ranks(n: int) -> int:
     """`--gpus N` without a launcher: run this script under torch.distributed.run with N local ranks (one per
     GPU) as a child process and return its exit status. Nothing here initialises the GPU."""
@@ -449,8 +468,8 @@ def main():
     # the driver's multi-GPU runs use the default: RCCL ("nccl"), one GPU per rank
     backend = os.environ.get("FDDM_DIST_BACKEND", "nccl")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        if backend == "nccl" and not args.dry_run and torch.cuda.device_count() < args.gpus:
-            sys.exit(f"bench.py: --gpus {args.gpus} but only {torch.cuda.device_count()} GPU(s) visible")
+        if backend == "nccl" and not args.dry_run and visible_gpus() < args.gpus:
+            sys.exit(f"bench.py: --gpus {args.gpus} but only {visible_gpus()} GPU(s) visible")
         sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -501,11 +520,13 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+    T_.ALLREDUCE_TAIL = [] if world > 1 else None   # DP: end of backward -> all gradient slices reduced
     t0 = time.perf_counter()
     with rt.probing(["wavlm.conv1"]) as probes:   # HIP events around the dominant launch, on its stream
         gs, avg_loss = T_.train_one_epoch(enc, dec, sp, te, tp, sch, loader_t, opt, device, cfg, gs, None, 1, False)
     host_s = T_.LAST_ENQUEUE_DONE - t0     # host enqueue time of the K steps (before the epoch's closing loss read)
     torch.cuda.synchronize()
+    tail_ev, T_.ALLREDUCE_TAIL = T_.ALLREDUCE_TAIL, None
     el = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
@@ -572,6 +593,11 @@ def main():
             "avg_loss": round(avg_loss, 4),
             "cpu_baseline": cpu,
         }
+        if tail_ev:
+            # the part of the gradient all-reduce that outlasts the backward (DESIGN §5's overlap), per step
+            tl = [a.elapsed_time(b) for a, b in tail_ev]
+            out["allreduce_tail_ms"] = {"avg": round(sum(tl) / len(tl), 3), "max": round(max(tl), 3),
+                                        "steps": len(tl)}
         if checks is not None:
             out["param_checksums"] = checks
         print(json.dumps(out), flush=True)

@@ -1,6 +1,7 @@
 // Fused clip_grad_norm_(5.0) + AdamW over all trainable tensors in two launches (train.py:411-423):
 //   1) sum of squares of every gradient (multi-tensor, chunked) -> one fp32 accumulator
-//   2) per element: g' = g * min(1, max_norm / (sqrt(total) + 1e-6));
+//   2) per element: g' = s g * min(1, max_norm / (s sqrt(total) + 1e-6)), s = grad_scale (1/W under data
+//      parallelism: the ranks' gradient all-reduce leaves SUMS, the 1/W average is folded in here);
 //      p *= (1 - lr*wd); m = lerp(m, g', 1-b1); v = b2 v + (1-b2) g'^2;
 //      p -= (lr/bc1) * m / (sqrt(v)/sqrt(bc2) + eps)          (torch.optim.AdamW single-tensor form)
 //      and optionally a bf16 copy of p for the next forward's MFMA operands.
@@ -69,12 +70,12 @@ __global__ void __launch_bounds__(1024) sumsq_kernel(MTTable t, float* total) {
 }
 
 template <bool ZG>
-__global__ void __launch_bounds__(256) adamw_kernel(MTTable t, const float* total, float max_norm, float lr, float lr_wd,
-                                                    float b1, float b2, float eps) {
+__global__ void __launch_bounds__(256) adamw_kernel(MTTable t, const float* total, float gscale, float max_norm, float lr,
+                                                    float lr_wd, float b1, float b2, float eps) {
   const long ci = blockIdx.x;
   const long ti = t.chunk_tensor[ci], s0 = t.chunk_start[ci];
   const long n = min(MT_CHUNK, t.numel[ti] - s0);
-  float coef = 1.f;
+  float coef = gscale;
   if (total) {
     if (!isfinite(total[0])) {  // non-finite gradients: skip the step (GradScaler semantics)
       if constexpr (ZG) {       // ... but still leave the gradients zeroed for the next step
@@ -83,10 +84,7 @@ __global__ void __launch_bounds__(256) adamw_kernel(MTTable t, const float* tota
       }
       return;
     }
-    if (max_norm > 0.f) {
-      coef = max_norm / (sqrtf(total[0]) + 1e-6f);
-      coef = fminf(coef, 1.f);
-    }
+    if (max_norm > 0.f) coef = gscale * fminf(max_norm / (gscale * sqrtf(total[0]) + 1e-6f), 1.f);
   }
   // bias corrections of this step (torch: step_size = lr / (1 - b1^step), bc2_sqrt = sqrt(1 - b2^step), in double)
   const double stp = (double)t.step[ti][0] + 1.0;
@@ -187,15 +185,15 @@ FDDM_API int fddm_grad_sumsq(const long* chunk_tensor, const long* chunk_start, 
 FDDM_API int fddm_adamw(const long* chunk_tensor, const long* chunk_start, const long* numel, float* const* p,
                         const float* const* g, float* const* m, float* const* v, bf16_t* const* pbf, float* const* step,
                         long ntensors, long nchunks, const float* total, float max_norm, float lr, float lr_wd, float b1,
-                        float b2, float eps, int* skipped, int zero_g, void* hs) {
+                        float b2, float eps, int* skipped, int zero_g, float grad_scale, void* hs) {
   if (nchunks <= 0) return 0;
   MTTable t{chunk_tensor, chunk_start, numel, p, g, m, v, pbf, step};
   if (zero_g)
-    hipLaunchKernelGGL(adamw_kernel<true>, dim3((unsigned)nchunks), dim3(256), 0, (hipStream_t)hs, t, total, max_norm, lr,
-                       lr_wd, b1, b2, eps);
+    hipLaunchKernelGGL(adamw_kernel<true>, dim3((unsigned)nchunks), dim3(256), 0, (hipStream_t)hs, t, total, grad_scale,
+                       max_norm, lr, lr_wd, b1, b2, eps);
   else
-    hipLaunchKernelGGL(adamw_kernel<false>, dim3((unsigned)nchunks), dim3(256), 0, (hipStream_t)hs, t, total, max_norm,
-                       lr, lr_wd, b1, b2, eps);
+    hipLaunchKernelGGL(adamw_kernel<false>, dim3((unsigned)nchunks), dim3(256), 0, (hipStream_t)hs, t, total, grad_scale,
+                       max_norm, lr, lr_wd, b1, b2, eps);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(adamw_step_kernel, dim3(1), dim3(256), 0, (hipStream_t)hs, step, ntensors, total, skipped);

@@ -59,13 +59,16 @@ class OverlapReducer:
         self.works.append((dist.all_reduce(sl, op=dist.ReduceOp.SUM, async_op=True), sl))
         self.launched = hi
 
-    def finish(self):
+    def finish(self, average: bool = True):
+        """Launch the tail slices and make the compute stream wait for every slice. average=False leaves the
+        ranks' SUM in the arena (the fused AdamW folds 1/W into its read, FusedAdamW.clip_and_step(grad_scale))."""
         n = self.arena.offs[-1]
         while self.launched < n:
             self._launch(min(n, self.launched + self.bucket))
         for w, sl in self.works:
             w.wait()
-            sl.mul_(1.0 / self.W)
+            if average:
+                sl.mul_(1.0 / self.W)
         self.reset()
 
 
@@ -115,14 +118,17 @@ def broadcast_params(tensors, src: int = 0, bucket_bytes: int = BUCKET_BYTES) ->
 
 
 @torch.no_grad()
-def allreduce_grads(params, bucket_bytes: int = BUCKET_BYTES) -> None:
+def allreduce_grads(params, bucket_bytes: int = BUCKET_BYTES, average: bool = True) -> None:
+    """All-reduce the gradients of `params` over the ranks. average=True leaves the mean (torch DDP semantics);
+    average=False leaves the SUM, for a consumer that applies 1/W itself (the fused AdamW's grad_scale), which saves
+    a pass over every gradient."""
     W = world()
     if W <= 1:
         return
     params = list(params)
     arena = next((a for a in (getattr(p, "_fddm_arena", None) for p in params) if a is not None), None)
     if arena is not None and getattr(arena, "reducer", None) is not None:
-        arena.reducer.finish()     # slices already in flight since backward; launch the tail, wait
+        arena.reducer.finish(average)     # slices already in flight since backward; launch the tail, wait
         inside = set(id(p) for p in arena.params)
         params = [p for p in params if id(p) not in inside]
     elif arena is not None and all(p.grad is not None and p.grad.data_ptr() == v.data_ptr()
@@ -133,7 +139,8 @@ def allreduce_grads(params, bucket_bytes: int = BUCKET_BYTES) -> None:
         for s0 in range(0, flat.numel(), step):
             sl = flat[s0:s0 + step]
             dist.all_reduce(sl, op=dist.ReduceOp.SUM)
-            sl.mul_(1.0 / W)
+            if average:
+                sl.mul_(1.0 / W)
         inside = set(id(p) for p in arena.params)
         params = [p for p in params if id(p) not in inside]
     grads = [p.grad for p in params if p.grad is not None]
@@ -144,7 +151,8 @@ def allreduce_grads(params, bucket_bytes: int = BUCKET_BYTES) -> None:
             return
         flat = torch.cat([g.reshape(-1) for g in bk])
         dist.all_reduce(flat, op=dist.ReduceOp.SUM)
-        flat.mul_(1.0 / W)
+        if average:
+            flat.mul_(1.0 / W)
         off = 0
         for g in bk:
             n = g.numel()

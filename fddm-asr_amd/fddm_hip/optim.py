@@ -126,10 +126,12 @@ class FusedAdamW(torch.optim.Optimizer):
         return self._skipped
 
     @torch.no_grad()
-    def clip_and_step(self, max_norm: float | None = None, zero_grads: bool = False):
+    def clip_and_step(self, max_norm: float | None = None, zero_grads: bool = False, grad_scale: float = 1.0):
         """clip_grad_norm_(all params with grads, max_norm) followed by AdamW.step(); returns the
         (device) total gradient norm. zero_grads: the step also zeroes every gradient it reads (the train loop's
-        next zero_grad then has no arena fill to do; .grad reads as zero after the call)."""
+        next zero_grad then has no arena fill to do; .grad reads as zero after the call). grad_scale: every gradient
+        is multiplied by it before the clip and the update (data parallelism: the all-reduce leaves the ranks' sum,
+        grad_scale = 1/W averages it inside the kernel instead of a pass over the gradients)."""
         groups = []
         for group in self.param_groups:
             plist = [p for p in group["params"] if p.grad is not None]
@@ -156,11 +158,16 @@ class FusedAdamW(torch.optim.Optimizer):
                  tab["g"].data_ptr(), tab["m"].data_ptr(), tab["v"].data_ptr(), tab["b"].data_ptr(), tab["s"].data_ptr(),
                  tab["nt"], tab["n"], total.data_ptr(), float(max_norm or 0.0), float(group["lr"]),
                  float(group["lr"] * group["weight_decay"]), float(b1), float(b2), float(group["eps"]),
-                 self._skipped.data_ptr() if gi == 0 else 0, int(bool(zero_grads)), stream())   # skip counted once
+                 self._skipped.data_ptr() if gi == 0 else 0, int(bool(zero_grads)), float(grad_scale),
+                 stream())   # skip counted once
         if zero_grads and self.arena is not None:
-            self.arena.clean = all(p.grad is not None for p in self.arena.params)   # every arena slot was in a table
+            # every arena slot was in a table AND each .grad is still the arena view the kernel just zeroed (a grad
+            # rebound above or by user code leaves its arena slot holding this step's values: zero_grad must fill)
+            a = self.arena
+            self.arena.clean = all(p.grad is not None and p.grad.data_ptr() == v.data_ptr()
+                                   for p, v in zip(a.params, a.views))
         self.last_total_sq = total
-        return total.sqrt()
+        return total.sqrt() * grad_scale if grad_scale != 1.0 else total.sqrt()
 
     @torch.no_grad()
     def step(self, closure=None):

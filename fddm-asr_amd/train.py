@@ -178,6 +178,20 @@ def _encoded(encoder, loader, device, optimizer):
 
 
 LAST_ENQUEUE_DONE = 0.0
+# DP all-reduce tail (bench.py --gpus N): HIP events on the compute stream at the end of backward and after
+# allreduce_grads (the stream has waited for every gradient slice); ALLREDUCE_TAIL collects the event pairs
+ALLREDUCE_TAIL: list | None = None
+
+
+def _mark_allreduce_tail(start=None):
+    """Records the tail probe's events when bench.py enabled it (ALLREDUCE_TAIL is a list) and the run is DP."""
+    if ALLREDUCE_TAIL is None or fdist.world() <= 1:
+        return None
+    ev = torch.cuda.Event(enable_timing=True)
+    ev.record()
+    if start is not None:
+        ALLREDUCE_TAIL.append((start, ev))
+    return ev
 _ENC_STREAMS: dict = {}
 _ENC_GRAPHS = weakref.WeakKeyDictionary()     # encoder -> GraphedEncoder (released with the encoder)
 
@@ -261,10 +275,14 @@ def train_one_epoch(encoder, decoder, s_proj, t_embed, t_proj, scheduler, loader
             scaler.update()
         else:
             loss.backward()
-            fdist.allreduce_grads(trainable)
-            if hasattr(optimizer, "clip_and_step"):
+            fused = hasattr(optimizer, "clip_and_step")
+            # DP: the fused AdamW averages the all-reduced SUM itself (grad_scale = 1/W, no pass over the gradients)
+            t_bwd = _mark_allreduce_tail()
+            fdist.allreduce_grads(trainable, average=not fused)
+            _mark_allreduce_tail(t_bwd)
+            if fused:
                 # the step zeroes the gradients it reads (the next zero_grad's 156 MB arena fill folded into AdamW)
-                optimizer.clip_and_step(max_norm=5.0, zero_grads=True)
+                optimizer.clip_and_step(max_norm=5.0, zero_grads=True, grad_scale=1.0 / fdist.world())
             else:
                 torch.nn.utils.clip_grad_norm_([p for p in trainable if p.grad is not None], max_norm=5.0)
                 optimizer.step()

@@ -182,13 +182,16 @@ int fddm_lfd_std_bwd_apply(int zt_dtype, const float* dzt, const void* zt, const
  *      max_norm > 0 clips by the gradient norm sqrt(*total); a non-finite *total skips the whole step (the
  *      reference's GradScaler skip, train.py:401-413) and increments *skipped (optional). zero_g != 0: every
  *      gradient element is set to 0 in the same pass, applied or skipped (the next step's zero_grad of the grad
- *      arena, folded into the optimizer's read of it). */
+ *      arena, folded into the optimizer's read of it). grad_scale multiplies every gradient before the clip and the
+ *      update (1 normally; 1/W under data parallelism, where the gradient all-reduce leaves the ranks' SUM and the
+ *      average is folded in here instead of a separate pass over the gradients). */
 int fddm_grad_sumsq(const long* chunk_tensor, const long* chunk_start, const long* numel, const float* const* g,
                     long nchunks, float* total, void* hip_stream);
 int fddm_adamw(const long* chunk_tensor, const long* chunk_start, const long* numel, float* const* p,
                const float* const* g, float* const* m, float* const* v, unsigned short* const* pbf,
                float* const* step, long ntensors, long nchunks, const float* total, float max_norm, float lr,
-               float lr_wd, float b1, float b2, float eps, int* skipped, int zero_g, void* hip_stream);
+               float lr_wd, float b1, float b2, float eps, int* skipped, int zero_g, float grad_scale,
+               void* hip_stream);
 
 /* ---- small per-batch ops (rows = the batch, fp32): the decoder's conditioning path and the KL reduction.
  *      rows_mean: out[b][j] = mean_s x[b][s][j] — the pooled condition of FiLM (models/denoise_decoder.py:185).

@@ -74,7 +74,7 @@ def _overlap_worker(rank, world, port, q):
                 p.grad.add_(torch.randn(p.shape, generator=g))
                 rt.grads_ready([p])
                 inflight.append(len(red.works))
-            fdist.allreduce_grads(params)
+            fdist.allreduce_grads(params, average=(step == 0))     # step 1: the SUM (fused AdamW applies 1/W)
             q.put((rank, step, [p.grad.numpy().copy() for p in order], max(inflight)))   # by value
     finally:
         dist.destroy_process_group()
@@ -82,7 +82,8 @@ def _overlap_worker(rank, world, port, q):
 
 def test_overlap_reducer_gloo_world2():
     """Arena laid out in backward order; slices all-reduced asynchronously as soon as a bucket's worth of
-    slots is final (fddm_hip.dist.OverlapReducer), the tail at allreduce_grads; two steps (reset between)."""
+    slots is final (fddm_hip.dist.OverlapReducer), the tail at allreduce_grads; two steps (reset between), the
+    second leaving the ranks' sum (average=False, the fused AdamW's grad_scale path)."""
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -102,7 +103,7 @@ def test_overlap_reducer_gloo_world2():
     for step in range(2):
         for i, s in enumerate(order_shapes):
             exp = sum(torch.randn(s, generator=torch.Generator().manual_seed(1000 * step + 100 * r + i))
-                      for r in range(world)) / world
+                      for r in range(world)) / (world if step == 0 else 1)
             for r in range(world):
                 torch.testing.assert_close(torch.from_numpy(got[(r, step)][i]), exp, rtol=1e-6, atol=1e-6)
 

@@ -1,4 +1,5 @@
-"""Parity of the benchmark's own path (bench.py at C2, BASELINE.json configs[1]) at the benchmark's batch.
+"""Parity of the benchmark's own path (bench.py at C2 = BASELINE.json configs[1], and at C4 = configs[3] per GPU) at
+the benchmark's batch.
 
 `bench.build()` builds the models exactly as the timed run does: WavLM-base encoder (random init) + 6-layer
 d_model 512 / 8 heads / ff 2048 decoder, V = 8000, T = 200, dropout 0.1, bf16, fused AdamW. Two teacher-forced
@@ -8,6 +9,11 @@ FF1 (GELU + dropout epilogue), the vocabulary head and the fused cross-attention
 on their CU caps under HIP-graph replay on the side stream (both graph slots), the decoder attention kernels at
 their benchmark grids. The tests in tests/test_gpu_step_configs.py run the same geometry at B = 2, where those
 GEMMs fall to gemm128.
+
+C4 (`bench.py --config c4`): 12-layer d_model 768 / 12 heads decoder, L = 512 > S = 499 (the repeat branch of the
+S -> L alignment, reference train.py:382-387), B = 16. At this batch the d768-wide GEMMs have 96 tiles of 256^2 and
+run on gemm256 (`prefer_256` from 64 tiles), and the L = 512 attention kernels (fwd3 with K / V resident, dq2 / dkv2
+streamed backward) run at their full grid; the encoder's hidden width equals d_model, so encoder.proj is the identity.
 
 The CPU oracle (oracle/fddm_oracle.py: oracle_train_step, decoder dropout under the RNG contract) is run twice per
 step's evidence:
@@ -38,19 +44,23 @@ def rel(a, b):
     return float((a - b).norm() / b.norm().clamp_min(1e-300))
 
 
-def _args():
-    return SimpleNamespace(batch=32, seconds=10.0, seq_len=256, layers=6, d_model=512, heads=8, precision="bf16")
+CONFIGS = {"c2": dict(batch=32, seq_len=256, layers=6, d_model=512, heads=8),
+           "c4": dict(batch=16, seq_len=512, layers=12, d_model=768, heads=12)}
 
 
-@pytest.fixture(scope="module")
-def bench_run():
+def _args(name):
+    return SimpleNamespace(seconds=10.0, precision="bf16", config=name, **CONFIGS[name])
+
+
+@pytest.fixture(scope="module", params=sorted(CONFIGS))
+def bench_run(request):
     import bench
     import train as T_
     from fddm_hip import functions as FN
     from fddm_hip import runtime as rt
     from models.denoise_decoder import DecoderBlock
 
-    args = _args()
+    args = _args(request.param)
     B, L, V, Tn = args.batch, args.seq_len, 8000, 200
     old_prec = rt.precision()
     torch.manual_seed(1337)
@@ -160,7 +170,14 @@ def bench_run():
         r.pop("c")
         ref.append(r)
     assert ref[0]["lfd"] is None and ref[1]["lfd"] is not None
-    return SimpleNamespace(rec=rec, ref=ref, c_ref2=c_ref2, args=args)
+    if args.seq_len > rec["c"][0].shape[1]:
+        assert args.config == "c4"     # C4 takes the S < L repeat branch of the alignment (train.py:382-387)
+    return SimpleNamespace(rec=rec, ref=ref, c_ref2=c_ref2, args=args, tol=TOL[args.config])
+
+
+# tolerances per config (about 2x the measured worst; the measured values are in the comments of each test)
+TOL = {"c2": dict(kl=2e-4, lfd=1e-3, logits=1e-2, dlogits=5e-3, dx=1e-2, gnorm=2e-2, grad=(1.2e-2, 3e-2)),
+       "c4": dict(kl=2e-4, lfd=1e-3, logits=1e-2, dlogits=5e-3, dx=1e-2, gnorm=2e-2, grad=(2e-2, 4e-2))}
 
 
 def test_bench_encoder_output_matches_oracle(bench_run):
@@ -182,10 +199,10 @@ def test_bench_step_values_match_oracle(bench_run):
     for i in range(2):
         e = abs(R.rec["kl"][i] - R.ref[i]["kl"]) / abs(R.ref[i]["kl"])
         print(f"KL step {i}: {R.rec['kl'][i]:.6f} vs {R.ref[i]['kl']:.6f} (rel {e:.2e})")
-        assert e < 2e-4          # measured 7e-7 / 9e-6
+        assert e < R.tol["kl"]          # measured C2 7e-7 / 9e-6
     e = abs(R.rec["lfd"] - R.ref[1]["lfd"]) / abs(R.ref[1]["lfd"])
     print(f"L_fd: {R.rec['lfd']:.6f} vs {R.ref[1]['lfd']:.6f} (rel {e:.2e})")
-    assert e < 1e-3
+    assert e < R.tol["lfd"]
 
 
 def test_bench_step_error_budget(bench_run):
@@ -200,7 +217,7 @@ def test_bench_step_error_budget(bench_run):
         dxs = [rel(R.rec["dx"][(i, k)].view_as(R.ref[i]["dx"][k]), R.ref[i]["dx"][k]) for k in range(R.args.layers)]
         print(f"step {i}: logits {el:.3e}  dlogits {ed:.3e}  dX per block " + " ".join(f"{v:.3e}" for v in dxs))
         # measured (both steps): logits <= 4.0e-3, dlogits <= 2.2e-3, dX <= 3.8e-3
-        assert el < 1e-2 and ed < 5e-3 and max(dxs) < 1e-2, (el, ed, dxs)
+        assert el < R.tol["logits"] and ed < R.tol["dlogits"] and max(dxs) < R.tol["dx"], (el, ed, dxs)
         g, r = R.rec["grads"][i], R.ref[i]["grads"]
         assert g.keys() == r.keys()
         assert {n for n in g if g[n] is None} == {n for n in r if r[n] is None}, f"step {i}: None grads"
@@ -216,5 +233,5 @@ def test_bench_step_error_budget(bench_run):
         print(f"step {i}: global grad norm {Gg:.6e} vs {G:.6e}; worst grad rel err " +
               ", ".join(f"{n} {v:.2e}" for n, v in worst))
         # measured: global norm 2e-4 / 8.5e-3; worst parameter 5.4e-3 (KL step), 1.4e-2 (L_fd step: projectors)
-        assert abs(Gg - G) <= 2e-2 * G
-        assert worst[0][1] <= (1.2e-2, 3e-2)[i], worst
+        assert abs(Gg - G) <= R.tol["gnorm"] * G
+        assert worst[0][1] <= R.tol["grad"][i], worst

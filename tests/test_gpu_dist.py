@@ -291,8 +291,9 @@ def _c2_dp_grads(rank, world):
         grads = []
         inner = opt.clip_and_step
 
-        def snap(*a, **k):
-            grads.append({n: (None if p.grad is None else p.grad.detach().cpu().clone()) for n, p in named})
+        def snap(*a, **k):      # the averaged gradients: the DP step leaves the SUM, AdamW applies grad_scale = 1/W
+            gs_ = k.get("grad_scale", 1.0)
+            grads.append({n: (None if p.grad is None else (p.grad.detach() * gs_).cpu()) for n, p in named})
             return inner(*a, **k)
 
         opt.clip_and_step = snap
