@@ -177,7 +177,10 @@ def bench_run(request):
 
 # tolerances per config (about 2x the measured worst; the measured values are in the comments of each test)
 TOL = {"c2": dict(kl=2e-4, lfd=1e-3, logits=1e-2, dlogits=5e-3, dx=1e-2, gnorm=2e-2, grad=(1.2e-2, 3e-2)),
-       "c4": dict(kl=2e-4, lfd=1e-3, logits=1e-2, dlogits=5e-3, dx=1e-2, gnorm=2e-2, grad=(2e-2, 4e-2))}
+       # C4 measured (B = 16, 12 blocks): logits 4.0e-3, dlogits 2.0e-3, dX <= 7.5e-3 (deepest block, L_fd step), global
+       # norm 7e-5 / 4.1e-3, worst parameter 6.2e-3 (KL step: ff.0.weight) and 2.85e-2 (L_fd step: t_embed.proj.weight;
+       # worst decoder parameter there 9.7e-3), KL 2e-6, L_fd 0
+       "c4": dict(kl=2e-4, lfd=1e-3, logits=1e-2, dlogits=5e-3, dx=1.5e-2, gnorm=2e-2, grad=(1.2e-2, 6e-2))}
 
 
 def test_bench_encoder_output_matches_oracle(bench_run):
