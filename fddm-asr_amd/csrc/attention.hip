@@ -190,6 +190,7 @@ struct AttnArgs {
   uint64_t seed, stream;
   unsigned thr16;
   float drop_scale;
+  int bits_ready;  // host side only: dbits already holds this site's keep bits (fddm_attn_drop_bits)
 };
 
 __device__ __forceinline__ bool key_ok(const AttnArgs& a, int b, int key) {
@@ -1180,6 +1181,342 @@ __global__ void __launch_bounds__(64 * NW, 1) fwd3_kernel(AttnArgs a) {
   ARTIME(15);
 }
 
+// ------------------------------------------------------------------ dropout keep bits (contract v2, producer)
+// The keep bits of one or more attention sites, written ahead of the attention forward (fwd6 reads them; the backward
+// kernels read the same words): word ((bh * ntiles + t) * Lq + q) of site s, bit kk = keep(q, key 64 t + kk) under
+// rng stream stream0 + s * stream_step. One workgroup per (b, h, site) builds that pair's three 4096-entry draw tables
+// in LDS (one splitmix64 per 4 entries), then each thread owns queries and walks their key tiles (coalesced word
+// stores per tile). Bit-identical to the words the table-staging forward (fwd3) records.
+struct DbArgs {
+  uint64_t* out;
+  long site_words;  // words per site
+  int BH, Lq, Lk;
+  uint64_t seed, stream0, stream_step;
+  unsigned thr16;
+};
+
+__global__ void __launch_bounds__(256) dbits_kernel(DbArgs d) {
+  __shared__ __attribute__((aligned(16))) uint64_t tab[3 * ATTN_R / 4];
+  const int bh = blockIdx.x, site = blockIdx.y, tid = threadIdx.x;
+  const uint64_t stream = d.stream0 + (uint64_t)site * d.stream_step;
+  for (int wi = tid; wi < 3 * ATTN_R / 4; wi += 256) {
+    const int tau = wi / (ATTN_R / 4), jw = wi % (ATTN_R / 4);
+    tab[wi] = mix64(d.seed, stream, ATTN_TAB0 + ((uint64_t)bh * 3 + tau) * (ATTN_R / 4) + jw);
+  }
+  __syncthreads();
+  const int ntiles = (d.Lk + 63) / 64;
+  uint64_t* out = d.out + (long)site * d.site_words + (long)bh * ntiles * d.Lq;
+  const unsigned char* tb = (const unsigned char*)tab;
+  for (int q = tid; q < d.Lq; q += 256) {
+    const uint64_t off = mix64(d.seed, stream, ATTN_OFF0 + (uint64_t)bh * d.Lq + q);
+    const unsigned o0 = (unsigned)(off & 0xFFCu), o1 = (unsigned)((off >> 16) & 0xFFCu),
+                   o2 = (unsigned)((off >> 32) & 0xFFCu);
+    for (int t = 0; t < ntiles; ++t) {
+      uint64_t word = 0;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        const unsigned kq = 64 * t + 4 * c;
+        const uint64_t w = *(const uint64_t*)(tb + (((o0 + kq) & (ATTN_R - 1)) << 1)) ^
+                           *(const uint64_t*)(tb + ATTN_R * 2 + (((o1 + kq) & (ATTN_R - 1)) << 1)) ^
+                           *(const uint64_t*)(tb + ATTN_R * 4 + (((o2 + kq) & (ATTN_R - 1)) << 1));
+        unsigned keep = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) keep |= (((unsigned)(w >> (16 * j)) & 0xFFFFu) >= d.thr16 ? 1u : 0u) << j;
+        word |= (uint64_t)keep << (4 * c);
+      }
+      out[(long)t * d.Lq + q] = word;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- fwd (bf16, decoder, streamed ring, v6)
+// The decoder's self- and cross-attention forward (key-padding mask, dropout from precomputed keep bits): fwd5's
+// streamed K / V ring (2 LDS stages filled by LDS-DMA one tile ahead, counted vmcnt + one barrier per tile) with
+// fwd3's tile body, and the dropout keep bits read from the words dbits_kernel wrote (staged in LDS for the
+// workgroup's queries: one ds_read_b64 per tile and query instead of three table lookups, two XORs and four compares
+// per 4 keys). 4 waves x NG query groups of 16 = 64 NG queries per workgroup and 34-38 KB of LDS at Lk <= 512, so
+// three to four workgroups share a CU and one workgroup's K / V loads overlap another's MFMA / softmax work (fwd3 held
+// the whole K / V range of a (b, h) in ~158 KB at Lk = 512: one workgroup per CU, 1.5 rounds of workgroups at C4).
+// Key tiles whose 64 keys are all padding are skipped (neither loaded nor computed).
+// MK: 0 no mask, 1 the ragged last tile only (Lk % 64 != 0, no key-padding mask), 2 key-padding mask on every tile.
+// DM: 0 no dropout, 1 keep bits read from words dbits_kernel wrote, 2 keep bits drawn from the contract's three
+// tables built in LDS (fwd3's scheme) and recorded in dbits for the backward.
+template <int DM, int MK, int NG>
+__global__ void __launch_bounds__(256, NG == 1 ? 4 : 2) fwd6_kernel(AttnArgs a) {
+  constexpr bool MASK = MK != 0, DROP = DM != 0;
+  constexpr int QW = 64 * NG, TB = 64 * 128, RB = 128, NST = 2;
+  extern __shared__ __attribute__((aligned(16))) unsigned char sm6[];
+  const int ntiles = (a.Lk + 63) / 64, LkP = ntiles * 64;
+  unsigned char* kst = sm6;                     // [NST][64 rows][128 B] K, KC image
+  unsigned char* vst = sm6 + NST * TB;          // [NST][64 rows][128 B] V, tr-read image
+  float* mfull = (float*)(sm6 + 2 * NST * TB);  // [LkP] 0 / -inf
+  uint64_t* kbits = (uint64_t*)(mfull + LkP);   // DM 1: [ntiles][QW] keep words of the workgroup's queries
+  unsigned char* dtab = (unsigned char*)(mfull + LkP);  // DM 2: [3][4096] u16 draw tables
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
+            i = lane & 15;
+  int bxi, bh;
+  xcd_tile(bxi, bh);
+  const int b = bh / a.H, h = bh % a.H;
+  const int qbase = bxi * QW;
+  const bf16_t* Qb = (const bf16_t*)a.Q + (long)b * a.Lq * a.sq + h * DH;
+  const bf16_t* Kb = (const bf16_t*)a.K + (long)b * a.Lk * a.sk + h * DH;
+  const bf16_t* Vb = (const bf16_t*)a.V + (long)b * a.Lk * a.sv + h * DH;
+  // ---- ordinary loads first (Q fragments, mask row, keep words); hipcc waits for them before the stream starts
+  int q[NG];
+  bool qv[NG];
+  uint4 qf[NG][2];
+#pragma unroll
+  for (int gq = 0; gq < NG; ++gq) {
+    q[gq] = qbase + w * (16 * NG) + gq * 16 + i;
+    qv[gq] = q[gq] < a.Lq;
+    row_frags<bf16_t>(qf[gq], Qb, a.sq, qv[gq] ? q[gq] : 0, qv[gq], lane);
+  }
+  for (int k = tid; k < LkP; k += 256) mfull[k] = (MASK && !key_ok(a, b, k)) ? -INFINITY : 0.f;
+  if constexpr (DM == 1) {
+    const uint64_t* src = a.dbits + (long)bh * ntiles * a.Lq;
+    for (int e = tid; e < ntiles * QW; e += 256) {
+      const int t = e / QW, qq = e - t * QW;
+      kbits[e] = (qbase + qq < a.Lq) ? src[(long)t * a.Lq + qbase + qq] : 0ull;
+    }
+  }
+  unsigned ooff[NG][3];  // DM 2: the rows' table offsets
+  if constexpr (DM == 2) {
+    for (int wi = tid; wi < 3 * ATTN_R / 4; wi += 256) {
+      const int tau = wi / (ATTN_R / 4), jw = wi % (ATTN_R / 4);
+      *(uint64_t*)(dtab + (size_t)wi * 8) =
+          mix64(a.seed, a.stream, ATTN_TAB0 + ((uint64_t)bh * 3 + tau) * (ATTN_R / 4) + jw);
+    }
+#pragma unroll
+    for (int gq = 0; gq < NG; ++gq) {
+      const uint64_t off = attn_offsets(a, bh, q[gq]);
+#pragma unroll
+      for (int tau = 0; tau < 3; ++tau) ooff[gq][tau] = (unsigned)((off >> (16 * tau)) & 0xFFCu);
+    }
+  }
+  // active key tiles (wave-uniform): with a key-padding mask, tiles whose keys are all padding add exactly nothing
+  unsigned tmask = ntiles >= 32 ? 0xFFFFFFFFu : ((1u << ntiles) - 1u);
+  if (MK == 2) {
+    tmask = 0;
+    for (int t = 0; t < ntiles; ++t)
+      if (__any(key_ok(a, b, 64 * t + lane))) tmask |= 1u << t;
+  }
+#pragma unroll
+  for (int gq = 0; gq < NG; ++gq) {
+    pin16(qf[gq][0]);
+    pin16(qf[gq][1]);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  // ---- K / V stream: wave w fills rows 16w .. 16w+15 of a tile (2 K + 2 V instructions; XOR swizzles on the
+  // per-lane source addresses, as fwd3_kernel)
+  auto fill = [&](int tt, int st) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int R = 16 * w + 8 * u;
+      const int r = 64 * tt + R + (lane >> 3), pch = lane & 7;
+      const int rr = min(r, a.Lk - 1);
+      const int ck = pch ^ ((r >> 1) & 7), cv = pch ^ (((r >> 1) & 3) << 1);
+      dma16_asm(Kb + (long)rr * a.sk + ck * 8, kst + st * TB + R * 128);
+      dma16_asm(Vb + (long)rr * a.sv + cv * 8, vst + st * TB + R * 128);
+    }
+  };
+  unsigned rem = tmask;
+  int tcur = rem ? __builtin_ctz(rem) : -1;
+  if (tcur >= 0) fill(tcur, 0);
+
+  const float sl2 = a.scale * 1.4426950408889634f;  // running max m is kept in raw units, p = 2^(x*sl2 - m*sl2)
+  float m[NG], l[NG];
+  f32x4_t o[NG][4];
+#pragma unroll
+  for (int gq = 0; gq < NG; ++gq) {
+    m[gq] = -INFINITY;
+    l[gq] = 0.f;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) o[gq][d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  }
+  const float th_raw = 8.f / sl2;  // lazy rescale threshold (raw score units), as in fwd2_kernel
+  auto tile = [&](const int t, const int st, auto mc) {
+    constexpr bool MT = decltype(mc)::value;  // this tile adds the mask row
+    const int k0 = t * 64;
+    const unsigned char* kimg = kst + st * TB;
+    const unsigned char* vimg = vst + st * TB;
+    f32x4_t s[NG][4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+#pragma unroll
+      for (int gq = 0; gq < NG; ++gq) s[gq][kb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub) {
+        const uint4 af = *(const uint4*)(kimg + kc_off(RB, kb * 16 + i, sub * 4 + g));
+#pragma unroll
+        for (int gq = 0; gq < NG; ++gq) mma<bf16_t>(s[gq][kb], af, qf[gq][sub]);
+      }
+    }
+    f32x2_t mrow[4][2];
+    if constexpr (MT) {
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        const float4 mv4 = *(const float4*)(&mfull[k0 + kb * 16 + 4 * g]);
+        mrow[kb][0] = f32x2_t{mv4.x, mv4.y};
+        mrow[kb][1] = f32x2_t{mv4.z, mv4.w};
+      }
+    }
+    float p[NG][4][4];
+#pragma unroll
+    for (int gq = 0; gq < NG; ++gq) {
+      uint64_t kw = 0;
+      if constexpr (DM == 1) kw = kbits[t * QW + w * (16 * NG) + gq * 16 + i];
+      if constexpr (DM == 2) {
+        // 4 x 16-bit draws per 4 keys: one aligned 8-byte word from each table, XORed (fwd3_kernel's form)
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) {
+          const int kq = k0 + kb * 16 + 4 * g;
+          const uint64_t wd = *(const uint64_t*)(dtab + (((ooff[gq][0] + kq) & (ATTN_R - 1)) << 1)) ^
+                              *(const uint64_t*)(dtab + ATTN_R * 2 + (((ooff[gq][1] + kq) & (ATTN_R - 1)) << 1)) ^
+                              *(const uint64_t*)(dtab + ATTN_R * 4 + (((ooff[gq][2] + kq) & (ATTN_R - 1)) << 1));
+          unsigned keep = 0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) keep |= (((unsigned)(wd >> (16 * j)) & 0xFFFFu) >= a.thr16 ? 1u : 0u) << j;
+          kw |= (uint64_t)keep << (kb * 16 + 4 * g);
+        }
+      }
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          f32x2_t x = {s[gq][kb][2 * jj], s[gq][kb][2 * jj + 1]};
+          if constexpr (MT) x += mrow[kb][jj];
+          p[gq][kb][2 * jj] = x.x;
+          p[gq][kb][2 * jj + 1] = x.y;
+        }
+        tmax = fmaxf(tmax, fmaxf(fmaxf(p[gq][kb][0], p[gq][kb][1]), fmaxf(p[gq][kb][2], p[gq][kb][3])));
+      }
+      tmax = xmax16(tmax);
+      tmax = xmax32(tmax);
+      if (__any(tmax > m[gq] + th_raw)) {
+        const float mn = fmaxf(m[gq], tmax);
+        const float mref = (mn == -INFINITY) ? 0.f : mn;
+        const float alpha = __builtin_amdgcn_exp2f((m[gq] - mref) * sl2);
+        l[gq] *= alpha;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) o[gq][d] *= alpha;
+        m[gq] = mn;
+      }
+      const float mref = (m[gq] == -INFINITY) ? 0.f : m[gq];
+      const float nbias = -mref * sl2;
+      const f32x2_t sl2v = {sl2, sl2}, nb2 = {nbias, nbias};
+      f32x2_t ls2 = {0.f, 0.f};
+      const unsigned kwh[2] = {(unsigned)kw, (unsigned)(kw >> 32)};
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          const f32x2_t arg = f32x2_t{p[gq][kb][2 * jj], p[gq][kb][2 * jj + 1]} * sl2v + nb2;
+          f32x2_t e = {__builtin_amdgcn_exp2f(arg.x), __builtin_amdgcn_exp2f(arg.y)};
+          ls2 += e;
+          if constexpr (DROP) {
+            // keep bit of key kb*16 + 4g + 2jj (+1) as an all-ones / zero AND mask (v_bfe_i32)
+            const unsigned hw = kwh[kb >> 1];
+            const int pos = (kb & 1) * 16 + 4 * g + 2 * jj;
+            const unsigned m0 = (unsigned)__builtin_amdgcn_sbfe((int)hw, pos, 1);
+            const unsigned m1 = (unsigned)__builtin_amdgcn_sbfe((int)hw, pos + 1, 1);
+            e.x = __uint_as_float(__float_as_uint(e.x) & m0);
+            e.y = __uint_as_float(__float_as_uint(e.y) & m1);
+          }
+          p[gq][kb][2 * jj] = e.x;
+          p[gq][kb][2 * jj + 1] = e.y;
+        }
+      }
+      l[gq] += ls2.x + ls2.y;
+      if constexpr (DM == 2) {
+        if (a.dbits) {  // the 4 lanes of a query hold disjoint key nibbles: OR them into the tile's 64-bit word
+          unsigned lo = (unsigned)kw, hi = (unsigned)(kw >> 32);
+          lo = xor16(lo);
+          hi = xor16(hi);
+          lo = xor32(lo);
+          hi = xor32(hi);
+          if (g == 0 && qv[gq]) a.dbits[((long)bh * ntiles + t) * a.Lq + q[gq]] = ((uint64_t)hi << 32) | lo;
+        }
+      }
+    }
+    {
+      const int qq = i >> 2, pp = i & 3;
+      typedef __attribute__((address_space(3))) s16x4_t* lp;
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        uint4 bq[NG];
+#pragma unroll
+        for (int gq = 0; gq < NG; ++gq) {
+          bq[gq].x = pk(p[gq][2 * ss][0], p[gq][2 * ss][1]);
+          bq[gq].y = pk(p[gq][2 * ss][2], p[gq][2 * ss][3]);
+          bq[gq].z = pk(p[gq][2 * ss + 1][0], p[gq][2 * ss + 1][1]);
+          bq[gq].w = pk(p[gq][2 * ss + 1][2], p[gq][2 * ss + 1][3]);
+        }
+        const int k1 = 32 * ss + 4 * g + qq, k2 = k1 + 16;
+#pragma unroll
+        for (int db = 0; db < 4; ++db) {
+          const int u = db * 4 + pp;
+          const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(vimg + k1 * 128 + ((u ^ hatt(k1)) << 3)));
+          const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(vimg + k2 * 128 + ((u ^ hatt(k2)) << 3)));
+          const uint4 af = join_tr(lo, hi);
+#pragma unroll
+          for (int gq = 0; gq < NG; ++gq) mma<bf16_t>(o[gq][db], af, bq[gq]);
+        }
+      }
+    }
+  };
+  // one active tile per iteration: wait for its pieces (the only DMA in flight), barrier (every wave's pieces landed
+  // and every wave finished the previous tile, whose stage the next fill overwrites), fill the next active tile, run
+  int st = 0;
+  auto arrive = [&]() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    rem &= rem - 1;
+    const int tnext = rem ? __builtin_ctz(rem) : -1;
+    if (tnext >= 0) fill(tnext, st ^ 1);
+    return tnext;
+  };
+  if constexpr (MK == 1) {  // every tile active; the mask row only on the ragged last one
+    while (tcur >= 0 && tcur < ntiles - 1) {
+      const int tnext = arrive();
+      tile(tcur, st, std::false_type{});
+      tcur = tnext;
+      st ^= 1;
+    }
+    if (tcur >= 0) {
+      arrive();
+      tile(tcur, st, std::true_type{});
+    }
+  } else {
+    while (tcur >= 0) {
+      const int tnext = arrive();
+      tile(tcur, st, std::integral_constant<bool, MK == 2>{});
+      tcur = tnext;
+      st ^= 1;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may land after the workgroup retires
+#pragma unroll
+  for (int gq = 0; gq < NG; ++gq) {
+    float lt = l[gq];
+    lt = xsum16(lt);
+    lt = xsum32(lt);
+    if (!qv[gq]) continue;
+    const float inv = (lt > 0.f) ? (DROP ? a.drop_scale : 1.f) / lt : NAN;
+    bf16_t* Ob = (bf16_t*)a.Out + ((long)b * a.Lq + q[gq]) * a.so + h * DH;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      uint2 u2;
+      u2.x = pk(o[gq][d][0] * inv, o[gq][d][1] * inv);
+      u2.y = pk(o[gq][d][2] * inv, o[gq][d][3] * inv);
+      *(uint2*)(Ob + d * 16 + 4 * g) = u2;
+    }
+    if (a.lse && g == 0)
+      a.lse[(long)bh * a.Lq + q[gq]] = (lt > 0.f) ? (m[gq] * sl2 + __log2f(lt)) * 0.69314718055994531f : NAN;
+  }
+}
+
 // ------------------------------------------------------------------------------------------- dQ
 // query-owned: recompute S^T, dP^T = V dO^T; dS = P (dP - delta); dQ^T = K^T dS^T
 template <typename T>
@@ -2067,6 +2404,368 @@ __global__ void __launch_bounds__(1024, 1) dkv3_kernel(AttnArgs a) {
   ARTIME(15);
 }
 
+// --------------------------------------------------------------------- bwd (bf16, streamed ring, v4)
+// dq3 / dkv3's tile bodies (one KC image per operand serving the row reads and, through kc_tr_off, the transposed
+// reads; 16 rows per wave) with the streamed operand pair in a 2-stage LDS ring filled by LDS-DMA one tile ahead
+// (fwd6's scheme: inline-asm DMA, vmcnt(0) + one barrier per tile, no other vector-memory instruction in the loop)
+// instead of resident in LDS: 4 waves x 16 rows = 64 rows per workgroup and 36-40 KB of LDS at L <= 512, so four
+// workgroups share a CU (the resident v3 kernels need one 133-148 KB workgroup per CU at L = 512; the register-staged
+// v2 kernels run two 2-group workgroups at 2 waves per SIMD). The side data (mask row, LSE / delta rows, the
+// forward's keep words) is staged in LDS once. DM: 0 no dropout, 2 the recorded keep bits.
+template <int DM, bool MASK>
+__global__ void __launch_bounds__(256, 4) dq4_kernel(AttnArgs a) {
+  static_assert(DM == 0 || DM == 2, "dq4: no-dropout or recorded keep bits");
+  constexpr int QW = 64, TB = 64 * 128;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smq4[];
+  const int ntiles = (a.Lk + 63) / 64, LkP = ntiles * 64;
+  unsigned char* kst = smq4;                      // [2][64 rows][128 B] K, KC image
+  unsigned char* vst = smq4 + 2 * TB;             // [2][64 rows][128 B] V, KC image
+  float* mfull = (float*)(smq4 + 4 * TB);         // [LkP] 0 / -inf
+  uint64_t* kw_s = (uint64_t*)(mfull + LkP);      // [ntiles][QW] keep words of the workgroup's queries (DM 2)
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
+            i = lane & 15;
+  int bxi, bh;
+  xcd_tile(bxi, bh);
+  const int b = bh / a.H, h = bh % a.H;
+  const int qbase = bxi * QW;
+  const bf16_t* Qb = (const bf16_t*)a.Q + (long)b * a.Lq * a.sq + h * DH;
+  const bf16_t* Ob = (const bf16_t*)a.O + (long)b * a.Lq * a.so + h * DH;
+  const bf16_t* dOb = (const bf16_t*)a.dO + (long)b * a.Lq * a.sdo + h * DH;
+  const bf16_t* Kb = (const bf16_t*)a.K + (long)b * a.Lk * a.sk + h * DH;
+  const bf16_t* Vb = (const bf16_t*)a.V + (long)b * a.Lk * a.sv + h * DH;
+  const float sl2 = a.scale * 1.4426950408889634f;
+  const int q = qbase + w * 16 + i;
+  const bool qv = q < a.Lq;
+  const int qq0 = qv ? q : 0;
+  uint4 qf[2], dof[2], of[2];
+  row_frags<bf16_t>(qf, Qb, a.sq, qq0, qv, lane);
+  row_frags<bf16_t>(dof, dOb, a.sdo, qq0, qv, lane);
+  row_frags<bf16_t>(of, Ob, a.so, qq0, qv, lane);
+  for (int k = tid; k < LkP; k += 256) mfull[k] = (MASK && !key_ok(a, b, k)) ? -INFINITY : 0.f;
+  if constexpr (DM == 2) {
+    const uint64_t* src = a.dbits + (long)bh * ntiles * a.Lq;
+    for (int e = tid; e < ntiles * QW; e += 256) {
+      const int t = e / QW, qq = e - t * QW;
+      kw_s[e] = (qbase + qq < a.Lq) ? src[(long)t * a.Lq + qbase + qq] : 0ull;
+    }
+  }
+  unsigned tmask = ntiles >= 32 ? 0xFFFFFFFFu : ((1u << ntiles) - 1u);
+  if (MASK && a.key_keep != nullptr) {  // fully padded key tiles skipped (wave-uniform), as in fwd3_kernel
+    tmask = 0;
+    for (int t = 0; t < ntiles; ++t)
+      if (__any(key_ok(a, b, 64 * t + lane))) tmask |= 1u << t;
+  }
+  float dl = 0.f;
+#pragma unroll
+  for (int sb = 0; sb < 2; ++sb) {
+    const bf16_t* x = (const bf16_t*)&dof[sb];
+    const bf16_t* y = (const bf16_t*)&of[sb];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dl += bf2f(x[e]) * bf2f(y[e]);
+  }
+  dl = xsum16(dl);
+  dl = xsum32(dl);
+  const float delta = dl;
+  if (qv && g == 0) a.delta[(long)bh * a.Lq + q] = dl;
+  const float lse2 = qv ? a.lse[(long)bh * a.Lq + q] * 1.4426950408889634f : 0.f;
+  pin16(qf[0]);
+  pin16(qf[1]);
+  pin16(dof[0]);
+  pin16(dof[1]);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  auto fill = [&](int tt, int st) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int R = 16 * w + 8 * u;
+      const int r = 64 * tt + R + (lane >> 3), pch = lane & 7;
+      const int rr = min(r, a.Lk - 1);
+      const int ck = pch ^ ((r >> 1) & 7);
+      dma16_asm(Kb + (long)rr * a.sk + ck * 8, kst + st * TB + R * 128);
+      dma16_asm(Vb + (long)rr * a.sv + ck * 8, vst + st * TB + R * 128);
+    }
+  };
+  unsigned rem = tmask;
+  int tcur = rem ? __builtin_ctz(rem) : -1;
+  if (tcur >= 0) fill(tcur, 0);
+  f32x4_t dq[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) dq[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const f32x2_t sl2v = {sl2, sl2}, dscv = {a.drop_scale, a.drop_scale}, ndl = {-delta, -delta};
+  auto tile = [&](const int t, const int st, auto mc) {
+    constexpr bool MT = decltype(mc)::value;
+    const int k0 = t * 64;
+    const unsigned char* kimg = kst + st * TB;
+    const unsigned char* vimg = vst + st * TB;
+    uint64_t wbits = 0;
+    if constexpr (DM == 2) wbits = kw_s[t * QW + w * 16 + i];
+    f32x4_t sc[4], dp[4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      sc[kb] = dp[kb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub) {
+        const uint4 ak = *(const uint4*)(kimg + kc_off(128, kb * 16 + i, sub * 4 + g));
+        const uint4 av = *(const uint4*)(vimg + kc_off(128, kb * 16 + i, sub * 4 + g));
+        mma<bf16_t>(sc[kb], ak, qf[sub]);
+        mma<bf16_t>(dp[kb], av, dof[sub]);
+      }
+    }
+    float ds[4][4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      unsigned keep = 0xF;
+      if constexpr (DM == 2) keep = (unsigned)(wbits >> (kb * 16 + 4 * g)) & 0xFu;
+      float4 m4 = make_float4(0.f, 0.f, 0.f, 0.f);
+      if constexpr (MT) m4 = *(const float4*)(&mfull[k0 + kb * 16 + 4 * g]);
+      const float mr[4] = {m4.x, m4.y, m4.z, m4.w};
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        f32x2_t off = {-lse2, -lse2};
+        if constexpr (MT) off += f32x2_t{mr[2 * jj], mr[2 * jj + 1]};
+        const f32x2_t arg = f32x2_t{sc[kb][2 * jj], sc[kb][2 * jj + 1]} * sl2v + off;
+        const f32x2_t pr = {__builtin_amdgcn_exp2f(arg.x), __builtin_amdgcn_exp2f(arg.y)};
+        f32x2_t dpv = {dp[kb][2 * jj], dp[kb][2 * jj + 1]};
+        if constexpr (DM == 2) {
+          dpv.x = __int_as_float(__float_as_int(dpv.x) & __builtin_amdgcn_sbfe((int)keep, 2 * jj, 1));
+          dpv.y = __int_as_float(__float_as_int(dpv.y) & __builtin_amdgcn_sbfe((int)keep, 2 * jj + 1, 1));
+          dpv = dpv * dscv + ndl;
+        } else {
+          dpv += ndl;
+        }
+        const f32x2_t d2 = pr * dpv;
+        ds[kb][2 * jj] = d2.x;
+        ds[kb][2 * jj + 1] = d2.y;
+      }
+    }
+    const int qq = i >> 2, pp = i & 3;
+    typedef __attribute__((address_space(3))) s16x4_t* lp;
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) {
+      uint4 bq;
+      bq.x = pk(ds[2 * ss][0], ds[2 * ss][1]);
+      bq.y = pk(ds[2 * ss][2], ds[2 * ss][3]);
+      bq.z = pk(ds[2 * ss + 1][0], ds[2 * ss + 1][1]);
+      bq.w = pk(ds[2 * ss + 1][2], ds[2 * ss + 1][3]);
+      const int k1 = 32 * ss + 4 * g + qq, k2 = k1 + 16;
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        const int u = db * 4 + pp;
+        const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(kimg + kc_tr_off(k1, u)));
+        const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(kimg + kc_tr_off(k2, u)));
+        mma<bf16_t>(dq[db], join_tr(lo, hi), bq);
+      }
+    }
+  };
+  int st = 0;
+  auto arrive = [&]() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    rem &= rem - 1;
+    const int tnext = rem ? __builtin_ctz(rem) : -1;
+    if (tnext >= 0) fill(tnext, st ^ 1);
+    return tnext;
+  };
+  const bool mask_all = MASK && a.key_keep != nullptr;
+  if (!MASK || mask_all) {
+    while (tcur >= 0) {
+      const int tnext = arrive();
+      tile(tcur, st, std::integral_constant<bool, MASK>{});
+      tcur = tnext;
+      st ^= 1;
+    }
+  } else {  // every tile active; the mask row only on the ragged last one
+    while (tcur >= 0 && tcur < ntiles - 1) {
+      const int tnext = arrive();
+      tile(tcur, st, std::false_type{});
+      tcur = tnext;
+      st ^= 1;
+    }
+    if (tcur >= 0) {
+      arrive();
+      tile(tcur, st, std::true_type{});
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may land after the workgroup retires
+  if (qv) {
+    bf16_t* dQb = (bf16_t*)a.dQ + ((long)b * a.Lq + q) * a.sdq + h * DH;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      uint2 u2;
+      u2.x = pk(dq[d][0] * a.scale, dq[d][1] * a.scale);
+      u2.y = pk(dq[d][2] * a.scale, dq[d][3] * a.scale);
+      *(uint2*)(dQb + d * 16 + 4 * g) = u2;
+    }
+  }
+}
+
+// dK / dV, v4: key-owned, 4 waves x 16 keys = one 64-key tile per workgroup; the Q / dO query tiles streamed
+// through the ring; the query rows' LSE / delta and the forward's keep words of this key tile staged in LDS.
+template <int DM>
+__global__ void __launch_bounds__(256, 4) dkv4_kernel(AttnArgs a) {
+  static_assert(DM == 0 || DM == 2, "dkv4: no-dropout or recorded keep bits");
+  constexpr bool DROP = DM != 0;
+  constexpr int TB = 64 * 128;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smk4[];
+  const int nq = (a.Lq + 63) / 64, LqP = nq * 64;
+  const int ntk = (a.Lk + 63) / 64;
+  unsigned char* qst = smk4;                       // [2][64 rows][128 B] Q, KC image
+  unsigned char* ost = smk4 + 2 * TB;              // [2][64 rows][128 B] dO, KC image
+  float* lse_s = (float*)(smk4 + 4 * TB);          // [LqP] lse * log2(e) (+inf past Lq: P = 0)
+  float* del_s = lse_s + LqP;                      // [LqP] delta
+  uint64_t* wb_s = (uint64_t*)(del_s + LqP);       // [LqP] keep words of this key tile (DM 2)
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
+            i = lane & 15;
+  int bxi, bh;
+  xcd_tile(bxi, bh);
+  const int b = bh / a.H, h = bh % a.H;
+  const bf16_t* Qb = (const bf16_t*)a.Q + (long)b * a.Lq * a.sq + h * DH;
+  const bf16_t* dOb = (const bf16_t*)a.dO + (long)b * a.Lq * a.sdo + h * DH;
+  const bf16_t* Kb = (const bf16_t*)a.K + (long)b * a.Lk * a.sk + h * DH;
+  const bf16_t* Vb = (const bf16_t*)a.V + (long)b * a.Lk * a.sv + h * DH;
+  for (int j = tid; j < 2 * LqP; j += 256) {
+    const int qq = j < LqP ? j : j - LqP;
+    float v = j < LqP ? INFINITY : 0.f;
+    if (qq < a.Lq) v = j < LqP ? a.lse[(long)bh * a.Lq + qq] * 1.4426950408889634f : a.delta[(long)bh * a.Lq + qq];
+    (j < LqP ? lse_s : del_s)[qq] = v;
+  }
+  if constexpr (DM == 2) {
+    for (int qq = tid; qq < LqP; qq += 256)
+      wb_s[qq] = (qq < a.Lq && bxi < ntk) ? a.dbits[((long)bh * ntk + bxi) * a.Lq + qq] : 0ull;
+  }
+  const float sl2 = a.scale * 1.4426950408889634f;
+  const int key = bxi * 64 + w * 16 + i;
+  const bool kvld = key < a.Lk;
+  const bool kok = kvld && key_ok(a, b, key);
+  uint4 kf[2], vf[2];
+  row_frags<bf16_t>(kf, Kb, a.sk, kvld ? key : 0, kvld, lane);
+  row_frags<bf16_t>(vf, Vb, a.sv, kvld ? key : 0, kvld, lane);
+  pin16(kf[0]);
+  pin16(kf[1]);
+  pin16(vf[0]);
+  pin16(vf[1]);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  // a workgroup whose 64 keys are all padding writes zeros (epilogue), no query loop
+  const bool any_key = __syncthreads_or(kok);
+  auto fill = [&](int tt, int st) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int R = 16 * w + 8 * u;
+      const int r = 64 * tt + R + (lane >> 3), pch = lane & 7;
+      const int rr = min(r, a.Lq - 1);
+      const int ck = pch ^ ((r >> 1) & 7);
+      dma16_asm(Qb + (long)rr * a.sq + ck * 8, qst + st * TB + R * 128);
+      dma16_asm(dOb + (long)rr * a.sdo + ck * 8, ost + st * TB + R * 128);
+    }
+  };
+  f32x4_t dk[4], dv[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) dk[d] = dv[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int kbit = w * 16 + i;  // key bit within the 64-key tile
+  const f32x2_t sl2v = {sl2, sl2}, dscv = {a.drop_scale, a.drop_scale};
+  const int qq_ = i >> 2, pp = i & 3;
+  typedef __attribute__((address_space(3))) s16x4_t* lp;
+  const int nt = any_key ? nq : 0;
+  if (nt > 0) fill(0, 0);
+  for (int t = 0; t < nt; ++t) {
+    const int st = t & 1, q0 = t * 64;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (t + 1 < nt) fill(t + 1, st ^ 1);
+    const unsigned char* qimg = qst + st * TB;
+    const unsigned char* oimg = ost + st * TB;
+    f32x4_t sc[4], dp[4];
+#pragma unroll
+    for (int qb = 0; qb < 4; ++qb) {
+      sc[qb] = dp[qb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub) {
+        const uint4 aq = *(const uint4*)(qimg + kc_off(128, qb * 16 + i, sub * 4 + g));
+        const uint4 ao = *(const uint4*)(oimg + kc_off(128, qb * 16 + i, sub * 4 + g));
+        mma<bf16_t>(sc[qb], aq, kf[sub]);
+        mma<bf16_t>(dp[qb], ao, vf[sub]);
+      }
+    }
+    float pd[4][4], ds[4][4];
+#pragma unroll
+    for (int qb = 0; qb < 4; ++qb) {
+      const float4 l4 = *(const float4*)(&lse_s[q0 + qb * 16 + 4 * g]);
+      const float4 d4 = *(const float4*)(&del_s[q0 + qb * 16 + 4 * g]);
+      const f32x2_t nl[2] = {f32x2_t{-l4.x, -l4.y}, f32x2_t{-l4.z, -l4.w}};
+      const f32x2_t nd[2] = {f32x2_t{-d4.x, -d4.y}, f32x2_t{-d4.z, -d4.w}};
+      unsigned wq[4] = {0, 0, 0, 0};  // the 32-bit half of each query's keep word holding this key's bit
+      if constexpr (DM == 2) {
+        const unsigned* src = (const unsigned*)&wb_s[q0 + qb * 16 + 4 * g] + (kbit >> 5);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) wq[j] = src[2 * j];
+      }
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const f32x2_t arg = f32x2_t{sc[qb][2 * jj], sc[qb][2 * jj + 1]} * sl2v + nl[jj];
+        const f32x2_t pr = {__builtin_amdgcn_exp2f(arg.x), __builtin_amdgcn_exp2f(arg.y)};
+        f32x2_t dpv = {dp[qb][2 * jj], dp[qb][2 * jj + 1]};
+        f32x2_t pdv = pr;
+        if constexpr (DROP) {
+          const int m0 = __builtin_amdgcn_sbfe((int)wq[2 * jj], kbit & 31, 1);
+          const int m1 = __builtin_amdgcn_sbfe((int)wq[2 * jj + 1], kbit & 31, 1);
+          pdv.x = __int_as_float(__float_as_int(pr.x) & m0);
+          pdv.y = __int_as_float(__float_as_int(pr.y) & m1);
+          dpv.x = __int_as_float(__float_as_int(dpv.x) & m0);
+          dpv.y = __int_as_float(__float_as_int(dpv.y) & m1);
+          dpv = dpv * dscv + nd[jj];
+        } else {
+          dpv += nd[jj];
+        }
+        const f32x2_t d2 = pr * dpv;
+        pd[qb][2 * jj] = pdv.x;
+        pd[qb][2 * jj + 1] = pdv.y;
+        ds[qb][2 * jj] = d2.x;
+        ds[qb][2 * jj + 1] = d2.y;
+      }
+    }
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) {
+      uint4 bp, bs;
+      bp.x = pk(pd[2 * ss][0], pd[2 * ss][1]);
+      bp.y = pk(pd[2 * ss][2], pd[2 * ss][3]);
+      bp.z = pk(pd[2 * ss + 1][0], pd[2 * ss + 1][1]);
+      bp.w = pk(pd[2 * ss + 1][2], pd[2 * ss + 1][3]);
+      bs.x = pk(ds[2 * ss][0], ds[2 * ss][1]);
+      bs.y = pk(ds[2 * ss][2], ds[2 * ss][3]);
+      bs.z = pk(ds[2 * ss + 1][0], ds[2 * ss + 1][1]);
+      bs.w = pk(ds[2 * ss + 1][2], ds[2 * ss + 1][3]);
+      const int k1 = 32 * ss + 4 * g + qq_, k2 = k1 + 16;
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        const int u = db * 4 + pp;
+        const s16x4_t olo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(oimg + kc_tr_off(k1, u)));
+        const s16x4_t ohi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(oimg + kc_tr_off(k2, u)));
+        const s16x4_t qlo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(qimg + kc_tr_off(k1, u)));
+        const s16x4_t qhi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(qimg + kc_tr_off(k2, u)));
+        mma<bf16_t>(dv[db], join_tr(olo, ohi), bp);
+        mma<bf16_t>(dk[db], join_tr(qlo, qhi), bs);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may land after the workgroup retires
+  if (kvld) {
+    bf16_t* dKb = (bf16_t*)a.dK + ((long)b * a.Lk + key) * a.sdk + h * DH;
+    bf16_t* dVb = (bf16_t*)a.dV + ((long)b * a.Lk + key) * a.sdv + h * DH;
+    // masked key: zero gradient (its P was never zeroed); dV carries the dropout scale of P'
+    const float ksc = kok ? a.scale : 0.f, vsc = kok ? (DROP ? a.drop_scale : 1.f) : 0.f;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      uint2 uk, uv;
+      uk.x = pk(kok ? dk[d][0] * ksc : 0.f, kok ? dk[d][1] * ksc : 0.f);
+      uk.y = pk(kok ? dk[d][2] * ksc : 0.f, kok ? dk[d][3] * ksc : 0.f);
+      uv.x = pk(kok ? dv[d][0] * vsc : 0.f, kok ? dv[d][1] * vsc : 0.f);
+      uv.y = pk(kok ? dv[d][2] * vsc : 0.f, kok ? dv[d][3] * vsc : 0.f);
+      *(uint2*)(dKb + d * 16 + 4 * g) = uk;
+      *(uint2*)(dVb + d * 16 + 4 * g) = uv;
+    }
+  }
+}
+
 // dQ, dK, dV of one (b, h) in ONE workgroup when Lq == Lk <= 256 (the decoder's self-attention; round 3): dq3 and
 // dkv3 fused. The K, V, Q and dO rows are staged into four KC images once (LDS-DMA, 128 KB at L = 256) with the LSE
 // rows, the forward's keep words and the key mask; delta = rowsum(dO * O) is formed in registers and shared through
@@ -2382,6 +3081,29 @@ static int run(int which, AttnArgs& a, hipStream_t s) {
       if (!getenv("FDDM_ATTN_V1")) {
         const bool drop = a.thr16 != 0, mask = a.key_keep != nullptr || (a.Lk % 64) != 0;
         const bool rel = a.table != nullptr && (a.gate != nullptr || a.graw != nullptr);
+        // decoder self / cross attention: the streamed-ring forward with precomputed dropout keep bits (fwd6)
+        const bool fwd6_on = !getenv("FDDM_ATTN_FWD6") || atoi(getenv("FDDM_ATTN_FWD6")) != 0;
+        if (fwd6_on && !rel && a.Lk <= 1024) {
+          const int ntiles = (a.Lk + 63) / 64, LkP = ntiles * 64;
+          const int dm = !drop ? 0 : (a.bits_ready && a.dbits) ? 1 : 2;
+          const int ng_env = getenv("FDDM_ATTN_NG6") ? atoi(getenv("FDDM_ATTN_NG6")) : 0;
+          const int ng = ng_env ? ng_env : 2;
+          const int qw = 64 * ng;
+          const size_t lds = (size_t)2 * 2 * 64 * 128 + (size_t)LkP * 4 +
+                             (dm == 1 ? (size_t)ntiles * qw * 8 : dm == 2 ? (size_t)3 * ATTN_R * 2 : 0);
+          dim3 g6((a.Lq + qw - 1) / qw, a.B * a.H);
+          const int mk = a.key_keep != nullptr ? 2 : (a.Lk % 64) != 0 ? 1 : 0;
+#define FWD6(D, M, G) hipLaunchKernelGGL((fwd6_kernel<D, M, G>), g6, dim3(256), lds, s, a)
+#define FWD6G(D, M) do { if (ng == 2) FWD6(D, M, 2); else FWD6(D, M, 1); } while (0)
+#define FWD6M(D) do { if (mk == 2) FWD6G(D, 2); else if (mk == 1) FWD6G(D, 1); else FWD6G(D, 0); } while (0)
+          if (dm == 2) FWD6M(2);
+          else if (dm == 1) FWD6M(1);
+          else FWD6M(0);
+#undef FWD6M
+#undef FWD6G
+#undef FWD6
+          return (int)hipGetLastError();
+        }
         // FDDM_ATTN_NG=1: 64-query workgroups (one 16-query group per wave). Measured at the decoder's
         // Lq = 256 (tools/attn_bench.py): no faster with dropout (24.4 vs 24.0 us), slower without (19.4 vs
         // 15.1 us) — the launch is not short of workgroups; kept as a probe, off by default.
@@ -2474,6 +3196,17 @@ static int run(int which, AttnArgs& a, hipStream_t s) {
         // backward 38.6 -> 35.3 us with dkv3; at the cross-attention's Lk = 499 — 130 KB of LDS, one workgroup per
         // CU — no faster than the streamed kernels, 64.0 vs 62.8 us); FDDM_ATTN_DQ2=1 keeps the streamed kernel
         static const int v3max = getenv("FDDM_ATTN_V3_MAX") ? atoi(getenv("FDDM_ATTN_V3_MAX")) : 256;
+        const bool v4 = !getenv("FDDM_ATTN_BWD4") || atoi(getenv("FDDM_ATTN_BWD4")) != 0;
+        if (v4 && dm != 1 && a.Lk <= 1024) {  // streamed v4
+          const int ntiles = (a.Lk + 63) / 64;
+          const size_t lds = (size_t)4 * 64 * 128 + (size_t)ntiles * 64 * 4 + (dm == 2 ? (size_t)ntiles * 64 * 8 : 0);
+          dim3 g4((a.Lq + 63) / 64, a.B * a.H);
+#define DQ4(D, M) hipLaunchKernelGGL((dq4_kernel<D, M>), g4, dim3(256), lds, s, a)
+          if (dm == 2) { if (mask) DQ4(2, true); else DQ4(2, false); }
+          else { if (mask) DQ4(0, true); else DQ4(0, false); }
+#undef DQ4
+          return (int)hipGetLastError();
+        }
         if (a.Lk <= v3max && a.Lk <= 512 && dm != 1 && !getenv("FDDM_ATTN_DQ2")) {
           const int LkP = (a.Lk + 63) / 64 * 64;
           const size_t lds = (size_t)LkP * 256 + (size_t)LkP * 4;
@@ -2514,6 +3247,15 @@ static int run(int which, AttnArgs& a, hipStream_t s) {
         // v3: Q/dO resident, 256 keys per workgroup, for Lq, Lk <= 256 (see dq3 above); FDDM_ATTN_DKV2=1 keeps the
         // streamed kernel
         static const int v3max = getenv("FDDM_ATTN_V3_MAX") ? atoi(getenv("FDDM_ATTN_V3_MAX")) : 256;
+        const bool v4 = !getenv("FDDM_ATTN_BWD4") || atoi(getenv("FDDM_ATTN_BWD4")) != 0;
+        if (v4 && (!a.thr16 || a.dbits) && a.Lq <= 1024) {  // streamed v4
+          const int LqP = (a.Lq + 63) / 64 * 64;
+          const size_t lds = (size_t)4 * 64 * 128 + (size_t)LqP * 8 + (a.thr16 ? (size_t)LqP * 8 : 0);
+          dim3 g4((a.Lk + 63) / 64, a.B * a.H);
+          if (a.thr16) hipLaunchKernelGGL((dkv4_kernel<2>), g4, dim3(256), lds, s, a);
+          else hipLaunchKernelGGL((dkv4_kernel<0>), g4, dim3(256), lds, s, a);
+          return (int)hipGetLastError();
+        }
         if (a.Lq <= v3max && a.Lk <= v3max && a.Lq <= 512 && (!a.thr16 || a.dbits) && !getenv("FDDM_ATTN_DKV2")) {
           const int LqP = (a.Lq + 63) / 64 * 64;
           const size_t lds = (size_t)LqP * 256 + (size_t)LqP * 8 + (a.thr16 ? (size_t)4 * LqP * 8 : 0);
@@ -2577,14 +3319,27 @@ FDDM_API int fddm_attn_stamps_clear() {
 FDDM_API int fddm_attn_fwd(int dtype, const void* Q, long sq, const void* K, long sk, const void* V, long sv, void* O,
                            long so, float* lse, const unsigned char* key_keep, const float* gate, const float* table,
                            int B, int H, int Lq, int Lk, float scale, float drop_p, unsigned long long seed,
-                           unsigned long long stream, unsigned long long* drop_bits, void* hs) {
+                           unsigned long long stream, unsigned long long* drop_bits, int drop_bits_ready, void* hs) {
   AttnArgs a{};
   a.dbits = (uint64_t*)drop_bits;
+  a.bits_ready = drop_bits_ready;
   a.Q = Q; a.K = K; a.V = V; a.Out = O; a.lse = lse;
   a.sq = sq; a.sk = sk; a.sv = sv; a.so = so;
   a.key_keep = key_keep; a.gate = gate; a.table = table;
   a.B = B; a.H = H; a.Lq = Lq; a.Lk = Lk; a.scale = scale; a.seed = seed; a.stream = stream;
   return attn_dispatch(0, dtype, a, drop_p, hs);
+}
+
+// Dropout keep bits of nsites attention sites with the same shape, rng streams stream0 + s * stream_step (site s at
+// out + s * site_words): the words fddm_attn_fwd(..., drop_bits_ready = 1) and fddm_attn_bwd read.
+FDDM_API int fddm_attn_drop_bits(unsigned long long* out, long site_words, int nsites, int B, int H, int Lq, int Lk,
+                                 float drop_p, unsigned long long seed, unsigned long long stream0,
+                                 unsigned long long stream_step, void* hs) {
+  if (B <= 0 || H <= 0 || Lq <= 0 || Lk <= 0 || nsites <= 0) return 0;
+  if (!out || drop_p <= 0.f || site_words < (long)B * H * Lq * ((Lk + 63) / 64)) return (int)hipErrorInvalidValue;
+  DbArgs d{(uint64_t*)out, site_words, B * H, Lq, Lk, seed, stream0, stream_step, (unsigned)llrintf(drop_p * 65536.f)};
+  hipLaunchKernelGGL(dbits_kernel, dim3(B * H, nsites), dim3(256), 0, (hipStream_t)hs, d);
+  return (int)hipGetLastError();
 }
 
 // WavLM forward with the gate computed in the kernel from 8 bf16 pre-activations per (token, head) that the Q|K|V
@@ -2617,7 +3372,7 @@ FDDM_API int fddm_attn_bwd(int dtype, const void* Q, long sq, const void* K, lon
   a.B = B; a.H = H; a.Lq = Lq; a.Lk = Lk; a.scale = scale; a.seed = seed; a.stream = stream;
   // self-attention shapes (Lq == Lk <= 256, bf16, no rehashed dropout): dQ, dK and dV in one fused launch
   if (dtype == FDDM_BF16 && Lq == Lk && Lk <= 256 && (drop_p <= 0.f || drop_bits) && !getenv("FDDM_ATTN_BWD_SPLIT") &&
-      !getenv("FDDM_ATTN_V1"))
+      !getenv("FDDM_ATTN_V1") && !(getenv("FDDM_ATTN_BWD4") && atoi(getenv("FDDM_ATTN_BWD4")) == 2))
     return attn_dispatch(3, dtype, a, drop_p, hs);
   int e = attn_dispatch(1, dtype, a, drop_p, hs);
   if (e) return e;

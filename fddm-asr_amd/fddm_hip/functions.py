@@ -225,9 +225,14 @@ class DecoderBlockFn(torch.autograd.Function):
         v = ops.linear(xT, W["sa"][2 * d:], sa_b[2 * d:], out_dtype=cd)
         o = torch.empty(N, d, device=dev, dtype=cd)
         lse = torch.empty(B * H, L, device=dev, dtype=F32)
-        bits_s = ops.drop_bits(B, H, L, L, dev) if p > 0 else None
+        # dropout keep bits of both attention sites: written for every block ahead of the forward
+        # (DenoisingTransformerDecoder._drop_bits, two launches per step) or here by the forward itself
+        pre = meta[11] if len(meta) > 11 else None
+        ready = pre is not None and p > 0
+        bits_s = pre[0] if ready else (ops.drop_bits(B, H, L, L, dev) if p > 0 else None)
+        bits_c = pre[1] if ready else (ops.drop_bits(B, H, L, S, dev) if p > 0 else None)
         fwd_s = lambda: ops.attn_fwd(qk, qk[:, d:], v, o, lse, B, H, L, L, key_keep=key_keep, drop_p=p,  # noqa: E731
-                                     seed=seed, rng_stream=st + 1, dbits=bits_s)
+                                     seed=seed, rng_stream=st + 1, dbits=bits_s, bits_ready=ready)
         with rt.probe("decoder.self_attn_fwd", replay=fwd_s):
             fwd_s()
         y = ops.linear(o, W["so"], so_b, out_dtype=cd)
@@ -244,9 +249,8 @@ class DecoderBlockFn(torch.autograd.Function):
             ops.linear(cT, W["ca"][d:], ca_b[d:], out_dtype=cd)      # (precomputed for all blocks in one GEMM)
         oc = torch.empty(N, d, device=dev, dtype=cd)
         lsec = torch.empty(B * H, L, device=dev, dtype=F32)
-        bits_c = ops.drop_bits(B, H, L, S, dev) if p > 0 else None
         fwd_c = lambda: ops.attn_fwd(qc, kvc, kvc[:, d:], oc, lsec, B, H, L, S, drop_p=p, seed=seed,  # noqa: E731
-                                     rng_stream=st + 3, dbits=bits_c)
+                                     rng_stream=st + 3, dbits=bits_c, bits_ready=ready)
         with rt.probe("decoder.cross_attn_fwd", replay=fwd_c):
             fwd_c()
         yc = ops.linear(oc, W["co"], co_b, out_dtype=cd)

@@ -95,11 +95,16 @@ def _gemm_padded(A, B, C, M, N, K, a_kc, b_kc, lda, ldb, ldc, epi, bias, alpha, 
 
 def gemm(A, B, C, M, N, K, *, a_kc=True, b_kc=True, lda, ldb, ldc, epi=EPI_STORE, bias=None, alpha=1.0,
          C2=None, Mi=0, sAb=0, drop_p=0.0, seed=0, rng_stream=0, colsum=None):
-    """C[m][n] = alpha * sum_k A(m,k) B(n,k) (+bias, epilogue). Compute dtype = B.dtype."""
+    """C[m][n] = alpha * sum_k A(m,k) B(n,k) (+bias, epilogue). Compute dtype = B.dtype.
+    Operands that miss the kernels' layout preconditions (a dimension or leading dimension not a multiple of 8, e.g.
+    a ragged vocabulary) run zero-padded copies (_gemm_padded) — unbatched calls only: a batched / strided call
+    (Mi or sAb set) with such operands raises."""
     _chk(B.dtype in (torch.float32, torch.bfloat16), "B dtype")
     if M == 0 or N == 0:
         return C
-    if Mi == 0 and sAb == 0 and not _layout_ok(A, B, M, N, K, a_kc, b_kc, lda, ldb):
+    if not _layout_ok(A, B, M, N, K, a_kc, b_kc, lda, ldb):
+        _chk(Mi == 0 and sAb == 0, "batched / strided GEMM operands must meet the 8-element layout preconditions "
+                                   "(the zero-padded fallback covers unbatched calls only)")
         return _gemm_padded(A, B, C, M, N, K, a_kc, b_kc, lda, ldb, ldc, epi, bias, alpha, colsum)
     call("fddm_gemm", code(B), code(A), int(a_kc), int(b_kc), epi, code(C), ptr(A), lda, Mi, sAb, ptr(B), ldb,
          ptr(C), ldc, ptr(C2), ptr(bias), float(alpha), M, N, K, seed, rng_stream, float(drop_p), ptr(colsum),
@@ -236,10 +241,21 @@ def _pad64(x, rows, H, dh):
     return xp.view(rows, H * 64)
 
 
+def attn_drop_bits(out, nsites, B, H, Lq, Lk, drop_p, seed, stream0, stream_step):
+    """The dropout keep-bit words of `nsites` attention sites of one shape (rng streams stream0 + s * stream_step)
+    into out [nsites, words] (int64): what attn_fwd(..., dbits=out[s], bits_ready=True) and attn_bwd read."""
+    _chk(out.dtype == torch.int64 and out.is_contiguous() and out.dim() == 2 and out.shape[0] >= nsites,
+         "drop-bit buffer layout")
+    call("fddm_attn_drop_bits", ptr(out), out.shape[1], nsites, B, H, Lq, Lk, float(drop_p), seed, stream0,
+         stream_step, stream())
+    return out
+
+
 def attn_fwd(q, k, v, out, lse, B, H, Lq, Lk, *, key_keep=None, gate=None, table=None, drop_p=0.0, seed=0,
-             rng_stream=0, scale=None, dbits=None):
+             rng_stream=0, scale=None, dbits=None, bits_ready=False):
     """q: [B*Lq, >=H*dh] row stride q.stride(0); k/v: [B*Lk, ...]; out [B*Lq, H*dh]; lse [B*H, Lq], dh =
-    out.shape[1] // H. dbits (optional, drop_bits()): records the dropout keep bits for the backward.
+    out.shape[1] // H. dbits (optional, drop_bits()): the dropout keep bits the backward reads; bits_ready: they
+    were already written by attn_drop_bits (the forward only reads them), else the forward writes them.
     The kernels are built for head_dim 64; a smaller head_dim (the reference's nn.MultiheadAttention takes any
     d_model / nhead) runs them on zero-padded 64-wide head slots — the scores, the softmax, the dropout
     element indices (b, h, query, key) and hence the RNG stream are those of the unpadded heads."""
@@ -253,12 +269,12 @@ def attn_fwd(q, k, v, out, lse, B, H, Lq, Lk, *, key_keep=None, gate=None, table
         op = torch.empty(B * Lq, H * 64, device=out.device, dtype=out.dtype)
         attn_fwd(_pad64(q, B * Lq, H, dh), _pad64(k, B * Lk, H, dh), _pad64(v, B * Lk, H, dh), op, lse, B, H, Lq,
                  Lk, key_keep=key_keep, gate=gate, table=table, drop_p=drop_p, seed=seed, rng_stream=rng_stream,
-                 scale=sc, dbits=dbits)
+                 scale=sc, dbits=dbits, bits_ready=bits_ready)
         _heads(out, B * Lq, H, dh).copy_(op.view(B * Lq, H, 64)[:, :, :dh])
         return out
     call("fddm_attn_fwd", code(q), ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out),
          out.stride(0), ptr(lse), ptr(key_keep), ptr(gate), ptr(table), B, H, Lq, Lk, float(sc), float(drop_p), seed,
-         rng_stream, ptr(dbits), stream())
+         rng_stream, ptr(dbits), int(bool(bits_ready) and dbits is not None), stream())
     return out
 
 

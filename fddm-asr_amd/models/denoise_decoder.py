@@ -21,6 +21,7 @@ import torch.nn.functional as F
 
 from fddm_hip import functions as FN
 from fddm_hip import runtime as rt
+from fddm_hip.ops import attn_drop_bits as ops_attn_drop_bits
 from fddm_hip.ops import linear as ops_linear
 from fddm_hip.ops import rows_mean as ops_rows_mean
 
@@ -123,12 +124,13 @@ class DecoderBlock(nn.Module):
                 self.ff[3].weight, self.ff[3].bias, self.norm1.weight, self.norm1.bias, self.norm2.weight,
                 self.norm2.bias, self.norm3.weight, self.norm3.bias)
 
-    def run(self, x, xT, cT, key_keep, film, B, L, S, layer, seed, cos, sin, kv=None):
+    def run(self, x, xT, cT, key_keep, film, B, L, S, layer, seed, cos, sin, kv=None, bits=None):
         """film = (scale, shift, (dscale, dshift) accumulators or None) from DenoisingTransformerDecoder's
-        conditioning Function; kv = this block's precomputed cross-attention K|V [B*S, 2d] (strided view) or None."""
+        conditioning Function; kv = this block's precomputed cross-attention K|V [B*S, 2d] (strided view) or None;
+        bits = (self, cross) attention-dropout keep-bit words already written for this block, or None."""
         fscale, fshift, gfilm = film
         p = self.p if self.training else 0.0
-        meta = (B, L, S, self.nhead, layer, p, seed, cos, sin, gfilm, kv)
+        meta = (B, L, S, self.nhead, layer, p, seed, cos, sin, gfilm, kv, bits)
         return FN.DecoderBlockFn.apply(x, xT, cT, key_keep, fscale, fshift, meta, *self.block_params())
 
 
@@ -187,12 +189,32 @@ class DenoisingTransformerDecoder(nn.Module):
         cos, sin = self.pos_emb(L, dev)
         seed = rt.next_seed()
         kv_all = self._cross_kv(cT)
+        bits = self._drop_bits(B, L, S, seed, dev)
         for i, blk in enumerate(self.blocks):
             film = (films[2 * i], films[2 * i + 1], (gbuf[2 * i], gbuf[2 * i + 1]))
             kv = None if kv_all is None else kv_all[:, 2 * self.d_model * i: 2 * self.d_model * (i + 1)]
-            x, xT = blk.run(x, xT, cT, key_keep, film, B, L, S, i, seed, cos, sin, kv)
+            bi = None if bits is None else (bits[0][i], bits[1][i])
+            x, xT = blk.run(x, xT, cT, key_keep, film, B, L, S, i, seed, cos, sin, kv, bi)
         logits = FN.HeadFn.apply(x, xT, self.head.weight, self.head.bias)           # (:286)
         return logits.view(B, L, -1)
+
+    @torch.no_grad()
+    def _drop_bits(self, B, L, S, seed, dev):
+        """The attention-probability dropout keep bits of every block's two attention sites (rng streams 6i+1 self,
+        6i+3 cross; RNG contract v2, oracle.attn_dropout_keep), written by two launches ahead of the blocks: the
+        attention forward kernels then read one word per (query, 64-key tile) instead of drawing them, and the
+        backward reads the same words. bf16 training only (the fp32 parity kernels draw their own)."""
+        p = self.blocks[0].p if (self.training and len(self.blocks)) else 0.0
+        if p <= 0 or rt.compute_dtype() != torch.bfloat16 or os.environ.get("FDDM_PRE_BITS") == "0":
+            return None
+        H, nb = self.nhead, len(self.blocks)
+        ws = B * H * L * ((L + 63) // 64)
+        wc = B * H * L * ((S + 63) // 64)
+        bs = torch.empty(nb, ws, device=dev, dtype=torch.int64)
+        bc = torch.empty(nb, wc, device=dev, dtype=torch.int64)
+        ops_attn_drop_bits(bs, nb, B, H, L, L, p, seed, 1, 6)
+        ops_attn_drop_bits(bc, nb, B, H, L, S, p, seed, 3, 6)
+        return bs, bc
 
     @torch.no_grad()
     def _cross_kv(self, cT):

@@ -82,14 +82,22 @@ int fddm_wavlm_gate(int dtype, const void* x, const float* W, const float* bias,
 
 /* ---- attention (head_dim 64). Element (b,pos,h,d) at base + (b*L+pos)*stride + h*64 + d.
  *      nn.MultiheadAttention (models/denoise_decoder.py:129-130,164,169-174) with key_padding_mask
- *      (key_keep[b][k] != 0 keeps) and attention-prob dropout (drop_bits, optional: the forward records
- *      the keep bits as [B*H][ceil(Lk/64)][Lq] u64 words, the backward reads them instead of rehashing);
+ *      (key_keep[b][k] != 0 keeps) and attention-prob dropout (drop_bits, optional: the keep bits as
+ *      [B*H][ceil(Lk/64)][Lq] u64 words, bit kk of word (bh, t, q) = keep(q, key 64t + kk); the backward reads them
+ *      instead of rehashing); drop_bits_ready != 0: fddm_attn_drop_bits already wrote this site's words (the forward
+ *      only reads them), else the forward produces them itself;
  *      WavLM relative-bias attention
- *      (HF modeling_wavlm.py:152-200) via gate [B*H][Lq] and table [H][2*Lk-1]. lse: [B*H][Lq]. */
+ *      (HF modeling_wavlm.py:152-200) via gate [B*H][Lq] and table [H][2*Lk-1]. lse: [B*H][Lq].
+ *      fddm_attn_drop_bits: the keep-bit words of nsites sites of one shape at once (rng streams stream0 +
+ *      s*stream_step, site s at out + s*site_words) — the decoder produces every block's words in two launches ahead
+ *      of its forward (models/denoise_decoder.py:164,169-176 dropout sites 1 and 3 of each block). */
 int fddm_attn_fwd(int dtype, const void* Q, long sq, const void* K, long sk, const void* V, long sv, void* O, long so,
                   float* lse, const unsigned char* key_keep, const float* gate, const float* table, int B, int H,
                   int Lq, int Lk, float scale, float drop_p, unsigned long long seed, unsigned long long stream,
-                  unsigned long long* drop_bits, void* hip_stream);
+                  unsigned long long* drop_bits, int drop_bits_ready, void* hip_stream);
+int fddm_attn_drop_bits(unsigned long long* out, long site_words, int nsites, int B, int H, int Lq, int Lk,
+                        float drop_p, unsigned long long seed, unsigned long long stream0,
+                        unsigned long long stream_step, void* hip_stream);
 /* WavLM variant (bf16): the gate is computed in the kernel from the 8 gru_rel_pos_linear pre-activations per
  * (token, head) stored at graw + (b*Lq+q)*sgr + h*8 (bf16, appended to the Q|K|V projection's output) and
  * gconst [H] (gru_rel_pos_const) — HF modeling_wavlm.py:177-186. */

@@ -430,6 +430,28 @@ def test_attention_fwd_bwd(dtype, Lq, Lk, masked, p, bits):
     close(dv.float(), back(vr.grad), rtol=3 * tol, what="dv")
 
 
+@pytest.mark.parametrize("Lq,Lk", [(256, 256), (40, 499), (129, 70)])
+def test_attention_drop_bits_producer_matches_oracle(Lq, Lk):
+    """fddm_attn_drop_bits (the decoder writes every block's attention-dropout keep bits in two launches ahead of the
+    forward): 3 sites of one shape, rng streams 7, 13, 19, against the oracle's contract-v2 mask bit for bit, in the
+    word layout the forward / backward kernels read (bit kk of word (bh, t, q) = keep(q, key 64t + kk))."""
+    o = ops()
+    B, H, p, seed = 2, 3, 0.1, 77
+    nt = (Lk + 63) // 64
+    words = B * H * nt * Lq
+    out = torch.zeros(3, words + 5, device=dev, dtype=torch.int64)
+    o.attn_drop_bits(out, 3, B, H, Lq, Lk, p, seed, 7, 6)
+    torch.cuda.synchronize()
+    assert (out[:, words:] == 0).all(), "wrote past the site's words"
+    bitpos = torch.arange(64, dtype=torch.int64)
+    for s_ in range(3):
+        w = out[s_, :words].cpu().view(B * H, nt, Lq)
+        bits = ((w[..., None] >> bitpos) & 1).bool()                       # [BH, nt, Lq, 64]
+        got = bits.permute(0, 2, 1, 3).reshape(B * H, Lq, nt * 64)[:, :, :Lk]
+        ref = O.attn_dropout_keep(seed, 7 + 6 * s_, B, H, Lq, Lk, p).reshape(B * H, Lq, Lk)
+        assert torch.equal(got, ref), f"site {s_}: {(got != ref).sum().item()} bits differ"
+
+
 @pytest.mark.parametrize("L,masked,p", [(256, False, 0.1), (200, True, 0.1), (70, True, 0.0), (32, False, 0.1)])
 def test_attention_fused_self_bwd_equals_split(L, masked, p, monkeypatch):
     """Self-attention shapes (Lq == Lk <= 256, bf16) take the fused one-launch backward (bwd3s_kernel); it runs the
@@ -979,13 +1001,15 @@ def test_conv0_gn_gelu_matches_reference():
     """WavLM conv layer 0 + per-channel GroupNorm over time + GELU (HF modeling_wavlm.py:723-744) in bf16 (Gram-
     matrix statistics; the bf16 output's conv + affine on the matrix cores as a hi/lo bf16 split, the f32 output's
     on the VALU) vs a float64 torch reference within bf16 rounding (2^-8 relative + 2e-3 absolute) resp. 1e-4;
-    16007 samples = 3200 frames, 12345 = 2468 frames (ragged 512-frame blocks and 16-frame tiles)."""
+    16007 samples = 3200 frames, 12345 = 2468 frames (ragged 512-frame blocks and 16-frame tiles), 45007 = 9000 frames
+    (three 4096-frame statistics blocks, the last one ragged: the per-block partial statistics summed in a fixed
+    order by the affine kernel; the 10 s training input has eight)."""
     o = ops()
     C, K, S = 512, 10, 5
     w = torch.randn(C, K, generator=g(82)) * 0.3
     gamma = 1 + 0.1 * torch.randn(C, generator=g(83))
     beta = 0.1 * torch.randn(C, generator=g(84))
-    for B, nsamp in ((3, 16000 + 7), (2, 12345)):
+    for B, nsamp in ((3, 16000 + 7), (2, 12345), (2, 45007)):
         wave = torch.randn(B, nsamp, generator=g(81)) * 0.1
         y = F.conv1d(wave.double()[:, None], w.double()[:, None], stride=S)            # [B, C, T]
         y = F.group_norm(y, C, gamma.double(), beta.double(), eps=1e-5)
