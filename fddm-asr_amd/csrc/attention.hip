@@ -191,6 +191,7 @@ struct AttnArgs {
   unsigned thr16;
   float drop_scale;
   int bits_ready;  // host side only: dbits already holds this site's keep bits (fddm_attn_drop_bits)
+  const uint64_t* seed_off;  // graph-replay seed offset (common.h eff_seed) or null
 };
 
 __device__ __forceinline__ bool key_ok(const AttnArgs& a, int b, int key) {
@@ -235,7 +236,7 @@ __device__ unsigned long long attn_stamps[8192 * 16];
 constexpr int ATTN_R = 4096;
 constexpr uint64_t ATTN_TAB0 = 1ull << 62, ATTN_OFF0 = 3ull << 62;
 __device__ __forceinline__ uint64_t attn_offsets(const AttnArgs& a, int bh, int q) {
-  return mix64(a.seed, a.stream, ATTN_OFF0 + (uint64_t)bh * a.Lq + q);
+  return mix64(eff_seed(a.seed, a.seed_off), a.stream, ATTN_OFF0 + (uint64_t)bh * a.Lq + q);
 }
 // the 4 keep bits of keys k0..k0+3 (k0 % 4 == 0) of query q: generic form (4 hashes), for the kernels that do not
 // stage the tables
@@ -245,7 +246,7 @@ __device__ __forceinline__ unsigned attn_keep4(const AttnArgs& a, int bh, int q,
 #pragma unroll
   for (int tau = 0; tau < 3; ++tau) {
     const unsigned j = ((unsigned)((off >> (16 * tau)) & 0xFFCu) + (unsigned)k0) & (ATTN_R - 1);
-    w ^= mix64(a.seed, a.stream, ATTN_TAB0 + ((uint64_t)bh * 3 + tau) * (ATTN_R / 4) + (j >> 2));
+    w ^= mix64(eff_seed(a.seed, a.seed_off), a.stream, ATTN_TAB0 + ((uint64_t)bh * 3 + tau) * (ATTN_R / 4) + (j >> 2));
   }
   unsigned keep = 0;
 #pragma unroll
@@ -954,7 +955,7 @@ __global__ void __launch_bounds__(64 * NW, 1) fwd3_kernel(AttnArgs a) {
     for (int wi = tid; wi < 3 * ATTN_R / 4; wi += 64 * NW) {
       const int tau = wi / (ATTN_R / 4), jw = wi % (ATTN_R / 4);
       *(uint64_t*)(dtab + (size_t)wi * 8) =
-          mix64(a.seed, a.stream, ATTN_TAB0 + ((uint64_t)bh * 3 + tau) * (ATTN_R / 4) + jw);
+          mix64(eff_seed(a.seed, a.seed_off), a.stream, ATTN_TAB0 + ((uint64_t)bh * 3 + tau) * (ATTN_R / 4) + jw);
     }
   }
   if constexpr (REL) {
@@ -1193,22 +1194,24 @@ struct DbArgs {
   int BH, Lq, Lk;
   uint64_t seed, stream0, stream_step;
   unsigned thr16;
+  const uint64_t* seed_off;  // graph-replay seed offset (common.h eff_seed) or null
 };
 
 __global__ void __launch_bounds__(256) dbits_kernel(DbArgs d) {
   __shared__ __attribute__((aligned(16))) uint64_t tab[3 * ATTN_R / 4];
   const int bh = blockIdx.x, site = blockIdx.y, tid = threadIdx.x;
   const uint64_t stream = d.stream0 + (uint64_t)site * d.stream_step;
+  const uint64_t seed = eff_seed(d.seed, d.seed_off);
   for (int wi = tid; wi < 3 * ATTN_R / 4; wi += 256) {
     const int tau = wi / (ATTN_R / 4), jw = wi % (ATTN_R / 4);
-    tab[wi] = mix64(d.seed, stream, ATTN_TAB0 + ((uint64_t)bh * 3 + tau) * (ATTN_R / 4) + jw);
+    tab[wi] = mix64(seed, stream, ATTN_TAB0 + ((uint64_t)bh * 3 + tau) * (ATTN_R / 4) + jw);
   }
   __syncthreads();
   const int ntiles = (d.Lk + 63) / 64;
   uint64_t* out = d.out + (long)site * d.site_words + (long)bh * ntiles * d.Lq;
   const unsigned char* tb = (const unsigned char*)tab;
   for (int q = tid; q < d.Lq; q += 256) {
-    const uint64_t off = mix64(d.seed, stream, ATTN_OFF0 + (uint64_t)bh * d.Lq + q);
+    const uint64_t off = mix64(seed, stream, ATTN_OFF0 + (uint64_t)bh * d.Lq + q);
     const unsigned o0 = (unsigned)(off & 0xFFCu), o1 = (unsigned)((off >> 16) & 0xFFCu),
                    o2 = (unsigned)((off >> 32) & 0xFFCu);
     for (int t = 0; t < ntiles; ++t) {
@@ -1284,7 +1287,7 @@ __global__ void __launch_bounds__(256, NG == 1 ? 4 : 2) fwd6_kernel(AttnArgs a) 
     for (int wi = tid; wi < 3 * ATTN_R / 4; wi += 256) {
       const int tau = wi / (ATTN_R / 4), jw = wi % (ATTN_R / 4);
       *(uint64_t*)(dtab + (size_t)wi * 8) =
-          mix64(a.seed, a.stream, ATTN_TAB0 + ((uint64_t)bh * 3 + tau) * (ATTN_R / 4) + jw);
+          mix64(eff_seed(a.seed, a.seed_off), a.stream, ATTN_TAB0 + ((uint64_t)bh * 3 + tau) * (ATTN_R / 4) + jw);
     }
 #pragma unroll
     for (int gq = 0; gq < NG; ++gq) {
@@ -3326,7 +3329,7 @@ FDDM_API int fddm_attn_fwd(int dtype, const void* Q, long sq, const void* K, lon
   a.Q = Q; a.K = K; a.V = V; a.Out = O; a.lse = lse;
   a.sq = sq; a.sk = sk; a.sv = sv; a.so = so;
   a.key_keep = key_keep; a.gate = gate; a.table = table;
-  a.B = B; a.H = H; a.Lq = Lq; a.Lk = Lk; a.scale = scale; a.seed = seed; a.stream = stream;
+  a.B = B; a.H = H; a.Lq = Lq; a.Lk = Lk; a.scale = scale; a.seed = seed; a.stream = stream; a.seed_off = g_seed_off;
   return attn_dispatch(0, dtype, a, drop_p, hs);
 }
 
@@ -3337,7 +3340,8 @@ FDDM_API int fddm_attn_drop_bits(unsigned long long* out, long site_words, int n
                                  unsigned long long stream_step, void* hs) {
   if (B <= 0 || H <= 0 || Lq <= 0 || Lk <= 0 || nsites <= 0) return 0;
   if (!out || drop_p <= 0.f || site_words < (long)B * H * Lq * ((Lk + 63) / 64)) return (int)hipErrorInvalidValue;
-  DbArgs d{(uint64_t*)out, site_words, B * H, Lq, Lk, seed, stream0, stream_step, (unsigned)llrintf(drop_p * 65536.f)};
+  DbArgs d{(uint64_t*)out, site_words, B * H, Lq, Lk, seed, stream0, stream_step, (unsigned)llrintf(drop_p * 65536.f),
+           g_seed_off};
   hipLaunchKernelGGL(dbits_kernel, dim3(B * H, nsites), dim3(256), 0, (hipStream_t)hs, d);
   return (int)hipGetLastError();
 }
@@ -3369,7 +3373,7 @@ FDDM_API int fddm_attn_bwd(int dtype, const void* Q, long sq, const void* K, lon
   a.dQ = dQ; a.dK = dK; a.dV = dV;
   a.sq = sq; a.sk = sk; a.sv = sv; a.so = so; a.sdo = sdo; a.sdq = sdq; a.sdk = sdk; a.sdv = sdv;
   a.key_keep = key_keep;
-  a.B = B; a.H = H; a.Lq = Lq; a.Lk = Lk; a.scale = scale; a.seed = seed; a.stream = stream;
+  a.B = B; a.H = H; a.Lq = Lq; a.Lk = Lk; a.scale = scale; a.seed = seed; a.stream = stream; a.seed_off = g_seed_off;
   // self-attention shapes (Lq == Lk <= 256, bf16, no rehashed dropout): dQ, dK and dV in one fused launch
   if (dtype == FDDM_BF16 && Lq == Lk && Lk <= 256 && (drop_p <= 0.f || drop_bits) && !getenv("FDDM_ATTN_BWD_SPLIT") &&
       !getenv("FDDM_ATTN_V1") && !(getenv("FDDM_ATTN_BWD4") && atoi(getenv("FDDM_ATTN_BWD4")) == 2))

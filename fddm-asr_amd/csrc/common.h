@@ -48,6 +48,14 @@ __device__ __forceinline__ uint64_t mix64(uint64_t seed, uint64_t stream, uint64
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
   return z ^ (z >> 31);
 }
+// Seed offset of HIP-graph replays (fddm_set_seed_offset): a launch enqueued while an offset buffer is set reads its
+// effective dropout seed as seed + *off (a scalar load from the constant address space), so one captured train step
+// replays with the seeds the host counter has moved on to — identical to the seeds an eager step would use (the
+// contract's mix64 takes the seed linearly). Null for every other launch. Host side: the current offset buffer.
+inline const uint64_t* g_seed_off = nullptr;
+__device__ __forceinline__ uint64_t eff_seed(uint64_t seed, const uint64_t* off) {
+  return off ? seed + *(const __attribute__((address_space(4))) uint64_t*)(uintptr_t)off : seed;
+}
 // dropout keep decision for flat element e (oracle: dropout_keep)
 __device__ __forceinline__ bool drop_keep(uint64_t seed, uint64_t stream, uint64_t e, unsigned thr16) {
   uint64_t h = mix64(seed, stream, e >> 2);

@@ -22,6 +22,7 @@ struct GemmArgs {
   long sAz, sBz, sCz, sbiasz;  // per-blockIdx.z offsets (grouped conv)
   long ksplit;                 // K elements per split-K slice (plain GEMM)
   float* colsum;               // optional: colsum[m] += sum_k A(m,k) (MC A operand) — fused bias gradient
+  const uint64_t* seed_off;    // graph-replay seed offset (common.h eff_seed) or null
 };
 
 // KC LDS image: 16-B chunk c of 128-B row r at r*128 + ((c ^ ((r>>1)&7))<<4) — conflict-free ds_read_b128 of

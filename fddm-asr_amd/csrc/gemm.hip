@@ -361,7 +361,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, unsigned char* smem
         for (int t = 0; t < 8; ++t) {
           a[t] = gelu_f(v[t]);
           if (g.thr16)
-            a[t] = drop_keep(g.seed, g.stream, (uint64_t)(m * g.N + n + t), g.thr16) ? a[t] * g.drop_scale : 0.f;
+            a[t] = drop_keep(eff_seed(g.seed, g.seed_off), g.stream, (uint64_t)(m * g.N + n + t), g.thr16) ? a[t] * g.drop_scale : 0.f;
         }
         OT* c2 = (OT*)g.C2 + m * g.ldc + n;
         if (vec) {
@@ -385,7 +385,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, unsigned char* smem
         for (int t = 0; t < 8; ++t) {
           v[t] *= gelu_grad(pv[t]);
           if (g.thr16)
-            v[t] = drop_keep(g.seed, g.stream, (uint64_t)(m * g.N + n + t), g.thr16) ? v[t] * g.drop_scale : 0.f;
+            v[t] = drop_keep(eff_seed(g.seed, g.seed_off), g.stream, (uint64_t)(m * g.N + n + t), g.thr16) ? v[t] * g.drop_scale : 0.f;
         }
         if (vec) st_vec8(crow, v);
         else for (int t = 0; t < 8 && n + t < g.N; ++t) st<OT>(crow + t, v[t]);
@@ -586,7 +586,7 @@ __global__ void __launch_bounds__(512) gemm_big_kernel(GemmArgs g) {
         } else if constexpr (EPI == EPI_GELU) {
           st<OT>(c, v);
           float a = gelu_f(v);
-          if (g.thr16) a = drop_keep(g.seed, g.stream, (uint64_t)(m * g.N + n), g.thr16) ? a * g.drop_scale : 0.f;
+          if (g.thr16) a = drop_keep(eff_seed(g.seed, g.seed_off), g.stream, (uint64_t)(m * g.N + n), g.thr16) ? a * g.drop_scale : 0.f;
           st<OT>((OT*)g.C2 + m * g.ldc + n, a);
         } else if constexpr (EPI == EPI_GELU_ONLY) {
           st<OT>(c, gelu_f(v));
@@ -728,7 +728,8 @@ FDDM_API int fddm_gemm(int dtype, int a_dtype, int a_kc, int b_kc, int epi, int 
   if (!C || ((epi == EPI_GELU || epi == EPI_DGELU) && !C2)) return (int)hipErrorInvalidValue;  // second output
   if (!a_kc && Mi > 0 && Mi != M) return (int)hipErrorInvalidValue;
   if (Mi <= 0) Mi = 1L << 62;
-  GemmArgs g{A, lda, Mi, sAb, B, ldb, C, ldc, C2, bias, alpha, M, N, K, seed, stream, 0u, 1.f, ConvGeo{1, 0, 0, 0}, 0, 0, 0, 0, K, nullptr};
+  GemmArgs g{A, lda, Mi, sAb, B, ldb, C, ldc, C2, bias, alpha, M, N, K, seed, stream, 0u, 1.f, ConvGeo{1, 0, 0, 0}, 0, 0, 0, 0, K, nullptr,
+             g_seed_off};
   if (colsum) {
     if (a_kc || a_dtype != dtype) return (int)hipErrorInvalidValue;
     if (epi != EPI_ACC_F32) {  // colsum follows C: overwritten by STORE, accumulated by ACC

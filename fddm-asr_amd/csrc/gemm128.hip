@@ -341,7 +341,7 @@ __device__ __forceinline__ void tile128(const GemmArgs& g, unsigned char* smem, 
             if constexpr (EPI == EPI_GELU) {
               *(uint2*)cp = make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));  // pre-activation
               const unsigned keep =
-                  g.thr16 ? drop_keep4(g.seed, g.stream, ((uint64_t)m * (uint64_t)N + n) >> 2, g.thr16) : 0xfu;
+                  g.thr16 ? drop_keep4(eff_seed(g.seed, g.seed_off), g.stream, ((uint64_t)m * (uint64_t)N + n) >> 2, g.thr16) : 0xfu;
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
                 const float a = gelu_f(v[e]);
@@ -356,7 +356,7 @@ __device__ __forceinline__ void tile128(const GemmArgs& g, unsigned char* smem, 
               const float pv[4] = {__uint_as_float(pu.x << 16), __uint_as_float(pu.x & 0xffff0000u),
                                    __uint_as_float(pu.y << 16), __uint_as_float(pu.y & 0xffff0000u)};
               const unsigned keep =
-                  g.thr16 ? drop_keep4(g.seed, g.stream, ((uint64_t)m * (uint64_t)N + n) >> 2, g.thr16) : 0xfu;
+                  g.thr16 ? drop_keep4(eff_seed(g.seed, g.seed_off), g.stream, ((uint64_t)m * (uint64_t)N + n) >> 2, g.thr16) : 0xfu;
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
                 const float a = v[e] * gelu_grad(pv[e]);

@@ -331,7 +331,7 @@ __global__ void __launch_bounds__(512) gemm256_kernel(GemmArgs g) {
             if (thr) {  // 4 consecutive columns (N % 8 == 0): one hash
               const unsigned m = (unsigned)(em0 + wr * 128 + (ib + i) * 16 + fr);
               const unsigned n = (unsigned)(en0 + wc * 64 + j * 16 + 4 * fg);
-              keep = drop_keep4(g.seed, g.stream, ((uint64_t)m * (uint64_t)Nc + n) >> 2, thr);
+              keep = drop_keep4(eff_seed(g.seed, g.seed_off), g.stream, ((uint64_t)m * (uint64_t)Nc + n) >> 2, thr);
             }
 #pragma unroll
             for (int e = 0; e < 4; ++e) {

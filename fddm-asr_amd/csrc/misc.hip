@@ -338,3 +338,12 @@ FDDM_API int fddm_cast(int src_dtype, int dst_dtype, const void* x, void* y, lon
 FDDM_API const char* fddm_error_string(int code) { return hipGetErrorString((hipError_t)code); }
 
 FDDM_API int fddm_abi_version() { return 2; }
+
+// HIP-graph replays of the train step (fddm_hip.graphs.StepGraphs): launches enqueued while `off` is set read their
+// dropout seed as seed + *off (common.h eff_seed); null restores plain seeds. Returns the previous setting's state
+// (0 = none was set, 1 = one was).
+FDDM_API int fddm_set_seed_offset(const unsigned long long* off) {
+  const int had = g_seed_off != nullptr;
+  g_seed_off = (const uint64_t*)off;
+  return had;
+}

@@ -20,6 +20,7 @@ struct LnFwdArgs {
   long N, d, rows_per_batch;
   float eps;
   uint64_t seed, stream; unsigned thr16; float drop_scale;
+  const uint64_t* seed_off;  // graph-replay seed offset (common.h eff_seed) or null
 };
 
 // 8 consecutive elements per lane per chunk (16-B bf16 / 32-B f32 accesses); d % 8 == 0
@@ -113,7 +114,7 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(LnFwdArgs a) {
         unsigned keep = 0xffu;  // d % 8 == 0: two hashes per 8 elements
         if (a.thr16) {
           const uint64_t e4 = (uint64_t)(row * d + ch * 8) >> 2;
-          keep = drop_keep4(a.seed, a.stream, e4, a.thr16) | (drop_keep4(a.seed, a.stream, e4 + 1, a.thr16) << 4);
+          keep = drop_keep4(eff_seed(a.seed, a.seed_off), a.stream, e4, a.thr16) | (drop_keep4(eff_seed(a.seed, a.seed_off), a.stream, e4 + 1, a.thr16) << 4);
         }
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -169,6 +170,7 @@ struct LnBwdArgs {
   float *dgamma, *dbeta, *dfsc, *dfsh;
   long N, d, rows_per_batch;
   uint64_t seed, stream; unsigned thr16; float drop_scale;
+  const uint64_t* seed_off;  // graph-replay seed offset (common.h eff_seed) or null
 };
 
 // pass 1: one wave per row: ds (residual gradient) and the dropout-masked dy for the GEMM
@@ -207,7 +209,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
       if (a.dres) a.dres[row * d + c] = ds;
       if (a.dy_t) {
         float dy = ds;
-        if (a.thr16) dy = drop_keep(a.seed, a.stream, (uint64_t)(row * d + c), a.thr16) ? dy * a.drop_scale : 0.f;
+        if (a.thr16) dy = drop_keep(eff_seed(a.seed, a.seed_off), a.stream, (uint64_t)(row * d + c), a.thr16) ? dy * a.drop_scale : 0.f;
         st<OT>((OT*)a.dy_t + row * d + c, dy);
       }
     }
@@ -298,7 +300,7 @@ __global__ void __launch_bounds__(512) ln_bwd_fused_kernel(LnBwdArgs a) {
         if (a.dres) st8<float>(a.dres + row * d + ch * 8, ds);
         if (a.dy_t) {
           if (a.thr16) {
-            const unsigned k = keep8(a.seed, a.stream, (uint64_t)(row * d + ch * 8), a.thr16);
+            const unsigned k = keep8(eff_seed(a.seed, a.seed_off), a.stream, (uint64_t)(row * d + ch * 8), a.thr16);
 #pragma unroll
             for (int e = 0; e < 8; ++e) ds[e] = ((k >> e) & 1u) ? ds[e] * a.drop_scale : 0.f;
           }
@@ -418,7 +420,7 @@ FDDM_API int fddm_ln_fwd(int x_dtype, int y_dtype, int out_dtype, const void* x,
         (uintptr_t)y) & 15))
     return (int)hipErrorInvalidValue;  // 16-B vector accesses
   LnFwdArgs a{x, y, gamma, beta, film_scale, film_shift, out_f32, out_t, save_s, mean, rstd, N, d,
-              rows_per_batch > 0 ? rows_per_batch : N, eps, seed, stream, 0u, 1.f};
+              rows_per_batch > 0 ? rows_per_batch : N, eps, seed, stream, 0u, 1.f, g_seed_off};
   if (drop_p > 0.f) {
     a.thr16 = (unsigned)llrintf(drop_p * 65536.f);
     a.drop_scale = 1.f / (1.f - drop_p);
@@ -465,7 +467,7 @@ FDDM_API int fddm_ln_bwd(int dy_dtype, const float* dout, const float* s, const 
   if (N <= 0) return 0;
   if (d > 64 * LN_MAXPL) return (int)hipErrorInvalidValue;
   LnBwdArgs a{dout, s, mean, rstd, gamma, beta, film_scale, dres, dy_t, dgamma, dbeta, dfilm_scale, dfilm_shift,
-              N, d, rows_per_batch > 0 ? rows_per_batch : N, seed, stream, 0u, 1.f};
+              N, d, rows_per_batch > 0 ? rows_per_batch : N, seed, stream, 0u, 1.f, g_seed_off};
   if (drop_p > 0.f) {
     a.thr16 = (unsigned)llrintf(drop_p * 65536.f);
     a.drop_scale = 1.f / (1.f - drop_p);

@@ -511,7 +511,9 @@ class TextEmbedFn(torch.autograd.Function):
         cd = rt.compute_dtype()
         dzt = _t(dz2)       # compute-dtype operand: the f32-A form fell back to the register-staged GEMM (121 us)
         dxhat = ops.linear_dx(dzt, rt.wt(weight), out_dtype=cd)
-        dW = ops.linear_dw(dzt, xhat)
+        dW, aw = _gdst(weight)           # the optimizer's aux-arena view (accumulated in place) or a fresh tensor
+        ops.linear_dw(dzt, xhat, out=dW, accumulate=aw)
+        dW = _ret(dW, aw)
         ptr = ctx.lptr
         kl = _kl_dz.get(ptr)
         if (kl is not None and cd == torch.bfloat16 and ptr in _head_outputs and ptr not in _dlogits_bf16

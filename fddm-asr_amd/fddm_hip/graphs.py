@@ -91,3 +91,88 @@ class GraphedEncoder:
         self.enc.backbone.stage_conv1(s.h0, out=s.h1)
         s.gC.replay()
         return s.out
+
+
+class StepGraphs:
+    """HIP-graph replay of the decoder's train step (reference train.py:340-443 from the decoder forward to the
+    optimizer step): decoder forward, KL, the L_fd branch, backward, clip + AdamW — ~230 (C2) / ~450 (C4) launches
+    per step enqueued from Python — captured once per step kind (KL-only / L_fd) and replayed as one graph launch.
+
+    The train loop runs the FIRST step of each kind eagerly (its launches create every cached weight copy, table,
+    optimizer chunk table and gradient-arena binding the step reads), then captures that kind right away (capture
+    executes nothing); later steps of the kind copy their inputs (condition c, x0, t, x_t) into the graphs' static
+    buffers and replay. Inputs stay eager: q_sample and the t draw run before the replay, so user schedulers and
+    t-draws keep working.
+
+    Dropout seeds: the captured launches read their seed as seed + *off (fddm_set_seed_offset, common.h eff_seed).
+    At capture the seed counter is restored afterwards (capturing draws no seeds); before a replay `off` is filled
+    with (counter now - counter at capture) and the counter is advanced by the number of seeds the step draws, so a
+    replayed step uses exactly the seeds — and dropout masks — an eager step would.
+
+    Validity: a graph reads parameters, cached bf16 weights, optimizer moments / chunk tables and gradient-arena views
+    by address. It is dropped (and the step runs eagerly, then recaptures) when the runtime cache epoch changes
+    (clear_cache), when any trainable parameter is replaced or changed by a torch op (data_ptr / _version), or when
+    the optimizer rebuilt its tables (FusedAdamW.table_epoch). The two kinds share one memory pool (they replay on one
+    stream, never concurrently; their outputs stay live)."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.graphs: dict = {}
+        self.static: dict = {}
+        self.pool = None
+        self.off = torch.zeros(1, device=self.device, dtype=torch.int64)
+
+    def reset(self):
+        """Drop every graph; their memory pool goes with them (a new capture starts a new pool)."""
+        self.graphs.clear()
+        self.static.clear()
+        self.pool = None
+
+    def _token(self, params, optimizer):
+        return (rt.cache_epoch(), getattr(optimizer, "table_epoch", 0),
+                tuple((p.data_ptr(), p._version) for p in params))
+
+    def get(self, kind, params, optimizer, shapes):
+        s = self.graphs.get(kind)
+        if s is None:
+            return None
+        if s.shapes != shapes or s.token != self._token(params, optimizer):
+            self.reset()             # stale addresses: recapture both kinds
+            return None
+        return s
+
+    def capture(self, kind, fn, inputs: dict, params, optimizer):
+        """Capture fn(**static inputs) -> tuple of output tensors as step kind `kind`."""
+        from ._lib import lib
+        shapes = tuple((k, tuple(v.shape), v.dtype) for k, v in sorted(inputs.items()))
+        if any(self.static.get(k) is None or self.static[k].shape != v.shape or self.static[k].dtype != v.dtype
+               for k, v in inputs.items()):
+            self.reset()
+            self.static = {k: torch.empty_like(v) for k, v in inputs.items()}
+        for k, v in inputs.items():
+            self.static[k].copy_(v)
+        c0 = rt.seed_counter()
+        g = torch.cuda.CUDAGraph()
+        with rt.retaining() as keep:
+            lib().fddm_set_seed_offset(self.off.data_ptr())
+            try:
+                with torch.cuda.graph(g, pool=self.pool):
+                    outs = fn(**self.static)
+            finally:
+                lib().fddm_set_seed_offset(None)
+        nseeds = rt.seed_counter() - c0
+        rt.set_seed_counter(c0)
+        if self.pool is None:
+            self.pool = g.pool()
+        self.graphs[kind] = SimpleNamespace(g=g, outs=outs, c0=c0, nseeds=nseeds, keep=keep, shapes=shapes,
+                                            token=self._token(params, optimizer))
+
+    def replay(self, kind, inputs: dict):
+        s = self.graphs[kind]
+        for k, v in inputs.items():
+            self.static[k].copy_(v, non_blocking=True)
+        c = rt.seed_counter()
+        self.off.fill_(c - s.c0)
+        rt.set_seed_counter(c + s.nseeds)
+        s.g.replay()
+        return s.outs

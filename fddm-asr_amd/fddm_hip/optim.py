@@ -22,8 +22,10 @@ class FusedAdamW(torch.optim.Optimizer):
     def __init__(self, params, lr=2e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
         self._tables = {}
+        self.table_epoch = 0     # bumped whenever a chunk table is (re)built: captured step graphs key on it
         self.last_total_sq = None
         self.arena = None
+        self.aux_arena = None
         self._skipped = None     # device int32: steps skipped by the non-finite guard
 
     def use_grad_arena(self, params, order=None):
@@ -32,6 +34,27 @@ class FusedAdamW(torch.optim.Optimizer):
         instead of dropping grads."""
         self.arena = rt.GradArena(params, order)
         return self.arena
+
+    def use_aux_arena(self, params):
+        """Back the grads of `params` that get a gradient only on some steps (the L_fd projectors, train.py:372-397)
+        by a second flat buffer: zero_grad() still leaves them None (AdamW skips them on KL-only steps, the reference's
+        set_to_none semantics) and attach_aux() binds them to their zeroed views on the steps that produce them, so
+        their gradient buffers keep one address (the kernels accumulate into them; the optimizer's chunk table and a
+        captured step graph stay valid). The fused AdamW's zero_grads pass leaves the views zeroed again."""
+        self.aux_arena = rt.GradArena(params)
+        self.aux_arena.views_zero = True
+        for p in self.aux_arena.params:
+            p.grad = None
+        return self.aux_arena
+
+    def attach_aux(self):
+        a = self.aux_arena
+        if a is None:
+            return
+        if not getattr(a, "views_zero", False):
+            a.flat.zero_()
+        a.attach()
+        a.views_zero = False
 
     def zero_grad(self, set_to_none: bool = True):
         if self.arena is None:
@@ -50,6 +73,9 @@ class FusedAdamW(torch.optim.Optimizer):
             self.arena.attach()
         else:
             self.arena.zero_()
+        if self.aux_arena is not None and set_to_none:
+            for p in self.aux_arena.params:
+                p.grad = None
 
     @staticmethod
     def _bufs_live(plist, bufs) -> bool:
@@ -74,8 +100,13 @@ class FusedAdamW(torch.optim.Optimizer):
                 t["gen"] = rt.wcache_generation()
                 return t
             del self._tables[key]
+            self.table_epoch += 1   # a table a captured step may read was replaced
         if len(self._tables) >= 8:  # the train step alternates between a few parameter sets (L_fd steps add the
             self._tables.clear()    # projectors): keep each set's device table instead of rebuilding it per switch
+            self.table_epoch += 1
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("FusedAdamW: a chunk table would be built inside a HIP-graph capture (its host-to-"
+                               "device copy cannot be captured); run one eager step of this parameter set first")
         ct, cs, numel, pp, gp, mp, vp, bp, sp, bufs = [], [], [], [], [], [], [], [], [], []
         for i, p in enumerate(plist):
             st = self.state[p]
@@ -116,6 +147,7 @@ class FusedAdamW(torch.optim.Optimizer):
     def load_state_dict(self, state_dict):
         super().load_state_dict(state_dict)
         self._tables.clear()
+        self.table_epoch += 1
         for group in self.param_groups:
             for p in group["params"]:
                 if self.state.get(p):
@@ -166,6 +198,12 @@ class FusedAdamW(torch.optim.Optimizer):
             a = self.arena
             self.arena.clean = all(p.grad is not None and p.grad.data_ptr() == v.data_ptr()
                                    for p, v in zip(a.params, a.views))
+        if self.aux_arena is not None:
+            a = self.aux_arena
+            used = [p.grad is not None for p in a.params]
+            if any(used):   # zeroed by this pass only when every view was read through its own address
+                a.views_zero = bool(zero_grads) and all(
+                    p.grad is not None and p.grad.data_ptr() == v.data_ptr() for p, v in zip(a.params, a.views))
         self.last_total_sq = total
         return total.sqrt() * grad_scale if grad_scale != 1.0 else total.sqrt()
 

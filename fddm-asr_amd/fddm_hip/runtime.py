@@ -164,6 +164,19 @@ def next_seed() -> int:
     return (_base_seed * 1000003 + _seed_counter) & 0x7FFFFFFFFFFFFFFF
 
 
+def seed_counter() -> int:
+    """The dropout-seed counter (next_seed returns base * 1000003 + counter + 1); graph replays advance it."""
+    global _base_seed
+    if _base_seed is None:       # fixed now (as next_seed would), not inside a capture
+        _base_seed = int(torch.initial_seed()) & 0xFFFFFFFF
+    return _seed_counter
+
+
+def set_seed_counter(c: int) -> None:
+    global _seed_counter
+    _seed_counter = int(c)
+
+
 def reseed(seed: int) -> None:
     global _base_seed, _seed_counter
     _base_seed = int(seed) & 0xFFFFFFFF
@@ -335,6 +348,11 @@ def probe(name: str, replay=None):
             replay()
         r1.record(s)
         _probes.setdefault(name + "#replay", []).append((r0, r1, _replay_n))
+
+
+def probing_any(prefix: str) -> bool:
+    """True while probing() collects a launch site whose name starts with `prefix`."""
+    return _probes is not None and any(n.startswith(prefix) for n in _probes)
 
 
 @contextlib.contextmanager

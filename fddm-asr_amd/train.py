@@ -28,7 +28,7 @@ from fddm_hip import dist as fdist
 from fddm_hip import functions as FN
 from fddm_hip import runtime as rt
 from fddm_hip._lib import lib as _fddm_lib
-from fddm_hip.graphs import GraphedEncoder
+from fddm_hip.graphs import GraphedEncoder, StepGraphs
 from fddm_hip.optim import FusedAdamW
 from losses.fddm_losses import lfd_loss
 from models.acoustic_encoder import AcousticEncoder
@@ -178,6 +178,7 @@ def _encoded(encoder, loader, device, optimizer):
 
 
 LAST_ENQUEUE_DONE = 0.0
+_STEP_GRAPHS = weakref.WeakKeyDictionary()    # decoder -> StepGraphs (HIP-graph replay of the decoder step)
 # DP all-reduce tail (bench.py --gpus N): HIP events on the compute stream at the end of backward and after
 # allreduce_grads (the stream has waited for every gradient slice); ALLREDUCE_TAIL collects the event pairs
 ALLREDUCE_TAIL: list | None = None
@@ -194,6 +195,18 @@ def _mark_allreduce_tail(start=None):
     return ev
 _ENC_STREAMS: dict = {}
 _ENC_GRAPHS = weakref.WeakKeyDictionary()     # encoder -> GraphedEncoder (released with the encoder)
+
+
+def _step_graph_ok(device, scaler, optimizer, arena) -> bool:
+    """HIP-graph replay of the decoder step (fddm_hip.graphs.StepGraphs), opt-in with FDDM_STEP_GRAPH=1: bf16 on a GPU
+    with the fused optimizer and its grad arena, no GradScaler, one process (the DP all-reduce is issued from
+    backward callbacks and stays eager). Off by default: on this ROCm 7 / torch 2.10 stack a replayed step ran 12.9
+    ms against 9.94 eager at C2 (tools/ab_graph.sh; the graph launch runs ~1.3 ms longer on the GPU than the same
+    launches enqueued eagerly and no longer overlaps the encoder's side stream; DEBUG_CLR_GRAPH_PACKET_CAPTURE and
+    DEBUG_HIP_FORCE_GRAPH_QUEUES did not change that) — it pays only where the host, not the GPU, bounds the step."""
+    return (torch.device(device).type == "cuda" and rt.compute_dtype() == torch.bfloat16 and scaler is None and
+            arena is not None and hasattr(optimizer, "clip_and_step") and fdist.world() == 1 and
+            os.environ.get("FDDM_STEP_GRAPH", "0") == "1")
 
 
 def _enc_stream(dev):
@@ -246,16 +259,20 @@ def train_one_epoch(encoder, decoder, s_proj, t_embed, t_proj, scheduler, loader
         pbar = tqdm(loader, desc=f"Epoch {epoch} [train]", leave=False)
     loss_sum = torch.zeros((), device=device)
     nsteps = 0
-    for c, c_mask, x0 in _encoded(encoder, pbar, device, optimizer):
-        B, L = x0.shape
-        t = draw_t(B) if draw_t is not None else torch.randint(1, T_total + 1, (B,), device=device)
-        xt = scheduler.sample_q(x0, t)
+    aux = [p for m in (s_proj, t_embed, t_proj) for p in m.parameters() if p.requires_grad]
+    if (arena is not None and getattr(optimizer, "aux_arena", 1) is None and aux and
+            all(id(p) in set(id(q) for g in optimizer.param_groups for q in g["params"]) for p in aux)):
+        optimizer.use_aux_arena(aux)    # L_fd projector grads at fixed addresses (None on KL-only steps)
+
+    def step(c, c_mask, x0, t, xt, fd):
+        """train.py:351-423 from the decoder forward to the optimizer step; returns (loss, loss_diff, loss_fd)."""
         x_mask = x0 != pad_id
         logits = decoder(xt, t, c, x_mask=x_mask, c_mask=c_mask)
         loss_diff = scheduler.kl_term(xt, x0, logits, t, x_mask)
         loss = loss_diff
         loss_fd = None
-        if global_step % n_step_fd == 0:
+        if fd:
+            L = x0.shape[1]
             z_text = t_proj(t_embed(logits))
             z_speech = align_speech(s_proj(c), L)
             w_t = scheduler.w_t(t).mean()
@@ -266,6 +283,8 @@ def train_one_epoch(encoder, decoder, s_proj, t_embed, t_proj, scheduler, loader
                 loss_fd = lfd_loss(z_speech, z_text, lambda_offdiag=lambda_off)
             loss = loss + tau * w_t * loss_fd
         optimizer.zero_grad(set_to_none=True)
+        if fd and hasattr(optimizer, "attach_aux"):
+            optimizer.attach_aux()
         if scaler is not None:
             scaler.scale(loss).backward()
             fdist.allreduce_grads(trainable)    # before unscale_: overlapped slices may still be in flight
@@ -286,6 +305,31 @@ def train_one_epoch(encoder, decoder, s_proj, t_embed, t_proj, scheduler, loader
             else:
                 torch.nn.utils.clip_grad_norm_([p for p in trainable if p.grad is not None], max_norm=5.0)
                 optimizer.step()
+        return loss, loss_diff, loss_fd
+
+    graphs = None
+    if _step_graph_ok(device, scaler, optimizer, arena):
+        graphs = _STEP_GRAPHS.get(decoder)
+        if graphs is None:
+            graphs = _STEP_GRAPHS[decoder] = StepGraphs(device)
+    for c, c_mask, x0 in _encoded(encoder, pbar, device, optimizer):
+        B, L = x0.shape
+        t = draw_t(B) if draw_t is not None else torch.randint(1, T_total + 1, (B,), device=device)
+        xt = scheduler.sample_q(x0, t)
+        fd = global_step % n_step_fd == 0
+        # HIP-event probes of decoder launches (bench.py's attention rows) need the eager launches
+        if graphs is not None and c_mask is None and not rt.probing_any("decoder."):
+            inputs = {"c": c, "x0": x0, "t": t, "xt": xt}
+            shapes = tuple((k, tuple(v.shape), v.dtype) for k, v in sorted(inputs.items()))
+            if graphs.get(fd, trainable, optimizer, shapes) is not None:
+                loss, loss_diff, loss_fd = graphs.replay(fd, inputs)
+            else:
+                # the first step of this kind runs eagerly (creating every cache / table it reads), then the kind is
+                # captured for the next one (a capture executes nothing)
+                loss, loss_diff, loss_fd = step(c, None, x0, t, xt, fd)
+                graphs.capture(fd, lambda c, x0, t, xt: step(c, None, x0, t, xt, fd), inputs, trainable, optimizer)
+        else:
+            loss, loss_diff, loss_fd = step(c, c_mask, x0, t, xt, fd)
         loss_sum += loss.detach()
         nsteps += 1
         if tqdm is not None and print_epoch_summary and (global_step % log_every == 0):

@@ -185,6 +185,11 @@ int fddm_lfd_bwd_colstat(int zt_dtype, const float* dzt, const void* zt, float* 
 int fddm_lfd_std_bwd_apply(int zt_dtype, const float* dzt, const void* zt, const float* inv_std, const float* sums,
                            float inv_n, float scale, float* dz, long B, long C, void* hip_stream);
 
+/* ---- dropout-seed offset for HIP-graph replays of the train step: every launch enqueued while `off` (a device u64)
+ *      is set reads its effective dropout seed as seed + *off at run time (null: none), so one captured step replays
+ *      with the seeds the host's counter has moved on to (identical to an eager step's). Returns 1 if one was set. */
+int fddm_set_seed_offset(const unsigned long long* off);
+
 /* ---- clip_grad_norm_ + AdamW (train.py:411-423), multi-tensor over a chunk table.
  *      fddm_adamw: bias corrections from the per-tensor device step counters `step` (advanced by the call);
  *      max_norm > 0 clips by the gradient norm sqrt(*total); a non-finite *total skips the whole step (the

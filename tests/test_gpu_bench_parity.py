@@ -2,27 +2,33 @@
 the benchmark's batch.
 
 `bench.build()` builds the models exactly as the timed run does: WavLM-base encoder (random init) + 6-layer
-d_model 512 / 8 heads / ff 2048 decoder, V = 8000, T = 200, dropout 0.1, bf16, fused AdamW. Two teacher-forced
-steps of `train.train_one_epoch` (global steps 3 and 4: a KL step and an L_fd step, reference train.py:340-443) run
-on B = 32 utterances of 10 s audio, so every launch takes the benchmark's kernel choice — gemm256 for the decoder's
-FF1 (GELU + dropout epilogue), the vocabulary head and the fused cross-attention K|V GEMM, persistent encoder GEMMs
-on their CU caps under HIP-graph replay on the side stream (both graph slots), the decoder attention kernels at
-their benchmark grids. The tests in tests/test_gpu_step_configs.py run the same geometry at B = 2, where those
-GEMMs fall to gemm128.
+d_model 512 / 8 heads / ff 2048 decoder, V = 8000, T = 200, dropout 0.1, bf16, fused AdamW. Four teacher-forced
+steps of `train.train_one_epoch` (global steps 3..6 with n_step_fd 2: KL, L_fd, KL, L_fd, reference
+train.py:340-443) run on B = 32 utterances of 10 s audio, so every launch takes the benchmark's kernel choice — gemm256
+for the decoder's FF1 (GELU + dropout epilogue), the vocabulary head and the fused cross-attention K|V GEMM,
+persistent encoder GEMMs on their CU caps under HIP-graph replay on the side stream (both graph slots), the decoder
+attention kernels (fwd6 with the dropout keep bits of every block written ahead, dq4 / dkv4 or the fused
+self-attention backward) at their benchmark grids. The tests in tests/test_gpu_step_configs.py run the same geometry
+at B = 2, where those GEMMs fall to gemm128.
 
 C4 (`bench.py --config c4`): 12-layer d_model 768 / 12 heads decoder, L = 512 > S = 499 (the repeat branch of the
 S -> L alignment, reference train.py:382-387), B = 16. At this batch the d768-wide GEMMs have 96 tiles of 256^2 and
-run on gemm256 (`prefer_256` from 64 tiles), and the L = 512 attention kernels (fwd3 with K / V resident, dq2 / dkv2
-streamed backward) run at their full grid; the encoder's hidden width equals d_model, so encoder.proj is the identity.
+run on gemm256 (`prefer_256` from 64 tiles), and the L = 512 attention kernels run at their full grid; the encoder's
+hidden width equals d_model, so encoder.proj is the identity.
+
+"c2-graph": the same C2 run with the decoder step replayed from HIP graphs (FDDM_STEP_GRAPH=1, train.StepGraphs):
+steps 3 and 4 run eagerly and capture their kind, steps 5 and 6 are replays. The taps below are device clones, so
+they work inside the captures (a capture's clones hold its replay's values).
 
 The CPU oracle (oracle/fddm_oracle.py: oracle_train_step, decoder dropout under the RNG contract) is run twice per
 step's evidence:
-* the encoder: 2 utterances of each batch (one per graph slot) through O.acoustic_encoder against the GPU's
-  B = 32 output;
-* the decoder step: from the GPU's own bf16 acoustic condition c (upcast to fp32), so the encoder's rounding is
-  removed and what remains is the decoder forward / KL / L_fd / backward error of the bf16 path. The per-stage
-  errors (logits, dlogits, each block's dX, every parameter gradient) are printed as the error budget and the
-  tolerances below are set from them (about 2x the measured worst).
+* the encoder: 2 utterances of 2 batches (one per graph slot) through O.acoustic_encoder against the GPU's B = 32
+  output;
+* the decoder step: from the GPU's own bf16 acoustic condition c (upcast to fp32) and the GPU's parameters at the
+  step's start, so the encoder's rounding and the earlier steps' bf16 drift are removed and what remains is the
+  decoder forward / KL / L_fd / backward error of the bf16 path. The per-stage errors (logits, dlogits, each block's
+  dX, every parameter gradient) are printed as the error budget and the tolerances below are set from them (about 2x
+  the measured worst).
 """
 from types import SimpleNamespace
 
@@ -52,7 +58,12 @@ def _args(name):
     return SimpleNamespace(seconds=10.0, precision="bf16", config=name, **CONFIGS[name])
 
 
-@pytest.fixture(scope="module", params=sorted(CONFIGS))
+NSTEP = 4          # global steps 3..6 with n_step_fd 2: KL, L_fd, KL, L_fd
+KINDS = ("kl", "lfd", "kl", "lfd")
+
+
+@pytest.fixture(scope="module", params=[("c2", False), ("c4", False), ("c2", True)],
+                ids=["c2", "c4", "c2-graph"])
 def bench_run(request):
     import bench
     import train as T_
@@ -60,27 +71,30 @@ def bench_run(request):
     from fddm_hip import runtime as rt
     from models.denoise_decoder import DecoderBlock
 
-    args = _args(request.param)
+    cname, graph = request.param
+    args = _args(cname)
     B, L, V, Tn = args.batch, args.seq_len, 8000, 200
     old_prec = rt.precision()
     torch.manual_seed(1337)
     T_, cfg, models, opt = bench.build(args, dev)
+    cfg.lfd["n_step_fd"] = 2       # both step kinds run eagerly once, are captured, then replay once each
     enc, dec, sp, te, tp, sch = models
     named = [("decoder." + n, p) for n, p in dec.named_parameters()]
     for pre, m in (("s_proj.", sp), ("t_embed.", te), ("t_proj.", tp)):
         named += [(pre + n, p) for n, p in m.named_parameters()]
-    init = {n: p.detach().float().cpu().clone() for n, p in named}
     enc_sd = {k: v.detach().float().cpu() for k, v in enc.state_dict().items()}
-    batches = bench.synthetic_batches(args, dev, 2, 77)
+    batches = bench.synthetic_batches(args, dev, NSTEP, 77)
     g = torch.Generator().manual_seed(9)
-    ts = [torch.randint(1, Tn + 1, (B,), generator=g) for _ in range(2)]
+    ts = [torch.randint(1, Tn + 1, (B,), generator=g) for _ in range(NSTEP)]
     ts[0][:3] = torch.tensor([1, 2, Tn])          # t = 1 (beta_{t-1} = 0 rule), t = 2 and t = T
     _, ab = O.sched_tables(Tn)
     betas, _ = O.sched_tables(Tn)
     x0s = [b[1].cpu() for b in batches]
     xts = [O.sample_xt(x0, t, V, ab, seed=60 + i) for i, (x0, t) in enumerate(zip(x0s, ts))]
 
-    rec = {"c": [], "logits": [], "kl": [], "lfd": [], "grads": [], "dlogits": [], "dx": {}}
+    # taps: device clones only (they run inside the step-graph captures too; a capture's clones hold the values of
+    # that graph's replay). rec lists are in host-call order; `cap` marks the records made while capturing.
+    rec = {"c": [], "logits": [], "kl": [], "lfd": [], "grads": [], "params": [], "dlogits": [], "dx": {}, "cap": []}
     step = [-1]
     xq = iter([x.to(dev) for x in xts])
     tq = iter([t.to(dev) for t in ts])
@@ -99,9 +113,10 @@ def bench_run(request):
 
     def dec_forward(xt, t, cond, *a, **k):
         step[0] += 1
-        rec["c"].append(cond.detach().float().cpu())
+        rec["cap"].append(torch.cuda.is_current_stream_capturing())
+        rec["c"].append(cond.detach().clone())
         out = fwd(xt, t, cond, *a, **k)
-        rec["logits"].append(out.detach().float().cpu())
+        rec["logits"].append(out.detach().clone())
         return out
 
     run_blk = DecoderBlock.run
@@ -109,7 +124,7 @@ def bench_run(request):
     def run_tap(self, x, xT, cT, key_keep, film, B_, L_, S_, layer, *a, **k):
         x3, x3T = run_blk(self, x, xT, cT, key_keep, film, B_, L_, S_, layer, *a, **k)
         key = (step[0], layer)
-        x3.register_hook(lambda gr: rec["dx"].__setitem__(key, gr.detach().float().cpu()))
+        x3.register_hook(lambda gr: rec["dx"].__setitem__(key, gr.detach().clone()))
         return x3, x3T
 
     head_bwd = FN.HeadFn.backward
@@ -119,13 +134,14 @@ def bench_run(request):
         eff = None if dz16 is None else dz16.float()
         if dlogits is not None and not all(s_ == 0 for s_ in dlogits.stride()):
             eff = dlogits.float() if eff is None else eff + dlogits.float().reshape(eff.shape)
-        rec["dlogits"].append(None if eff is None else eff.cpu())
+        rec["dlogits"].append(None if eff is None else eff.clone())
         return head_bwd(ctx, dlogits)
 
     inner = opt.clip_and_step
 
-    def snap(*a, **k):
-        rec["grads"].append({n: (None if p.grad is None else p.grad.detach().float().cpu().clone()) for n, p in named})
+    def snap(*a, **k):     # the step's gradients as clip_grad_norm_ sees them, and its parameters (before the update)
+        rec["grads"].append({n: (None if p.grad is None else p.grad.detach().clone()) for n, p in named})
+        rec["params"].append({n: p.detach().clone() for n, p in named})
         return inner(*a, **k)
 
     orig_lfd = T_.lfd_loss
@@ -136,6 +152,7 @@ def bench_run(request):
         return v
 
     with pytest.MonkeyPatch.context() as mp:
+        mp.setenv("FDDM_STEP_GRAPH", "1" if graph else "0")
         mp.setattr(rt, "next_seed", lambda: SEED)
         mp.setattr(dec, "forward", dec_forward)
         mp.setattr(DecoderBlock, "run", run_tap)
@@ -145,42 +162,56 @@ def bench_run(request):
         gs, _ = T_.train_one_epoch(enc, dec, sp, te, tp, sch_tf, batches, opt, dev, cfg, 3, None, 1, False,
                                    draw_t=lambda B_: next(tq))
         torch.cuda.synchronize()
-    assert gs == 5 and len(rec["kl"]) == 2 and len(rec["lfd"]) == 1 and len(rec["grads"]) == 2
-    rec["kl"] = [float(v.detach()) for v in rec["kl"]]
-    rec["lfd"] = float(rec["lfd"][0].detach())
-    waves2 = [b[0][[0, B - 1]].cpu() for b in batches]      # 2 utterances per batch for the encoder check
-    del enc, dec, sp, te, tp, opt, models, batches
+    assert gs == 3 + NSTEP and len(rec["kl"]) == NSTEP and len(rec["lfd"]) == 2 and len(rec["grads"]) == NSTEP
+    graphed = any(rec["cap"])
+    # host-call order -> step: eager, the graph-mode train loop calls step 3 (KL eager), capture KL (replayed at 5),
+    # step 4 (L_fd eager), capture L_fd (replayed at 6)
+    order = [0, 2, 1, 3] if graphed else [0, 1, 2, 3]
+    assert rec["cap"] == ([False, True, False, True] if graphed else [False] * 4), rec["cap"]
+    lfd_order = [0, 1]          # L_fd records: step 4 (eager), then the capture replayed at step 6 (or step 6 eager)
+    cpu = lambda x: None if x is None else x.float().cpu()  # noqa: E731
+    R = {"c": [cpu(rec["c"][j]) for j in order], "logits": [cpu(rec["logits"][j]) for j in order],
+         "kl": [float(rec["kl"][j].detach()) for j in order], "lfd": [float(rec["lfd"][j].detach()) for j in lfd_order],
+         "dlogits": [cpu(rec["dlogits"][j]) for j in order],
+         "grads": [{n: cpu(v) for n, v in rec["grads"][j].items()} for j in order],
+         "params": [{n: cpu(v) for n, v in rec["params"][j].items()} for j in order],
+         "dx": {(i, k): cpu(rec["dx"][(j, k)]) for i, j in enumerate(order) for k in range(args.layers)},
+         "graphed": graphed}
+    waves2 = [b[0][[0, B - 1]].cpu() for b in batches[:2]]      # 2 utterances of 2 batches for the encoder check
+    del enc, dec, sp, te, tp, opt, models, batches, rec
     rt.set_precision(old_prec)
     torch.cuda.empty_cache()
 
-    # ---- CPU oracle: the encoder on 2 utterances of each batch, the two steps from the GPU's condition
+    # ---- CPU oracle: the encoder on 2 utterances of 2 batches; every step from the GPU's condition and the GPU's
+    # parameters at the step's start (the step's own error, not the bf16 drift of earlier AdamW updates)
     torch.set_num_threads(min(16, torch.get_num_threads()))
     geom = O.wavlm_geometry()
     c_ref2 = [O.acoustic_encoder(enc_sd, w, geom, args.d_model) for w in waves2]
-    params = {k: v.clone() for k, v in init.items()}
-    ocfg = dict(d_model=args.d_model, nhead=args.heads, num_layers=args.layers, pad_id=0, n_step_fd=4, tau=1.0,
+    ocfg = dict(d_model=args.d_model, nhead=args.heads, num_layers=args.layers, pad_id=0, n_step_fd=2, tau=1.0,
                 lambda_offdiag=5e-3)
-    oopt = O.OracleAdamW()
     ref = []
-    for i in range(2):
+    for i in range(NSTEP):
         taps = []
-        r = O.oracle_train_step(params, None, None, None, x0s[i], ts[i], xts[i], ocfg, oopt, 3 + i, betas, ab,
-                                c=rec["c"][i], dropout=0.1, seed=SEED, taps=taps)
+        params = {k: v.clone() for k, v in R["params"][i].items()}
+        r = O.oracle_train_step(params, None, None, None, x0s[i], ts[i], xts[i], ocfg, O.OracleAdamW(), 3 + i, betas,
+                                ab, c=R["c"][i], dropout=0.1, seed=SEED, taps=taps)
         r["dx"] = [x.grad.detach().clone() for x in taps]
         r.pop("c")
         ref.append(r)
-    assert ref[0]["lfd"] is None and ref[1]["lfd"] is not None
-    if args.seq_len > rec["c"][0].shape[1]:
+    assert [r["lfd"] is not None for r in ref] == [k == "lfd" for k in KINDS]
+    if args.seq_len > R["c"][0].shape[1]:
         assert args.config == "c4"     # C4 takes the S < L repeat branch of the alignment (train.py:382-387)
-    return SimpleNamespace(rec=rec, ref=ref, c_ref2=c_ref2, args=args, tol=TOL[args.config])
+    return SimpleNamespace(rec=R, ref=ref, c_ref2=c_ref2, args=args, tol=TOL[args.config], graph=graph)
 
 
 # tolerances per config (about 2x the measured worst; the measured values are in the comments of each test)
-TOL = {"c2": dict(kl=2e-4, lfd=1e-3, logits=1e-2, dlogits=5e-3, dx=1e-2, gnorm=2e-2, grad=(1.2e-2, 3e-2)),
-       # C4 measured (B = 16, 12 blocks): logits 4.0e-3, dlogits 2.0e-3, dX <= 7.5e-3 (deepest block, L_fd step), global
-       # norm 7e-5 / 4.1e-3, worst parameter 6.2e-3 (KL step: ff.0.weight) and 2.85e-2 (L_fd step: t_embed.proj.weight;
-       # worst decoder parameter there 9.7e-3), KL 2e-6, L_fd 0
-       "c4": dict(kl=2e-4, lfd=1e-3, logits=1e-2, dlogits=5e-3, dx=1.5e-2, gnorm=2e-2, grad=(1.2e-2, 6e-2))}
+TOL = {"c2": dict(kl=2e-4, lfd=1e-3, logits=1e-2, dlogits=5e-3, dx=1e-2, gnorm=(5e-3, 2e-2), grad=(1.2e-2, 4e-2)),
+       # C4 measured (B = 16, 12 blocks, 4 steps): logits <= 4.0e-3, dlogits <= 2.6e-3, dX <= 4.6e-3, global norm
+       # <= 1e-4 (KL steps) / 3.8e-2 (L_fd steps: the projector gradients, whose batch-dim standardisation amplifies
+       # the bf16 rounding of z_text / z_speech), worst parameter 6.2e-3 (KL) and 3.2e-2 (L_fd: t_proj / t_embed;
+       # worst decoder parameter 6.1e-3), KL <= 3e-6, L_fd <= 1.2e-7. C2: global norm <= 2e-4 / 9.9e-3, worst
+       # parameter 5.4e-3 / 1.9e-2
+       "c4": dict(kl=2e-4, lfd=1e-3, logits=1e-2, dlogits=5e-3, dx=1e-2, gnorm=(5e-3, 8e-2), grad=(1.2e-2, 6e-2))}
 
 
 def test_bench_encoder_output_matches_oracle(bench_run):
@@ -199,13 +230,16 @@ def test_bench_encoder_output_matches_oracle(bench_run):
 def test_bench_step_values_match_oracle(bench_run):
     """KL (both steps) and L_fd at B = 32 from the same condition: the bf16 decoder's loss values."""
     R = bench_run
-    for i in range(2):
+    assert R.rec["graphed"] == R.graph, "graph mode: steps 5 and 6 must be HIP-graph replays"
+    for i in range(NSTEP):
         e = abs(R.rec["kl"][i] - R.ref[i]["kl"]) / abs(R.ref[i]["kl"])
-        print(f"KL step {i}: {R.rec['kl'][i]:.6f} vs {R.ref[i]['kl']:.6f} (rel {e:.2e})")
+        print(f"KL step {i} ({'replay' if (i >= 2 and R.graph) else 'eager'}): {R.rec['kl'][i]:.6f} vs {R.ref[i]['kl']:.6f} "
+              f"(rel {e:.2e})")
         assert e < R.tol["kl"]          # measured C2 7e-7 / 9e-6
-    e = abs(R.rec["lfd"] - R.ref[1]["lfd"]) / abs(R.ref[1]["lfd"])
-    print(f"L_fd: {R.rec['lfd']:.6f} vs {R.ref[1]['lfd']:.6f} (rel {e:.2e})")
-    assert e < R.tol["lfd"]
+    for j, i in enumerate((1, 3)):
+        e = abs(R.rec["lfd"][j] - R.ref[i]["lfd"]) / abs(R.ref[i]["lfd"])
+        print(f"L_fd step {i}: {R.rec['lfd'][j]:.6f} vs {R.ref[i]['lfd']:.6f} (rel {e:.2e})")
+        assert e < R.tol["lfd"]
 
 
 def test_bench_step_error_budget(bench_run):
@@ -214,7 +248,7 @@ def test_bench_step_error_budget(bench_run):
     then every parameter gradient as clip_grad_norm_ sees it (norm-wise, floor 1e-3 of the global norm; same None
     pattern) and the global gradient norm."""
     R = bench_run
-    for i in range(2):
+    for i in range(NSTEP):
         el = rel(R.rec["logits"][i], R.ref[i]["logits"])
         ed = rel(R.rec["dlogits"][i].view_as(R.ref[i]["dlogits"]), R.ref[i]["dlogits"])
         dxs = [rel(R.rec["dx"][(i, k)].view_as(R.ref[i]["dx"][k]), R.ref[i]["dx"][k]) for k in range(R.args.layers)]
@@ -236,5 +270,5 @@ def test_bench_step_error_budget(bench_run):
         print(f"step {i}: global grad norm {Gg:.6e} vs {G:.6e}; worst grad rel err " +
               ", ".join(f"{n} {v:.2e}" for n, v in worst))
         # measured: global norm 2e-4 / 8.5e-3; worst parameter 5.4e-3 (KL step), 1.4e-2 (L_fd step: projectors)
-        assert abs(Gg - G) <= R.tol["gnorm"] * G
-        assert worst[0][1] <= R.tol["grad"][i], worst
+        assert abs(Gg - G) <= R.tol["gnorm"][KINDS[i] == "lfd"] * G
+        assert worst[0][1] <= R.tol["grad"][KINDS[i] == "lfd"], worst
