@@ -37,7 +37,7 @@ def main():
     rows = list(csv.DictReader(open(path)))
     ks = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Stream_Id"], r["Kernel_Name"]) for r in rows]
     ks.sort()
-    c0 = [k for k in ks if "conv0_apply" in k[3]]
+    c0 = [k for k in ks if "conv0_gram_kernel" in k[3]]   # one per encoded batch (the side stream)
     t0, t1 = c0[first][0], c0[first + n][0]
     win = [k for k in ks if t0 <= k[0] < t1]
     per = defaultdict(list)
