@@ -513,7 +513,7 @@ __global__ void __launch_bounds__(256, ATTN_FWD_WPS) fwd2_kernel(AttnArgs a) {
       const f32x2_t sl2v = {sl2, sl2}, nb2 = {nbias, nbias};
       f32x2_t ls2 = {0.f, 0.f};
       uint64_t bits = 0;
-      // dropout keep bits of the lane's 4 keys per block (generic contract form; fwd3 stages the tables in LDS)
+      // dropout keep bits of the lane's 4 keys per block (generic contract form; fwd6 reads precomputed words)
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb) {
         unsigned keep = 0xF;
@@ -626,7 +626,7 @@ __device__ __forceinline__ void pin16(uint4& x) {
 // (NST - 1 tiles in flight) instead of register staging (global loads, LDS writes and their address arithmetic per
 // tile, and a __syncthreads fence that drained the next tile's loads); the smaller LDS footprint lets three
 // workgroups share a CU (fwd2: two). The
-// bias slice of the workgroup's query range and the key mask row are staged once (fwd3's layout). The DMA is
+// bias slice of the workgroup's query range and the key mask row are staged once (as fwd6). The DMA is
 // inline asm (dma16_asm): hipcc does not track it, so it inserts no stream-draining wait before the tile's LDS
 // reads; each tile waits for its own pieces with a counted vmcnt (every wave issues exactly 4 DMA instructions per
 // tile — past the end the last tile is re-read into a free stage — and no other vector-memory instruction in the
@@ -689,7 +689,7 @@ __global__ void __launch_bounds__(256, NG == 1 ? 4 : 2) fwd5_kernel(AttnArgs a) 
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   // ---- K / V stream: wave w fills rows 16w .. 16w+15 of a tile (2 K + 2 V instructions; XOR swizzles on the
-  // per-lane source addresses, as fwd3_kernel)
+  // per-lane source addresses)
   auto fill = [&](int tt, int st) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -787,7 +787,7 @@ __global__ void __launch_bounds__(256, NG == 1 ? 4 : 2) fwd5_kernel(AttnArgs a) 
       const f32x2_t sl2v = {sl2, sl2}, nb2 = {nbias, nbias};
       f32x2_t ls2 = {0.f, 0.f};
       uint64_t bits = 0;
-      // dropout keep bits of the lane's 4 keys per block (generic contract form; fwd3 stages the tables in LDS)
+      // dropout keep bits of the lane's 4 keys per block (generic contract form; fwd6 reads precomputed words)
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb) {
         unsigned keep = 0xF;
@@ -888,306 +888,12 @@ __global__ void __launch_bounds__(256, NG == 1 ? 4 : 2) fwd5_kernel(AttnArgs a) 
   }
 }
 
-// ------------------------------------------------------------------------------- fwd (bf16, v3)
-// K/V resident in LDS: for Lk <= 512 the whole key range of one (b, h) fits (2 x Lk_pad x 128 B <= 128 KB), so
-// the workgroup streams every K and V row into LDS once, by LDS-DMA issued up front in tile order (8 rows of
-// 128 B per wave instruction, the XOR swizzles applied to the per-lane SOURCE addresses), and the tile loop
-// then runs on LDS reads, MFMAs and VALU only: no per-tile register staging, no per-tile workgroup barrier
-// once the tiles have landed (a tile's barrier is passed while later tiles are still in flight). The per-key
-// mask row (key padding, keys >= Lk) and, for WavLM, the relative-bias slice of the workgroup's whole query
-// range are staged once as well. NW waves x 2 query groups x 16 = 32*NW queries per workgroup; the per-tile
-// softmax / dropout / P.V code is that of fwd2_kernel.
-// NG = 1 with NW = 16 (round 2 probe): 16 queries per wave, 16 waves per workgroup — 4 waves per SIMD instead of
-// 2 for the same LDS footprint, each K / V fragment feeding one MFMA instead of two.
-template <bool DROP, bool MASK, bool REL, int NW, int NG = 2>
-__global__ void __launch_bounds__(64 * NW, 1) fwd3_kernel(AttnArgs a) {
-  constexpr int QW = 16 * NG * NW;
-  static_assert(NW == 4 || NW == 8 || NW == 16, "fwd3 wave count");
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem3[];
-  const int ntiles = (a.Lk + 63) / 64, LkP = ntiles * 64;
-  unsigned char* kres = smem3;                                  // [LkP][128 B] KC image
-  unsigned char* vres = smem3 + LkP * 128;                      // [LkP][128 B] tr-read image
-  float* mfull = (float*)(smem3 + 2 * LkP * 128);               // [LkP] 0 / -inf
-  float* tfull = mfull + LkP;                                   // [LkP + QW] relative-bias slice (REL)
-  unsigned char* dtab = (unsigned char*)(mfull + LkP + (REL ? LkP + QW : 0));  // [3][4096] u16 (DROP)
-  ARTIME(14);
-  ASTAMP(0);
-  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
-            i = lane & 15;
-  int bxi, bh;
-  xcd_tile(bxi, bh);
-  const int b = bh / a.H, h = bh % a.H;
-  const int qbase = bxi * QW;
-  const bf16_t* Qb = (const bf16_t*)a.Q + (long)b * a.Lq * a.sq + h * DH;
-  const bf16_t* Kb = (const bf16_t*)a.K + (long)b * a.Lk * a.sk + h * DH;
-  const bf16_t* Vb = (const bf16_t*)a.V + (long)b * a.Lk * a.sv + h * DH;
-  // ---- LDS-DMA fill, tile order: wave w's instruction for tile t covers rows 64t + 8w' .. +7 for w' = w, w+NW..
-  {
-    typedef __attribute__((address_space(1))) const void* gp_t;
-    typedef __attribute__((address_space(3))) void* lp_t;
-    for (int t = 0; t < ntiles; ++t) {
-      if constexpr (NW == 16) {  // waves 0-7: K rows 8w.., waves 8-15: V rows 8(w-8)..
-        const int R = 64 * t + 8 * (w & 7);
-        const int r = R + (lane >> 3), pch = lane & 7;
-        const int rr = min(r, a.Lk - 1);
-        if (w < 8) {
-          const int ck = pch ^ ((r >> 1) & 7);
-          __builtin_amdgcn_global_load_lds((gp_t)(Kb + (long)rr * a.sk + ck * 8), (lp_t)(kres + R * 128), 16, 0, 0);
-        } else {
-          const int cv = pch ^ (((r >> 1) & 3) << 1);
-          __builtin_amdgcn_global_load_lds((gp_t)(Vb + (long)rr * a.sv + cv * 8), (lp_t)(vres + R * 128), 16, 0, 0);
-        }
-      } else {
-#pragma unroll
-        for (int u = 0; u < 8 / NW; ++u) {
-          const int R = 64 * t + 8 * (w + NW * u);
-          const int r = R + (lane >> 3), pch = lane & 7;
-          const int rr = min(r, a.Lk - 1);
-          const int ck = pch ^ ((r >> 1) & 7), cv = pch ^ (((r >> 1) & 3) << 1);
-          __builtin_amdgcn_global_load_lds((gp_t)(Kb + (long)rr * a.sk + ck * 8), (lp_t)(kres + R * 128), 16, 0, 0);
-          __builtin_amdgcn_global_load_lds((gp_t)(Vb + (long)rr * a.sv + cv * 8), (lp_t)(vres + R * 128), 16, 0, 0);
-        }
-      }
-    }
-  }
-  for (int k = tid; k < LkP; k += 64 * NW) mfull[k] = (MASK && !key_ok(a, b, k)) ? -INFINITY : 0.f;
-  if constexpr (DROP) {  // the (b, h) draw tables of the dropout contract: one hash per 4 entries
-    for (int wi = tid; wi < 3 * ATTN_R / 4; wi += 64 * NW) {
-      const int tau = wi / (ATTN_R / 4), jw = wi % (ATTN_R / 4);
-      *(uint64_t*)(dtab + (size_t)wi * 8) =
-          mix64(eff_seed(a.seed, a.seed_off), a.stream, ATTN_TAB0 + ((uint64_t)bh * 3 + tau) * (ATTN_R / 4) + jw);
-    }
-  }
-  if constexpr (REL) {
-    const float* tabh = a.table + (long)h * (2 * a.Lk - 1);
-    const long off0 = (long)(a.Lk - 1) - (qbase + QW - 1);  // tfull[j] = table[h][off0 + j]
-    for (int j = tid; j < LkP + QW; j += 64 * NW) {
-      const long ti = off0 + j;
-      tfull[j] = (ti >= 0 && ti < 2L * a.Lk - 1) ? tabh[ti] : 0.f;
-    }
-  }
-  int q[NG];
-  bool qv[NG];
-  uint4 qf[NG][2];
-  float gate[NG];
-#pragma unroll
-  for (int gq = 0; gq < NG; ++gq) {
-    q[gq] = qbase + w * (16 * NG) + gq * 16 + i;
-    qv[gq] = q[gq] < a.Lq;
-    row_frags<bf16_t>(qf[gq], Qb, a.sq, qv[gq] ? q[gq] : 0, qv[gq], lane);
-    gate[gq] = 0.f;
-    if (REL && a.graw && qv[gq]) {
-      const uint4 u = *(const uint4*)((const bf16_t*)a.graw + ((long)b * a.Lq + q[gq]) * a.sgr + h * 8);
-      const float ra = bf2f((bf16_t)(u.x & 0xffff)) + bf2f((bf16_t)(u.x >> 16)) + bf2f((bf16_t)(u.y & 0xffff)) +
-                       bf2f((bf16_t)(u.y >> 16));
-      const float rb = bf2f((bf16_t)(u.z & 0xffff)) + bf2f((bf16_t)(u.z >> 16)) + bf2f((bf16_t)(u.w & 0xffff)) +
-                       bf2f((bf16_t)(u.w >> 16));
-      const float ga = 1.f / (1.f + __expf(-ra)), gb = 1.f / (1.f + __expf(-rb));
-      gate[gq] = ga * (gb * a.gconst[h] - 1.f) + 2.f;
-    } else if (REL && a.gate && qv[gq]) {
-      gate[gq] = a.gate[(long)bh * a.Lq + q[gq]];
-    }
-  }
-  const float sl2 = a.scale * 1.4426950408889634f;
-  float graw[NG];
-#pragma unroll
-  for (int gq = 0; gq < NG; ++gq) graw[gq] = REL ? gate[gq] / a.scale : 0.f;
-  unsigned ooff[NG][3];  // the rows' table offsets (dropout contract)
-#pragma unroll
-  for (int gq = 0; gq < NG; ++gq) {
-    const uint64_t off = DROP ? attn_offsets(a, bh, q[gq]) : 0;
-#pragma unroll
-    for (int tau = 0; tau < 3; ++tau) ooff[gq][tau] = (unsigned)((off >> (16 * tau)) & 0xFFCu);
-  }
-  float m[NG], l[NG];
-  f32x4_t o[NG][4];
-#pragma unroll
-  for (int gq = 0; gq < NG; ++gq) {
-    m[gq] = -INFINITY;
-    l[gq] = 0.f;
-#pragma unroll
-    for (int d = 0; d < 4; ++d) o[gq][d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  }
-  ASTAMP(1);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  ASTAMP(2);
-
-  const float th_raw = 8.f / sl2;  // lazy rescale threshold (raw score units), as in fwd2_kernel
-  auto tile = [&](const int t, auto mc) {
-    constexpr bool MT = decltype(mc)::value;  // this tile adds the mask row
-    const int k0 = t * 64;
-    const unsigned char* kimg = kres + k0 * 128;
-    const unsigned char* vimg = vres + k0 * 128;
-    f32x4_t s[NG][4];
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
-#pragma unroll
-      for (int gq = 0; gq < NG; ++gq) s[gq][kb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int sub = 0; sub < 2; ++sub) {
-        const uint4 af = *(const uint4*)(kimg + kc_off(128, kb * 16 + i, sub * 4 + g));
-#pragma unroll
-        for (int gq = 0; gq < NG; ++gq) mma<bf16_t>(s[gq][kb], af, qf[gq][sub]);
-      }
-    }
-    f32x2_t mrow[4][2];
-    if constexpr (MT) {
-#pragma unroll
-      for (int kb = 0; kb < 4; ++kb) {
-        const float4 mv4 = *(const float4*)(&mfull[k0 + kb * 16 + 4 * g]);
-        mrow[kb][0] = f32x2_t{mv4.x, mv4.y};
-        mrow[kb][1] = f32x2_t{mv4.z, mv4.w};
-      }
-    }
-    float p[NG][4][4];
-#pragma unroll
-    for (int gq = 0; gq < NG; ++gq) {
-      float tmax = -INFINITY;
-      const int toff = (QW - 1) - (q[gq] - qbase) + k0;
-      const f32x2_t gr2 = {graw[gq], graw[gq]};
-#pragma unroll
-      for (int kb = 0; kb < 4; ++kb) {
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj) {
-          f32x2_t x = {s[gq][kb][2 * jj], s[gq][kb][2 * jj + 1]};
-          if constexpr (REL) {
-            const int kl = kb * 16 + 4 * g + 2 * jj + toff;
-            x = gr2 * f32x2_t{tfull[kl], tfull[kl + 1]} + x;
-          }
-          if constexpr (MT) x += mrow[kb][jj];
-          p[gq][kb][2 * jj] = x.x;
-          p[gq][kb][2 * jj + 1] = x.y;
-        }
-        tmax = fmaxf(tmax, fmaxf(fmaxf(p[gq][kb][0], p[gq][kb][1]), fmaxf(p[gq][kb][2], p[gq][kb][3])));
-      }
-      tmax = xmax16(tmax);
-      tmax = xmax32(tmax);
-      if (__any(tmax > m[gq] + th_raw)) {
-        const float mn = fmaxf(m[gq], tmax);
-        const float mref = (mn == -INFINITY) ? 0.f : mn;
-        const float alpha = __builtin_amdgcn_exp2f((m[gq] - mref) * sl2);
-        l[gq] *= alpha;
-#pragma unroll
-        for (int d = 0; d < 4; ++d) o[gq][d] *= alpha;
-        m[gq] = mn;
-      }
-      const float mref = (m[gq] == -INFINITY) ? 0.f : m[gq];
-      const float nbias = -mref * sl2;
-      const f32x2_t sl2v = {sl2, sl2}, nb2 = {nbias, nbias};
-      f32x2_t ls2 = {0.f, 0.f};
-      uint64_t bits = 0;
-#pragma unroll
-      for (int kb = 0; kb < 4; ++kb) {
-        unsigned keep = 0xF;
-        if constexpr (DROP) {
-          // 4 x 16-bit draws of keys k0+kb*16+4g .. +3: one aligned 8-byte word from each table, XORed
-          const int kq = k0 + kb * 16 + 4 * g;
-          const uint64_t w = *(const uint64_t*)(dtab + (((ooff[gq][0] + kq) & (ATTN_R - 1)) << 1)) ^
-                             *(const uint64_t*)(dtab + ATTN_R * 2 + (((ooff[gq][1] + kq) & (ATTN_R - 1)) << 1)) ^
-                             *(const uint64_t*)(dtab + ATTN_R * 4 + (((ooff[gq][2] + kq) & (ATTN_R - 1)) << 1));
-          keep = 0;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) keep |= (((unsigned)(w >> (16 * j)) & 0xFFFFu) >= a.thr16 ? 1u : 0u) << j;
-          bits |= (uint64_t)keep << (kb * 16 + 4 * g);
-        }
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj) {
-          const f32x2_t arg = f32x2_t{p[gq][kb][2 * jj], p[gq][kb][2 * jj + 1]} * sl2v + nb2;
-          f32x2_t e = {__builtin_amdgcn_exp2f(arg.x), __builtin_amdgcn_exp2f(arg.y)};
-          ls2 += e;
-          if constexpr (DROP) {
-            e.x = ((keep >> (2 * jj)) & 1u) ? e.x : 0.f;
-            e.y = ((keep >> (2 * jj + 1)) & 1u) ? e.y : 0.f;
-          }
-          p[gq][kb][2 * jj] = e.x;
-          p[gq][kb][2 * jj + 1] = e.y;
-        }
-      }
-      const float ls = ls2.x + ls2.y;
-      if constexpr (DROP) {
-        if (a.dbits) {
-          unsigned lo = (unsigned)bits, hi = (unsigned)(bits >> 32);
-          lo = xor16(lo);
-          hi = xor16(hi);
-          lo = xor32(lo);
-          hi = xor32(hi);
-          if (g == 0 && qv[gq]) a.dbits[((long)bh * ntiles + t) * a.Lq + q[gq]] = ((uint64_t)hi << 32) | lo;
-        }
-      }
-      l[gq] += ls;
-    }
-    {
-      const int qq = i >> 2, pp = i & 3;
-      typedef __attribute__((address_space(3))) s16x4_t* lp;
-#pragma unroll
-      for (int ss = 0; ss < 2; ++ss) {
-        uint4 bq[NG];
-#pragma unroll
-        for (int gq = 0; gq < NG; ++gq) {
-          bq[gq].x = pk(p[gq][2 * ss][0], p[gq][2 * ss][1]);
-          bq[gq].y = pk(p[gq][2 * ss][2], p[gq][2 * ss][3]);
-          bq[gq].z = pk(p[gq][2 * ss + 1][0], p[gq][2 * ss + 1][1]);
-          bq[gq].w = pk(p[gq][2 * ss + 1][2], p[gq][2 * ss + 1][3]);
-        }
-        const int k1 = 32 * ss + 4 * g + qq, k2 = k1 + 16;
-#pragma unroll
-        for (int db = 0; db < 4; ++db) {
-          const int u = db * 4 + pp;
-          const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(vimg + k1 * 128 + ((u ^ hatt(k1)) << 3)));
-          const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(vimg + k2 * 128 + ((u ^ hatt(k2)) << 3)));
-          const uint4 af = join_tr(lo, hi);
-#pragma unroll
-          for (int gq = 0; gq < NG; ++gq) mma<bf16_t>(o[gq][db], af, bq[gq]);
-        }
-      }
-    }
-    ASTAMP(3 + (t < 8 ? t : 8));
-  };
-  if (MASK && a.key_keep != nullptr) {
-    // key tiles whose 64 keys are all padding add exactly nothing (exp(-inf) = 0): skipped (wave-uniform flags;
-    // their dropout words are never read — dQ skips the same tiles and dK/dV zeroes masked keys)
-    unsigned tmask = 0;
-    for (int t = 0; t < ntiles; ++t)
-      if (__any(key_ok(a, b, 64 * t + lane))) tmask |= 1u << t;
-    for (int t = 0; t < ntiles; ++t)
-      if ((tmask >> t) & 1u) tile(t, std::integral_constant<bool, MASK>{});
-  } else {
-    for (int t = 0; t + 1 < ntiles; ++t) tile(t, std::false_type{});
-    tile(ntiles - 1, std::integral_constant<bool, MASK>{});
-  }
-#pragma unroll
-  for (int gq = 0; gq < NG; ++gq) {
-    float lt = l[gq];
-    lt = xsum16(lt);
-    lt = xsum32(lt);
-    if (!qv[gq]) continue;
-    const float inv = (lt > 0.f) ? (DROP ? a.drop_scale : 1.f) / lt : NAN;
-    bf16_t* Ob = (bf16_t*)a.Out + ((long)b * a.Lq + q[gq]) * a.so + h * DH;
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      uint2 u2;
-      u2.x = pk(o[gq][d][0] * inv, o[gq][d][1] * inv);
-      u2.y = pk(o[gq][d][2] * inv, o[gq][d][3] * inv);
-      *(uint2*)(Ob + d * 16 + 4 * g) = u2;
-    }
-    if (a.lse && g == 0)
-      a.lse[(long)bh * a.Lq + q[gq]] = (lt > 0.f) ? (m[gq] * sl2 + __log2f(lt)) * 0.69314718055994531f : NAN;
-  }
-  ASTAMP(12);
-#ifdef ATTN_STAMPS
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-  ASTAMP(13);
-  ARTIME(15);
-}
-
 // ------------------------------------------------------------------ dropout keep bits (contract v2, producer)
 // The keep bits of one or more attention sites, written ahead of the attention forward (fwd6 reads them; the backward
 // kernels read the same words): word ((bh * ntiles + t) * Lq + q) of site s, bit kk = keep(q, key 64 t + kk) under
 // rng stream stream0 + s * stream_step. One workgroup per (b, h, site) builds that pair's three 4096-entry draw tables
 // in LDS (one splitmix64 per 4 entries), then each thread owns queries and walks their key tiles (coalesced word
-// stores per tile). Bit-identical to the words the table-staging forward (fwd3) records.
+// stores per tile). Bit-identical to the words fwd6 records when it draws the bits from its own LDS tables (DM 2).
 struct DbArgs {
   uint64_t* out;
   long site_words;  // words per site
@@ -1235,15 +941,15 @@ __global__ void __launch_bounds__(256) dbits_kernel(DbArgs d) {
 // ---------------------------------------------------------------- fwd (bf16, decoder, streamed ring, v6)
 // The decoder's self- and cross-attention forward (key-padding mask, dropout from precomputed keep bits): fwd5's
 // streamed K / V ring (2 LDS stages filled by LDS-DMA one tile ahead, counted vmcnt + one barrier per tile) with
-// fwd3's tile body, and the dropout keep bits read from the words dbits_kernel wrote (staged in LDS for the
+// the round-2 resident-K/V forward's tile body, and the dropout keep bits read from the words dbits_kernel wrote (staged in LDS for the
 // workgroup's queries: one ds_read_b64 per tile and query instead of three table lookups, two XORs and four compares
 // per 4 keys). 4 waves x NG query groups of 16 = 64 NG queries per workgroup and 34-38 KB of LDS at Lk <= 512, so
-// three to four workgroups share a CU and one workgroup's K / V loads overlap another's MFMA / softmax work (fwd3 held
+// three to four workgroups share a CU and one workgroup's K / V loads overlap another's MFMA / softmax work (the resident forward held
 // the whole K / V range of a (b, h) in ~158 KB at Lk = 512: one workgroup per CU, 1.5 rounds of workgroups at C4).
 // Key tiles whose 64 keys are all padding are skipped (neither loaded nor computed).
 // MK: 0 no mask, 1 the ragged last tile only (Lk % 64 != 0, no key-padding mask), 2 key-padding mask on every tile.
 // DM: 0 no dropout, 1 keep bits read from words dbits_kernel wrote, 2 keep bits drawn from the contract's three
-// tables built in LDS (fwd3's scheme) and recorded in dbits for the backward.
+// tables built in LDS and recorded in dbits for the backward.
 template <int DM, int MK, int NG>
 __global__ void __launch_bounds__(256, NG == 1 ? 4 : 2) fwd6_kernel(AttnArgs a) {
   constexpr bool MASK = MK != 0, DROP = DM != 0;
@@ -1311,7 +1017,7 @@ __global__ void __launch_bounds__(256, NG == 1 ? 4 : 2) fwd6_kernel(AttnArgs a) 
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
   // ---- K / V stream: wave w fills rows 16w .. 16w+15 of a tile (2 K + 2 V instructions; XOR swizzles on the
-  // per-lane source addresses, as fwd3_kernel)
+  // per-lane source addresses)
   auto fill = [&](int tt, int st) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -1370,7 +1076,7 @@ __global__ void __launch_bounds__(256, NG == 1 ? 4 : 2) fwd6_kernel(AttnArgs a) 
       uint64_t kw = 0;
       if constexpr (DM == 1) kw = kbits[t * QW + w * (16 * NG) + gq * 16 + i];
       if constexpr (DM == 2) {
-        // 4 x 16-bit draws per 4 keys: one aligned 8-byte word from each table, XORed (fwd3_kernel's form)
+        // 4 x 16-bit draws per 4 keys: one aligned 8-byte word from each table, XORed
 #pragma unroll
         for (int kb = 0; kb < 4; ++kb) {
           const int kq = k0 + kb * 16 + 4 * g;
@@ -1856,7 +1562,7 @@ __global__ void __launch_bounds__(256, 2) dq2_kernel(AttnArgs a) {
     }
   };
   if (MASK && a.key_keep != nullptr) {
-    unsigned tmask = 0;  // fully padded key tiles, skipped as in fwd3_kernel
+    unsigned tmask = 0;  // fully padded key tiles, skipped as in fwd6_kernel
     for (int t = 0; t < ntiles; ++t)
       if (__any(key_ok(a, b, 64 * t + lane))) tmask |= 1u << (t & 31);
     for (int t = 0; t < ntiles; ++t) {
@@ -1885,169 +1591,10 @@ __global__ void __launch_bounds__(256, 2) dq2_kernel(AttnArgs a) {
   }
 }
 
-// dQ, v3 (round 2): the whole K / V range of one (b, h) resident in LDS for Lk <= 512 (LDS-DMA up front, as
-// fwd3_kernel), 16 waves x one 16-query group = 256 queries per workgroup (4 waves per SIMD). One K image in the
-// KC (row-read) layout serves both the S^T = K Q^T row reads and the dQ^T += K^T dS^T transposed reads
-// (ds_read_b64_tr_b16 addresses the 8-byte units through the same XOR swizzle), so K + V take 2 x Lk x 128 B
-// (128 KB at the decoder's cross-attention Lk = 499). DM: 0 no dropout, 2 the forward's recorded keep bits.
+// One KC-layout image per operand serves both the row reads and the transposed ds_read_b64_tr_b16 reads: the
+// 8-byte unit u of row k sits at kc_tr_off(k, u), through the same XOR swizzle as kc_off.
 __device__ __forceinline__ int kc_tr_off(int k, int u) {  // 8-byte unit u of row k in a KC image
   return k * 128 + ((((u >> 1) ^ ((k >> 1) & 7)) << 4) | ((u & 1) << 3));
-}
-template <int DM, bool MASK>
-__global__ void __launch_bounds__(1024, 1) dq3_kernel(AttnArgs a) {
-  static_assert(DM == 0 || DM == 2, "dq3: no-dropout or recorded keep bits");
-  constexpr int NW = 16, QW = 16 * NW;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smq[];
-  const int ntiles = (a.Lk + 63) / 64, LkP = ntiles * 64;
-  unsigned char* kres = smq;               // [LkP][128 B] KC image
-  unsigned char* vres = smq + LkP * 128;   // [LkP][128 B] KC image
-  float* mfull = (float*)(smq + 2 * LkP * 128);
-  ARTIME(14);
-  ASTAMP(0);
-  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
-            i = lane & 15;
-  int bxi, bh;
-  xcd_tile(bxi, bh);
-  const int b = bh / a.H, h = bh % a.H;
-  const bf16_t* Qb = (const bf16_t*)a.Q + (long)b * a.Lq * a.sq + h * DH;
-  const bf16_t* Ob = (const bf16_t*)a.O + (long)b * a.Lq * a.so + h * DH;
-  const bf16_t* dOb = (const bf16_t*)a.dO + (long)b * a.Lq * a.sdo + h * DH;
-  const bf16_t* Kb = (const bf16_t*)a.K + (long)b * a.Lk * a.sk + h * DH;
-  const bf16_t* Vb = (const bf16_t*)a.V + (long)b * a.Lk * a.sv + h * DH;
-  {
-    typedef __attribute__((address_space(1))) const void* gp_t;
-    typedef __attribute__((address_space(3))) void* lp_t;
-    for (int t = 0; t < ntiles; ++t) {  // waves 0-7: K rows 8w.., waves 8-15: V rows 8(w-8).. of every tile
-      const int R = 64 * t + 8 * (w & 7);
-      const int r = R + (lane >> 3), pch = lane & 7;
-      const int rr = min(r, a.Lk - 1);
-      const int ck = pch ^ ((r >> 1) & 7);
-      if (w < 8)
-        __builtin_amdgcn_global_load_lds((gp_t)(Kb + (long)rr * a.sk + ck * 8), (lp_t)(kres + R * 128), 16, 0, 0);
-      else
-        __builtin_amdgcn_global_load_lds((gp_t)(Vb + (long)rr * a.sv + ck * 8), (lp_t)(vres + R * 128), 16, 0, 0);
-    }
-  }
-  for (int k = tid; k < LkP; k += 64 * NW) mfull[k] = (MASK && !key_ok(a, b, k)) ? -INFINITY : 0.f;
-  const float sl2 = a.scale * 1.4426950408889634f;
-  const int q = bxi * QW + w * 16 + i;
-  const bool qv = q < a.Lq;
-  const int qq0 = qv ? q : 0;
-  uint4 qf[2], dof[2], of[2];
-  row_frags<bf16_t>(qf, Qb, a.sq, qq0, qv, lane);
-  row_frags<bf16_t>(dof, dOb, a.sdo, qq0, qv, lane);
-  row_frags<bf16_t>(of, Ob, a.so, qq0, qv, lane);
-  float dl = 0.f;
-#pragma unroll
-  for (int sb = 0; sb < 2; ++sb) {
-    const bf16_t* x = (const bf16_t*)&dof[sb];
-    const bf16_t* y = (const bf16_t*)&of[sb];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) dl += bf2f(x[e]) * bf2f(y[e]);
-  }
-  dl = xsum16(dl);
-  dl = xsum32(dl);
-  const float delta = dl;
-  if (qv && g == 0) a.delta[(long)bh * a.Lq + q] = dl;
-  const float lse2 = qv ? a.lse[(long)bh * a.Lq + q] * 1.4426950408889634f : 0.f;
-  f32x4_t dq[4];
-#pragma unroll
-  for (int d = 0; d < 4; ++d) dq[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  ASTAMP(1);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  ASTAMP(2);
-  const f32x2_t sl2v = {sl2, sl2}, dscv = {a.drop_scale, a.drop_scale}, ndl = {-delta, -delta};
-  auto tile = [&](const int t, auto mc) {
-    constexpr bool MT = decltype(mc)::value;
-    const int k0 = t * 64;
-    const unsigned char* kimg = kres + k0 * 128;
-    const unsigned char* vimg = vres + k0 * 128;
-    uint64_t wbits = 0;
-    if constexpr (DM == 2) wbits = qv ? a.dbits[((long)bh * ntiles + t) * a.Lq + q] : 0;
-    f32x4_t sc[4], dp[4];
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
-      sc[kb] = dp[kb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int sub = 0; sub < 2; ++sub) {
-        const uint4 ak = *(const uint4*)(kimg + kc_off(128, kb * 16 + i, sub * 4 + g));
-        const uint4 av = *(const uint4*)(vimg + kc_off(128, kb * 16 + i, sub * 4 + g));
-        mma<bf16_t>(sc[kb], ak, qf[sub]);
-        mma<bf16_t>(dp[kb], av, dof[sub]);
-      }
-    }
-    float ds[4][4];
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
-      unsigned keep = 0xF;
-      if constexpr (DM == 2) keep = (unsigned)(wbits >> (kb * 16 + 4 * g)) & 0xFu;
-      float4 m4 = make_float4(0.f, 0.f, 0.f, 0.f);
-      if constexpr (MT) m4 = *(const float4*)(&mfull[k0 + kb * 16 + 4 * g]);
-      const float mr[4] = {m4.x, m4.y, m4.z, m4.w};
-#pragma unroll
-      for (int jj = 0; jj < 2; ++jj) {
-        f32x2_t off = {-lse2, -lse2};
-        if constexpr (MT) off += f32x2_t{mr[2 * jj], mr[2 * jj + 1]};
-        const f32x2_t arg = f32x2_t{sc[kb][2 * jj], sc[kb][2 * jj + 1]} * sl2v + off;
-        const f32x2_t pr = {__builtin_amdgcn_exp2f(arg.x), __builtin_amdgcn_exp2f(arg.y)};
-        f32x2_t dpv = {dp[kb][2 * jj], dp[kb][2 * jj + 1]};
-        if constexpr (DM == 2) {
-          dpv.x = __int_as_float(__float_as_int(dpv.x) & __builtin_amdgcn_sbfe((int)keep, 2 * jj, 1));
-          dpv.y = __int_as_float(__float_as_int(dpv.y) & __builtin_amdgcn_sbfe((int)keep, 2 * jj + 1, 1));
-          dpv = dpv * dscv + ndl;
-        } else {
-          dpv += ndl;
-        }
-        const f32x2_t d2 = pr * dpv;
-        ds[kb][2 * jj] = d2.x;
-        ds[kb][2 * jj + 1] = d2.y;
-      }
-    }
-    // dQ^T[d][q] += sum_k K[k][d] dS^T[k][q]: A = K^T fragments by transposed reads of the KC image
-    const int qq = i >> 2, pp = i & 3;
-    typedef __attribute__((address_space(3))) s16x4_t* lp;
-#pragma unroll
-    for (int ss = 0; ss < 2; ++ss) {
-      uint4 bq;
-      bq.x = pk(ds[2 * ss][0], ds[2 * ss][1]);
-      bq.y = pk(ds[2 * ss][2], ds[2 * ss][3]);
-      bq.z = pk(ds[2 * ss + 1][0], ds[2 * ss + 1][1]);
-      bq.w = pk(ds[2 * ss + 1][2], ds[2 * ss + 1][3]);
-      const int k1 = 32 * ss + 4 * g + qq, k2 = k1 + 16;
-#pragma unroll
-      for (int db = 0; db < 4; ++db) {
-        const int u = db * 4 + pp;
-        const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(kimg + kc_tr_off(k1, u)));
-        const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(kimg + kc_tr_off(k2, u)));
-        mma<bf16_t>(dq[db], join_tr(lo, hi), bq);
-      }
-    }
-    ASTAMP(3 + (t < 8 ? t : 8));
-  };
-  if (MASK && a.key_keep != nullptr) {
-    for (int t = 0; t < ntiles; ++t)  // fully padded key tiles skipped (wave-uniform), as in fwd3_kernel
-      if (__any(key_ok(a, b, 64 * t + lane))) tile(t, std::integral_constant<bool, MASK>{});
-  } else {
-    for (int t = 0; t + 1 < ntiles; ++t) tile(t, std::false_type{});
-    tile(ntiles - 1, std::integral_constant<bool, MASK>{});
-  }
-  if (qv) {
-    bf16_t* dQb = (bf16_t*)a.dQ + ((long)b * a.Lq + q) * a.sdq + h * DH;
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      uint2 u2;
-      u2.x = pk(dq[d][0] * a.scale, dq[d][1] * a.scale);
-      u2.y = pk(dq[d][2] * a.scale, dq[d][3] * a.scale);
-      *(uint2*)(dQb + d * 16 + 4 * g) = u2;
-    }
-  }
-  ASTAMP(12);
-#ifdef ATTN_STAMPS
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-  ASTAMP(13);
-  ARTIME(15);
 }
 
 // dK, dV, key-owned: 128 keys per workgroup (two 16-key groups per wave), Q/dO tiles double-buffered
@@ -2228,187 +1775,8 @@ __global__ void __launch_bounds__(256, (DM == 1 ? 1 : 2)) dkv2_kernel(AttnArgs a
   }
 }
 
-// dK / dV, v3 (round 2): key-owned, the whole Q / dO range of one (b, h) resident in LDS for Lq <= 512 (LDS-DMA
-// up front) with the query rows' LSE, delta and — DM == 2 — the forward's keep words of this workgroup's key tiles;
-// 16 waves x one 16-key group = 256 keys per workgroup. Row reads of the KC images give S = Q K^T and dP = dO V^T;
-// transposed reads of the same images give dV^T += dO^T P' and dK^T += Q^T dS. DM: 0 no dropout, 2 recorded bits.
-template <int DM>
-__global__ void __launch_bounds__(1024, 1) dkv3_kernel(AttnArgs a) {
-  static_assert(DM == 0 || DM == 2, "dkv3: no-dropout or recorded keep bits");
-  constexpr bool DROP = DM != 0;
-  constexpr int NW = 16, KW = 16 * NW, KT = KW / 64;  // keys per workgroup, key tiles per workgroup
-  extern __shared__ __attribute__((aligned(16))) unsigned char smk[];
-  const int nq = (a.Lq + 63) / 64, LqP = nq * 64;
-  const int ntk = (a.Lk + 63) / 64;
-  unsigned char* qres = smk;                       // [LqP][128 B] KC image of Q
-  unsigned char* ores = smk + LqP * 128;           // [LqP][128 B] KC image of dO
-  float* lse_s = (float*)(smk + 2 * LqP * 128);    // [LqP] lse * log2(e)
-  float* del_s = lse_s + LqP;                      // [LqP] delta
-  uint64_t* wb_s = (uint64_t*)(del_s + LqP);       // [KT][LqP] keep words (DM == 2)
-  ARTIME(14);
-  ASTAMP(0);
-  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6), g = lane >> 4,
-            i = lane & 15;
-  int bxi, bh;
-  xcd_tile(bxi, bh);
-  const int b = bh / a.H, h = bh % a.H;
-  const bf16_t* Qb = (const bf16_t*)a.Q + (long)b * a.Lq * a.sq + h * DH;
-  const bf16_t* dOb = (const bf16_t*)a.dO + (long)b * a.Lq * a.sdo + h * DH;
-  const bf16_t* Kb = (const bf16_t*)a.K + (long)b * a.Lk * a.sk + h * DH;
-  const bf16_t* Vb = (const bf16_t*)a.V + (long)b * a.Lk * a.sv + h * DH;
-  {
-    typedef __attribute__((address_space(1))) const void* gp_t;
-    typedef __attribute__((address_space(3))) void* lp_t;
-    for (int t = 0; t < nq; ++t) {  // waves 0-7: Q rows 8w.., waves 8-15: dO rows 8(w-8).. of every query tile
-      const int R = 64 * t + 8 * (w & 7);
-      const int r = R + (lane >> 3), pch = lane & 7;
-      const int rr = min(r, a.Lq - 1);
-      const int ck = pch ^ ((r >> 1) & 7);
-      if (w < 8)
-        __builtin_amdgcn_global_load_lds((gp_t)(Qb + (long)rr * a.sq + ck * 8), (lp_t)(qres + R * 128), 16, 0, 0);
-      else
-        __builtin_amdgcn_global_load_lds((gp_t)(dOb + (long)rr * a.sdo + ck * 8), (lp_t)(ores + R * 128), 16, 0, 0);
-    }
-  }
-  // query rows past Lq (their Q / dO images repeat the last row) get lse = +inf: P = 0, so they add nothing
-  for (int j = tid; j < 2 * LqP; j += 64 * NW) {
-    const int qq = j < LqP ? j : j - LqP;
-    float v = j < LqP ? INFINITY : 0.f;
-    if (qq < a.Lq) v = j < LqP ? a.lse[(long)bh * a.Lq + qq] * 1.4426950408889634f : a.delta[(long)bh * a.Lq + qq];
-    (j < LqP ? lse_s : del_s)[qq] = v;
-  }
-  if constexpr (DM == 2) {
-    for (int j = tid; j < KT * LqP; j += 64 * NW) {
-      const int kt = bxi * KT + j / LqP, qq = j % LqP;
-      wb_s[j] = (qq < a.Lq && kt < ntk) ? a.dbits[((long)bh * ntk + kt) * a.Lq + qq] : 0;
-    }
-  }
-  const float sl2 = a.scale * 1.4426950408889634f;
-  const int key = bxi * KW + w * 16 + i;
-  const bool kvld = key < a.Lk;
-  const bool kok = kvld && key_ok(a, b, key);
-  uint4 kf[2], vf[2];
-  row_frags<bf16_t>(kf, Kb, a.sk, kvld ? key : 0, kvld, lane);
-  row_frags<bf16_t>(vf, Vb, a.sv, kvld ? key : 0, kvld, lane);
-  f32x4_t dk[4], dv[4];
-#pragma unroll
-  for (int d = 0; d < 4; ++d) dk[d] = dv[d] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  ASTAMP(1);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  ASTAMP(2);
-  const int kbit = (w & 3) * 16 + i;      // key bit within its 64-key tile; the tile is w >> 2 of the workgroup's
-  const int kts = w >> 2;
-  const f32x2_t sl2v = {sl2, sl2}, dscv = {a.drop_scale, a.drop_scale};
-  const int qq_ = i >> 2, pp = i & 3;
-  typedef __attribute__((address_space(3))) s16x4_t* lp;
-  if (__any(kok)) {  // a wave whose 16 keys are all padding writes zeros (epilogue), no query loop
-    for (int t = 0; t < nq; ++t) {
-      const int q0 = t * 64;
-      const unsigned char* qimg = qres + q0 * 128;
-      const unsigned char* oimg = ores + q0 * 128;
-      f32x4_t sc[4], dp[4];
-#pragma unroll
-      for (int qb = 0; qb < 4; ++qb) {
-        sc[qb] = dp[qb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int sub = 0; sub < 2; ++sub) {
-          const uint4 aq = *(const uint4*)(qimg + kc_off(128, qb * 16 + i, sub * 4 + g));
-          const uint4 ao = *(const uint4*)(oimg + kc_off(128, qb * 16 + i, sub * 4 + g));
-          mma<bf16_t>(sc[qb], aq, kf[sub]);
-          mma<bf16_t>(dp[qb], ao, vf[sub]);
-        }
-      }
-      float pd[4][4], ds[4][4];
-#pragma unroll
-      for (int qb = 0; qb < 4; ++qb) {
-        const float4 l4 = *(const float4*)(&lse_s[q0 + qb * 16 + 4 * g]);
-        const float4 d4 = *(const float4*)(&del_s[q0 + qb * 16 + 4 * g]);
-        const f32x2_t nl[2] = {f32x2_t{-l4.x, -l4.y}, f32x2_t{-l4.z, -l4.w}};
-        const f32x2_t nd[2] = {f32x2_t{-d4.x, -d4.y}, f32x2_t{-d4.z, -d4.w}};
-        unsigned wq[4] = {0, 0, 0, 0};  // the 32-bit half of each query's keep word holding this key's bit
-        if constexpr (DM == 2) {
-          const unsigned* src = (const unsigned*)&wb_s[kts * LqP + q0 + qb * 16 + 4 * g] + (kbit >> 5);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) wq[j] = src[2 * j];
-        }
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj) {
-          const f32x2_t arg = f32x2_t{sc[qb][2 * jj], sc[qb][2 * jj + 1]} * sl2v + nl[jj];
-          const f32x2_t pr = {__builtin_amdgcn_exp2f(arg.x), __builtin_amdgcn_exp2f(arg.y)};
-          f32x2_t dpv = {dp[qb][2 * jj], dp[qb][2 * jj + 1]};
-          f32x2_t pdv = pr;
-          if constexpr (DROP) {
-            const int m0 = __builtin_amdgcn_sbfe((int)wq[2 * jj], kbit & 31, 1);
-            const int m1 = __builtin_amdgcn_sbfe((int)wq[2 * jj + 1], kbit & 31, 1);
-            pdv.x = __int_as_float(__float_as_int(pr.x) & m0);
-            pdv.y = __int_as_float(__float_as_int(pr.y) & m1);
-            dpv.x = __int_as_float(__float_as_int(dpv.x) & m0);
-            dpv.y = __int_as_float(__float_as_int(dpv.y) & m1);
-            dpv = dpv * dscv + nd[jj];
-          } else {
-            dpv += nd[jj];
-          }
-          const f32x2_t d2 = pr * dpv;
-          pd[qb][2 * jj] = pdv.x;
-          pd[qb][2 * jj + 1] = pdv.y;
-          ds[qb][2 * jj] = d2.x;
-          ds[qb][2 * jj + 1] = d2.y;
-        }
-      }
-      // dV^T[d][key] += sum_q dO[q][d] P'[q][key], dK^T[d][key] += sum_q Q[q][d] dS[q][key]: transposed reads
-#pragma unroll
-      for (int ss = 0; ss < 2; ++ss) {
-        uint4 bp, bs;
-        bp.x = pk(pd[2 * ss][0], pd[2 * ss][1]);
-        bp.y = pk(pd[2 * ss][2], pd[2 * ss][3]);
-        bp.z = pk(pd[2 * ss + 1][0], pd[2 * ss + 1][1]);
-        bp.w = pk(pd[2 * ss + 1][2], pd[2 * ss + 1][3]);
-        bs.x = pk(ds[2 * ss][0], ds[2 * ss][1]);
-        bs.y = pk(ds[2 * ss][2], ds[2 * ss][3]);
-        bs.z = pk(ds[2 * ss + 1][0], ds[2 * ss + 1][1]);
-        bs.w = pk(ds[2 * ss + 1][2], ds[2 * ss + 1][3]);
-        const int k1 = 32 * ss + 4 * g + qq_, k2 = k1 + 16;
-#pragma unroll
-        for (int db = 0; db < 4; ++db) {
-          const int u = db * 4 + pp;
-          const s16x4_t olo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(oimg + kc_tr_off(k1, u)));
-          const s16x4_t ohi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(oimg + kc_tr_off(k2, u)));
-          const s16x4_t qlo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(qimg + kc_tr_off(k1, u)));
-          const s16x4_t qhi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(qimg + kc_tr_off(k2, u)));
-          mma<bf16_t>(dv[db], join_tr(olo, ohi), bp);
-          mma<bf16_t>(dk[db], join_tr(qlo, qhi), bs);
-        }
-      }
-      ASTAMP(3 + (t < 8 ? t : 8));
-    }
-  }
-  if (kvld) {
-    bf16_t* dKb = (bf16_t*)a.dK + ((long)b * a.Lk + key) * a.sdk + h * DH;
-    bf16_t* dVb = (bf16_t*)a.dV + ((long)b * a.Lk + key) * a.sdv + h * DH;
-    // masked key: zero gradient (its P was never zeroed); dV carries the dropout scale of P'
-    const float ksc = kok ? a.scale : 0.f, vsc = kok ? (DROP ? a.drop_scale : 1.f) : 0.f;
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      uint2 uk, uv;
-      uk.x = pk(kok ? dk[d][0] * ksc : 0.f, kok ? dk[d][1] * ksc : 0.f);
-      uk.y = pk(kok ? dk[d][2] * ksc : 0.f, kok ? dk[d][3] * ksc : 0.f);
-      uv.x = pk(kok ? dv[d][0] * vsc : 0.f, kok ? dv[d][1] * vsc : 0.f);
-      uv.y = pk(kok ? dv[d][2] * vsc : 0.f, kok ? dv[d][3] * vsc : 0.f);
-      *(uint2*)(dKb + d * 16 + 4 * g) = uk;
-      *(uint2*)(dVb + d * 16 + 4 * g) = uv;
-    }
-  }
-  ASTAMP(12);
-#ifdef ATTN_STAMPS
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-  ASTAMP(13);
-  ARTIME(15);
-}
-
 // --------------------------------------------------------------------- bwd (bf16, streamed ring, v4)
-// dq3 / dkv3's tile bodies (one KC image per operand serving the row reads and, through kc_tr_off, the transposed
+// the round-2 resident-operand kernels' (dq3 / dkv3) tile bodies (one KC image per operand serving the row reads and, through kc_tr_off, the transposed
 // reads; 16 rows per wave) with the streamed operand pair in a 2-stage LDS ring filled by LDS-DMA one tile ahead
 // (fwd6's scheme: inline-asm DMA, vmcnt(0) + one barrier per tile, no other vector-memory instruction in the loop)
 // instead of resident in LDS: 4 waves x 16 rows = 64 rows per workgroup and 36-40 KB of LDS at L <= 512, so four
@@ -2453,7 +1821,7 @@ __global__ void __launch_bounds__(256, 4) dq4_kernel(AttnArgs a) {
     }
   }
   unsigned tmask = ntiles >= 32 ? 0xFFFFFFFFu : ((1u << ntiles) - 1u);
-  if (MASK && a.key_keep != nullptr) {  // fully padded key tiles skipped (wave-uniform), as in fwd3_kernel
+  if (MASK && a.key_keep != nullptr) {  // fully padded key tiles skipped (wave-uniform), as in fwd6_kernel
     tmask = 0;
     for (int t = 0; t < ntiles; ++t)
       if (__any(key_ok(a, b, 64 * t + lane))) tmask |= 1u << t;
@@ -2938,7 +2306,7 @@ __global__ void __launch_bounds__(1024, 1) bwd3s_kernel(AttnArgs a) {
       ASTAMP(3 + (t < 4 ? t : 4));
     };
     if (MASK && a.key_keep != nullptr) {
-      for (int t = 0; t < nt; ++t)  // fully padded key tiles skipped (wave-uniform), as in fwd3_kernel
+      for (int t = 0; t < nt; ++t)  // fully padded key tiles skipped (wave-uniform), as in fwd6_kernel
         if (__any(mfull[64 * t + lane] == 0.f)) tile(t, std::integral_constant<bool, MASK>{});
     } else {
       for (int t = 0; t + 1 < nt; ++t) tile(t, std::false_type{});
@@ -3076,164 +2444,87 @@ __global__ void __launch_bounds__(1024, 1) bwd3s_kernel(AttnArgs a) {
   ARTIME(15);
 }
 
+// Kernel choice per launch shape (bf16; the fp32 parity mode runs the generic kernels):
+//  forward  WavLM gated rel-pos bias: fwd5 (streamed ring, bias slice staged); decoder, Lk <= 1024: fwd6 (streamed ring;
+//           dropout keep bits precomputed (bits_ready) or drawn from LDS tables and recorded); Lk > 1024: fwd2.
+//  backward Lq == Lk <= 256 with recorded bits or no dropout: bwd3s (one fused launch per (b, h));
+//           else dq4 + dkv4 (streamed rings) for L <= 1024 with recorded bits or no dropout; dq2 + dkv2 otherwise
+//           (keep bits rehashed when the forward recorded none, or longer sequences).
 template <typename T>
 static int run(int which, AttnArgs& a, hipStream_t s) {
   constexpr int RB = Cfg<T>::RB;
-  if (which == 0) {
-    if constexpr (sizeof(T) == 2) {
-      if (!getenv("FDDM_ATTN_V1")) {
-        const bool drop = a.thr16 != 0, mask = a.key_keep != nullptr || (a.Lk % 64) != 0;
-        const bool rel = a.table != nullptr && (a.gate != nullptr || a.graw != nullptr);
-        // decoder self / cross attention: the streamed-ring forward with precomputed dropout keep bits (fwd6)
-        const bool fwd6_on = !getenv("FDDM_ATTN_FWD6") || atoi(getenv("FDDM_ATTN_FWD6")) != 0;
-        if (fwd6_on && !rel && a.Lk <= 1024) {
-          const int ntiles = (a.Lk + 63) / 64, LkP = ntiles * 64;
-          const int dm = !drop ? 0 : (a.bits_ready && a.dbits) ? 1 : 2;
-          const int ng_env = getenv("FDDM_ATTN_NG6") ? atoi(getenv("FDDM_ATTN_NG6")) : 0;
-          const int ng = ng_env ? ng_env : 2;
-          const int qw = 64 * ng;
-          const size_t lds = (size_t)2 * 2 * 64 * 128 + (size_t)LkP * 4 +
-                             (dm == 1 ? (size_t)ntiles * qw * 8 : dm == 2 ? (size_t)3 * ATTN_R * 2 : 0);
-          dim3 g6((a.Lq + qw - 1) / qw, a.B * a.H);
-          const int mk = a.key_keep != nullptr ? 2 : (a.Lk % 64) != 0 ? 1 : 0;
-#define FWD6(D, M, G) hipLaunchKernelGGL((fwd6_kernel<D, M, G>), g6, dim3(256), lds, s, a)
-#define FWD6G(D, M) do { if (ng == 2) FWD6(D, M, 2); else FWD6(D, M, 1); } while (0)
-#define FWD6M(D) do { if (mk == 2) FWD6G(D, 2); else if (mk == 1) FWD6G(D, 1); else FWD6G(D, 0); } while (0)
-          if (dm == 2) FWD6M(2);
-          else if (dm == 1) FWD6M(1);
-          else FWD6M(0);
+  const bool drop = a.thr16 != 0, mask = a.key_keep != nullptr || (a.Lk % 64) != 0;
+  if constexpr (sizeof(T) == 2) {
+    if (which == 0) {
+      const bool rel = a.table != nullptr && (a.gate != nullptr || a.graw != nullptr);
+      const int LkP = (a.Lk + 63) / 64 * 64;
+      if (rel) {
+        if (drop) return (int)hipErrorInvalidValue;    // WavLM attention has no dropout in the frozen encoder
+        const size_t lds5 = (size_t)2 * 2 * 64 * 128 + (size_t)LkP * 4 + (size_t)(LkP + 128) * 4;
+        dim3 grid5((a.Lq + 127) / 128, a.B * a.H);
+        if (mask) hipLaunchKernelGGL((fwd5_kernel<true, 2, 2>), grid5, dim3(256), lds5, s, a);
+        else hipLaunchKernelGGL((fwd5_kernel<false, 2, 2>), grid5, dim3(256), lds5, s, a);
+        return (int)hipGetLastError();
+      }
+      if (a.Lk <= 1024) {
+        const int ntiles = LkP / 64, qw = 128;
+        const int dm = !drop ? 0 : (a.bits_ready && a.dbits) ? 1 : 2;
+        const size_t lds = (size_t)2 * 2 * 64 * 128 + (size_t)LkP * 4 +
+                           (dm == 1 ? (size_t)ntiles * qw * 8 : dm == 2 ? (size_t)3 * ATTN_R * 2 : 0);
+        dim3 g6((a.Lq + qw - 1) / qw, a.B * a.H);
+        const int mk = a.key_keep != nullptr ? 2 : (a.Lk % 64) != 0 ? 1 : 0;
+#define FWD6(D, M) hipLaunchKernelGGL((fwd6_kernel<D, M, 2>), g6, dim3(256), lds, s, a)
+#define FWD6M(D) do { if (mk == 2) FWD6(D, 2); else if (mk == 1) FWD6(D, 1); else FWD6(D, 0); } while (0)
+        if (dm == 2) FWD6M(2);
+        else if (dm == 1) FWD6M(1);
+        else FWD6M(0);
 #undef FWD6M
-#undef FWD6G
 #undef FWD6
-          return (int)hipGetLastError();
-        }
-        // FDDM_ATTN_NG=1: 64-query workgroups (one 16-query group per wave). Measured at the decoder's
-        // Lq = 256 (tools/attn_bench.py): no faster with dropout (24.4 vs 24.0 us), slower without (19.4 vs
-        // 15.1 us) — the launch is not short of workgroups; kept as a probe, off by default.
-        const char* ng_env = getenv("FDDM_ATTN_NG");
-        const int ng = ng_env ? atoi(ng_env) : 2;
-        if (ng == 1 && !rel) {
-          dim3 grid1((a.Lq + 63) / 64, a.B * a.H);
-#define FWD1(D, M) hipLaunchKernelGGL((fwd2_kernel<D, M, false, 1>), grid1, dim3(256), 0, s, a)
-          if (drop) { if (mask) FWD1(true, true); else FWD1(true, false); }
-          else { if (mask) FWD1(false, true); else FWD1(false, false); }
-#undef FWD1
-          return (int)hipGetLastError();
-        }
-        // v3 (K/V resident in LDS) for Lk <= 512 unless FDDM_ATTN_V2 is set
-        if (a.Lk <= 512 && (!rel || getenv("FDDM_ATTN_REL3")) && !getenv("FDDM_ATTN_V2")) {  // WavLM (rel): fwd2's 2 workgroups per CU measure faster
-          const int LkP = (a.Lk + 63) / 64 * 64;
-          const char* nw_env = getenv("FDDM_ATTN_NW");
-          // 16 waves x 16 queries (4 waves per SIMD) by default: tools/attn_bench.py, decoder self (kpm, dropout)
-          // 16.3 -> 15.2 us, cross 31.7 -> 30.0 us against 8 waves x 32 queries (same LDS footprint)
-          const int nw = nw_env ? atoi(nw_env) : 16;
-          const int QW = nw == 16 ? 16 * nw : 32 * nw;
-          const size_t lds = (size_t)LkP * 256 + (size_t)LkP * 4 + (rel ? (size_t)(LkP + QW) * 4 : 0) +
-                             (drop ? (size_t)3 * ATTN_R * 2 : 0);
-          const bool mask3 = a.key_keep != nullptr || (a.Lk % 64) != 0;
-          dim3 grid3((a.Lq + QW - 1) / QW, a.B * a.H);
-#define FWD3(D, M, R, W) hipLaunchKernelGGL((fwd3_kernel<D, M, R, W>), grid3, dim3(64 * W), lds, s, a)
-#define FWD3W(D, M, R)                                                                                 \
-  do {                                                                                                  \
-    if (nw == 4) FWD3(D, M, R, 4);                                                                      \
-    else if (nw == 16) hipLaunchKernelGGL((fwd3_kernel<D, M, R, 16, 1>), grid3, dim3(1024), lds, s, a); \
-    else FWD3(D, M, R, 8);                                                                              \
-  } while (0)
-          if (rel) {
-            if (mask3) FWD3W(false, true, true); else FWD3W(false, false, true);
-          } else if (drop) {
-            if (mask3) FWD3W(true, true, false); else FWD3W(true, false, false);
-          } else {
-            if (mask3) FWD3W(false, true, false); else FWD3W(false, false, false);
-          }
-#undef FWD3W
-#undef FWD3
-          return (int)hipGetLastError();
-        }
-        dim3 grid((a.Lq + 127) / 128, a.B * a.H);
-        // WavLM: the streamed-ring forward (fwd5_kernel); FDDM_ATTN_FWD5=0 keeps fwd2
-        if (rel && !drop && (!getenv("FDDM_ATTN_FWD5") || atoi(getenv("FDDM_ATTN_FWD5")) != 0)) {
-          const int LkP = (a.Lk + 63) / 64 * 64;
-          // ring depth 2 (one tile ahead; 37 KB of LDS, three workgroups per CU by registers): tools/attn_bench.py at
-          // the C2 shape 51.7-52.0 us; 3 stages 53.5, 4 stages (two workgroups per CU) 58.6-59.3, 64-query workgroups
-          // (4 waves per SIMD) 55.3 / 62.4 / 69.0 with 2 / 3 / 4 stages; fwd2 56.4-57.0 (FDDM_ATTN_FWD5=0).
-          // FDDM_ATTN_NST=3|4 and FDDM_ATTN_NG5=1 are probes
-          const int nst = getenv("FDDM_ATTN_NST") ? atoi(getenv("FDDM_ATTN_NST")) : 2;
-          const int ng5 = getenv("FDDM_ATTN_NG5") ? atoi(getenv("FDDM_ATTN_NG5")) : 2;
-          const int qw5 = 64 * ng5;
-          const size_t lds5 = (size_t)2 * nst * 64 * 128 + (size_t)LkP * 4 + (size_t)(LkP + qw5) * 4;
-          dim3 grid5((a.Lq + qw5 - 1) / qw5, a.B * a.H);
-#define FWD5(N, G)                                                                                          \
-  do {                                                                                                       \
-    if (mask) hipLaunchKernelGGL((fwd5_kernel<true, N, G>), grid5, dim3(256), lds5, s, a);                   \
-    else hipLaunchKernelGGL((fwd5_kernel<false, N, G>), grid5, dim3(256), lds5, s, a);                       \
-  } while (0)
-          if (ng5 == 1) {
-            if (nst == 2) FWD5(2, 1); else if (nst == 4) FWD5(4, 1); else FWD5(3, 1);
-          } else {
-            if (nst == 2) FWD5(2, 2); else if (nst == 4) FWD5(4, 2); else FWD5(3, 2);
-          }
-#undef FWD5
-          return (int)hipGetLastError();
-        }
-#define FWD2(D, M, R) hipLaunchKernelGGL((fwd2_kernel<D, M, R>), grid, dim3(256), 0, s, a)
-        if (rel) {
-          if (drop) { if (mask) FWD2(true, true, true); else FWD2(true, false, true); }
-          else { if (mask) FWD2(false, true, true); else FWD2(false, false, true); }
-        } else {
-          if (drop) { if (mask) FWD2(true, true, false); else FWD2(true, false, false); }
-          else { if (mask) FWD2(false, true, false); else FWD2(false, false, false); }
-        }
+        return (int)hipGetLastError();
+      }
+      dim3 grid((a.Lq + 127) / 128, a.B * a.H);
+#define FWD2(D, M) hipLaunchKernelGGL((fwd2_kernel<D, M, false>), grid, dim3(256), 0, s, a)
+      if (drop) { if (mask) FWD2(true, true); else FWD2(true, false); }
+      else { if (mask) FWD2(false, true); else FWD2(false, false); }
 #undef FWD2
-        return (int)hipGetLastError();
-      }
+      return (int)hipGetLastError();
     }
-    dim3 grid((a.Lq + 63) / 64, a.B * a.H);
-    hipLaunchKernelGGL(fwd_kernel<T>, grid, dim3(256), 128 * RB, s, a);
-  } else if (which == 1) {
-    if constexpr (sizeof(T) == 2) {
-      if (!getenv("FDDM_ATTN_V1")) {
-        const bool drop = a.thr16 != 0, mask = a.key_keep != nullptr || (a.Lk % 64) != 0;
-        const int dm = drop ? (a.dbits ? 2 : 1) : 0;
-        // v3: K/V resident, 256 queries per workgroup, for Lk <= 256 (tools/attn_bench.py: decoder self-attention
-        // backward 38.6 -> 35.3 us with dkv3; at the cross-attention's Lk = 499 — 130 KB of LDS, one workgroup per
-        // CU — no faster than the streamed kernels, 64.0 vs 62.8 us); FDDM_ATTN_DQ2=1 keeps the streamed kernel
-        static const int v3max = getenv("FDDM_ATTN_V3_MAX") ? atoi(getenv("FDDM_ATTN_V3_MAX")) : 256;
-        const bool v4 = !getenv("FDDM_ATTN_BWD4") || atoi(getenv("FDDM_ATTN_BWD4")) != 0;
-        if (v4 && dm != 1 && a.Lk <= 1024) {  // streamed v4
-          const int ntiles = (a.Lk + 63) / 64;
-          const size_t lds = (size_t)4 * 64 * 128 + (size_t)ntiles * 64 * 4 + (dm == 2 ? (size_t)ntiles * 64 * 8 : 0);
-          dim3 g4((a.Lq + 63) / 64, a.B * a.H);
+    const int dm = drop ? (a.dbits ? 2 : 1) : 0;
+    if (which == 1) {
+      if (dm != 1 && a.Lk <= 1024) {
+        const int ntiles = (a.Lk + 63) / 64;
+        const size_t lds = (size_t)4 * 64 * 128 + (size_t)ntiles * 64 * 4 + (dm == 2 ? (size_t)ntiles * 64 * 8 : 0);
+        dim3 g4((a.Lq + 63) / 64, a.B * a.H);
 #define DQ4(D, M) hipLaunchKernelGGL((dq4_kernel<D, M>), g4, dim3(256), lds, s, a)
-          if (dm == 2) { if (mask) DQ4(2, true); else DQ4(2, false); }
-          else { if (mask) DQ4(0, true); else DQ4(0, false); }
+        if (dm == 2) { if (mask) DQ4(2, true); else DQ4(2, false); }
+        else { if (mask) DQ4(0, true); else DQ4(0, false); }
 #undef DQ4
-          return (int)hipGetLastError();
-        }
-        if (a.Lk <= v3max && a.Lk <= 512 && dm != 1 && !getenv("FDDM_ATTN_DQ2")) {
-          const int LkP = (a.Lk + 63) / 64 * 64;
-          const size_t lds = (size_t)LkP * 256 + (size_t)LkP * 4;
-          dim3 g3((a.Lq + 255) / 256, a.B * a.H);
-#define DQ3(D, M) hipLaunchKernelGGL((dq3_kernel<D, M>), g3, dim3(1024), lds, s, a)
-          if (dm == 2) { if (mask) DQ3(2, true); else DQ3(2, false); }
-          else { if (mask) DQ3(0, true); else DQ3(0, false); }
-#undef DQ3
-          return (int)hipGetLastError();
-        }
-        dim3 grid((a.Lq + 127) / 128, a.B * a.H);
-#define DQ2(D, M) hipLaunchKernelGGL((dq2_kernel<D, M>), grid, dim3(256), 0, s, a)
-        if (dm == 2) { if (mask) DQ2(2, true); else DQ2(2, false); }
-        else if (dm == 1) { if (mask) DQ2(1, true); else DQ2(1, false); }
-        else { if (mask) DQ2(0, true); else DQ2(0, false); }
-#undef DQ2
         return (int)hipGetLastError();
       }
+      dim3 grid((a.Lq + 127) / 128, a.B * a.H);
+#define DQ2(D, M) hipLaunchKernelGGL((dq2_kernel<D, M>), grid, dim3(256), 0, s, a)
+      if (dm == 2) { if (mask) DQ2(2, true); else DQ2(2, false); }
+      else if (dm == 1) { if (mask) DQ2(1, true); else DQ2(1, false); }
+      else { if (mask) DQ2(0, true); else DQ2(0, false); }
+#undef DQ2
+      return (int)hipGetLastError();
     }
-    dim3 grid((a.Lq + 63) / 64, a.B * a.H);
-    hipLaunchKernelGGL(dq_kernel<T>, grid, dim3(256), 192 * RB, s, a);
-  } else if (which == 3) {
-    if constexpr (sizeof(T) == 2) {
-      const bool drop = a.thr16 != 0, mask = a.key_keep != nullptr || (a.Lk % 64) != 0;
+    if (which == 2) {
+      if (dm != 1 && a.Lq <= 1024) {
+        const int LqP = (a.Lq + 63) / 64 * 64;
+        const size_t lds = (size_t)4 * 64 * 128 + (size_t)LqP * 8 + (dm == 2 ? (size_t)LqP * 8 : 0);
+        dim3 g4((a.Lk + 63) / 64, a.B * a.H);
+        if (dm == 2) hipLaunchKernelGGL((dkv4_kernel<2>), g4, dim3(256), lds, s, a);
+        else hipLaunchKernelGGL((dkv4_kernel<0>), g4, dim3(256), lds, s, a);
+        return (int)hipGetLastError();
+      }
+      dim3 grid((a.Lk + 127) / 128, a.B * a.H);
+      if (dm == 2) hipLaunchKernelGGL((dkv2_kernel<2>), grid, dim3(256), 0, s, a);
+      else if (dm == 1) hipLaunchKernelGGL((dkv2_kernel<1>), grid, dim3(256), 0, s, a);
+      else hipLaunchKernelGGL((dkv2_kernel<0>), grid, dim3(256), 0, s, a);
+      return (int)hipGetLastError();
+    }
+    if (which == 3) {
       const int LP = (a.Lk + 63) / 64 * 64;
       const size_t lds = (size_t)LP * 512 + (size_t)LP * 12 + (drop ? (size_t)(LP / 64) * LP * 8 : 0);
       dim3 g3(1, a.B * a.H);
@@ -3245,39 +2536,20 @@ static int run(int which, AttnArgs& a, hipStream_t s) {
     }
     return (int)hipErrorInvalidValue;
   } else {
-    if constexpr (sizeof(T) == 2) {
-      if (!getenv("FDDM_ATTN_V1")) {
-        // v3: Q/dO resident, 256 keys per workgroup, for Lq, Lk <= 256 (see dq3 above); FDDM_ATTN_DKV2=1 keeps the
-        // streamed kernel
-        static const int v3max = getenv("FDDM_ATTN_V3_MAX") ? atoi(getenv("FDDM_ATTN_V3_MAX")) : 256;
-        const bool v4 = !getenv("FDDM_ATTN_BWD4") || atoi(getenv("FDDM_ATTN_BWD4")) != 0;
-        if (v4 && (!a.thr16 || a.dbits) && a.Lq <= 1024) {  // streamed v4
-          const int LqP = (a.Lq + 63) / 64 * 64;
-          const size_t lds = (size_t)4 * 64 * 128 + (size_t)LqP * 8 + (a.thr16 ? (size_t)LqP * 8 : 0);
-          dim3 g4((a.Lk + 63) / 64, a.B * a.H);
-          if (a.thr16) hipLaunchKernelGGL((dkv4_kernel<2>), g4, dim3(256), lds, s, a);
-          else hipLaunchKernelGGL((dkv4_kernel<0>), g4, dim3(256), lds, s, a);
-          return (int)hipGetLastError();
-        }
-        if (a.Lq <= v3max && a.Lk <= v3max && a.Lq <= 512 && (!a.thr16 || a.dbits) && !getenv("FDDM_ATTN_DKV2")) {
-          const int LqP = (a.Lq + 63) / 64 * 64;
-          const size_t lds = (size_t)LqP * 256 + (size_t)LqP * 8 + (a.thr16 ? (size_t)4 * LqP * 8 : 0);
-          dim3 g3((a.Lk + 255) / 256, a.B * a.H);
-          if (a.thr16) hipLaunchKernelGGL((dkv3_kernel<2>), g3, dim3(1024), lds, s, a);
-          else hipLaunchKernelGGL((dkv3_kernel<0>), g3, dim3(1024), lds, s, a);
-          return (int)hipGetLastError();
-        }
-        dim3 grid((a.Lk + 127) / 128, a.B * a.H);
-        if (a.thr16 && a.dbits) hipLaunchKernelGGL((dkv2_kernel<2>), grid, dim3(256), 0, s, a);
-        else if (a.thr16) hipLaunchKernelGGL((dkv2_kernel<1>), grid, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((dkv2_kernel<0>), grid, dim3(256), 0, s, a);
-        return (int)hipGetLastError();
-      }
+    if (which == 0) {
+      dim3 grid((a.Lq + 63) / 64, a.B * a.H);
+      hipLaunchKernelGGL(fwd_kernel<T>, grid, dim3(256), 128 * RB, s, a);
+    } else if (which == 1) {
+      dim3 grid((a.Lq + 63) / 64, a.B * a.H);
+      hipLaunchKernelGGL(dq_kernel<T>, grid, dim3(256), 192 * RB, s, a);
+    } else if (which == 2) {
+      dim3 grid((a.Lk + 63) / 64, a.B * a.H);
+      hipLaunchKernelGGL(dkv_kernel<T>, grid, dim3(256), 256 * RB + 512, s, a);
+    } else {
+      return (int)hipErrorInvalidValue;
     }
-    dim3 grid((a.Lk + 63) / 64, a.B * a.H);
-    hipLaunchKernelGGL(dkv_kernel<T>, grid, dim3(256), 256 * RB + 512, s, a);
+    return (int)hipGetLastError();
   }
-  return (int)hipGetLastError();
 }
 
 static bool aligned_ok(const void* p, long stride, int ech) {
@@ -3375,8 +2647,7 @@ FDDM_API int fddm_attn_bwd(int dtype, const void* Q, long sq, const void* K, lon
   a.key_keep = key_keep;
   a.B = B; a.H = H; a.Lq = Lq; a.Lk = Lk; a.scale = scale; a.seed = seed; a.stream = stream; a.seed_off = g_seed_off;
   // self-attention shapes (Lq == Lk <= 256, bf16, no rehashed dropout): dQ, dK and dV in one fused launch
-  if (dtype == FDDM_BF16 && Lq == Lk && Lk <= 256 && (drop_p <= 0.f || drop_bits) && !getenv("FDDM_ATTN_BWD_SPLIT") &&
-      !getenv("FDDM_ATTN_V1") && !(getenv("FDDM_ATTN_BWD4") && atoi(getenv("FDDM_ATTN_BWD4")) == 2))
+  if (dtype == FDDM_BF16 && Lq == Lk && Lk <= 256 && (drop_p <= 0.f || drop_bits))
     return attn_dispatch(3, dtype, a, drop_p, hs);
   int e = attn_dispatch(1, dtype, a, drop_p, hs);
   if (e) return e;

@@ -673,18 +673,11 @@ static hipError_t zero2d(float* C, long ldc, long M, long N, hipStream_t s) {
 
 using namespace fddm;
 
-// FDDM_GEMM_PATH (read per call, for A/B benchmarks): "small" routes every GEMM through the 128x128 kernel,
-// "big" disables the 256x256 kernel, unset = automatic choice;
-// "256" takes the 256x256 kernel wherever its preconditions hold
-static int gemm_path() {
-  const char* v = getenv("FDDM_GEMM_PATH");
-  if (!v) return 0;
-  if (v[0] == 's') return 2;
-  if (v[0] == 'b') return 1;
-  if (v[0] == '2') return 3;
-  if (v[0] == '1') return 4;  // "128": the 128x128 LDS-DMA ring kernel wherever its preconditions hold
-  return 0;
-}
+// Kernel-family override for tests and diagnostics (fddm_gemm_force_path; 0 = the automatic choice below):
+// 1 "big" disables the 256x256 kernel, 2 "small" routes every GEMM through the register-staged 128x128 kernel,
+// 3 "256" takes the 256x256 kernel wherever its preconditions hold, 4 "128" the 128x128 LDS-DMA ring kernel
+static int g_gemm_path = 0;
+static int gemm_path() { return g_gemm_path; }
 static bool big_enabled() { return gemm_path() != 2 && gemm_path() != 4; }
 static bool g256_enabled() { return gemm_path() == 0 || gemm_path() == 3; }
 static bool g128_enabled() { return gemm_path() == 0 || gemm_path() == 4; }
@@ -692,27 +685,16 @@ static bool g128_enabled() { return gemm_path() == 0 || gemm_path() == 4; }
 // to the 128x128 kernel, but beside the encoder's persistent GEMMs (half or a quarter of the CUs free) one round of
 // 64 tiles beats two rounds of 256: the decoder's d-wide forward GEMMs (out-proj, cross Q / out, V, FF2) — C4
 // (d 768: 96 tiles) 17.79-17.87 -> 17.36-17.37 ms/step, C2 (64 tiles) 9.89 -> 9.87 ms average of 6 alternating rounds
-// (threshold 128 before; FDDM_G256_MIN_TILES, read once, is the probe)
-static bool prefer_256(long M, long N) {
-  if (gemm_path() == 3) return true;
-  static const long min_tiles = []() {
-    const char* v = getenv("FDDM_G256_MIN_TILES");
-    return v ? atol(v) : 64L;
-  }();
-  return gemm256_tiles(M, N) >= min_tiles;
-}
-static long env_long(const char* name, long dflt) {
-  const char* v = getenv(name);
-  return v ? atol(v) : dflt;
-}
-// split-K tuning (FDDM_SPLITK_TARGET workgroups, FDDM_SPLITK_MINK minimum K per split; read once)
-static long splitk_target() {
-  static const long v = env_long("FDDM_SPLITK_TARGET", 512);
-  return v;
-}
-static long splitk_mink() {
-  static const long v = env_long("FDDM_SPLITK_MINK", 512);
-  return v;
+// (threshold 128 before; 32 measured neutral, round 3)
+static bool prefer_256(long M, long N) { return gemm_path() == 3 || gemm256_tiles(M, N) >= 64; }
+// split-K: aim at ~512 workgroups, at least 512 K elements per split
+static long splitk_target() { return 512; }
+static long splitk_mink() { return 512; }
+
+FDDM_API int fddm_gemm_force_path(int path) {
+  const int old = g_gemm_path;
+  g_gemm_path = (path >= 0 && path <= 4) ? path : 0;
+  return old;
 }
 
 FDDM_API int fddm_gemm(int dtype, int a_dtype, int a_kc, int b_kc, int epi, int out_dtype, const void* A, long lda,
@@ -904,7 +886,6 @@ static void g128_balance(int n, const long* tiles, const long* ktiles, int* nz, 
 
 static int g128_ncu() {
   static int ncu = 0;
-  if (ncu == 0) ncu = (int)env_long("FDDM_G128_NCU", 0);  // scheduling slots the split choice assumes (probe)
   if (ncu == 0) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||

@@ -94,102 +94,12 @@ struct LinJobs {
   float* out2[MAXJ];
 };
 
-// Block: 32 rows x 8 columns of one job, thread = (row, column) with the whole K; K in chunks of 128 staged in
-// LDS (in [32][128], W as [8][128]), the next chunk's global loads issued into registers before the current chunk's
-// FMAs (one exposed load latency per launch instead of one per chunk). Fixed summation order per output.
-constexpr int LKC = 128, LNC = 8;
-template <bool TW>
-__global__ void __launch_bounds__(256) linear_kernel(const float* __restrict__ in, long ldi, LinJobs J, long ldw,
-                                                     long ldo, const float* __restrict__ aux, long R, long N, long K,
-                                                     int act) {
-  __shared__ float Is[32][LKC + 4];
-  __shared__ float Ws[LNC][LKC + 4];
-  const int tid = threadIdx.x, c = tid & (LNC - 1), rr = tid >> 3;
-  const long n0 = (long)blockIdx.x * LNC, r0 = (long)blockIdx.z * 32;
-  const int j = blockIdx.y;
-  const float* W = J.W[j];
-  // per chunk each thread fetches 4 x 4 floats of `in` (rows ri, k 4*kq..) and 4 floats of W
-  float4 pin[4];
-  float pw[4];
-  auto fetch = [&](long k0) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int e = tid + 256 * q;          // 1024 float4 slots = 32 rows x 32 float4
-      const int ri = e >> 5, kq = e & 31;
-      const long r = r0 + ri, k = k0 + 4 * kq;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (r < R) {
-        const float* src = in + r * ldi + k;
-        if (k + 3 < K && ((((uintptr_t)src) & 15) == 0)) {
-          v = *(const float4*)src;
-        } else {
-          if (k < K) v.x = src[0];
-          if (k + 1 < K) v.y = src[1];
-          if (k + 2 < K) v.z = src[2];
-          if (k + 3 < K) v.w = src[3];
-        }
-      }
-      pin[q] = v;
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int e = tid + 256 * q;          // 1024 W elements = 8 columns x 128 k
-      int cc, kk;
-      if (TW) { kk = e >> 3; cc = e & 7; } else { cc = e >> 7; kk = e & 127; }
-      const long n = n0 + cc, k = k0 + kk;
-      pw[q] = (n < N && k < K) ? (TW ? W[k * ldw + n] : W[n * ldw + k]) : 0.f;
-    }
-  };
-  auto stash = [&]() {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int e = tid + 256 * q;
-      *(float4*)&Is[e >> 5][4 * (e & 31)] = pin[q];
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int e = tid + 256 * q;
-      if (TW) Ws[e & 7][e >> 3] = pw[q];
-      else Ws[e >> 7][e & 127] = pw[q];
-    }
-  };
-  float acc = 0.f;
-  fetch(0);
-  for (long k0 = 0; k0 < K; k0 += LKC) {
-    __syncthreads();                        // the previous chunk's reads are done
-    stash();
-    __syncthreads();
-    if (k0 + LKC < K) fetch(k0 + LKC);
-#pragma unroll 8
-    for (int kk = 0; kk < LKC; kk += 4) {
-      const float4 a = *(const float4*)&Is[rr][kk];
-      const float4 w = *(const float4*)&Ws[c][kk];
-      acc = fmaf(a.x, w.x, acc);
-      acc = fmaf(a.y, w.y, acc);
-      acc = fmaf(a.z, w.z, acc);
-      acc = fmaf(a.w, w.w, acc);
-    }
-  }
-  const long n = n0 + c, r = r0 + rr;
-  if (n >= N || r >= R) return;
-  const float bias = J.b[j] ? J.b[j][n] : 0.f;
-  const float v = acc + bias;
-  if (act == 1) {
-    J.out[j][r * ldo + n] = v;
-    J.out2[j][r * ldo + n] = v / (1.f + expf(-v));
-  } else if (act == 2) {
-    const float x = aux[r * ldo + n];
-    const float sg = 1.f / (1.f + expf(-x));
-    J.out[j][r * ldo + n] = acc * (sg * (1.f + x * (1.f - sg)));
-  } else {
-    J.out[j][r * ldo + n] = v;
-  }
-}
+constexpr int LNC = 8;  // output columns per block
 
 // Round 2: 1024 threads per block = 4 K-quarters x (32 rows x 8 columns); K in chunks of 512 staged in LDS (the
 // decoder's conditioning Linears have K = d_model: one chunk), each thread a 128-long FMA chain over its quarter,
 // the four partial sums added through LDS in a fixed order. A [32, 512] x [512, 512] Linear: 11.7 us with the
-// 256-thread block above (512-long chains, four chunk rounds), the 12 FiLM projections 28 us (tools/cond_bench.py).
+// round-1 256-thread block (512-long chains, four chunk rounds), the 12 FiLM projections 28 us (tools/cond_bench.py).
 constexpr int LKC2 = 512, LKQ = LKC2 / 4;
 template <bool TW>
 __global__ void __launch_bounds__(1024) linear4_kernel(const float* __restrict__ in, long ldi, LinJobs J, long ldw,
@@ -407,13 +317,6 @@ FDDM_API int fddm_small_linear(const float* in, long ldi, int njobs, const float
   }
   if (act == 2 && !aux) return (int)hipErrorInvalidValue;
   dim3 g((unsigned)((N + LNC - 1) / LNC), (unsigned)njobs, (unsigned)((R + 31) / 32));
-  if (getenv("FDDM_SMALL_LIN1")) {  // the 256-thread form (probe)
-    if (transpose_w)
-      hipLaunchKernelGGL(linear_kernel<true>, g, dim3(256), 0, (hipStream_t)hs, in, ldi, J, ldw, ldo, aux, R, N, K, act);
-    else
-      hipLaunchKernelGGL(linear_kernel<false>, g, dim3(256), 0, (hipStream_t)hs, in, ldi, J, ldw, ldo, aux, R, N, K, act);
-    return (int)hipGetLastError();
-  }
   if (transpose_w)
     hipLaunchKernelGGL(linear4_kernel<true>, g, dim3(1024), 0, (hipStream_t)hs, in, ldi, J, ldw, ldo, aux, R, N, K, act);
   else

@@ -301,8 +301,7 @@ FDDM_API int fddm_conv0_gn_gelu(int out_dtype, const float* x, const float* w, c
   float* scsh = (float*)(ws + B * nb * c0_nq<10>());
   hipLaunchKernelGGL(conv0_gn_affine_kernel<10>, dim3((unsigned)B), dim3(512), 0, s, ws, nb, w, gamma, beta, scsh, T0, C,
                      eps);
-  static const bool valu = getenv("FDDM_CONV0_VALU") != nullptr;  // A/B probe: the VALU recompute kernel
-  if (out_dtype == FDDM_BF16 && C % 512 == 0 && !valu) {
+  if (out_dtype == FDDM_BF16 && C % 512 == 0) {
     dim3 gm((unsigned)((T0 + C0M_FRAMES - 1) / C0M_FRAMES), (unsigned)B, (unsigned)(C / 512));
     hipLaunchKernelGGL(conv0_mfma_kernel, gm, dim3(512), 0, s, x, w, scsh, (bf16_t*)out, nsamp, T0, C, S);
     return (int)hipGetLastError();

@@ -93,6 +93,17 @@ def _gemm_padded(A, B, C, M, N, K, a_kc, b_kc, lda, ldb, ldc, epi, bias, alpha, 
     return C
 
 
+GEMM_PATHS = {"auto": 0, "big": 1, "small": 2, "256": 3, "128": 4}
+
+
+def gemm_force_path(name: str) -> str:
+    """Force a GEMM kernel family for every following fddm_gemm / conv GEMM launch (tests and diagnostics; "auto"
+    restores the shape-based choice). Returns the previous setting's name."""
+    from ._lib import lib
+    old = lib().fddm_gemm_force_path(GEMM_PATHS[name])     # returns the previous path, not an error code
+    return {v: k for k, v in GEMM_PATHS.items()}[old]
+
+
 def gemm(A, B, C, M, N, K, *, a_kc=True, b_kc=True, lda, ldb, ldc, epi=EPI_STORE, bias=None, alpha=1.0,
          C2=None, Mi=0, sAb=0, drop_p=0.0, seed=0, rng_stream=0, colsum=None):
     """C[m][n] = alpha * sum_k A(m,k) B(n,k) (+bias, epilogue). Compute dtype = B.dtype.

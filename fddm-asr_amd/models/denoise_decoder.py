@@ -12,7 +12,6 @@ produced (the encoder is frozen and its projection is never optimised, train.py:
 from __future__ import annotations
 
 import math
-import os
 from typing import Literal, Optional, Tuple
 
 import torch
@@ -205,7 +204,7 @@ class DenoisingTransformerDecoder(nn.Module):
         attention forward kernels then read one word per (query, 64-key tile) instead of drawing them, and the
         backward reads the same words. bf16 training only (the fp32 parity kernels draw their own)."""
         p = self.blocks[0].p if (self.training and len(self.blocks)) else 0.0
-        if p <= 0 or rt.compute_dtype() != torch.bfloat16 or os.environ.get("FDDM_PRE_BITS") == "0":
+        if p <= 0 or rt.compute_dtype() != torch.bfloat16:
             return None
         H, nb = self.nhead, len(self.blocks)
         ws = B * H * L * ((L + 63) // 64)
@@ -223,7 +222,7 @@ class DenoisingTransformerDecoder(nn.Module):
         state, so NL launches of [B*S, 2d] (one 256^2-tile round each at C2) become one launch of NL x the work.
         Block i attends to columns [2d*i, 2d*(i+1)) (row stride NL*2d); the K|V weight gradients stay in each
         block's backward (cond carries no gradient)."""
-        if len(self.blocks) < 2 or os.environ.get("FDDM_CROSS_KV_FUSED", "1") == "0":
+        if len(self.blocks) < 2:
             return None
         d = self.d_model
         w = torch.cat([rt.wt(blk.cross_attn.in_proj_weight)[d:] for blk in self.blocks])

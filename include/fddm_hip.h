@@ -185,6 +185,11 @@ int fddm_lfd_bwd_colstat(int zt_dtype, const float* dzt, const void* zt, float* 
 int fddm_lfd_std_bwd_apply(int zt_dtype, const float* dzt, const void* zt, const float* inv_std, const float* sums,
                            float inv_n, float scale, float* dz, long B, long C, void* hip_stream);
 
+/* ---- GEMM kernel-family override for tests and diagnostics (0 = automatic; 1 no 256x256 kernel, 2 register-staged
+ *      128x128 only, 3 256x256 wherever its preconditions hold, 4 128x128 LDS-DMA ring wherever they hold). Returns
+ *      the previous setting. Process-wide; the train step never sets it. */
+int fddm_gemm_force_path(int path);
+
 /* ---- dropout-seed offset for HIP-graph replays of the train step: every launch enqueued while `off` (a device u64)
  *      is set reads its effective dropout seed as seed + *off at run time (null: none), so one captured step replays
  *      with the seeds the host's counter has moved on to (identical to an eager step's). Returns 1 if one was set. */

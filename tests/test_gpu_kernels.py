@@ -27,6 +27,14 @@ def _lib():
     return ops
 
 
+@pytest.fixture
+def gemm_path():
+    """Setter of the GEMM kernel-family override (ops.gemm_force_path); restores the automatic choice afterwards."""
+    from fddm_hip import ops as o
+    yield o.gemm_force_path
+    o.gemm_force_path("auto")
+
+
 def ops():
     from fddm_hip import ops as o
     return o
@@ -110,8 +118,8 @@ def test_weight_grad_gemm_with_fused_bias_grad(dtype, M, N, K):
 @pytest.mark.parametrize("M,N,K,epi,odt", [(8192, 2048, 512, 0, "bf16"), (15968, 768, 3072, 1, "bf16"),
                                            (8200, 2056, 768, 3, "bf16"), (8192, 8000, 512, 0, "f32"),
                                            (300, 264, 64, 0, "bf16"), (1000, 3072, 192, 1, "bf16")])
-def test_big_gemm_matches_torch(M, N, K, epi, odt, path, monkeypatch):
-    """256x256 8-phase GEMM / 256x128 LDS-DMA GEMM (FDDM_GEMM_PATH) vs torch fp32 on the same bf16 operands,
+def test_big_gemm_matches_torch(M, N, K, epi, odt, path, monkeypatch, gemm_path):
+    """256x256 8-phase GEMM / 256x128 LDS-DMA GEMM (ops.gemm_force_path) vs torch fp32 on the same bf16 operands,
     and vs the 128x128 path — ragged M/N edges, f32 output, dropout-free GELU epilogues included."""
     o = ops()
     gen = torch.Generator(device=dev).manual_seed(3)
@@ -122,7 +130,7 @@ def test_big_gemm_matches_torch(M, N, K, epi, odt, path, monkeypatch):
     odtype = torch.float32 if odt == "f32" else torch.bfloat16
     out = torch.full((M, N), float("nan"), device=dev, dtype=odtype)
     act = torch.full((M, N), float("nan"), device=dev, dtype=odtype)
-    monkeypatch.setenv("FDDM_GEMM_PATH", path)
+    gemm_path(path)
     o.gemm(A, W, out, M, N, K, lda=K, ldb=K, ldc=N, bias=b, epi=epi, C2=act if epi == 1 else None)
     chk = (act if epi == 1 else out).float()
     want = F.gelu(ref) if epi in (1, 3) else ref
@@ -130,7 +138,7 @@ def test_big_gemm_matches_torch(M, N, K, epi, odt, path, monkeypatch):
     assert err <= 2e-2 * want.abs().max().item(), err
     if epi == 1:
         assert (out.float() - ref).abs().max().item() <= 2e-2 * ref.abs().max().item()
-    monkeypatch.setenv("FDDM_GEMM_PATH", "small")
+    gemm_path("small")
     out2 = torch.empty_like(out)
     act2 = torch.empty_like(act)
     o.gemm(A, W, out2, M, N, K, lda=K, ldb=K, ldc=N, bias=b, epi=epi, C2=act2 if epi == 1 else None)
@@ -176,11 +184,11 @@ def test_grouped_weight_grads_match_torch():
 
 
 @pytest.mark.parametrize("M,N,K", [(1000, 520, 512), (8192, 512, 2048), (128, 128, 64)])
-def test_gemm128_input_grad_layout(M, N, K, monkeypatch):
+def test_gemm128_input_grad_layout(M, N, K, monkeypatch, gemm_path):
     """128x128 LDS-DMA kernel, A K-contiguous x B as stored [K][N] (dX = dY W): f32 store / accumulate,
     bf16 store, dGELU+dropout epilogue — against torch in fp64 on the same bf16 operands."""
     o = ops()
-    monkeypatch.setenv("FDDM_GEMM_PATH", "128")
+    gemm_path("128")
     gen = torch.Generator(device=dev).manual_seed(21)
     dy = torch.randn(M, K, device=dev, generator=gen).bfloat16()
     W = (torch.randn(K, N, device=dev, generator=gen) / math.sqrt(K)).bfloat16()
@@ -202,18 +210,18 @@ def test_gemm128_input_grad_layout(M, N, K, monkeypatch):
     gg = 0.5 * (1 + torch.erf(x / math.sqrt(2))) + x * torch.exp(-0.5 * x * x) / math.sqrt(2 * math.pi)
     keep = O.dropout_keep(9, 4, M * N, 0.1).view(M, N).to(dev)
     close(dh.float(), ref * gg * keep / 0.9, rtol=2e-2, what="dgelu")
-    monkeypatch.setenv("FDDM_GEMM_PATH", "small")
+    gemm_path("small")
     dh2 = torch.empty_like(dh)
     o.linear_dx(dy, W, out=dh2, epi=o.EPI_DGELU, C2=pre, drop_p=0.1, seed=9, rng_stream=4)
     assert torch.equal(dh == 0, dh2 == 0)
 
 
 @pytest.mark.parametrize("M,N,K", [(264, 200, 1000), (512, 512, 8192), (128, 128, 4096), (1024, 512, 15968)])
-def test_gemm128_weight_grad_layout(M, N, K, monkeypatch):
+def test_gemm128_weight_grad_layout(M, N, K, monkeypatch, gemm_path):
     """128x128 LDS-DMA kernel, both operands token-major (dW = dY^T X): ragged token counts read zeros past the
     end, split-K slices accumulate atomically, the bias gradient (colsum) is fused."""
     o = ops()
-    monkeypatch.setenv("FDDM_GEMM_PATH", "128")
+    gemm_path("128")
     gen = torch.Generator(device=dev).manual_seed(22)
     dy = torch.randn(K, M, device=dev, generator=gen).bfloat16()
     x = torch.randn(K, N, device=dev, generator=gen).bfloat16()
@@ -228,11 +236,11 @@ def test_gemm128_weight_grad_layout(M, N, K, monkeypatch):
     close(db, 2 * dy.double().sum(0), rtol=1e-4, what="db acc")
 
 
-def test_gemm128_grouped_weight_grads(monkeypatch):
+def test_gemm128_grouped_weight_grads(monkeypatch, gemm_path):
     """The decoder block's 8 weight-gradient GEMMs in one 128x128 grouped launch (automatic split balance):
     token counts 8192 / 15968 (ragged), column slices of shared gradient buffers, fused bias gradients."""
     o = ops()
-    monkeypatch.delenv("FDDM_GEMM_PATH", raising=False)
+    gemm_path("auto")
     gen = torch.Generator(device=dev).manual_seed(23)
     T, d, FF, TS = 2048, 256, 1024, 3992
     specs = [(T, d, FF), (T, FF, d), (T, d, d), (T, d, d), (TS, 2 * d, d), (T, d, d), (T, 2 * d, d), (T, d, d)]
@@ -250,12 +258,12 @@ def test_gemm128_grouped_weight_grads(monkeypatch):
         close(db, rb, rtol=1e-4, what=f"db job{i}")
 
 
-def test_grouped_weight_grads_ragged_tiles(monkeypatch):
+def test_grouped_weight_grads_ragged_tiles(monkeypatch, gemm_path):
     """Grouped weight gradients: ragged rows and columns (shifted last tiles, overlap added once), ragged token
     counts, a split-K problem among read-modify-write ones (the batched read-modify-write epilogue), strided
     destinations, fused bias gradients."""
     o = ops()
-    monkeypatch.delenv("FDDM_GEMM_PATH", raising=False)
+    gemm_path("auto")
     gen = torch.Generator(device=dev).manual_seed(29)
     specs = [(1000, 200, 320), (8192, 1536, 512), (3992, 136, 264), (15968, 256, 512), (2048, 384, 768)]
     jobs, refs = [], []
@@ -272,7 +280,7 @@ def test_grouped_weight_grads_ragged_tiles(monkeypatch):
         close(db, rb, rtol=1e-4, what=f"db job{i}")
 
 
-def test_gemm256_dropout_gelu_matches_small_path(monkeypatch):
+def test_gemm256_dropout_gelu_matches_small_path(monkeypatch, gemm_path):
     """EPI_GELU with dropout: the 256x256 epilogue draws the same keep mask (counter-based hash of m*N+n)."""
     o = ops()
     M, N, K, p = 1100, 2048, 512, 0.1
@@ -282,7 +290,7 @@ def test_gemm256_dropout_gelu_matches_small_path(monkeypatch):
     b = torch.randn(N, device=dev, generator=gen)
     outs = []
     for path in ("256", "small"):
-        monkeypatch.setenv("FDDM_GEMM_PATH", path)
+        gemm_path(path)
         pre = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
         act = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
         o.gemm(A, W, pre, M, N, K, lda=K, ldb=K, ldc=N, bias=b, epi=1, C2=act, drop_p=p, seed=7, rng_stream=3)
@@ -292,7 +300,7 @@ def test_gemm256_dropout_gelu_matches_small_path(monkeypatch):
 
 
 @pytest.mark.parametrize("path", ["256", "big"])
-def test_big_conv_gemm_matches_torch(path, monkeypatch):
+def test_big_conv_gemm_matches_torch(path, monkeypatch, gemm_path):
     o = ops()
     B, Cin, Tin, Cout, k, s = 8, 512, 4001, 512, 3, 2
     gen = torch.Generator(device=dev).manual_seed(4)
@@ -302,7 +310,7 @@ def test_big_conv_gemm_matches_torch(path, monkeypatch):
     Tout = ref.shape[1]
     Wp = w.permute(0, 2, 1).contiguous()
     out = torch.empty(B, Tout, Cout, device=dev, dtype=torch.bfloat16)
-    monkeypatch.setenv("FDDM_GEMM_PATH", path)
+    gemm_path(path)
     o.conv1d_gemm(x, Wp, out, lda=Cin, sAb=Tin * Cin, Tin=Tin, Cg=Cin, cstride=s, cpad=0, Bn=B, Tout=Tout, N=Cout,
                   K=k * Cin, gelu=True)
     err = (out.float() - ref).abs().max().item()
@@ -391,9 +399,13 @@ def _attn_ref(q, k, v, keep, p_drop, seed, stream, gate=None, table=None):
                                                  (129, 257, True, 0.1, True), (96, 256, True, 0.1, True),
                                                  (64, 499, False, 0.0, False), (256, 256, False, 0.1, True),
                                                  (200, 200, True, 0.1, True), (32, 32, False, 0.0, False),
-                                                 (512, 512, True, 0.1, True), (300, 499, False, 0.1, True)])
+                                                 (512, 512, True, 0.1, True), (300, 499, False, 0.1, True),
+                                                 (40, 1100, True, 0.1, True), (1100, 70, False, 0.1, True)])
 def test_attention_fwd_bwd(dtype, Lq, Lk, masked, p, bits):
-    """bits: the forward records the dropout keep bits and the backward reads them (bf16 path)."""
+    """bits: the forward records the dropout keep bits and the backward reads them (bf16 path). The shapes reach every
+    bf16 kernel the dispatch (csrc/attention.hip run<T>) selects: fwd6 for Lk <= 1024 (keep bits drawn in-kernel and
+    recorded, or rehashed later when no buffer is given), fwd2 past that; the fused bwd3s for Lq == Lk <= 256 with
+    recorded bits; dq4 / dkv4 up to 1024; dq2 / dkv2 for rehashed bits or longer sequences (1100)."""
     o = ops()
     B, H = 2, 3
     D = H * 64
@@ -450,37 +462,6 @@ def test_attention_drop_bits_producer_matches_oracle(Lq, Lk):
         got = bits.permute(0, 2, 1, 3).reshape(B * H, Lq, nt * 64)[:, :, :Lk]
         ref = O.attn_dropout_keep(seed, 7 + 6 * s_, B, H, Lq, Lk, p).reshape(B * H, Lq, Lk)
         assert torch.equal(got, ref), f"site {s_}: {(got != ref).sum().item()} bits differ"
-
-
-@pytest.mark.parametrize("L,masked,p", [(256, False, 0.1), (200, True, 0.1), (70, True, 0.0), (32, False, 0.1)])
-def test_attention_fused_self_bwd_equals_split(L, masked, p, monkeypatch):
-    """Self-attention shapes (Lq == Lk <= 256, bf16) take the fused one-launch backward (bwd3s_kernel); it runs the
-    same arithmetic as the dQ and dK/dV kernels (FDDM_ATTN_BWD_SPLIT=1), so the gradients are bit-identical."""
-    o = ops()
-    B, H = 3, 8
-    D = H * 64
-    x = [torch.randn(B * L, D, generator=g(40 + j)).to(dev, torch.bfloat16) for j in range(4)]
-    qd, kd, vd, dod = x
-    kk = None
-    if masked:
-        kk = torch.ones(B, L, dtype=torch.uint8, device=dev)
-        kk[2, L - 37:] = 0
-    od = torch.empty(B * L, D, device=dev, dtype=torch.bfloat16)
-    lse = torch.empty(B * H, L, device=dev)
-    db = o.drop_bits(B, H, L, L, dev) if p > 0 else None
-    o.attn_fwd(qd, kd, vd, od, lse, B, H, L, L, key_keep=kk, drop_p=p, seed=11, rng_stream=3, dbits=db)
-    outs = []
-    for split in (False, True):
-        if split:
-            monkeypatch.setenv("FDDM_ATTN_BWD_SPLIT", "1")
-        dq, dk, dv = (torch.full_like(qd, float("nan")) for _ in range(3))
-        o.attn_bwd(qd, kd, vd, od, dod, lse, dq, dk, dv, B, H, L, L, key_keep=kk, drop_p=p, seed=11, rng_stream=3,
-                   dbits=db)
-        torch.cuda.synchronize()
-        outs.append((dq, dk, dv))
-    for name, a, b in zip(("dq", "dk", "dv"), *outs):
-        assert torch.isfinite(a.float()).all(), name
-        assert torch.equal(a, b), f"{name}: fused self-attention backward differs from the split kernels"
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
