@@ -3,8 +3,8 @@
 # arm — a space-separated list of VAR=value settings, or "-" for the defaults — and the arms run alternating for
 # ROUNDS rounds (default 2). Replaces the round-2 one-offs (ab_env*.sh, cap_sweep*.sh, deccap/ncu/splitk sweeps):
 #   encoder CU caps:       bash tools/ab.sh "FDDM_ENC_CUS_CONV=128 FDDM_ENC_CUS=192" "FDDM_ENC_CUS_CONV=144 FDDM_ENC_CUS=192"
-#   grouped dW split plan: bash tools/ab.sh - "FDDM_G128_NCU=512"
-#   extra bench.py flags:  BENCH_ARGS="--config c4" ROUNDS=3 bash tools/ab.sh - "FDDM_CROSS_KV_FUSED=0"
+#   graph replay:          bash tools/ab.sh - "FDDM_STEP_GRAPH=1"
+#   extra bench.py flags:  BENCH_ARGS="--config c4" ROUNDS=3 bash tools/ab.sh - "FDDM_ENC_CUS=208"
 rounds=${ROUNDS:-2}
 args=${BENCH_ARGS:-}
 mkdir -p gpurun_out

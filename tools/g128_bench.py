@@ -6,10 +6,12 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "fddm-asr_amd"))
-os.environ.setdefault("FDDM_GEMM_PATH", "128")
+GEMM_PATH = "128"   # applied after the import below (ops.gemm_force_path)
 import torch  # noqa: E402
 
 from fddm_hip import ops  # noqa: E402
+
+ops.gemm_force_path(GEMM_PATH)
 
 dev = torch.device("cuda:0")
 bf = torch.bfloat16

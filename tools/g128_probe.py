@@ -13,7 +13,7 @@ from gemm_bench import timeit  # noqa: E402
 
 dev = torch.device("cuda:0")
 bf = torch.bfloat16
-os.environ["FDDM_GEMM_PATH"] = "128"
+__import__("fddm_hip.ops", fromlist=["ops"]).gemm_force_path("128")
 res = []
 for (M, N, K) in [(8192, 512, 2048), (8192, 512, 512), (15968, 512, 1024)]:
     dy = torch.randn(M, K, device=dev, dtype=bf)
@@ -28,7 +28,7 @@ for K, M, N in specs:
     jobs.append((torch.randn(K, M, device=dev, dtype=bf), torch.randn(K, N, device=dev, dtype=bf),
                  torch.zeros(M, N, device=dev), torch.zeros(M, device=dev)))
     fl += 2 * M * N * K
-os.environ.pop("FDDM_GEMM_PATH")
+__import__("fddm_hip.ops", fromlist=["ops"]).gemm_force_path("auto")
 ms = timeit(lambda: ops.linear_dw_grouped(jobs))
 res.append(f"dW grouped: {ms*1e3:6.1f} us {fl/ms/1e9:6.0f} TF/s")
 print(os.path.basename(os.environ.get("FDDM_HIP_LIB", "in-tree")), " | ".join(res), flush=True)

@@ -14,7 +14,7 @@ from fddm_hip._lib import lib  # noqa: E402
 
 NS = 48
 dev = torch.device("cuda:0")
-os.environ["FDDM_GEMM_PATH"] = "128"
+__import__("fddm_hip.ops", fromlist=["ops"]).gemm_force_path("128")
 
 
 def run(name, fn, nblk):

@@ -14,7 +14,7 @@ from fddm_hip import _lib, ops  # noqa: E402
 NS = 64
 M, N, K = (int(a) for a in sys.argv[1:4])
 EPI = int(sys.argv[4]) if len(sys.argv) > 4 else 0
-os.environ["FDDM_GEMM_PATH"] = "256"
+__import__("fddm_hip.ops", fromlist=["ops"]).gemm_force_path("256")
 dev = torch.device("cuda:0")
 A = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
 W = torch.randn(N, K, device=dev, dtype=torch.bfloat16) / 30

@@ -25,7 +25,7 @@ def timeit(fn, iters=20):
 
 
 tag = os.path.basename(os.environ.get("FDDM_HIP_LIB", "base"))
-os.environ["FDDM_GEMM_PATH"] = "256"
+__import__("fddm_hip.ops", fromlist=["ops"]).gemm_force_path("256")
 for (M, N, K, epi) in [(15968, 3072, 256, 0), (15968, 3072, 768, 0), (15968, 3072, 1536, 0), (15968, 3072, 3072, 0),
                        (15968, 3072, 768, 3), (15968, 2304, 768, 0), (15968, 768, 3072, 0), (8192, 8192, 8192, 0),
                        (4096, 4096, 4096, 0)]:

@@ -54,7 +54,7 @@ x1 = torch.zeros(1, device=dev)
 x256 = torch.zeros(256 * 1024, device=dev)
 print(f"fill 1 elem:      graph {graph_time(lambda: x1.fill_(1.0)):6.2f} us/launch  eager {eager_time(lambda: x1.fill_(1.0)):6.2f}")
 print(f"fill 256 blocks:  graph {graph_time(lambda: x256.fill_(1.0)):6.2f} us/launch  eager {eager_time(lambda: x256.fill_(1.0)):6.2f}")
-os.environ["FDDM_GEMM_PATH"] = "128"
+__import__("fddm_hip.ops", fromlist=["ops"]).gemm_force_path("128")
 bf = torch.bfloat16
 for K in (64, 512):
     x = torch.randn(8192, K, device=dev, dtype=bf)
