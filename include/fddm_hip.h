@@ -190,14 +190,6 @@ int fddm_lfd_std_bwd_apply(int zt_dtype, const float* dzt, const void* zt, const
  *      the previous setting. Process-wide; the train step never sets it. */
 int fddm_gemm_force_path(int path);
 
-/* ---- experimental one-wave-per-SIMD 256x256 bf16 NT GEMM (tools/g1w_bench.py): C[m][n] = A[m][:] . B[n][:] +
- *      bias[n] with bf16 A/B/C, f32 bias (may be NULL); M, N >= 256, K % 64 == 0, leading dims % 8 == 0. grid =
- *      persistent workgroups (<= 0: 256); variant: the
- *      K-loop schedule under test (0 next K-step's DMA spread over the MFMAs, 1 issued at once after the barrier, 2 one flat
- *      (tile, K-step) stream with the DMA two steps ahead across tiles).
- *      Not used by the train step. */
-int fddm_gemm1w_probe(const void* A, long lda, const void* B, long ldb, void* C, long ldc, const float* bias, long M,
-                      long N, long K, int grid, int variant, void* hip_stream);
 
 /* ---- dropout-seed offset for HIP-graph replays of the train step: every launch enqueued while `off` (a device u64)
  *      is set reads its effective dropout seed as seed + *off at run time (null: none), so one captured step replays
