@@ -425,22 +425,28 @@ __global__ void __launch_bounds__(NT) kl4_fused_kernel(const float* __restrict__
 
   // one row pass: the KL's generic log terms and the gradient's two sums; the mask count of this utterance rides
   // in the same block reduction
+  // VALU budget: the pass is as long as the row's HBM time, so per element one exp (above), one rcp (kept in
+  // registers for the output pass) and a quarter of a log: sum_k log(P_k + eps) is taken as log of the product of
+  // each float4's four factors (each >= eps = 1e-8, so a product >= 1e-32 stays a normal f32)
   float acc = 0.f, a1 = 0.f, a2 = 0.f, cnt = 0.f;
+  float r[NV][4];
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const bool ok = tid + (long)NT * i < V4;
+    float prod = 1.f;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const float xh = v[i][j] * resc;
       v[i][j] = xh;
-      const float P = fmaf(pa, xh, pb);
-      const float r = __builtin_amdgcn_rcpf(P + eps);
+      const float Pe = fmaf(pa, xh, pb) + eps;
+      r[i][j] = __builtin_amdgcn_rcpf(Pe);
+      prod *= Pe;
       if (ok) {
-        acc += LQg - __logf(P + eps);
-        a1 += P * r;
-        a2 += xh * r;
+        a1 += (Pe - eps) * r[i][j];
+        a2 += xh * r[i][j];
       }
     }
+    if (ok) acc += 4.f * LQg - __logf(prod);
   }
   if (mask)
     for (long l = tid; l < L; l += NT) cnt += mask[b * L + l] ? 1.f : 0.f;
@@ -474,7 +480,7 @@ __global__ void __launch_bounds__(NT) kl4_fused_kernel(const float* __restrict__
     if (q < iv4) {
       float o[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = wr * v[i][j] * (gc * __builtin_amdgcn_rcpf(fmaf(pa, v[i][j], pb) + eps) - G);
+      for (int j = 0; j < 4; ++j) o[j] = wr * v[i][j] * (gc * r[i][j] - G);
       if (q == qxt || q == qx0) {
         for (int j = 0; j < 4; ++j) {
           const long k = 4L * q + j;
