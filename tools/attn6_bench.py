@@ -57,6 +57,9 @@ def main():
             outs[tag] = (o.clone(), lse.clone(), db.clone())
             res.append(f"fwd6 {tag} {t*1e3:6.1f} us {fl/t/1e12*1e3/2500:5.3f}")
         tb = timeit(lambda: ops.attn_drop_bits(db.view(1, -1), 1, B, H, Lq, Lk, 0.1, 1, 1, 0))
+        ns = 6     # the train step produces all blocks' sites of one kind in one launch
+        db6 = torch.empty(ns, db.numel(), device=dev, dtype=torch.int64)
+        tb6 = timeit(lambda: ops.attn_drop_bits(db6, ns, B, H, Lq, Lk, 0.1, 1, 1, 6))
         same = all(torch.equal(a_, b_) for a_, b_ in zip(outs["words"][:2], outs["tables"][:2]))
         wsame = torch.equal(outs["words"][2].view(B * H, -1, Lq)[:, :1], outs["tables"][2].view(B * H, -1, Lq)[:, :1])
         o, lse, db = outs["words"]
@@ -66,7 +69,7 @@ def main():
         dv = torch.empty(B * Lk, H * 64, device=dev, dtype=bf)
         tbw = timeit(lambda: ops.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, B, H, Lq, Lk, key_keep=keep, drop_p=0.1,
                                           seed=1, rng_stream=1, dbits=db))
-        print(f"{name:28s} " + " | ".join(res) + f" | bits alone {tb*1e3:5.1f} us | bwd {tbw*1e3:6.1f} us "
+        print(f"{name:28s} " + " | ".join(res) + f" | bits alone {tb*1e3:5.1f} us, x{ns} sites {tb6*1e3/ns:5.1f} us/site | bwd {tbw*1e3:6.1f} us "
               f"{2.5*fl/tbw/1e12*1e3/2500:5.3f} | outputs equal {same}, tile-0 words equal {wsame}", flush=True)
 
 
