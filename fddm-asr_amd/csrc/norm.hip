@@ -21,6 +21,10 @@ struct LnFwdArgs {
   float eps;
   uint64_t seed, stream; unsigned thr16; float drop_scale;
   const uint64_t* seed_off;  // graph-replay seed offset (common.h eff_seed) or null
+  // optional RoPE of the output (the next decoder block's q = k input, misc.hip rope_fwd_kernel's formula):
+  // rope_out[r][4q + j] = o[8q + 2j] cs[p][8q + 2j] - o[8q + 2j + 1] sn[p][8q + 2j + 1],
+  // rope_out[r][d/2 + 4q + j] = o[8q + 2j] sn[p][8q + 2j] + o[8q + 2j + 1] cs[p][8q + 2j + 1], p = r % rope_L
+  const float *rcos, *rsin; void* rope_out; long rope_L;
 };
 
 // 8 consecutive elements per lane per chunk (16-B bf16 / 32-B f32 accesses); d % 8 == 0
@@ -54,6 +58,15 @@ __device__ __forceinline__ void st8(T* p, const float (&v)[8]) {
   }
 }
 
+template <typename OT>
+__device__ __forceinline__ void st4v(OT* p, float a, float b, float c, float d_) {
+  if constexpr (sizeof(OT) == 2) {
+    *(uint2*)p = make_uint2(pk_bf16(a, b), pk_bf16(c, d_));
+  } else {
+    *(float4*)p = make_float4(a, b, c, d_);
+  }
+}
+
 constexpr int LN_MAXCH = 2;  // chunks of 8 per lane: d <= 1024
 
 // wave-wide sum in the VALU: DPP within rows of 16 lanes (quad swaps, half-row and row mirrors), then the
@@ -78,7 +91,7 @@ __device__ __forceinline__ float wave_sum_v(float v) {
 // so a wave waits for one memory round trip, not three; the two row reductions run in the VALU (wave_sum_v).
 // HY: residual branch y present, HF: FiLM present (compile-time: a load under a runtime branch gets its own wait)
 // CH chunks of 8 per lane: 1 for d <= 512 (the decoder), 2 for d <= 1024 (WavLM 768)
-template <typename XT, typename YT, typename OT, bool HY, bool HF, int CH>
+template <typename XT, typename YT, typename OT, bool HY, bool HF, int CH, bool RP = false>
 __global__ void __launch_bounds__(256) ln_fwd_kernel(LnFwdArgs a) {
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
@@ -87,7 +100,8 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(LnFwdArgs a) {
   const XT* x = (const XT*)a.x + row * d;
   const YT* y = HY ? (const YT*)a.y + row * d : nullptr;
   const long b = HF ? row / a.rows_per_batch : 0;
-  float v[CH][8], yv[CH][8], gm[CH][8], bt[CH][8], fs[CH][8], fh[CH][8];
+  float v[CH][8], yv[CH][8], gm[CH][8], bt[CH][8], fs[CH][8], fh[CH][8], rc[CH][8], rs[CH][8];
+  const long rp = RP ? row % a.rope_L : 0;
   // lanes past the row end load its last chunk again (no divergent branch around the loads: a load inside one
   // would be waited for at the branch join) and contribute zeros
 #pragma unroll
@@ -100,6 +114,10 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(LnFwdArgs a) {
     if constexpr (HF) {
       ld8<float>(a.fsc + b * d + c0, fs[i]);
       ld8<float>(a.fsh + b * d + c0, fh[i]);
+    }
+    if constexpr (RP) {
+      ld8<float>(a.rcos + rp * d + c0, rc[i]);
+      ld8<float>(a.rsin + rp * d + c0, rs[i]);
     }
   }
   float sum = 0.f;
@@ -156,6 +174,17 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(LnFwdArgs a) {
       }
       if (a.out_f32) st8<float>(a.out_f32 + row * d + c0, o);
       if (a.out_t) st8<OT>((OT*)a.out_t + row * d + c0, o);
+      if constexpr (RP) {
+        float lo[4], hi[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          lo[j] = o[2 * j] * rc[i][2 * j] - o[2 * j + 1] * rs[i][2 * j + 1];
+          hi[j] = o[2 * j] * rs[i][2 * j] + o[2 * j + 1] * rc[i][2 * j + 1];
+        }
+        OT* ro = (OT*)a.rope_out + row * d;
+        st4v<OT>(ro + 4 * ch, lo[0], lo[1], lo[2], lo[3]);
+        st4v<OT>(ro + d / 2 + 4 * ch, hi[0], hi[1], hi[2], hi[3]);
+      }
     }
   }
   if (lane == 0) {
@@ -413,14 +442,19 @@ using namespace fddm;
 FDDM_API int fddm_ln_fwd(int x_dtype, int y_dtype, int out_dtype, const void* x, const void* y, const float* gamma,
                          const float* beta, const float* film_scale, const float* film_shift, float* out_f32,
                          void* out_t, float* save_s, float* mean, float* rstd, long N, long d, long rows_per_batch,
-                         float eps, float drop_p, unsigned long long seed, unsigned long long stream, void* hs) {
+                         float eps, float drop_p, unsigned long long seed, unsigned long long stream,
+                         const float* rope_cos, const float* rope_sin, void* rope_out, long rope_L, void* hs) {
   if (N <= 0) return 0;
   if (d > 64 * 8 * LN_MAXCH || d % 8) return (int)hipErrorInvalidValue;
+  if (rope_out && (!rope_cos || !rope_sin || rope_L <= 0 || d % 16 ||
+                   (((uintptr_t)rope_cos | (uintptr_t)rope_sin | (uintptr_t)rope_out) & 15)))
+    return (int)hipErrorInvalidValue;
   if ((((uintptr_t)gamma | (uintptr_t)beta | (uintptr_t)film_scale | (uintptr_t)film_shift | (uintptr_t)x |
         (uintptr_t)y) & 15))
     return (int)hipErrorInvalidValue;  // 16-B vector accesses
   LnFwdArgs a{x, y, gamma, beta, film_scale, film_shift, out_f32, out_t, save_s, mean, rstd, N, d,
-              rows_per_batch > 0 ? rows_per_batch : N, eps, seed, stream, 0u, 1.f, g_seed_off};
+              rows_per_batch > 0 ? rows_per_batch : N, eps, seed, stream, 0u, 1.f, g_seed_off, rope_cos, rope_sin,
+              rope_out, rope_L};
   if (drop_p > 0.f) {
     a.thr16 = (unsigned)llrintf(drop_p * 65536.f);
     a.drop_scale = 1.f / (1.f - drop_p);
@@ -432,6 +466,13 @@ FDDM_API int fddm_ln_fwd(int x_dtype, int y_dtype, int out_dtype, const void* x,
   // one chunk of 8 per lane when d <= 512: the two-chunk form re-loaded every lane's last chunk (x, y, gamma, beta,
   // FiLM) for the decoder's d = 512 rows
   const bool ch1 = d <= 512;
+  if (rope_out) {  // the decoder's LN3 (f32 residual + bf16 branch -> bf16) only
+    if (!(x_dtype == FDDM_F32 && y_dtype == FDDM_BF16 && out_dtype == FDDM_BF16 && hy && !hf))
+      return (int)hipErrorInvalidValue;
+    if (ch1) hipLaunchKernelGGL((ln_fwd_kernel<float, bf16_t, bf16_t, true, false, 1, true>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((ln_fwd_kernel<float, bf16_t, bf16_t, true, false, 2, true>), grid, dim3(256), 0, s, a);
+    return (int)hipGetLastError();
+  }
 #define LNF2(XT, YT, OT, C)                                                                                    \
   do {                                                                                                         \
     if (hy && hf) hipLaunchKernelGGL((ln_fwd_kernel<XT, YT, OT, true, true, C>), grid, dim3(256), 0, s, a);     \

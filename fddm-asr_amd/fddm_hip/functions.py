@@ -218,9 +218,13 @@ class DecoderBlockFn(torch.autograd.Function):
         st = 6 * layer
         W = {k: rt.wt(v) for k, v in (("sa", sa_w), ("so", so_w), ("ca", ca_w), ("co", co_w), ("f0", f0_w),
                                        ("f3", f3_w))}
-        # 1. RoPE on the block input (q = k = rope(x), v = x)
-        xr = torch.empty(N, d, device=dev, dtype=cd)
-        ops.rope_fwd(x, cos, sin, xr, L)
+        # 1. RoPE on the block input (q = k = rope(x), v = x): written by the previous block's LN3 when it was
+        # given a hand-off (meta[12]), else here
+        xr = meta[12] if len(meta) > 12 else None
+        if xr is None:
+            xr = torch.empty(N, d, device=dev, dtype=cd)
+            ops.rope_fwd(x, cos, sin, xr, L)
+        handoff = meta[13] if len(meta) > 13 else None
         qk = ops.linear(xr, W["sa"][: 2 * d], sa_b[: 2 * d], out_dtype=cd)
         v = ops.linear(xT, W["sa"][2 * d:], sa_b[2 * d:], out_dtype=cd)
         o = torch.empty(N, d, device=dev, dtype=cd)
@@ -273,8 +277,12 @@ class DecoderBlockFn(torch.autograd.Function):
         r3 = torch.empty(N, device=dev, dtype=F32)
         x3 = torch.empty(N, d, device=dev, dtype=F32)
         x3T = torch.empty(N, d, device=dev, dtype=cd)
+        rope = None
+        if handoff is not None and cd == torch.bfloat16:   # the next block's rope(x) from the same pass
+            handoff["xr"] = torch.empty(N, d, device=dev, dtype=cd)
+            rope = (cos, sin, handoff["xr"], L)
         ops.ln_fwd(x2, y3, n3w, n3b, out_f32=x3, out_t=x3T, save_s=s3, mean=m3, rstd=r3,
-                   drop_p=p, seed=seed, rng_stream=st + 6)
+                   drop_p=p, seed=seed, rng_stream=st + 6, rope=rope)
         ctx.save_for_backward(xT, xr, qk, v, o, lse, s1, m1, r1, x1T, qc, kvc, oc, lsec, s2, m2, r2, x2T, hpre, hact,
                               s3, m3, r3, cT, key_keep, fsc, *params)
         ctx.meta = meta

@@ -327,14 +327,17 @@ def attn_bwd(q, k, v, o, do, lse, dq, dk, dv, B, H, Lq, Lk, *, key_keep=None, dr
 
 # ----------------------------------------------------------------------------------- layernorm
 def ln_fwd(x, y, gamma, beta, *, out_f32=None, out_t=None, save_s=None, mean=None, rstd=None, film=None,
-           rows_per_batch=0, eps=1e-5, drop_p=0.0, seed=0, rng_stream=0):
+           rows_per_batch=0, eps=1e-5, drop_p=0.0, seed=0, rng_stream=0, rope=None):
+    """rope = (cos [L, d], sin [L, d], out bf16 [N, d], L): also write RoPE(output) — rope_fwd of the output — for the
+    decoder's next block (f32 x, bf16 y and out_t, no FiLM)."""
     N, d = x.shape
     fs, fh = film if film is not None else (None, None)
+    rc, rs, ro, rl = rope if rope is not None else (None, None, None, 0)
     out_code = code(out_t) if out_t is not None else code(x if y is None else y)
     ycode = code(y) if y is not None else code(x)
     call("fddm_ln_fwd", code(x), ycode, out_code, ptr(x), ptr(y), ptr(gamma), ptr(beta), ptr(fs), ptr(fh),
          ptr(out_f32), ptr(out_t), ptr(save_s), ptr(mean), ptr(rstd), N, d, rows_per_batch, float(eps), float(drop_p),
-         seed, rng_stream, stream())
+         seed, rng_stream, ptr(rc), ptr(rs), ptr(ro), rl, stream())
 
 
 def ln_bwd(dout, s, mean, rstd, gamma, beta, *, dres=None, dy_t=None, dgamma=None, dbeta=None, film_scale=None,

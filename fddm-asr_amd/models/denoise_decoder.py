@@ -123,13 +123,16 @@ class DecoderBlock(nn.Module):
                 self.ff[3].weight, self.ff[3].bias, self.norm1.weight, self.norm1.bias, self.norm2.weight,
                 self.norm2.bias, self.norm3.weight, self.norm3.bias)
 
-    def run(self, x, xT, cT, key_keep, film, B, L, S, layer, seed, cos, sin, kv=None, bits=None):
+    def run(self, x, xT, cT, key_keep, film, B, L, S, layer, seed, cos, sin, kv=None, bits=None, xr=None,
+            handoff=None):
         """film = (scale, shift, (dscale, dshift) accumulators or None) from DenoisingTransformerDecoder's
         conditioning Function; kv = this block's precomputed cross-attention K|V [B*S, 2d] (strided view) or None;
-        bits = (self, cross) attention-dropout keep-bit words already written for this block, or None."""
+        bits = (self, cross) attention-dropout keep-bit words already written for this block, or None;
+        xr = rope(x) already written by the previous block's LN3, or None; handoff = a dict in which this block's LN3
+        leaves rope(its output) under "xr" for the next block (bf16), or None."""
         fscale, fshift, gfilm = film
         p = self.p if self.training else 0.0
-        meta = (B, L, S, self.nhead, layer, p, seed, cos, sin, gfilm, kv, bits)
+        meta = (B, L, S, self.nhead, layer, p, seed, cos, sin, gfilm, kv, bits, xr, handoff)
         return FN.DecoderBlockFn.apply(x, xT, cT, key_keep, fscale, fshift, meta, *self.block_params())
 
 
@@ -189,11 +192,14 @@ class DenoisingTransformerDecoder(nn.Module):
         seed = rt.next_seed()
         kv_all = self._cross_kv(cT)
         bits = self._drop_bits(B, L, S, seed, dev)
+        xr = None
         for i, blk in enumerate(self.blocks):
             film = (films[2 * i], films[2 * i + 1], (gbuf[2 * i], gbuf[2 * i + 1]))
             kv = None if kv_all is None else kv_all[:, 2 * self.d_model * i: 2 * self.d_model * (i + 1)]
             bi = None if bits is None else (bits[0][i], bits[1][i])
-            x, xT = blk.run(x, xT, cT, key_keep, film, B, L, S, i, seed, cos, sin, kv, bi)
+            handoff = {} if i + 1 < len(self.blocks) else None
+            x, xT = blk.run(x, xT, cT, key_keep, film, B, L, S, i, seed, cos, sin, kv, bi, xr, handoff)
+            xr = None if handoff is None else handoff.get("xr")
         logits = FN.HeadFn.apply(x, xT, self.head.weight, self.head.bias)           # (:286)
         return logits.view(B, L, -1)
 

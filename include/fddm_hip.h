@@ -113,11 +113,14 @@ int fddm_attn_bwd(int dtype, const void* Q, long sq, const void* K, long sk, con
                   const unsigned long long* drop_bits, void* hip_stream);
 
 /* ---- residual + dropout + LayerNorm (+FiLM). models/denoise_decoder.py:87-89,165-191;
- *      HF modeling_wavlm.py:102,313-317,405. */
+ *      HF modeling_wavlm.py:102,313-317,405. rope_out (optional, bf16; the decoder's LN3 only: f32 x, bf16 y and
+ *      output, no FiLM): also writes RoPE(out) with the [rope_L][d] cos / sin tables, as fddm_rope_fwd would
+ *      (models/denoise_decoder.py:42-53,157-159: the next block's q = k input). */
 int fddm_ln_fwd(int x_dtype, int y_dtype, int out_dtype, const void* x, const void* y, const float* gamma,
                 const float* beta, const float* film_scale, const float* film_shift, float* out_f32, void* out_t,
                 float* save_s, float* mean, float* rstd, long N, long d, long rows_per_batch, float eps, float drop_p,
-                unsigned long long seed, unsigned long long stream, void* hip_stream);
+                unsigned long long seed, unsigned long long stream, const float* rope_cos, const float* rope_sin,
+                void* rope_out, long rope_L, void* hip_stream);
 int fddm_ln_bwd(int dy_dtype, const float* dout, const float* s, const float* mean, const float* rstd,
                 const float* gamma, const float* beta, const float* film_scale, float* dres, void* dy_t,
                 float* dgamma, float* dbeta, float* dfilm_scale, float* dfilm_shift, long N, long d,

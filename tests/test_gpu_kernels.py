@@ -567,6 +567,30 @@ def test_layernorm_fwd_bwd(film, L):
         close(dfh, fhr.grad, rtol=1e-4, what="dfilm shift")
 
 
+@pytest.mark.parametrize("d", [512, 768])
+def test_ln_fwd_rope_handoff_matches_rope_fwd(d):
+    """The decoder LN3's fused RoPE output (the next block's q = k input) equals rope_fwd of the LN's own f32
+    output (the unfused path), rounded to bf16: at most one bf16 ulp apart (an FMA contraction may differ), on
+    rows of several positions (N = 3 L, L = 37) at the decoder's d = 512 (one chunk per lane) and 768 (two)."""
+    o = ops()
+    L, N = 37, 111
+    x = torch.randn(N, d, generator=g(56)).to(dev)
+    y = torch.randn(N, d, generator=g(57)).to(torch.bfloat16).to(dev)
+    gm = (1 + 0.1 * torch.randn(d, generator=g(58))).to(dev)
+    bt = (0.1 * torch.randn(d, generator=g(59))).to(dev)
+    cos, sin = O.rope_cos_sin(L, O.rope_inv_freq(d))
+    cos, sin = cos.to(dev).contiguous(), sin.to(dev).contiguous()
+    of = torch.empty(N, d, device=dev)
+    ot = torch.empty(N, d, device=dev, dtype=torch.bfloat16)
+    xr = torch.empty(N, d, device=dev, dtype=torch.bfloat16)
+    o.ln_fwd(x, y, gm, bt, out_f32=of, out_t=ot, drop_p=0.1, seed=5, rng_stream=6, rope=(cos, sin, xr, L))
+    ref = torch.empty(N, d, device=dev, dtype=torch.bfloat16)
+    o.rope_fwd(of, cos, sin, ref, L)
+    ulp = (xr.float() - ref.float()).abs() / ref.float().abs().clamp_min(1e-30)
+    assert (ulp <= 2.0 ** -7).all(), f"rope hand-off vs rope_fwd: max rel {ulp.max().item():.2e}"
+    assert (xr == ref).float().mean().item() > 0.99
+
+
 @pytest.mark.parametrize("N,d", [(1001, 768), (37, 200), (64, 1024)])
 def test_ln_fwd_bf16_post_ln_rows(N, d):
     """The frozen encoder's post-LN (bf16 x + bf16 residual -> bf16, one row per wave, 2 chunks of 8 per lane):
