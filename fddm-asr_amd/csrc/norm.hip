@@ -197,6 +197,7 @@ struct LnBwdArgs {
   const float* dout; const float* s; const float *mean, *rstd, *gamma, *beta, *fsc;
   float* dres; void* dy_t;
   float *dgamma, *dbeta, *dfsc, *dfsh;
+  float* part;  // fused pass: per-slab dgamma / dbeta sums [slab][2][d] (folded by ln_fold_kernel) instead of atomics
   long N, d, rows_per_batch;
   uint64_t seed, stream; unsigned thr16; float drop_scale;
   const uint64_t* seed_off;  // graph-replay seed offset (common.h eff_seed) or null
@@ -252,6 +253,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
 // The device-scope atomics bound the kernel (every slab adds into the same d columns of dgamma/dbeta): at d 512,
 // N 8192, 16-row slabs of 4 waves took 24.0 us, 8 waves 23.4, 32-row slabs 18.5, 64-row slabs 21.8 (occupancy).
 constexpr int LNB_ROWS = 32;
+constexpr int LN_FOLD_MAX = 4;  // jobs per fddm_ln_fold launch
 // keep bits of the 8 dropout decisions of elements e0..e0+7 (e0 % 8 == 0): two hash words
 __device__ __forceinline__ unsigned keep8(uint64_t seed, uint64_t stream, uint64_t e0, unsigned thr) {
   unsigned k = 0;
@@ -382,7 +384,10 @@ __global__ void __launch_bounds__(512) ln_bwd_fused_kernel(LnBwdArgs a) {
     float v[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) v[q] = red[q][0][c] + red[q][1][c] + red[q][2][c] + red[q][3][c];
-    if (a.dgamma) {
+    if (a.part) {
+      a.part[(long)blockIdx.x * 2 * d + c] = v[0];
+      a.part[(long)blockIdx.x * 2 * d + d + c] = v[1];
+    } else if (a.dgamma) {
       atomicAdd(a.dgamma + c, v[0]);
       atomicAdd(a.dbeta + c, v[1]);
     }
@@ -431,6 +436,42 @@ __global__ void __launch_bounds__(256) ln_bwd_params_kernel(LnBwdArgs a) {
   if (a.fsc) {
     atomicAdd(a.dfsc + cur_b * d + c, dsc);
     atomicAdd(a.dfsh + cur_b * d + c, dsh);
+  }
+}
+
+// dgamma[c] += sum over slabs of part[slab][0][c], dbeta[c] likewise (one job per blockIdx.y): 64 columns x 16 slab
+// groups per workgroup, the groups' sums added in a fixed order (bit-reproducible, unlike the slab atomics)
+struct LnFoldJob {
+  const float* part;
+  long nslab, d;
+  float *dgamma, *dbeta;
+};
+struct LnFold {
+  LnFoldJob j[LN_FOLD_MAX];
+};
+__global__ void __launch_bounds__(1024) ln_fold_kernel(LnFold f) {
+  __shared__ float red[2][16][64];
+  const LnFoldJob& J = f.j[blockIdx.y];
+  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const long c = (long)blockIdx.x * 64 + cl;
+  float s0 = 0.f, s1 = 0.f;
+  if (c < J.d) {
+    const float* p = J.part + c;
+#pragma unroll 8
+    for (long k = g; k < J.nslab; k += 16) {
+      s0 += p[k * 2 * J.d];
+      s1 += p[k * 2 * J.d + J.d];
+    }
+  }
+  red[0][g][cl] = s0;
+  red[1][g][cl] = s1;
+  __syncthreads();
+  if (g < 2 && c < J.d) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += red[g][i][cl];
+    float* dst = g == 0 ? J.dgamma : J.dbeta;
+    dst[c] += t;
   }
 }
 
@@ -504,11 +545,11 @@ FDDM_API int fddm_ln_bwd(int dy_dtype, const float* dout, const float* s, const 
                          const float* gamma, const float* beta, const float* film_scale, float* dres, void* dy_t,
                          float* dgamma, float* dbeta, float* dfilm_scale, float* dfilm_shift, long N, long d,
                          long rows_per_batch, float drop_p, unsigned long long seed, unsigned long long stream,
-                         void* hs) {
+                         float* partials, void* hs) {
   if (N <= 0) return 0;
   if (d > 64 * LN_MAXPL) return (int)hipErrorInvalidValue;
   LnBwdArgs a{dout, s, mean, rstd, gamma, beta, film_scale, dres, dy_t, dgamma, dbeta, dfilm_scale, dfilm_shift,
-              N, d, rows_per_batch > 0 ? rows_per_batch : N, seed, stream, 0u, 1.f, g_seed_off};
+              partials, N, d, rows_per_batch > 0 ? rows_per_batch : N, seed, stream, 0u, 1.f, g_seed_off};
   if (drop_p > 0.f) {
     a.thr16 = (unsigned)llrintf(drop_p * 65536.f);
     a.drop_scale = 1.f / (1.f - drop_p);
@@ -518,8 +559,15 @@ FDDM_API int fddm_ln_bwd(int dy_dtype, const float* dout, const float* s, const 
   const bool vec_ok = d % 8 == 0 && d <= 1024 &&
                       !(((uintptr_t)dout | (uintptr_t)s | (uintptr_t)gamma | (uintptr_t)beta | (uintptr_t)film_scale |
                          (uintptr_t)dres | (uintptr_t)dy_t) & 15);
-  if ((dgamma || dfilm_scale) && (!film_scale || a.rows_per_batch % LNB_ROWS == 0) && (!dgamma || (beta && dbeta)) &&
-      vec_ok) {
+  const bool fused = (dgamma || dfilm_scale) && (!film_scale || a.rows_per_batch % LNB_ROWS == 0) &&
+                     (!dgamma || (beta && dbeta)) && vec_ok;
+  if (partials && !dgamma) return (int)hipErrorInvalidValue;
+  if (partials && !fused) {  // the two-pass form adds with atomics: the slabs the fold will read contribute zero
+    a.part = nullptr;
+    const hipError_t e = hipMemsetAsync(partials, 0, (size_t)((N + LNB_ROWS - 1) / LNB_ROWS) * 2 * d * sizeof(float), st_);
+    if (e != hipSuccess) return (int)e;
+  }
+  if (fused) {
     dim3 fg((unsigned)((N + LNB_ROWS - 1) / LNB_ROWS));
     const bool small = d <= 512;
     if (dy_dtype == FDDM_BF16) {
@@ -540,5 +588,22 @@ FDDM_API int fddm_ln_bwd(int dy_dtype, const float* dout, const float* s, const 
     dim3 pg((unsigned)((d + 255) / 256), (unsigned)((N + LNP_ROWS - 1) / LNP_ROWS));
     hipLaunchKernelGGL(ln_bwd_params_kernel, pg, dim3(256), 0, st_, a);
   }
+  return (int)hipGetLastError();
+}
+
+FDDM_API int fddm_ln_bwd_slab_rows(void) { return LNB_ROWS; }
+
+FDDM_API int fddm_ln_fold(int n, const float* const* partials, const long* nslab, const long* d, float* const* dgamma,
+                          float* const* dbeta, void* hs) {
+  if (n <= 0) return 0;
+  if (n > LN_FOLD_MAX) return (int)hipErrorInvalidValue;
+  LnFold f{};
+  long dmax = 0;
+  for (int i = 0; i < n; ++i) {
+    if (!partials[i] || !dgamma[i] || !dbeta[i] || nslab[i] <= 0 || d[i] <= 0) return (int)hipErrorInvalidValue;
+    f.j[i] = LnFoldJob{partials[i], nslab[i], d[i], dgamma[i], dbeta[i]};
+    dmax = d[i] > dmax ? d[i] : dmax;
+  }
+  hipLaunchKernelGGL(ln_fold_kernel, dim3((unsigned)((dmax + 63) / 64), (unsigned)n), dim3(1024), 0, (hipStream_t)hs, f);
   return (int)hipGetLastError();
 }

@@ -312,11 +312,13 @@ class DecoderBlockFn(torch.autograd.Function):
             (gf0_w, af0), (gf0_b, _), (gf3_w, af3), (gf3_b, _), (gn1w, _), (gn1b, _), (gn2w, _), (gn2b, _), \
             (gn3w, _), (gn3b, _) = G
         dx3 = dx3.contiguous()
+        # the three LayerNorms' dgamma / dbeta slab sums, added in one fold launch before the weight gradients
+        lnp = ops.LnPartials()
         # LN3
         dx2 = torch.empty(N, d, device=dev, dtype=F32)
         dy3 = torch.empty(N, d, device=dev, dtype=cd)
         ops.ln_bwd(dx3, s3, m3, r3, n3w, n3b, dres=dx2, dy_t=dy3, dgamma=gn3w, dbeta=gn3b, drop_p=p,
-                   seed=seed, rng_stream=st + 6)
+                   seed=seed, rng_stream=st + 6, partials=lnp)
         # FF
         dw_jobs = [(dy3, hact, gf3_w, gf3_b)]
         FF = f0_w.shape[0]
@@ -333,7 +335,7 @@ class DecoderBlockFn(torch.autograd.Function):
             dfs = torch.zeros(B, d, device=dev, dtype=F32)
             dfh = torch.zeros(B, d, device=dev, dtype=F32)
         ops.ln_bwd(dx2, s2, m2, r2, n2w, n2b, dres=dx1, dy_t=dyc, dgamma=gn2w, dbeta=gn2b, film_scale=fsc,
-                   dfilm=(dfs, dfh), rows_per_batch=L, drop_p=p, seed=seed, rng_stream=st + 4)
+                   dfilm=(dfs, dfh), rows_per_batch=L, drop_p=p, seed=seed, rng_stream=st + 4, partials=lnp)
         # cross out-proj + attention
         dw_jobs.append((dyc, oc, gco_w, gco_b))
         doc = ops.linear_dx(dyc, W["co"], out_dtype=cd)
@@ -350,7 +352,7 @@ class DecoderBlockFn(torch.autograd.Function):
         dx = torch.empty(N, d, device=dev, dtype=F32)
         dy = torch.empty(N, d, device=dev, dtype=cd)
         ops.ln_bwd(dx1, s1, m1, r1, n1w, n1b, dres=dx, dy_t=dy, dgamma=gn1w, dbeta=gn1b, drop_p=p, seed=seed,
-                   rng_stream=st + 2)
+                   rng_stream=st + 2, partials=lnp)
         # self out-proj + attention
         dw_jobs.append((dy, o, gso_w, gso_b))
         do = ops.linear_dx(dy, W["so"], out_dtype=cd)
@@ -364,6 +366,7 @@ class DecoderBlockFn(torch.autograd.Function):
         ops.linear_dx(dv, W["sa"][2 * d:], out=dx, accumulate=True)
         dxr = ops.linear_dx(dqk, W["sa"][: 2 * d])
         ops.rope_bwd(dxr, cos, sin, dx, L)
+        lnp.fold()
         _dw_flush(dw_jobs)
         rt.grads_ready(params)
         grads = tuple(_ret(t_, a_) for t_, a_ in G)

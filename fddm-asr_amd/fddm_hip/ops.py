@@ -10,7 +10,7 @@ import math
 
 import torch
 
-from ._lib import call
+from ._lib import call, lib
 
 F32, BF16 = 0, 1
 EPI_STORE, EPI_GELU, EPI_ACC, EPI_GELU_ONLY, EPI_DGELU = 0, 1, 2, 3, 4
@@ -341,12 +341,46 @@ def ln_fwd(x, y, gamma, beta, *, out_f32=None, out_t=None, save_s=None, mean=Non
 
 
 def ln_bwd(dout, s, mean, rstd, gamma, beta, *, dres=None, dy_t=None, dgamma=None, dbeta=None, film_scale=None,
-           dfilm=None, rows_per_batch=0, drop_p=0.0, seed=0, rng_stream=0):
+           dfilm=None, rows_per_batch=0, drop_p=0.0, seed=0, rng_stream=0, partials=None):
+    """partials: a LnPartials (ln_partials) collecting this LayerNorm's dgamma / dbeta slab sums for one ln_fold launch
+    (the fused pass only), or None: the sums are added to dgamma / dbeta with atomics."""
     N, d = dout.shape
     dfs, dfh = dfilm if dfilm is not None else (None, None)
+    part = None
+    if partials is not None:
+        _chk(dgamma is not None and dbeta is not None, "ln_bwd partials need dgamma and dbeta")
+        part = partials.add(N, d, dgamma, dbeta)
     call("fddm_ln_bwd", code(dy_t) if dy_t is not None else F32, ptr(dout), ptr(s), ptr(mean), ptr(rstd), ptr(gamma),
          ptr(beta), ptr(film_scale), ptr(dres), ptr(dy_t), ptr(dgamma), ptr(dbeta), ptr(dfs), ptr(dfh), N, d,
-         rows_per_batch, float(drop_p), seed, rng_stream, stream())
+         rows_per_batch, float(drop_p), seed, rng_stream, ptr(part), stream())
+
+
+class LnPartials:
+    """The dgamma / dbeta slab sums of up to 4 LayerNorm backwards (ln_bwd(partials=...)), added to their
+    destinations by one ln_fold launch: the slab atomics of ~5 us per LayerNorm backward become one short fold."""
+
+    def __init__(self):
+        self.jobs = []
+
+    def add(self, N, d, dgamma, dbeta):
+        _chk(len(self.jobs) < 4, "at most 4 LayerNorms per fold")
+        rows = lib().fddm_ln_bwd_slab_rows()
+        nslab = (N + rows - 1) // rows
+        part = torch.empty(nslab, 2, d, device=dgamma.device, dtype=torch.float32)
+        self.jobs.append((part, nslab, d, dgamma, dbeta))
+        return part
+
+    def fold(self):
+        import ctypes
+        n = len(self.jobs)
+        if n == 0:
+            return
+        P = ctypes.c_void_p * n
+        Lg = ctypes.c_long * n
+        call("fddm_ln_fold", n, P(*[j[0].data_ptr() for j in self.jobs]), Lg(*[j[1] for j in self.jobs]),
+             Lg(*[j[2] for j in self.jobs]), P(*[j[3].data_ptr() for j in self.jobs]),
+             P(*[j[4].data_ptr() for j in self.jobs]), stream())
+        self.jobs = []
 
 
 # -------------------------------------------------------------------------------- small kernels

@@ -520,11 +520,14 @@ def test_attention_relgate_matches_gate_kernel_path(S):
 
 
 # ----------------------------------------------------------------------------- LN / RoPE / embed
+@pytest.mark.parametrize("fold", [False, True])
 @pytest.mark.parametrize("film", [False, True])
 @pytest.mark.parametrize("L", [20, 32])
-def test_layernorm_fwd_bwd(film, L):
-    """L=32: FiLM rows fall in whole 16-row slabs -> the fused single-pass backward; L=20 with FiLM -> two
-    passes (row kernel + column-slab parameter kernel)."""
+def test_layernorm_fwd_bwd(film, L, fold):
+    """L=32: FiLM rows fall in whole 32-row slabs -> the fused single-pass backward; L=20 with FiLM -> two
+    passes (row kernel + column-slab parameter kernel). fold: dgamma / dbeta as slab sums added by one ln_fold
+    launch (the decoder block's path; the two-pass form zeroes the partials and adds with atomics), on top of
+    nonzero destinations (the fold accumulates, as the atomics do)."""
     o = ops()
     B, d = 3, 192
     N = B * L
@@ -552,16 +555,20 @@ def test_layernorm_fwd_bwd(film, L):
              film=(X(fs), X(fh)) if film else None, rows_per_batch=L, drop_p=p, seed=3, rng_stream=2)
     dres = torch.empty(N, d, device=dev)
     dy = torch.empty(N, d, device=dev)
-    dg, db = torch.zeros(d, device=dev), torch.zeros(d, device=dev)
+    base = torch.linspace(-1, 1, d, device=dev) if fold else torch.zeros(d, device=dev)
+    dg, db = base.clone(), 2 * base
     dfs, dfh = torch.zeros(B, d, device=dev), torch.zeros(B, d, device=dev)
+    lnp = o.LnPartials() if fold else None
     o.ln_bwd(X(dout), sv, mean, rstd, X(gm), X(bt), dres=dres, dy_t=dy, dgamma=dg, dbeta=db,
              film_scale=X(fs) if film else None, dfilm=(dfs, dfh) if film else None, rows_per_batch=L, drop_p=p,
-             seed=3, rng_stream=2)
+             seed=3, rng_stream=2, partials=lnp)
+    if fold:
+        lnp.fold()
     close(of, out.detach(), rtol=1e-5, what="ln out")
     close(dres, xr.grad, rtol=1e-4, what="ln dx")
     close(dy, yr.grad, rtol=1e-4, what="ln dy")
-    close(dg, gr.grad, rtol=1e-4, what="dgamma")
-    close(db, br.grad, rtol=1e-4, what="dbeta")
+    close(dg - base, gr.grad, rtol=1e-4, what="dgamma")
+    close(db - 2 * base, br.grad, rtol=1e-4, what="dbeta")
     if film:
         close(dfs, fsr.grad, rtol=1e-4, what="dfilm scale")
         close(dfh, fhr.grad, rtol=1e-4, what="dfilm shift")
