@@ -28,6 +28,10 @@ def main():
         ("FF2 dX, dGELU + dropout epilogue -> bf16", lambda: ops.linear_dx(dy3, wf3, out=dh, epi=ops.EPI_DGELU, C2=hpre,
                                                                           drop_p=0.1, seed=1, rng_stream=5),
          N * FF * d, (N * d + d * FF + 2 * N * FF) * 2),
+        ("FF2 dX shape, plain bf16 store (no epilogue)", lambda: ops.linear_dx(dy3, wf3, out=dh), N * FF * d,
+         (N * d + d * FF + N * FF) * 2),
+        ("FF2 dX shape, dGELU without dropout", lambda: ops.linear_dx(dy3, wf3, out=dh, epi=ops.EPI_DGELU, C2=hpre),
+         N * FF * d, (N * d + d * FF + 2 * N * FF) * 2),
         ("FF1 dX, f32 accumulate (K 2048)", lambda: ops.linear_dx(dh, wf0, out=dx, accumulate=True),
          N * d * FF, (N * FF + FF * d) * 2 + 2 * N * d * 4),
         ("cross out-proj dX -> bf16", lambda: ops.linear_dx(dy3, wco, out_dtype=bf), N * d * d, (2 * N * d + d * d) * 2 + N * d * 2),
