@@ -197,7 +197,7 @@ struct LnBwdArgs {
   const float* dout; const float* s; const float *mean, *rstd, *gamma, *beta, *fsc;
   float* dres; void* dy_t;
   float *dgamma, *dbeta, *dfsc, *dfsh;
-  float* part;  // fused pass: per-slab dgamma / dbeta sums [slab][2][d] (folded by ln_fold_kernel) instead of atomics
+  float* part;  // fused pass: per-slab dgamma / dbeta / dFiLM sums [slab][4][d] (ln_fold_kernel) instead of atomics
   long N, d, rows_per_batch;
   uint64_t seed, stream; unsigned thr16; float drop_scale;
   const uint64_t* seed_off;  // graph-replay seed offset (common.h eff_seed) or null
@@ -385,9 +385,16 @@ __global__ void __launch_bounds__(512) ln_bwd_fused_kernel(LnBwdArgs a) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) v[q] = red[q][0][c] + red[q][1][c] + red[q][2][c] + red[q][3][c];
     if (a.part) {
-      a.part[(long)blockIdx.x * 2 * d + c] = v[0];
-      a.part[(long)blockIdx.x * 2 * d + d + c] = v[1];
-    } else if (a.dgamma) {
+      float* pp = a.part + (long)blockIdx.x * 4 * d + c;
+      pp[0] = v[0];
+      pp[d] = v[1];
+      if (a.fsc) {
+        pp[2 * d] = v[2];
+        pp[3 * d] = v[3];
+      }
+      continue;
+    }
+    if (a.dgamma) {
       atomicAdd(a.dgamma + c, v[0]);
       atomicAdd(a.dbeta + c, v[1]);
     }
@@ -439,12 +446,14 @@ __global__ void __launch_bounds__(256) ln_bwd_params_kernel(LnBwdArgs a) {
   }
 }
 
-// dgamma[c] += sum over slabs of part[slab][0][c], dbeta[c] likewise (one job per blockIdx.y): 64 columns x 16 slab
-// groups per workgroup, the groups' sums added in a fixed order (bit-reproducible, unlike the slab atomics)
+// Slab sums -> parameter gradients (one job per blockIdx.y; 64 columns x 16 slab groups per workgroup, the groups'
+// sums added in a fixed order: bit-reproducible, unlike the slab atomics). blockIdx.z 0: dgamma[c] / dbeta[c] += the
+// sums of quantities 0 / 1 over all slabs; z = 1 + b: dfilm_scale[b][c] / dfilm_shift[b][c] += those of quantities
+// 2 / 3 over FiLM batch b's slabs (spb consecutive slabs per batch).
 struct LnFoldJob {
   const float* part;
-  long nslab, d;
-  float *dgamma, *dbeta;
+  long nslab, d, spb;
+  float *dgamma, *dbeta, *dfs, *dfh;
 };
 struct LnFold {
   LnFoldJob j[LN_FOLD_MAX];
@@ -452,15 +461,19 @@ struct LnFold {
 __global__ void __launch_bounds__(1024) ln_fold_kernel(LnFold f) {
   __shared__ float red[2][16][64];
   const LnFoldJob& J = f.j[blockIdx.y];
+  const int z = blockIdx.z;
+  const bool film = z > 0;
+  if (film && (J.dfs == nullptr || (long)(z - 1) * J.spb >= J.nslab)) return;  // workgroup-uniform
   const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
   const long c = (long)blockIdx.x * 64 + cl;
+  const long k0 = film ? (long)(z - 1) * J.spb : 0, k1 = film ? min(J.nslab, k0 + J.spb) : J.nslab;
   float s0 = 0.f, s1 = 0.f;
   if (c < J.d) {
-    const float* p = J.part + c;
-#pragma unroll 8
-    for (long k = g; k < J.nslab; k += 16) {
-      s0 += p[k * 2 * J.d];
-      s1 += p[k * 2 * J.d + J.d];
+    const float* p = J.part + (film ? 2 * J.d : 0) + c;
+#pragma unroll 16
+    for (long k = k0 + g; k < k1; k += 16) {
+      s0 += p[k * 4 * J.d];
+      s1 += p[k * 4 * J.d + J.d];
     }
   }
   red[0][g][cl] = s0;
@@ -470,7 +483,7 @@ __global__ void __launch_bounds__(1024) ln_fold_kernel(LnFold f) {
     float t = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) t += red[g][i][cl];
-    float* dst = g == 0 ? J.dgamma : J.dbeta;
+    float* dst = film ? (g == 0 ? J.dfs : J.dfh) + (long)(z - 1) * J.d : (g == 0 ? J.dgamma : J.dbeta);
     dst[c] += t;
   }
 }
@@ -564,7 +577,7 @@ FDDM_API int fddm_ln_bwd(int dy_dtype, const float* dout, const float* s, const 
   if (partials && !dgamma) return (int)hipErrorInvalidValue;
   if (partials && !fused) {  // the two-pass form adds with atomics: the slabs the fold will read contribute zero
     a.part = nullptr;
-    const hipError_t e = hipMemsetAsync(partials, 0, (size_t)((N + LNB_ROWS - 1) / LNB_ROWS) * 2 * d * sizeof(float), st_);
+    const hipError_t e = hipMemsetAsync(partials, 0, (size_t)((N + LNB_ROWS - 1) / LNB_ROWS) * 4 * d * sizeof(float), st_);
     if (e != hipSuccess) return (int)e;
   }
   if (fused) {
@@ -594,16 +607,23 @@ FDDM_API int fddm_ln_bwd(int dy_dtype, const float* dout, const float* s, const 
 FDDM_API int fddm_ln_bwd_slab_rows(void) { return LNB_ROWS; }
 
 FDDM_API int fddm_ln_fold(int n, const float* const* partials, const long* nslab, const long* d, float* const* dgamma,
-                          float* const* dbeta, void* hs) {
+                          float* const* dbeta, float* const* dfilm_scale, float* const* dfilm_shift,
+                          const long* slabs_per_batch, void* hs) {
   if (n <= 0) return 0;
   if (n > LN_FOLD_MAX) return (int)hipErrorInvalidValue;
   LnFold f{};
-  long dmax = 0;
+  long dmax = 0, zmax = 1;
   for (int i = 0; i < n; ++i) {
     if (!partials[i] || !dgamma[i] || !dbeta[i] || nslab[i] <= 0 || d[i] <= 0) return (int)hipErrorInvalidValue;
-    f.j[i] = LnFoldJob{partials[i], nslab[i], d[i], dgamma[i], dbeta[i]};
+    float* fs = dfilm_scale ? dfilm_scale[i] : nullptr;
+    float* fh = dfilm_shift ? dfilm_shift[i] : nullptr;
+    const long spb = slabs_per_batch ? slabs_per_batch[i] : 0;
+    if ((fs == nullptr) != (fh == nullptr) || (fs && spb <= 0)) return (int)hipErrorInvalidValue;
+    f.j[i] = LnFoldJob{partials[i], nslab[i], d[i], spb, dgamma[i], dbeta[i], fs, fh};
     dmax = d[i] > dmax ? d[i] : dmax;
+    if (fs && 1 + (nslab[i] + spb - 1) / spb > zmax) zmax = 1 + (nslab[i] + spb - 1) / spb;
   }
-  hipLaunchKernelGGL(ln_fold_kernel, dim3((unsigned)((dmax + 63) / 64), (unsigned)n), dim3(1024), 0, (hipStream_t)hs, f);
+  hipLaunchKernelGGL(ln_fold_kernel, dim3((unsigned)((dmax + 63) / 64), (unsigned)n, (unsigned)zmax), dim3(1024), 0,
+                     (hipStream_t)hs, f);
   return (int)hipGetLastError();
 }

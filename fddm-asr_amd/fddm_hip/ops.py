@@ -349,7 +349,7 @@ def ln_bwd(dout, s, mean, rstd, gamma, beta, *, dres=None, dy_t=None, dgamma=Non
     part = None
     if partials is not None:
         _chk(dgamma is not None and dbeta is not None, "ln_bwd partials need dgamma and dbeta")
-        part = partials.add(N, d, dgamma, dbeta)
+        part = partials.add(N, d, dgamma, dbeta, (dfs, dfh) if film_scale is not None else None, rows_per_batch)
     call("fddm_ln_bwd", code(dy_t) if dy_t is not None else F32, ptr(dout), ptr(s), ptr(mean), ptr(rstd), ptr(gamma),
          ptr(beta), ptr(film_scale), ptr(dres), ptr(dy_t), ptr(dgamma), ptr(dbeta), ptr(dfs), ptr(dfh), N, d,
          rows_per_batch, float(drop_p), seed, rng_stream, ptr(part), stream())
@@ -362,12 +362,19 @@ class LnPartials:
     def __init__(self):
         self.jobs = []
 
-    def add(self, N, d, dgamma, dbeta):
+    def add(self, N, d, dgamma, dbeta, dfilm=None, rows_per_batch=0):
+        """dfilm = (dfs, dfh) [B, d] with FiLM batches of rows_per_batch rows: folded per batch when the batches
+        are whole slabs (the fused pass); otherwise the backward adds them with atomics and leaves zeros here."""
         _chk(len(self.jobs) < 4, "at most 4 LayerNorms per fold")
         rows = lib().fddm_ln_bwd_slab_rows()
         nslab = (N + rows - 1) // rows
-        part = torch.empty(nslab, 2, d, device=dgamma.device, dtype=torch.float32)
-        self.jobs.append((part, nslab, d, dgamma, dbeta))
+        part = torch.empty(nslab, 4, d, device=dgamma.device, dtype=torch.float32)
+        dfs = dfh = None
+        spb = 0
+        if dfilm is not None and rows_per_batch > 0 and rows_per_batch % rows == 0:
+            dfs, dfh = dfilm
+            spb = rows_per_batch // rows
+        self.jobs.append((part, nslab, d, dgamma, dbeta, dfs, dfh, spb))
         return part
 
     def fold(self):
@@ -377,9 +384,10 @@ class LnPartials:
             return
         P = ctypes.c_void_p * n
         Lg = ctypes.c_long * n
-        call("fddm_ln_fold", n, P(*[j[0].data_ptr() for j in self.jobs]), Lg(*[j[1] for j in self.jobs]),
-             Lg(*[j[2] for j in self.jobs]), P(*[j[3].data_ptr() for j in self.jobs]),
-             P(*[j[4].data_ptr() for j in self.jobs]), stream())
+        J = self.jobs
+        call("fddm_ln_fold", n, P(*[j[0].data_ptr() for j in J]), Lg(*[j[1] for j in J]), Lg(*[j[2] for j in J]),
+             P(*[j[3].data_ptr() for j in J]), P(*[j[4].data_ptr() for j in J]), P(*[ptr(j[5]) for j in J]),
+             P(*[ptr(j[6]) for j in J]), Lg(*[j[7] for j in J]), stream())
         self.jobs = []
 
 

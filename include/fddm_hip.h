@@ -126,14 +126,16 @@ int fddm_ln_bwd(int dy_dtype, const float* dout, const float* s, const float* me
                 float* dgamma, float* dbeta, float* dfilm_scale, float* dfilm_shift, long N, long d,
                 long rows_per_batch, float drop_p, unsigned long long seed, unsigned long long stream,
                 float* partials, void* hip_stream);
-/* partials (optional; the fused pass, dgamma given): instead of adding its dgamma / dbeta sums to dgamma / dbeta with
- * device atomics, row slab k of fddm_ln_bwd_slab_rows() rows stores them to partials[k][0 / 1][0..d) (ceil(N / rows)
- * slabs); fddm_ln_fold adds them to dgamma / dbeta later, up to 4 LayerNorms in one launch, in a fixed order. Shapes
- * the fused pass does not take (unaligned rows, FiLM batches not a multiple of the slab) add with atomics and zero
- * the partials. */
+/* partials (optional; the fused pass, dgamma given): instead of adding its dgamma / dbeta (and FiLM) sums with device
+ * atomics, row slab k of fddm_ln_bwd_slab_rows() rows stores them to partials[k][q][0..d), q = dgamma, dbeta, dFiLM
+ * scale, dFiLM shift (ceil(N / rows) slabs x 4 x d floats); fddm_ln_fold adds them to their destinations later, up
+ * to 4 LayerNorms in one launch, in a fixed order (dfilm_* [B][d] per FiLM batch of slabs_per_batch slabs; NULL
+ * arrays or entries: no FiLM). Shapes the fused pass does not take (unaligned rows, FiLM batches not a multiple of
+ * the slab) add with atomics and zero the partials. */
 int fddm_ln_bwd_slab_rows(void);
 int fddm_ln_fold(int n, const float* const* partials, const long* nslab, const long* d, float* const* dgamma,
-                 float* const* dbeta, void* hip_stream);
+                 float* const* dbeta, float* const* dfilm_scale, float* const* dfilm_shift,
+                 const long* slabs_per_batch, void* hip_stream);
 
 /* ---- RoPE on the block input (models/denoise_decoder.py:42-53,157-159). cs/sn: [L][d]. */
 int fddm_rope_fwd(int out_dtype, const float* x, const float* cs, const float* sn, void* out, long N, long L, long d,
