@@ -1,7 +1,7 @@
 """The decoder block's dX GEMMs at C2 (B 32 x L 256, d 512, FF 2048) as DecoderBlockFn.backward issues them
 (functions.py), each timed alone (HIP events, 20 launches after 3 warm-ups) next to its FLOP rate and its HBM floor
 (operand + output bytes at 6.3 TB/s achievable). Library from FDDM_HIP_LIB.
-   python tools/dx_bench.py"""
+   python tools/dx_bench.py [gemm path]"""
 import os
 import sys
 
@@ -18,6 +18,8 @@ bf, f32 = torch.bfloat16, torch.float32
 
 
 def main():
+    if len(sys.argv) > 1:   # a GEMM family forced for every case (ops.GEMM_PATHS), e.g. "small"
+        ops.gemm_force_path(sys.argv[1])
     N, d, FF = 32 * 256, 512, 2048
     r = lambda *s, dt=bf: torch.randn(*s, device=dev, dtype=dt)  # noqa: E731
     dy3, hpre, dh = r(N, d), r(N, FF), torch.empty(N, FF, device=dev, dtype=bf)
