@@ -91,7 +91,7 @@ def main():
             print("   end time per round of 256 blocks (median):",
                   " ".join(f"{int(np.median(e[r:r + 256]))}" for r in range(0, len(a), 256)))
         return
-    for (M, N, K) in [(8192, 512, 2048), (8192, 512, 512)]:
+    for (M, N, K) in [(8192, 512, 2048), (8192, 512, 512), (8192, 2048, 512)]:
         dy = torch.randn(M, K, device=dev, dtype=bf)
         w = torch.randn(K, N, device=dev, dtype=bf)
         o = torch.empty(M, N, device=dev)
