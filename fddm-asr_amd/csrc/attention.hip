@@ -14,31 +14,16 @@
 //                    from a [key][d] LDS image through ds_read_b64_tr_b16 (hardware transpose).
 // Work split: 4 waves x 16 rows = 64 rows per workgroup; K/V (or Q/dO) tiles of 64 rows in LDS.
 // T = bf16 (mfma_f32_16x16x32_bf16) or f32 (mfma_f32_16x16x4f32, exact fp32 parity mode).
-#include "common.h"
+#include "attn_common.h"
 
 namespace fddm {
 namespace attn {
 
-// XCD-aware block order: the hardware deals workgroups round-robin over the 8 XCDs (linear id L -> XCD L % 8);
-// remap so that each XCD receives a contiguous range of (bh, tile) work items — all tiles of one (batch, head) run
-// on one XCD and read that head's K / V (or Q / dO) through one L2 instead of up to 8 (bijective for any grid size).
-__device__ __forceinline__ void xcd_tile(int& bx, int& by) {
-  const int nx = gridDim.x, n = nx * gridDim.y;
-  const int L = blockIdx.x + blockIdx.y * nx;
-  const int x = L & 7, j = L >> 3, q = n >> 3, r = n & 7;
-  const int W = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + j;
-  by = W / nx;
-  bx = W - by * nx;
-}
-
-
-constexpr int DH = 64;
 
 template <typename T> struct Cfg;
 template <> struct Cfg<bf16_t> { static constexpr int RB = 128, NSUB = 2, ECH = 8; };
 template <> struct Cfg<float> { static constexpr int RB = 256, NSUB = 4, ECH = 4; };
 
-__device__ __forceinline__ int kc_off(int RB, int r, int c) { return r * RB + ((c ^ ((r >> 1) & 7)) << 4); }
 __device__ __forceinline__ int hatt(int k) { return ((k >> 1) & 3) << 2; }
 
 template <typename T>
@@ -142,60 +127,6 @@ __device__ __forceinline__ void trans_times_vals(f32x4_t (&out)[4], const unsign
       }
     }
   }
-}
-
-// cross-row reductions of the 16x16 C layout (lanes l, l^16, l^32, l^48 hold one query's keys) with the gfx950
-// lane-swap instructions: v_permlane16_swap / v_permlane32_swap exchange a value between lanes l and l^16 (l^32) in
-// the VALU, so r[0] and r[1] hold {own, partner} in some order — no LDS round trip (__shfl_xor's ds_bpermute)
-__device__ __forceinline__ float xmax16(float x) {
-  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
-}
-__device__ __forceinline__ float xmax32(float x) {
-  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
-}
-__device__ __forceinline__ float xsum16(float x) {
-  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
-__device__ __forceinline__ float xsum32(float x) {
-  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
-__device__ __forceinline__ unsigned xor16(unsigned x) {
-  const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
-  return r[0] | r[1];
-}
-__device__ __forceinline__ unsigned xor32(unsigned x) {
-  const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
-  return r[0] | r[1];
-}
-
-struct AttnArgs {
-  const void *Q, *K, *V, *O, *dO;
-  void *Out, *dQ, *dK, *dV;
-  float* lse;
-  float* delta;  // [B*H][Lq] workspace: rowsum(dO*O), written by dq_kernel
-  uint64_t* dbits;  // [B*H][ceil(Lk/64)][Lq] dropout keep bits: written by the forward, read by the backward
-  long sq, sk, sv, so, sdo, sdq, sdk, sdv;
-  const unsigned char* key_keep;  // [B][Lk] or null
-  const float* gate;              // [B*H][Lq] or null (WavLM)
-  const float* table;             // [H][2*Lk-1]
-  const void* graw;               // WavLM gate pre-activations (bf16) at graw + (b*Lq + q)*sgr + h*8 + o, or null
-  long sgr;
-  const float* gconst;            // [H] gru_rel_pos_const
-  int B, H, Lq, Lk;
-  float scale;
-  uint64_t seed, stream;
-  unsigned thr16;
-  float drop_scale;
-  int bits_ready;  // host side only: dbits already holds this site's keep bits (fddm_attn_drop_bits)
-  const uint64_t* seed_off;  // graph-replay seed offset (common.h eff_seed) or null
-};
-
-__device__ __forceinline__ bool key_ok(const AttnArgs& a, int b, int key) {
-  return key < a.Lk && (a.key_keep == nullptr || a.key_keep[(long)b * a.Lk + key]);
 }
 
 // Diagnostic build only (-DATTN_STAMPS, tools/attn_stamps.py): s_memtime stamps of wave 0 of every workgroup at the
@@ -604,20 +535,6 @@ __global__ void __launch_bounds__(256, ATTN_FWD_WPS) fwd2_kernel(AttnArgs a) {
     if (a.lse && g == 0)
       a.lse[(long)bh * a.Lq + q[gq]] = (lt > 0.f) ? (m[gq] * sl2 + __log2f(lt)) * 0.69314718055994531f : NAN;
   }
-}
-
-// inline-asm loads for the streamed kernels (hipcc does not track them; the kernels wait explicitly): a 1-KB
-// LDS-DMA piece (16 B per lane into lds + 16 * lane; lds wave-uniform), and a register pin
-typedef unsigned u32x4v_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void dma16_asm(const void* src, const unsigned char* lds) {
-  typedef __attribute__((address_space(3))) const void* lcp_t;
-  const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lcp_t)(const void*)lds);
-  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(la) : "memory", "m0");
-}
-__device__ __forceinline__ void pin16(uint4& x) {
-  u32x4v_t v = __builtin_bit_cast(u32x4v_t, x);
-  asm volatile("" : "+v"(v));
-  x = __builtin_bit_cast(uint4, v);
 }
 
 // ------------------------------------------------------------------------- fwd (bf16, WavLM, streamed ring)
@@ -2450,6 +2367,11 @@ __global__ void __launch_bounds__(1024, 1) bwd3s_kernel(AttnArgs a) {
 //  backward Lq == Lk <= 256 with recorded bits or no dropout: bwd3s (one fused launch per (b, h));
 //           else dq4 + dkv4 (streamed rings) for L <= 1024 with recorded bits or no dropout; dq2 + dkv2 otherwise
 //           (keep bits rehashed when the forward recorded none, or longer sequences).
+// fddm_attn_set_kernels (tests / tools only): 1 selects the round-4 16x16x32 kernels (fwd6 / dq4 / dkv4 / bwd3s)
+// where the 32x32x16 family (attn7.hip) would run; 0 (default) the 32x32x16 family
+static int g_attn_v6 = 0;
+static bool attn7_enabled() { return g_attn_v6 == 0; }
+
 template <typename T>
 static int run(int which, AttnArgs& a, hipStream_t s) {
   constexpr int RB = Cfg<T>::RB;
@@ -2469,6 +2391,7 @@ static int run(int which, AttnArgs& a, hipStream_t s) {
       if (a.Lk <= 1024) {
         const int ntiles = LkP / 64, qw = 128;
         const int dm = !drop ? 0 : (a.bits_ready && a.dbits) ? 1 : 2;
+        if (dm != 2 && attn7_enabled()) return attn7_fwd(a, s);
         const size_t lds = (size_t)2 * 2 * 64 * 128 + (size_t)LkP * 4 +
                            (dm == 1 ? (size_t)ntiles * qw * 8 : dm == 2 ? (size_t)3 * ATTN_R * 2 : 0);
         dim3 g6((a.Lq + qw - 1) / qw, a.B * a.H);
@@ -2523,6 +2446,10 @@ static int run(int which, AttnArgs& a, hipStream_t s) {
       else if (dm == 1) hipLaunchKernelGGL((dkv2_kernel<1>), grid, dim3(256), 0, s, a);
       else hipLaunchKernelGGL((dkv2_kernel<0>), grid, dim3(256), 0, s, a);
       return (int)hipGetLastError();
+    }
+    if (which == 4) {  // the 32x32x16 family: dq7 (also writes dkv7's row terms), then dkv7
+      const int e = attn7_dq(a, s);
+      return e ? e : attn7_dkv(a, s);
     }
     if (which == 3) {
       const int LP = (a.Lk + 63) / 64 * 64;
@@ -2590,6 +2517,12 @@ FDDM_API int fddm_attn_stamps_clear() {
 }
 #endif
 
+FDDM_API int fddm_attn_set_kernels(int v6) {
+  const int old = g_attn_v6;
+  g_attn_v6 = v6 ? 1 : 0;
+  return old;
+}
+
 // Forward. Q/K/V/O: element (b, pos, h, d) at base + (b*L + pos)*stride + h*64 + d.
 FDDM_API int fddm_attn_fwd(int dtype, const void* Q, long sq, const void* K, long sk, const void* V, long sv, void* O,
                            long so, float* lse, const unsigned char* key_keep, const float* gate, const float* table,
@@ -2646,6 +2579,9 @@ FDDM_API int fddm_attn_bwd(int dtype, const void* Q, long sq, const void* K, lon
   a.sq = sq; a.sk = sk; a.sv = sv; a.so = so; a.sdo = sdo; a.sdq = sdq; a.sdk = sdk; a.sdv = sdv;
   a.key_keep = key_keep;
   a.B = B; a.H = H; a.Lq = Lq; a.Lk = Lk; a.scale = scale; a.seed = seed; a.stream = stream; a.seed_off = g_seed_off;
+  // bf16 with recorded or no dropout, Lk <= 1024: the 32x32x16 kernels (attn7.hip; delta_ws holds 2 * B*H*LqP)
+  if (dtype == FDDM_BF16 && attn7_enabled() && Lk <= 1024 && (drop_p <= 0.f || drop_bits))
+    return attn_dispatch(4, dtype, a, drop_p, hs);
   // self-attention shapes (Lq == Lk <= 256, bf16, no rehashed dropout): dQ, dK and dV in one fused launch
   if (dtype == FDDM_BF16 && Lq == Lk && Lk <= 256 && (drop_p <= 0.f || drop_bits))
     return attn_dispatch(3, dtype, a, drop_p, hs);

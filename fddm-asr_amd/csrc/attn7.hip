@@ -1,0 +1,790 @@
+// Decoder attention on 32x32x16 bf16 MFMAs (gfx950): forward (fwd7).
+//
+// The decoder's self- and cross-attention (models/denoise_decoder.py:129-130,164,169-176 -> nn.MultiheadAttention:
+// key-padding mask, dropout p on the attention probabilities, head_dim 64), bf16 in / out, fp32 softmax statistics.
+//
+// Why a second kernel family next to attention.hip's fwd6 (16x16x32 MFMAs): at head_dim 64 the forward is bound by
+// vector-instruction issue, not by the matrix cores (profiles/r04_summary.md: fwd6's tile loop issues
+// ~263 VALU instructions against 32 MFMAs per wave and 64-key tile). Per wave and tile fwd7 issues half the MFMA
+// instructions for the same work (16 x 32x32x16 instead of 32 x 16x16x32: the SIMD's vector issue is held 8 cycles
+// per MFMA either way), reduces each query's row over 2 lanes instead of 4 (one v_permlane32_swap), and skips the
+// tile maximum on every tile after a query block's first unless the tile's probabilities exceed 2^8 (checked on the
+// lane's row sum it needs anyway), which leaves the exponent, its FMA, the row sum, the keep-bit AND and the bf16 pack
+// per score. The prologue issues the first K / V tile's LDS-DMA, the Q fragments and the key-mask bytes together,
+// and the output goes out through LDS as whole 128-B rows.
+//
+// Layout (per workgroup: 4 waves x 32 queries = 128 queries of one (b, h)):
+//   S^T = K Q^T per 32-key block kb: A = K rows (LDS, KC swizzle, ds_read_b128), B = the lane's own query fragment
+//   (registers). Accumulator register r of lane l holds key 32 kb + 8 (r >> 2) + 4 (l >> 5) + (r & 3), query l & 31:
+//   a query's 64 keys of a tile sit in lanes l and l ^ 32.
+//   O^T += V^T P^T per k-step (kb, s): B = the lane's P values r = 8 s .. 8 s + 7 packed to bf16 (k position j <-> key
+//   32 kb + 16 s + 8 (j >> 2) + 4 (l >> 5) + (j & 3): the reduction order is permuted consistently on both operands);
+//   A = V^T from two ds_read_b64_tr_b16 of 4 keys each (V image swizzle vsw: the 4 rows a 32-lane half reads are
+//   conflict-free).
+// The key mask (0 / -inf per key) is the S accumulator's initial value (no add per score).
+#include <type_traits>
+
+#include "attn_common.h"
+
+namespace fddm {
+namespace attn {
+
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+
+__device__ __forceinline__ f32x16_t mfma32(const uint4& a, const uint4& b, const f32x16_t& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
+                                                 0, 0, 0);
+}
+
+// V image: 16-B chunk c of row r is stored at chunk c ^ vsw(r). A transposed read of a 32-lane half covers 4
+// consecutive rows (4j .. 4j + 3) x 64 B; rows 4j and 4j + 2 share a 256-B bank window and land in opposite 64-B
+// halves of it.
+__device__ __forceinline__ int vsw(int r) { return (r & 2) << 1; }
+
+// 4-B-per-lane LDS-DMA piece (256 B per wave-instruction into lds + 4 * lane)
+__device__ __forceinline__ void dma4_asm(const void* src, const unsigned char* lds) {
+  typedef __attribute__((address_space(3))) const void* lcp_t;
+  const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lcp_t)(const void*)lds);
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" ::"v"(src), "s"(la) : "memory", "m0");
+}
+
+// LDS-DMA piece from a wave-uniform 64-bit base (SGPRs) + a 32-bit per-lane byte offset: no 64-bit address math per
+// lane and piece
+__device__ __forceinline__ void dma16_sv(const void* sbase, unsigned voff, const unsigned char* lds) {
+  typedef __attribute__((address_space(3))) const void* lcp_t;
+  const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lcp_t)(const void*)lds);
+  asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(la) : "memory", "m0");
+}
+__device__ __forceinline__ void dma4_sv(const void* sbase, unsigned voff, const unsigned char* lds) {
+  typedef __attribute__((address_space(3))) const void* lcp_t;
+  const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lcp_t)(const void*)lds);
+  asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dword %0, %1" ::"v"(voff), "s"(sbase), "s"(la) : "memory", "m0");
+}
+
+__device__ __forceinline__ s16x4_t tr_read(const unsigned char* p) {
+  typedef __attribute__((address_space(3))) s16x4_t* lp;
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(p));
+}
+
+constexpr int A7_TB = 64 * 128;  // one K or V tile in LDS: 64 rows x 128 B
+
+// DM: 0 no dropout, 1 keep bits from the words fddm_attn_drop_bits wrote (word (bh, t, q), bit = key - 64 t).
+// MK: 0 no mask, 1 the ragged last tile only (Lk % 64 != 0, no key-padding mask), 2 key-padding mask on every tile.
+template <int DM, int MK>
+__global__ void __launch_bounds__(256, 3) fwd7_kernel(AttnArgs a) {
+  constexpr bool DROP = DM != 0;
+  extern __shared__ __attribute__((aligned(16))) unsigned char sm7[];
+  const int ntiles = (a.Lk + 63) >> 6, LkP = ntiles * 64;
+  unsigned char* kst = sm7;                      // [2][64 rows][128 B] K, KC swizzle
+  unsigned char* vst = sm7 + 2 * A7_TB;          // [2][64 rows][128 B] V, vsw swizzle
+  unsigned char* kwl = sm7 + 4 * A7_TB;          // [2][128 queries][8 B] keep words of the tile
+  unsigned* tact = (unsigned*)(kwl + 2048);      // [4] active-tile nibbles per wave (MK 2)
+  float* mfull = (float*)(kwl + 2048 + 16);      // [LkP] 0 / -inf
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hh = lane >> 5, qi = lane & 31;
+  int bxi, bh;
+  xcd_tile(bxi, bh);
+  const int b = bh / a.H, h = bh - b * a.H;
+  const int qw0 = bxi * 128 + 32 * w;
+  const int q = qw0 + qi;
+  const bool qv = q < a.Lq;
+  const bf16_t* Qb = (const bf16_t*)a.Q + (long)b * a.Lq * a.sq + h * DH;
+  const bf16_t* Kb = (const bf16_t*)a.K + (long)b * a.Lk * a.sk + h * DH;
+  const bf16_t* Vb = (const bf16_t*)a.V + (long)b * a.Lk * a.sv + h * DH;
+
+  // one tile's stream: wave w brings rows 16 w .. 16 w + 15 of K and V (2 + 2 KB pieces, XOR swizzles applied to the
+  // per-lane source addresses) and the keep words of its own 32 queries (one 256-B piece)
+  // byte offsets from the (b, h) bases: row * stride * 2 < 2^31 for every shape the dispatch admits (Lk <= 1024)
+  const unsigned sk2 = (unsigned)a.sk * 2u, sv2 = (unsigned)a.sv * 2u;
+  const uint64_t* kwb = a.dbits + (long)bh * ntiles * a.Lq;
+  auto fill = [&](int tt, int st) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int R = 16 * w + 8 * u;
+      const int r = 64 * tt + R + (lane >> 3), pch = lane & 7;
+      const unsigned rr = (unsigned)min(r, a.Lk - 1);
+      dma16_sv(Kb, rr * sk2 + (unsigned)((pch ^ ((r >> 1) & 7)) << 4), kst + st * A7_TB + R * 128);
+      dma16_sv(Vb, rr * sv2 + (unsigned)((pch ^ vsw(r)) << 4), vst + st * A7_TB + R * 128);
+    }
+    if constexpr (DM == 1) {
+      const unsigned qq = (unsigned)min(qw0 + (lane >> 1), a.Lq - 1);
+      dma4_sv(kwb, ((unsigned)tt * (unsigned)a.Lq + qq) * 8u + 4u * (lane & 1), kwl + st * 1024 + w * 256);
+    }
+  };
+
+  // ---- prologue: tile 0's stream, the Q fragments and the key mask in flight together
+  fill(0, 0);
+  uint4 qf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks)
+    qf[ks] = qv ? *(const uint4*)(Qb + (long)q * a.sq + 16 * ks + 8 * hh) : make_uint4(0, 0, 0, 0);
+  unsigned tmask = ntiles >= 32 ? 0xFFFFFFFFu : ((1u << ntiles) - 1u);
+  if constexpr (MK != 0) {
+    // thread tid owns keys 4 tid .. 4 tid + 3 (LkP <= 1024)
+    bool any = false;
+    if (4 * tid < LkP) {
+      float4 mv;
+      float* mp = (float*)&mv;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = 4 * tid + j;
+        const bool ok = k < a.Lk && (MK == 1 || a.key_keep[(long)b * a.Lk + k] != 0);
+        mp[j] = ok ? 0.f : -INFINITY;
+        any |= ok;
+      }
+      *(float4*)(mfull + 4 * tid) = mv;
+    }
+    if constexpr (MK == 2) {
+      const unsigned long long bal = __ballot(any);  // lanes 16 j .. 16 j + 15 of wave w: the keys of tile 4 w + j
+      if (lane == 0) {
+        unsigned nib = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) nib |= ((bal >> (16 * j)) & 0xFFFFull) ? (1u << j) : 0u;
+        tact[w] = nib;
+      }
+    }
+  }
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) pin16(qf[ks]);  // hipcc waits for the Q loads here, not inside the stream loop
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  if constexpr (MK == 2) tmask &= tact[0] | (tact[1] << 4) | (tact[2] << 8) | (tact[3] << 12);
+
+  // per-lane LDS offsets: K row reads (row qi of a 32-key block, chunk 2 ks + hh), V transposed reads (16-lane group
+  // G = lane >> 4 reads rows 4 hh + (i >> 2) of a 16-key step, 8-B units 8 db + 4 (G & 1) + (i & 3), i = lane & 15)
+  int koff[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) koff[ks] = qi * 128 + (((2 * ks + hh) ^ ((qi >> 1) & 7)) << 4);
+  const int vi = lane & 15, vrow = 4 * hh + (vi >> 2);
+  int voff[2];
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+    voff[db] = vrow * 128 + (((8 * db + 4 * ((lane >> 4) & 1) + (vi & 3)) ^ ((vrow & 2) << 2)) << 3);
+
+  const float sl2 = a.scale * 1.4426950408889634f;  // p = 2^(s sl2 - m sl2), m in raw score units
+  float m = -INFINITY, l = 0.f;
+  f32x16_t o0 = {}, o1 = {};
+  bool first = true;
+
+  // one 64-key tile as two 32-key halves, each an online-softmax step of its own (S, exponentials, PV), so that only
+  // one half's 16 scores and 8 packed probabilities are live next to O and Q
+  auto tile = [&](const int t, const int st, auto mc) {
+    constexpr bool MT = decltype(mc)::value;
+    const unsigned char* kimg = kst + st * A7_TB;
+    const unsigned char* vimg = vst + st * A7_TB;
+    unsigned kw2[2] = {0u, 0u};
+    if constexpr (DROP) {
+      const uint64_t kw = *(const uint64_t*)(kwl + st * 1024 + (32 * w + qi) * 8);
+      kw2[0] = (unsigned)(kw >> (4 * hh));
+      kw2[1] = (unsigned)(kw >> (32 + 4 * hh));
+    }
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      f32x16_t sc;
+      // S^T of the half (the mask row as the accumulator's initial value); recomputed on the rare slow path instead
+      // of keeping the raw scores live across the exponentials
+      auto scores = [&]() {
+        if constexpr (MT) {
+          const f32x4_t* m4 = (const f32x4_t*)(mfull + 64 * t + 32 * kb + 4 * hh);  // keys 8 j + 4 hh .. + 3
+          sc = __builtin_shufflevector(__builtin_shufflevector(m4[0], m4[2], 0, 1, 2, 3, 4, 5, 6, 7),
+                                       __builtin_shufflevector(m4[4], m4[6], 0, 1, 2, 3, 4, 5, 6, 7), 0, 1, 2, 3, 4,
+                                       5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+        } else {
+          sc = f32x16_t{};
+        }
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) sc = mfma32(*(const uint4*)(kimg + koff[ks] + kb * 32 * 128), qf[ks], sc);
+      };
+      scores();
+      // exponentials against the reference mref, the lane's row sum (before dropout), the keep-bit AND and the bf16
+      // pack into the PV operands bq[s]
+      uint4 bq[2];
+      float ls;
+      auto expall = [&](float mref) {
+        const float nb = -mref * sl2;
+        float la = 0.f, lb = 0.f;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          unsigned bw[4];
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            const int r = 8 * s + 2 * jj;
+            float x = __builtin_amdgcn_exp2f(fmaf(sc[r], sl2, nb));
+            float y = __builtin_amdgcn_exp2f(fmaf(sc[r + 1], sl2, nb));
+            la += x;
+            lb += y;
+            if constexpr (DROP) {
+              const int pos = 8 * (r >> 2) + (r & 3);
+              x = __uint_as_float(__float_as_uint(x) & (unsigned)__builtin_amdgcn_sbfe((int)kw2[kb], pos, 1));
+              y = __uint_as_float(__float_as_uint(y) & (unsigned)__builtin_amdgcn_sbfe((int)kw2[kb], pos + 1, 1));
+            }
+            bw[jj] = pk_bf16(x, y);
+          }
+          bq[s] = make_uint4(bw[0], bw[1], bw[2], bw[3]);
+        }
+        ls = la + lb;
+      };
+      // fast path: exponentials against the running reference m; slow path (a query block's first half-tile, or a
+      // lane sum above 2^8 / inf / NaN): the half's maximum from recomputed raw scores, rescale O and l, again
+      bool redo = first;
+      while (true) {
+        if (redo) {
+          float tm = fmaxf(sc[0], sc[1]);
+#pragma unroll
+          for (int r = 2; r < 16; r += 2) tm = fmaxf(tm, fmaxf(sc[r], sc[r + 1]));
+          tm = xmax32(tm);
+          const float mn = fmaxf(m, tm);
+          const float alpha = (mn == -INFINITY) ? 1.f : __builtin_amdgcn_exp2f((m - mn) * sl2);
+          l *= alpha;
+          o0 *= alpha;
+          o1 *= alpha;
+          m = mn;
+        }
+        const float mref = m == -INFINITY ? 0.f : m;
+        expall(mref);
+        if (redo) break;
+        m = mref;
+        if (!__any(!(ls <= 256.f))) break;
+        redo = true;
+        scores();
+      }
+      l += ls;
+      first = false;
+      // O^T += V^T P^T over the half's two 16-key steps
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int rb = (32 * kb + 16 * s) * 128;
+        const uint4 v0 = join_tr(tr_read(vimg + voff[0] + rb), tr_read(vimg + voff[0] + rb + 8 * 128));
+        const uint4 v1 = join_tr(tr_read(vimg + voff[1] + rb), tr_read(vimg + voff[1] + rb + 8 * 128));
+        o0 = mfma32(v0, bq[s], o0);
+        o1 = mfma32(v1, bq[s], o1);
+      }
+    }
+  };
+
+  // ---- the stream: tile t sits in stage st; the next active tile is filled into st ^ 1 before t is computed
+  int t = 0, st = 0;
+  bool act = (tmask & 1u) != 0;
+  while (true) {
+    const unsigned rest = t + 1 < 32 ? (tmask & ~((2u << t) - 1u)) : 0u;
+    const int tn = rest ? __builtin_ctz(rest) : -1;
+    if (tn >= 0) fill(tn, st ^ 1);
+    if (act) {
+      if (MK == 2 || (MK == 1 && t == ntiles - 1)) tile(t, st, std::true_type{});
+      else tile(t, st, std::false_type{});
+    }
+    if (tn < 0) break;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of tile tn landed
+    __builtin_amdgcn_s_barrier();                      // every wave's pieces landed; every wave finished tile t
+    t = tn;
+    st ^= 1;
+    act = true;
+  }
+
+  // ---- epilogue: normalise, stage the wave's 32 output rows in LDS (K ring, free after the barrier), store rows
+  __syncthreads();
+  const float lt = xsum32(l);
+  const float inv = (lt > 0.f) ? (DROP ? a.drop_scale : 1.f) / lt : NAN;
+  unsigned char* ost = kst + w * 4096;
+#pragma unroll
+  for (int db = 0; db < 2; ++db) {
+#pragma unroll
+    for (int mm = 0; mm < 4; ++mm) {
+      const f32x16_t& oo = db ? o1 : o0;
+      uint2 u2;
+      u2.x = pk_bf16(oo[4 * mm] * inv, oo[4 * mm + 1] * inv);
+      u2.y = pk_bf16(oo[4 * mm + 2] * inv, oo[4 * mm + 3] * inv);
+      *(uint2*)(ost + qi * 128 + (((4 * db + mm) ^ (qi & 7)) << 4) + 8 * hh) = u2;
+    }
+  }
+  if (a.lse && hh == 0 && qv)
+    a.lse[(long)bh * a.Lq + q] = (lt > 0.f) ? (m * sl2 + __log2f(lt)) * 0.69314718055994531f : NAN;
+  bf16_t* Ob = (bf16_t*)a.Out + (long)b * a.Lq * a.so + h * DH;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (lane >> 3) + 8 * i, c = lane & 7;
+    const uint4 v = *(const uint4*)(ost + row * 128 + ((c ^ (row & 7)) << 4));
+    if (qw0 + row < a.Lq) *(uint4*)(Ob + (long)(qw0 + row) * a.so + c * 8) = v;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------- backward
+// Images that serve both row reads (ds_read_b128, A = rows) and transposed reads (ds_read_b64_tr_b16, A = columns):
+// chunk c of row r at c ^ dsw(r), dsw(r) = a ^ ((a & 1) << 2) with a = (r >> 1) & 7. A row-read lane group's 16 rows
+// have distinct (r & 1, a), and a transposed read's rows 4j and 4j + 2 land 5 chunks apart (opposite 64-B halves).
+__device__ __forceinline__ int dsw(int r) {
+  const int a = (r >> 1) & 7;
+  return a ^ ((a & 1) << 2);
+}
+// the register-resident operand of the backward's score MFMA (Q in dq7, K in dkv7) pre-scaled by sl2 = scale *
+// log2(e) and rounded to bf16 once, so the product is the exponent in log2 units: 8 bf16 of one 16-B fragment
+__device__ __forceinline__ uint4 scale_frag(const uint4& x, float c) {
+  const u32x4v_t w = __builtin_bit_cast(u32x4v_t, x);
+  u32x4v_t o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    o[j] = pk_bf16(__uint_as_float(w[j] << 16) * c, __uint_as_float(w[j] & 0xFFFF0000u) * c);
+  return __builtin_bit_cast(uint4, o);
+}
+// -x as a bf16 pair (hi, lo) with hi + lo = -x to ~2^-16 relative: the exact-constant fifth k-step of a score MFMA
+__device__ __forceinline__ unsigned neg_split(float x) {
+  const float hi = __uint_as_float(((unsigned)pk_bf16(-x, 0.f)) << 16);
+  return pk_bf16(hi, -x - hi);
+}
+
+// dQ, query-owned (4 waves x 32 queries per workgroup, K / V tiles of 64 keys streamed through a 2-stage LDS-DMA
+// ring). Per 32-key half: S''^T = K Q'^T over 4 k-steps plus a fifth k-step that adds -LSE (log2 units, hi + lo bf16)
+// and the key mask, so p = exp2(S'') is one instruction; dP^T = V dO^T; dS = p (keep dscale dP - delta);
+// dQ^T += K^T dS^T (K^T by transposed reads of the same K image). Also writes the backward's per-query row terms for
+// dkv7: nlse2 = -LSE log2(e) (-inf past Lq) and delta = rowsum(dO O) (0 past Lq), both [B*H][LqP].
+template <int DM, int MK>
+__global__ void __launch_bounds__(256, 3) dq7_kernel(AttnArgs a) {
+  constexpr bool DROP = DM != 0;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smq7[];
+  const int ntiles = (a.Lk + 63) >> 6, LkP = ntiles * 64, LqP = (a.Lq + 63) & ~63;
+  unsigned char* kst = smq7;                      // [2][64 rows][128 B] K, dsw swizzle (row + transposed reads)
+  unsigned char* vst = smq7 + 2 * A7_TB;          // [2][64 rows][128 B] V, KC swizzle (row reads)
+  unsigned char* kwl = smq7 + 4 * A7_TB;          // [2][128 queries][8 B] keep words of the tile
+  unsigned* tact = (unsigned*)(kwl + 2048);       // [4] active-tile nibbles per wave (MK 2)
+  unsigned* mpk = (unsigned*)(kwl + 2048 + 16);   // [LkP] bf16 pair (mask, 0): the key's fifth-k-step operand
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hh = lane >> 5, qi = lane & 31;
+  int bxi, bh;
+  xcd_tile(bxi, bh);
+  const int b = bh / a.H, h = bh - b * a.H;
+  const int qw0 = bxi * 128 + 32 * w;
+  const int q = qw0 + qi;
+  const bool qv = q < a.Lq;
+  const bf16_t* Qb = (const bf16_t*)a.Q + (long)b * a.Lq * a.sq + h * DH;
+  const bf16_t* Ob = (const bf16_t*)a.O + (long)b * a.Lq * a.so + h * DH;
+  const bf16_t* dOb = (const bf16_t*)a.dO + (long)b * a.Lq * a.sdo + h * DH;
+  const bf16_t* Kb = (const bf16_t*)a.K + (long)b * a.Lk * a.sk + h * DH;
+  const bf16_t* Vb = (const bf16_t*)a.V + (long)b * a.Lk * a.sv + h * DH;
+  const unsigned sk2 = (unsigned)a.sk * 2u, sv2 = (unsigned)a.sv * 2u;
+  const uint64_t* kwb = a.dbits + (long)bh * ntiles * a.Lq;
+  auto fill = [&](int tt, int st) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int R = 16 * w + 8 * u;
+      const int r = 64 * tt + R + (lane >> 3), pch = lane & 7;
+      const unsigned rr = (unsigned)min(r, a.Lk - 1);
+      dma16_sv(Kb, rr * sk2 + (unsigned)((pch ^ dsw(r)) << 4), kst + st * A7_TB + R * 128);
+      dma16_sv(Vb, rr * sv2 + (unsigned)((pch ^ ((r >> 1) & 7)) << 4), vst + st * A7_TB + R * 128);
+    }
+    if constexpr (DM == 1) {
+      const unsigned qq = (unsigned)min(qw0 + (lane >> 1), a.Lq - 1);
+      dma4_sv(kwb, ((unsigned)tt * (unsigned)a.Lq + qq) * 8u + 4u * (lane & 1), kwl + st * 1024 + w * 256);
+    }
+  };
+
+  // ---- prologue: tile 0's stream; Q (pre-scaled), dO, O fragments; the key mask; delta and the row terms
+  fill(0, 0);
+  const float sl2 = a.scale * 1.4426950408889634f;
+  uint4 qf[4], dof[4];
+  float dl = 0.f;
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    // rows past Lq read row Lq - 1 (valid memory) and are zeroed: no contribution, never stored
+    const long c = 16 * ks + 8 * hh, qc = min(q, a.Lq - 1);
+    const unsigned zm = qv ? 0xFFFFFFFFu : 0u;
+    const uint4 x = *(const uint4*)(Qb + qc * a.sq + c);
+    const uint4 xo = *(const uint4*)(dOb + qc * a.sdo + c);
+    const uint4 y = *(const uint4*)(Ob + qc * a.so + c);
+    dof[ks] = make_uint4(xo.x & zm, xo.y & zm, xo.z & zm, xo.w & zm);
+    qf[ks] = scale_frag(make_uint4(x.x & zm, x.y & zm, x.z & zm, x.w & zm), sl2);
+    const u32x4v_t xd = __builtin_bit_cast(u32x4v_t, dof[ks]), yo = __builtin_bit_cast(u32x4v_t, y);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      dl += __uint_as_float(xd[j] << 16) * __uint_as_float(yo[j] << 16) +
+            __uint_as_float(xd[j] & 0xFFFF0000u) * __uint_as_float(yo[j] & 0xFFFF0000u);
+  }
+  dl = xsum32(dl);  // delta = rowsum(dO * O) over the query's 64 columns (lanes l, l ^ 32)
+  const float lse2 = qv ? a.lse[(long)bh * a.Lq + q] * 1.4426950408889634f : 0.f;
+  if (hh == 0 && q < LqP) {
+    a.delta[(long)bh * LqP + q] = qv ? dl : 0.f;
+    a.delta[(long)a.B * a.H * LqP + (long)bh * LqP + q] = qv ? -lse2 : -INFINITY;
+  }
+  // the query's fifth-k-step operand: (-lse2 hi, -lse2 lo, 1, 0, ...) on the lanes of the first 8 k positions
+  const uint4 q5 = hh ? make_uint4(0, 0, 0, 0) : make_uint4(neg_split(lse2), pk_bf16(1.f, 0.f), 0u, 0u);
+  unsigned tmask = ntiles >= 32 ? 0xFFFFFFFFu : ((1u << ntiles) - 1u);
+  if constexpr (MK != 0) {
+    bool any = false;
+    if (4 * tid < LkP) {
+      unsigned mv[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = 4 * tid + j;
+        const bool ok = k < a.Lk && (MK == 1 || a.key_keep[(long)b * a.Lk + k] != 0);
+        mv[j] = pk_bf16(ok ? 0.f : -INFINITY, 0.f);
+        any |= ok;
+      }
+      *(uint4*)(mpk + 4 * tid) = make_uint4(mv[0], mv[1], mv[2], mv[3]);
+    }
+    if constexpr (MK == 2) {
+      const unsigned long long bal = __ballot(any);
+      if (lane == 0) {
+        unsigned nib = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) nib |= ((bal >> (16 * j)) & 0xFFFFull) ? (1u << j) : 0u;
+        tact[w] = nib;
+      }
+    }
+  }
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    pin16(qf[ks]);
+    pin16(dof[ks]);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  if constexpr (MK == 2) tmask &= tact[0] | (tact[1] << 4) | (tact[2] << 8) | (tact[3] << 12);
+
+  int koff[4], voffr[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    koff[ks] = qi * 128 + (((2 * ks + hh) ^ dsw(qi)) << 4);
+    voffr[ks] = qi * 128 + (((2 * ks + hh) ^ ((qi >> 1) & 7)) << 4);
+  }
+  // K^T transposed reads: 16-lane group G reads rows kb0 + 4 hh + (i >> 2) (+ 8 for the hi half), units 8 db + 4 (G &
+  // 1) + (i & 3); the row's dsw depends only on hh, the hi half and i >> 3 (kb0 is a multiple of 16)
+  const int vi = lane & 15;
+  int ktr[2][2];
+#pragma unroll
+  for (int hi = 0; hi < 2; ++hi) {
+    const int row = 4 * hh + 8 * hi + (vi >> 2);
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+      const int u = 8 * db + 4 * ((lane >> 4) & 1) + (vi & 3);
+      ktr[hi][db] = row * 128 + ((((u >> 1) ^ dsw(row)) << 1 | (u & 1)) << 3);
+    }
+  }
+  f32x16_t g0 = {}, g1 = {};  // dQ^T, d-blocks 0 / 1
+
+  auto tile = [&](const int t, const int st) {
+    const bool mt = MK == 2 || (MK == 1 && t == ntiles - 1);  // this tile's keys carry a mask
+    const unsigned char* kimg = kst + st * A7_TB;
+    const unsigned char* vimg = vst + st * A7_TB;
+    unsigned kw2[2] = {0u, 0u};
+    if constexpr (DROP) {
+      const uint64_t kw = *(const uint64_t*)(kwl + st * 1024 + (32 * w + qi) * 8);
+      kw2[0] = (unsigned)(kw >> (4 * hh));
+      kw2[1] = (unsigned)(kw >> (32 + 4 * hh));
+    }
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      // the key's fifth-k-step operand: (1, 1, mask, 0, ...) on the lanes of the first 8 k positions
+      unsigned mk = 0u;
+      if (MK != 0 && mt) mk = mpk[64 * t + 32 * kb + qi];
+      const uint4 k5 = hh ? make_uint4(0, 0, 0, 0) : make_uint4(pk_bf16(1.f, 1.f), mk, 0u, 0u);
+      f32x16_t sc = mfma32(k5, q5, f32x16_t{});
+      f32x16_t dp = {};
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        sc = mfma32(*(const uint4*)(kimg + koff[ks] + kb * 32 * 128), qf[ks], sc);
+        dp = mfma32(*(const uint4*)(vimg + voffr[ks] + kb * 32 * 128), dof[ks], dp);
+      }
+      uint4 bs[2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        unsigned bw[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int r = 8 * s + 2 * jj;
+          float d0 = dp[r], d1 = dp[r + 1];
+          if constexpr (DROP) {
+            const int pos = 8 * (r >> 2) + (r & 3);
+            d0 = fmaf(__uint_as_float(__float_as_uint(d0) & (unsigned)__builtin_amdgcn_sbfe((int)kw2[kb], pos, 1)),
+                      a.drop_scale, -dl);
+            d1 = fmaf(__uint_as_float(__float_as_uint(d1) & (unsigned)__builtin_amdgcn_sbfe((int)kw2[kb], pos + 1, 1)),
+                      a.drop_scale, -dl);
+          } else {
+            d0 -= dl;
+            d1 -= dl;
+          }
+          bw[jj] = pk_bf16(__builtin_amdgcn_exp2f(sc[r]) * d0, __builtin_amdgcn_exp2f(sc[r + 1]) * d1);
+        }
+        bs[s] = make_uint4(bw[0], bw[1], bw[2], bw[3]);
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int rb = (32 * kb + 16 * s) * 128;
+        const uint4 k0 = join_tr(tr_read(kimg + ktr[0][0] + rb), tr_read(kimg + ktr[1][0] + rb));
+        const uint4 k1 = join_tr(tr_read(kimg + ktr[0][1] + rb), tr_read(kimg + ktr[1][1] + rb));
+        g0 = mfma32(k0, bs[s], g0);
+        g1 = mfma32(k1, bs[s], g1);
+      }
+    }
+  };
+
+  int t = 0, st = 0;
+  bool act = (tmask & 1u) != 0;
+  while (true) {
+    const unsigned rest = t + 1 < 32 ? (tmask & ~((2u << t) - 1u)) : 0u;
+    const int tn = rest ? __builtin_ctz(rest) : -1;
+    if (tn >= 0) fill(tn, st ^ 1);
+    if (act) tile(t, st);
+    if (tn < 0) break;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    t = tn;
+    st ^= 1;
+    act = true;
+  }
+
+  // ---- epilogue: dQ = scale * dQ^T, staged per wave in LDS (K ring, free after the barrier), stored as rows
+  __syncthreads();
+  unsigned char* ost = kst + w * 4096;
+#pragma unroll
+  for (int db = 0; db < 2; ++db) {
+#pragma unroll
+    for (int mm = 0; mm < 4; ++mm) {
+      const f32x16_t& gg = db ? g1 : g0;
+      uint2 u2;
+      u2.x = pk_bf16(gg[4 * mm] * a.scale, gg[4 * mm + 1] * a.scale);
+      u2.y = pk_bf16(gg[4 * mm + 2] * a.scale, gg[4 * mm + 3] * a.scale);
+      *(uint2*)(ost + qi * 128 + (((4 * db + mm) ^ (qi & 7)) << 4) + 8 * hh) = u2;
+    }
+  }
+  bf16_t* dQb = (bf16_t*)a.dQ + (long)b * a.Lq * a.sdq + h * DH;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (lane >> 3) + 8 * i, c = lane & 7;
+    const uint4 v = *(const uint4*)(ost + row * 128 + ((c ^ (row & 7)) << 4));
+    if (qw0 + row < a.Lq) *(uint4*)(dQb + (long)(qw0 + row) * a.sdq + c * 8) = v;
+  }
+}
+
+// dK / dV, key-owned (4 waves x 32 keys per workgroup, Q / dO tiles of 64 queries streamed through a 2-stage LDS-DMA
+// ring with the tiles' row terms nlse2 / delta from dq7 and the forward's keep words). Per 32-query half:
+// S'' = Q K'^T over 4 k-steps (K' = K pre-scaled by sl2, registers) plus a fifth k-step that adds the row's -LSE
+// (log2 units, hi + lo bf16), p = exp2(S''); dP = dO V^T; dS = p (keep dscale dP - delta); dV^T += dO^T (p keep) and
+// dK^T += Q^T dS with the key on the MFMA lane: the score accumulators are the B operands (no LDS round trip), and the
+// Q / dO images serve both the row reads and the transposed reads. Keys that are padding get zero gradients.
+template <int DM, bool MASK>
+__global__ void __launch_bounds__(256, 2) dkv7_kernel(AttnArgs a) {
+  constexpr bool DROP = DM != 0;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smk7[];
+  const int ntiles = (a.Lk + 63) >> 6, nqt = (a.Lq + 63) >> 6, LqP = nqt * 64;
+  unsigned char* qst = smk7;                      // [2][64 rows][128 B] Q, dsw swizzle
+  unsigned char* dost = smk7 + 2 * A7_TB;         // [2][64 rows][128 B] dO, dsw swizzle
+  float* rowt = (float*)(smk7 + 4 * A7_TB);       // [2][nlse2 64 | delta 64]
+  unsigned* kwd = (unsigned*)(smk7 + 4 * A7_TB + 1024);  // [2][4 waves][64 queries] keep dwords of the wave's keys
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hh = lane >> 5, qi = lane & 31;
+  int bxi, bh;
+  xcd_tile(bxi, bh);
+  const int b = bh / a.H, h = bh - b * a.H;
+  const int kw0 = bxi * 128 + 32 * w;
+  const int kk = kw0 + qi;
+  const bool kv = kk < a.Lk && (!MASK || a.key_keep[(long)b * a.Lk + min(kk, a.Lk - 1)] != 0);
+  const bf16_t* Qb = (const bf16_t*)a.Q + (long)b * a.Lq * a.sq + h * DH;
+  const bf16_t* dOb = (const bf16_t*)a.dO + (long)b * a.Lq * a.sdo + h * DH;
+  const bf16_t* Kb = (const bf16_t*)a.K + (long)b * a.Lk * a.sk + h * DH;
+  const bf16_t* Vb = (const bf16_t*)a.V + (long)b * a.Lk * a.sv + h * DH;
+  const float* nlse_g = a.delta + (long)a.B * a.H * LqP + (long)bh * LqP;
+  const float* dlt_g = a.delta + (long)bh * LqP;
+  const unsigned sq2 = (unsigned)a.sq * 2u, sdo2 = (unsigned)a.sdo * 2u;
+  // the wave's keep dwords: word (bh, t, q) of key tile t = kw0 / 64, half (kw0 / 32) & 1
+  const int tw = kw0 >> 6;
+  const uint64_t* kwb = a.dbits + ((long)bh * ntiles + min(tw, ntiles - 1)) * a.Lq;
+  auto fill = [&](int uu, int st) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int R = 16 * w + 8 * u;
+      const int r = 64 * uu + R + (lane >> 3), pch = lane & 7;
+      const unsigned rr = (unsigned)min(r, a.Lq - 1);
+      dma16_sv(Qb, rr * sq2 + (unsigned)((pch ^ dsw(r)) << 4), qst + st * A7_TB + R * 128);
+      dma16_sv(dOb, rr * sdo2 + (unsigned)((pch ^ dsw(r)) << 4), dost + st * A7_TB + R * 128);
+    }
+    if (w == 0) dma4_sv(nlse_g, (unsigned)(64 * uu + lane) * 4u, (const unsigned char*)(rowt + st * 128));
+    if (w == 1) dma4_sv(dlt_g, (unsigned)(64 * uu + lane) * 4u, (const unsigned char*)(rowt + st * 128 + 64));
+    if constexpr (DROP) {
+      const unsigned qq = (unsigned)min(64 * uu + lane, a.Lq - 1);
+      dma4_sv(kwb, qq * 8u + 4u * ((kw0 >> 5) & 1), (const unsigned char*)(kwd + st * 256 + w * 64));
+    }
+  };
+
+  fill(0, 0);
+  const float sl2 = a.scale * 1.4426950408889634f;
+  const int kc = min(kk, a.Lk - 1);
+  uint4 kf[4], vf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const long c = 16 * ks + 8 * hh;
+    kf[ks] = scale_frag(*(const uint4*)(Kb + (long)kc * a.sk + c), sl2);
+    vf[ks] = *(const uint4*)(Vb + (long)kc * a.sv + c);
+  }
+  // the key's fifth-k-step operand (1, 1, 0, ...) on the lanes of the first 8 k positions
+  const uint4 b5 = hh ? make_uint4(0, 0, 0, 0) : make_uint4(pk_bf16(1.f, 1.f), 0u, 0u, 0u);
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    pin16(kf[ks]);
+    pin16(vf[ks]);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  int qoff[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) qoff[ks] = qi * 128 + (((2 * ks + hh) ^ dsw(qi)) << 4);
+  const int vi = lane & 15;
+  int ttr[2][2];
+#pragma unroll
+  for (int hi = 0; hi < 2; ++hi) {
+    const int row = 4 * hh + 8 * hi + (vi >> 2);
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+      const int u = 8 * db + 4 * ((lane >> 4) & 1) + (vi & 3);
+      ttr[hi][db] = row * 128 + ((((u >> 1) ^ dsw(row)) << 1 | (u & 1)) << 3);
+    }
+  }
+  f32x16_t gk0 = {}, gk1 = {}, gv0 = {}, gv1 = {};  // dK^T, dV^T, d-blocks 0 / 1
+
+  auto tile = [&](const int st) {
+    const unsigned char* qimg = qst + st * A7_TB;
+    const unsigned char* doimg = dost + st * A7_TB;
+    const float* nl = rowt + st * 128;
+    const float* dl = nl + 64;
+    const unsigned* kd = kwd + st * 256 + w * 64;
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      // the query row's fifth-k-step operand (-LSE log2(e) as hi + lo bf16) on the lanes of the first 8 k positions
+      const float x = nl[32 * qb + qi];
+      const float xh = __uint_as_float(((unsigned)pk_bf16(x, 0.f)) << 16);
+      const float xl = (x == -INFINITY) ? 0.f : x - xh;
+      const uint4 a5 = hh ? make_uint4(0, 0, 0, 0) : make_uint4(pk_bf16(xh, xl), 0u, 0u, 0u);
+      f32x16_t sc = mfma32(a5, b5, f32x16_t{});
+      f32x16_t dp = {};
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        sc = mfma32(*(const uint4*)(qimg + qoff[ks] + qb * 32 * 128), kf[ks], sc);
+        dp = mfma32(*(const uint4*)(doimg + qoff[ks] + qb * 32 * 128), vf[ks], dp);
+      }
+      uint4 bp[2], bs[2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        unsigned pw[4], sw[4];
+#pragma unroll
+        for (int mh = 0; mh < 2; ++mh) {
+          // registers r = 8 s + 4 mh .. + 3: queries 32 qb + 8 (2 s + mh) + 4 hh + 0 .. 3
+          const int r0 = 8 * s + 4 * mh, qr = 32 * qb + 8 * (2 * s + mh) + 4 * hh;
+          const f32x4_t d4 = *(const f32x4_t*)(dl + qr);
+          u32x4v_t k4 = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+          if constexpr (DROP) k4 = *(const u32x4v_t*)(kd + qr);
+          float pv[4], dv[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float pr = __builtin_amdgcn_exp2f(sc[r0 + e]);
+            float dd = dp[r0 + e];
+            if constexpr (DROP) {
+              const unsigned m = (unsigned)__builtin_amdgcn_sbfe((int)k4[e], qi, 1);
+              pv[e] = __uint_as_float(__float_as_uint(pr) & m);
+              dd = fmaf(__uint_as_float(__float_as_uint(dd) & m), a.drop_scale, -d4[e]);
+            } else {
+              pv[e] = pr;
+              dd -= d4[e];
+            }
+            dv[e] = pr * dd;
+          }
+          pw[2 * mh] = pk_bf16(pv[0], pv[1]);
+          pw[2 * mh + 1] = pk_bf16(pv[2], pv[3]);
+          sw[2 * mh] = pk_bf16(dv[0], dv[1]);
+          sw[2 * mh + 1] = pk_bf16(dv[2], dv[3]);
+        }
+        bp[s] = make_uint4(pw[0], pw[1], pw[2], pw[3]);
+        bs[s] = make_uint4(sw[0], sw[1], sw[2], sw[3]);
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int rb = (32 * qb + 16 * s) * 128;
+        const uint4 o0 = join_tr(tr_read(doimg + ttr[0][0] + rb), tr_read(doimg + ttr[1][0] + rb));
+        const uint4 o1 = join_tr(tr_read(doimg + ttr[0][1] + rb), tr_read(doimg + ttr[1][1] + rb));
+        gv0 = mfma32(o0, bp[s], gv0);
+        gv1 = mfma32(o1, bp[s], gv1);
+        const uint4 q0 = join_tr(tr_read(qimg + ttr[0][0] + rb), tr_read(qimg + ttr[1][0] + rb));
+        const uint4 q1 = join_tr(tr_read(qimg + ttr[0][1] + rb), tr_read(qimg + ttr[1][1] + rb));
+        gk0 = mfma32(q0, bs[s], gk0);
+        gk1 = mfma32(q1, bs[s], gk1);
+      }
+    }
+  };
+
+  int st = 0;
+  for (int uu = 0; uu < nqt; ++uu) {
+    if (uu + 1 < nqt) fill(uu + 1, st ^ 1);
+    tile(st);
+    if (uu + 1 < nqt) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      st ^= 1;
+    }
+  }
+
+  // ---- epilogue: dV = dscale dV^T, dK = scale dK^T (zero for padding keys), staged per wave in LDS, stored as rows
+  __syncthreads();
+  unsigned char* ost = qst + w * 4096;
+  const float fv = kv ? (DROP ? a.drop_scale : 1.f) : 0.f, fk = kv ? a.scale : 0.f;
+#pragma unroll
+  for (int which = 0; which < 2; ++which) {
+    const float f = which ? fk : fv;
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+#pragma unroll
+      for (int mm = 0; mm < 4; ++mm) {
+        const f32x16_t& gg = which ? (db ? gk1 : gk0) : (db ? gv1 : gv0);
+        uint2 u2;
+        u2.x = pk_bf16(gg[4 * mm] * f, gg[4 * mm + 1] * f);
+        u2.y = pk_bf16(gg[4 * mm + 2] * f, gg[4 * mm + 3] * f);
+        *(uint2*)(ost + qi * 128 + (((4 * db + mm) ^ (qi & 7)) << 4) + 8 * hh) = u2;
+      }
+    }
+    bf16_t* Gb = which ? (bf16_t*)a.dK + (long)b * a.Lk * a.sdk + h * DH : (bf16_t*)a.dV + (long)b * a.Lk * a.sdv + h * DH;
+    const long sg = which ? a.sdk : a.sdv;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = (lane >> 3) + 8 * i, c = lane & 7;
+      const uint4 v = *(const uint4*)(ost + row * 128 + ((c ^ (row & 7)) << 4));
+      if (kw0 + row < a.Lk) *(uint4*)(Gb + (long)(kw0 + row) * sg + c * 8) = v;
+    }
+  }
+}
+
+int attn7_fwd(AttnArgs& a, hipStream_t s) {
+  const int dm = a.thr16 == 0 ? 0 : 1;
+  const int mk = a.key_keep != nullptr ? 2 : (a.Lk % 64) != 0 ? 1 : 0;
+  const int ntiles = (a.Lk + 63) / 64;
+  const size_t lds = (size_t)4 * A7_TB + 2048 + 16 + (size_t)ntiles * 64 * 4;
+  dim3 grid((a.Lq + 127) / 128, a.B * a.H);
+#define FWD7(D, M) hipLaunchKernelGGL((fwd7_kernel<D, M>), grid, dim3(256), lds, s, a)
+  if (dm) { if (mk == 2) FWD7(1, 2); else if (mk == 1) FWD7(1, 1); else FWD7(1, 0); }
+  else { if (mk == 2) FWD7(0, 2); else if (mk == 1) FWD7(0, 1); else FWD7(0, 0); }
+#undef FWD7
+  return (int)hipGetLastError();
+}
+
+int attn7_dq(AttnArgs& a, hipStream_t s) {
+  const int dm = a.thr16 == 0 ? 0 : 1;
+  const int mk = a.key_keep != nullptr ? 2 : (a.Lk % 64) != 0 ? 1 : 0;
+  const int ntiles = (a.Lk + 63) / 64;
+  const size_t lds = (size_t)4 * A7_TB + 2048 + 16 + (size_t)ntiles * 64 * 4;
+  dim3 grid((a.Lq + 127) / 128, a.B * a.H);
+#define DQ7(D, M) hipLaunchKernelGGL((dq7_kernel<D, M>), grid, dim3(256), lds, s, a)
+  if (dm) { if (mk == 2) DQ7(1, 2); else if (mk == 1) DQ7(1, 1); else DQ7(1, 0); }
+  else { if (mk == 2) DQ7(0, 2); else if (mk == 1) DQ7(0, 1); else DQ7(0, 0); }
+#undef DQ7
+  return (int)hipGetLastError();
+}
+
+int attn7_dkv(AttnArgs& a, hipStream_t s) {
+  const int dm = a.thr16 == 0 ? 0 : 1;
+  const size_t lds = (size_t)4 * A7_TB + 1024 + 2048;
+  dim3 grid((a.Lk + 127) / 128, a.B * a.H);
+#define DKV7(D, M) hipLaunchKernelGGL((dkv7_kernel<D, M>), grid, dim3(256), lds, s, a)
+  if (dm) { if (a.key_keep) DKV7(1, true); else DKV7(1, false); }
+  else { if (a.key_keep) DKV7(0, true); else DKV7(0, false); }
+#undef DKV7
+  return (int)hipGetLastError();
+}
+
+}  // namespace attn
+}  // namespace fddm

@@ -278,7 +278,9 @@ class DecoderBlockFn(torch.autograd.Function):
         x3 = torch.empty(N, d, device=dev, dtype=F32)
         x3T = torch.empty(N, d, device=dev, dtype=cd)
         rope = None
-        if handoff is not None and cd == torch.bfloat16:   # the next block's rope(x) from the same pass
+        # the next block's rope(x) from the same pass, where the fused LN kernel takes the shape (fddm_ln_fwd: bf16,
+        # d % 16 == 0, d <= 1024); otherwise handoff stays empty and the next block runs its own rope_fwd
+        if handoff is not None and cd == torch.bfloat16 and d % 16 == 0 and d <= 1024:
             handoff["xr"] = torch.empty(N, d, device=dev, dtype=cd)
             rope = (cos, sin, handoff["xr"], L)
         ops.ln_fwd(x2, y3, n3w, n3b, out_f32=x3, out_t=x3T, save_s=s3, mean=m3, rstd=r3,

@@ -111,9 +111,14 @@ class StepGraphs:
 
     Validity: a graph reads parameters, cached bf16 weights, optimizer moments / chunk tables and gradient-arena views
     by address. It is dropped (and the step runs eagerly, then recaptures) when the runtime cache epoch changes
-    (clear_cache), when any trainable parameter is replaced or changed by a torch op (data_ptr / _version), or when
-    the optimizer rebuilt its tables (FusedAdamW.table_epoch). The two kinds share one memory pool (they replay on one
-    stream, never concurrently; their outputs stay live)."""
+    (clear_cache), when any trainable parameter is replaced or changed by a torch op (data_ptr / _version), when
+    the optimizer rebuilt its tables (FusedAdamW.table_epoch) or when an optimizer hyperparameter the AdamW launch
+    takes by value changed (lr, weight decay, betas, eps: `_hparams`). The two kinds share one memory pool (they
+    replay on one stream, never concurrently; their outputs stay live).
+
+    Fixed shapes only: the graphs are keyed by the step's input shapes, and a batch of another shape drops both kinds
+    (reset) and runs eagerly. With variable-length batches (the real-data loader's per-batch padding) nearly every
+    step would capture again and none would replay; bucket the batches to a few fixed shapes before enabling it."""
 
     def __init__(self, device):
         self.device = torch.device(device)
@@ -128,8 +133,19 @@ class StepGraphs:
         self.static.clear()
         self.pool = None
 
+    @staticmethod
+    def _hparams(optimizer):
+        """The optimizer hyperparameters a captured AdamW launch bakes in as kernel arguments (lr, weight decay,
+        betas, eps per param group; max_norm / grad_scale where the optimizer keeps them): a change (e.g. an lr
+        schedule writing param_groups[i]['lr']) must recapture, or replays would keep the captured values."""
+        groups = tuple((float(g.get("lr", 0.0)), float(g.get("weight_decay", 0.0)),
+                        tuple(float(b) for b in g.get("betas", ())), float(g.get("eps", 0.0)))
+                       for g in getattr(optimizer, "param_groups", ()))
+        extra = tuple(getattr(optimizer, k, None) for k in ("max_norm", "grad_scale"))
+        return groups, extra
+
     def _token(self, params, optimizer):
-        return (rt.cache_epoch(), getattr(optimizer, "table_epoch", 0),
+        return (rt.cache_epoch(), getattr(optimizer, "table_epoch", 0), self._hparams(optimizer),
                 tuple((p.data_ptr(), p._version) for p in params))
 
     def get(self, kind, params, optimizer, shapes):

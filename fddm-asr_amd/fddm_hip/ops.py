@@ -104,6 +104,18 @@ def gemm_force_path(name: str) -> str:
     return {v: k for k, v in GEMM_PATHS.items()}[old]
 
 
+ATTN_KERNELS = {"auto": 0, "v6": 1}
+
+
+def attn_force_kernels(name: str) -> str:
+    """Select the attention kernel family for every following launch (tests and diagnostics): "v6" = the
+    16x16x32-MFMA kernels of attention.hip where the 32x32x16 family (attn7.hip) would run, "auto" = the default
+    choice. Returns the previous setting's name."""
+    from ._lib import lib
+    old = lib().fddm_attn_set_kernels(ATTN_KERNELS[name])
+    return {v: k for k, v in ATTN_KERNELS.items()}[old]
+
+
 def gemm(A, B, C, M, N, K, *, a_kc=True, b_kc=True, lda, ldb, ldc, epi=EPI_STORE, bias=None, alpha=1.0,
          C2=None, Mi=0, sAb=0, drop_p=0.0, seed=0, rng_stream=0, colsum=None):
     """C[m][n] = alpha * sum_k A(m,k) B(n,k) (+bias, epilogue). Compute dtype = B.dtype.
@@ -318,7 +330,9 @@ def attn_bwd(q, k, v, o, do, lse, dq, dk, dv, B, H, Lq, Lk, *, key_keep=None, dr
         for g, gp, r in ((dq, dqp, rq), (dk, dkp, rk), (dv, dvp, rk)):
             _heads(g, r, H, dh).copy_(gp.view(r, H, 64)[:, :, :dh])
         return
-    delta = torch.empty(B * H, Lq, device=q.device, dtype=torch.float32)
+    # row-term workspace: delta = rowsum(dO O) and -LSE log2(e) per query, [2][B*H][Lq rounded up to 64] (the
+    # 32x32x16 backward's layout; the other kernels use the first B*H*Lq floats)
+    delta = torch.empty(2 * B * H * ((Lq + 63) // 64 * 64), device=q.device, dtype=torch.float32)
     call("fddm_attn_bwd", code(q), ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(o),
          o.stride(0), ptr(do), do.stride(0), ptr(lse), ptr(dq), dq.stride(0), ptr(dk), dk.stride(0), ptr(dv),
          dv.stride(0), ptr(delta), ptr(key_keep), B, H, Lq, Lk, float(sc), float(drop_p), seed, rng_stream,

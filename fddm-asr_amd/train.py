@@ -203,7 +203,17 @@ def _step_graph_ok(device, scaler, optimizer, arena) -> bool:
     backward callbacks and stays eager). Off by default: on this ROCm 7 / torch 2.10 stack a replayed step ran 12.9
     ms against 9.94 eager at C2 (tools/ab_graph.sh; the graph launch runs ~1.3 ms longer on the GPU than the same
     launches enqueued eagerly and no longer overlaps the encoder's side stream; DEBUG_CLR_GRAPH_PACKET_CAPTURE and
-    DEBUG_HIP_FORCE_GRAPH_QUEUES did not change that) — it pays only where the host, not the GPU, bounds the step."""
+    DEBUG_HIP_FORCE_GRAPH_QUEUES did not change that) — it pays only where the host, not the GPU, bounds the step.
+    Fixed batch shapes only (StepGraphs: a new shape drops the graphs and runs eagerly).
+
+    Refused under DEBUG_HIP_FORCE_GRAPH_QUEUES=0: round 4's A/B arm that differed from its neighbours only by that
+    setting died with SIGFPE (gpurun_out/ab_g.log: bash reports `Floating point exception` for bench.py; its stderr
+    holds no Python traceback, so the signal came from native code). SIGFPE on x86 is an integer divide by zero;
+    the HIP runtime spreads a graph's launches over the number of queues that knob forces, so zero queues makes that
+    count a divisor. The cause is the runtime's knob, not this code; the arm is gone from
+    tools/ab_graph.sh and this check keeps the graph path off under that setting."""
+    if os.environ.get("DEBUG_HIP_FORCE_GRAPH_QUEUES", None) == "0":
+        return False
     return (torch.device(device).type == "cuda" and rt.compute_dtype() == torch.bfloat16 and scaler is None and
             arena is not None and hasattr(optimizer, "clip_and_step") and fdist.world() == 1 and
             os.environ.get("FDDM_STEP_GRAPH", "0") == "1")

@@ -104,8 +104,12 @@ int fddm_attn_drop_bits(unsigned long long* out, long site_words, int nsites, in
 int fddm_attn_fwd_relgate(const void* Q, long sq, const void* K, long sk, const void* V, long sv, void* O, long so,
                           const void* graw, long sgr, const float* gconst, const float* table, int B, int H, int Lq,
                           int Lk, float scale, void* hip_stream);
-/* Backward: dQ, dK, dV (bf16 self-attention shapes Lq == Lk <= 256 with recorded or no dropout: one fused launch,
- * delta_ws unused; otherwise a query-owned dQ launch that writes delta_ws [B*H][Lq] and a key-owned dK/dV launch). */
+/* Backward: dQ, dK, dV. bf16 with recorded or no dropout and Lk <= 1024: the 32x32x16-MFMA pair (a query-owned dQ
+ * launch that also writes the per-query row terms delta = rowsum(dO O) and -LSE log2(e) into delta_ws, laid out
+ * [2][B*H][LqP] with LqP = Lq rounded up to 64, then a key-owned dK/dV launch that reads them); delta_ws must hold
+ * 2 * B*H*LqP floats. Otherwise (fp32, rehashed dropout, longer keys, or fddm_attn_set_kernels(1)): bf16 self-
+ * attention shapes Lq == Lk <= 256 as one fused launch, else a dQ launch writing delta_ws [B*H][Lq] and a dK/dV
+ * launch. */
 int fddm_attn_bwd(int dtype, const void* Q, long sq, const void* K, long sk, const void* V, long sv, const void* O,
                   long so, const void* dO, long sdo, const float* lse, void* dQ, long sdq, void* dK, long sdk,
                   void* dV, long sdv, float* delta_ws, const unsigned char* key_keep, int B, int H, int Lq, int Lk,
@@ -202,6 +206,10 @@ int fddm_lfd_std_bwd_apply(int zt_dtype, const float* dzt, const void* zt, const
  *      128x128 only, 3 256x256 wherever its preconditions hold, 4 128x128 LDS-DMA ring wherever they hold). Returns
  *      the previous setting. Process-wide; the train step never sets it. */
 int fddm_gemm_force_path(int path);
+/* ---- attention kernel-family override for tests and diagnostics: 1 = the 16x16x32-MFMA kernels (fwd6, dq4 / dkv4,
+ *      bwd3s) wherever the 32x32x16-MFMA family (csrc/attn7.hip) would run, 0 = automatic (default). Returns the
+ *      previous setting. Process-wide; the train step never sets it. */
+int fddm_attn_set_kernels(int v6);
 
 
 /* ---- dropout-seed offset for HIP-graph replays of the train step: every launch enqueued while `off` (a device u64)

@@ -1,0 +1,183 @@
+"""GPU parity of the 32x32x16-MFMA decoder attention kernels (csrc/attn7.hip) against float64 references with the
+oracle's dropout mask (contract v2), at the shapes the decoder runs (keep bits written ahead by
+fddm_attn_drop_bits, as models/denoise_decoder.py does) and at ragged / masked / extreme-score edge cases.
+
+Tolerance: bf16 inputs and outputs, fp32 softmax statistics -> 2e-2 of the reference's max magnitude (tests/
+test_gpu_kernels.py TOL for bf16); the LSE within 1e-3 absolute (natural-log units) where the row is finite.
+Reference: models/denoise_decoder.py:129-130,164,169-176 (nn.MultiheadAttention, key_padding_mask, dropout on
+the probabilities).
+"""
+import pytest
+import torch
+
+from helpers import close
+from oracle import fddm_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+dev = torch.device("cuda:0")
+bf = torch.bfloat16
+
+
+def ops():
+    from fddm_hip import ops as o
+    return o
+
+
+def _ref(q, k, v, keep, p, seed, stream):
+    """q [B,H,Lq,64] float64 ... -> O [B,H,Lq,64], lse [B,H,Lq] (natural log, of the scaled scores)."""
+    B, H, Lq, _ = q.shape
+    Lk = k.shape[2]
+    s = (q @ k.transpose(-1, -2)) / 8.0
+    if keep is not None:
+        s = s.masked_fill(~keep[:, None, None, :], float("-inf"))
+    lse = torch.logsumexp(s, -1)
+    pr = torch.softmax(s, -1)
+    if p > 0:
+        m = O.attn_dropout_keep(seed, stream, B, H, Lq, Lk, p).double()
+        pr = pr * m / (1 - p)
+    return pr @ v, lse
+
+
+def _run(B, H, Lq, Lk, keep, p, q, k, v, do=None, seed=5, stream=9, family="auto"):
+    o = ops()
+    D = H * 64
+    to = lambda x: x.to(dev, bf).reshape(-1, D).contiguous()  # noqa: E731
+    qd, kd, vd = to(q), to(k), to(v)
+    od = torch.empty(B * Lq, D, device=dev, dtype=bf)
+    lse = torch.empty(B * H, Lq, device=dev)
+    kk = keep.to(dev).to(torch.uint8) if keep is not None else None
+    db = None
+    if p > 0:
+        db = o.drop_bits(B, H, Lq, Lk, dev).view(1, -1)
+        o.attn_drop_bits(db, 1, B, H, Lq, Lk, p, seed, stream, 0)
+        db = db.view(-1)
+    old = o.attn_force_kernels(family)
+    try:
+        o.attn_fwd(qd, kd, vd, od, lse, B, H, Lq, Lk, key_keep=kk, drop_p=p, seed=seed, rng_stream=stream, dbits=db,
+                   bits_ready=db is not None)
+        grads = None
+        if do is not None:
+            dq, dk, dv = torch.empty_like(qd), torch.empty_like(kd), torch.empty_like(vd)
+            o.attn_bwd(qd, kd, vd, od, to(do), lse, dq, dk, dv, B, H, Lq, Lk, key_keep=kk, drop_p=p, seed=seed,
+                       rng_stream=stream, dbits=db)
+            grads = (dq, dk, dv)
+    finally:
+        o.attn_force_kernels(old)
+    torch.cuda.synchronize()
+    return od, lse, grads
+
+
+def _heads(x, B, H):
+    return x.to(bf).double().view(B, -1, H, 64).transpose(1, 2)
+
+
+def _back(t):
+    B, H, L, _ = t.shape
+    return t.transpose(1, 2).reshape(B * L, H * 64)
+
+
+SHAPES = [  # (B, H, Lq, Lk, key-padding mask, dropout p)
+    (2, 3, 256, 256, True, 0.1),     # decoder self-attention (C2 geometry per head)
+    (2, 3, 256, 499, False, 0.1),    # cross-attention, 10 s of audio (ragged last key tile)
+    (2, 2, 512, 512, True, 0.1),     # C4 self
+    (2, 2, 512, 499, False, 0.1),    # C4 cross
+    (2, 3, 130, 70, True, 0.0),      # ragged queries and keys, no dropout
+    (1, 2, 40, 1000, False, 0.1),    # long key range, a partial query block
+    (2, 3, 129, 257, True, 0.1),
+    (3, 1, 64, 64, False, 0.0),
+    (2, 2, 200, 200, True, 0.1),
+]
+
+
+@pytest.mark.parametrize("B,H,Lq,Lk,masked,p", SHAPES)
+def test_attn7_forward_matches_float64(B, H, Lq, Lk, masked, p):
+    D = H * 64
+    gen = torch.Generator().manual_seed(Lq * 1000 + Lk)
+    q, k, v = (torch.randn(B, L, D, generator=gen) for L in (Lq, Lk, Lk))
+    keep = None
+    if masked:
+        keep = torch.ones(B, Lk, dtype=torch.bool)
+        keep[1, Lk - 9:] = False
+        keep[0, 3] = False
+        if Lk > 130:
+            keep[1, 64:128] = False      # a whole 64-key tile of padding inside the range (skipped tile)
+    od, lse, _ = _run(B, H, Lq, Lk, keep, p, q, k, v)
+    ref, rlse = _ref(_heads(q, B, H), _heads(k, B, H), _heads(v, B, H), keep, p, 5, 9)
+    close(od.float(), _back(ref), rtol=2e-2, what="attn7 out")
+    close(lse.view(B, H, Lq), rlse, rtol=0, atol=1e-3, what="attn7 lse")
+
+
+@pytest.mark.parametrize("B,H,Lq,Lk,masked,p", [SHAPES[0], SHAPES[1], SHAPES[4], SHAPES[6]])
+def test_attn7_forward_then_backward_matches_float64(B, H, Lq, Lk, masked, p):
+    """The backward kernels read the forward's LSE and the same keep words: gradients vs float64 autograd."""
+    D = H * 64
+    gen = torch.Generator().manual_seed(7 + Lq + Lk)
+    q, k, v, do = (torch.randn(B, L, D, generator=gen) for L in (Lq, Lk, Lk, Lq))
+    keep = None
+    if masked:
+        keep = torch.ones(B, Lk, dtype=torch.bool)
+        keep[1, Lk - 9:] = False
+    od, lse, (dq, dk, dv) = _run(B, H, Lq, Lk, keep, p, q, k, v, do)
+    qr, kr, vr = (_heads(x, B, H).requires_grad_(True) for x in (q, k, v))
+    ref, _ = _ref(qr, kr, vr, keep, p, 5, 9)
+    ref.backward(_heads(do, B, H))
+    close(od.float(), _back(ref.detach()), rtol=2e-2, what="out")
+    close(dq.float(), _back(qr.grad), rtol=6e-2, what="dq")
+    close(dk.float(), _back(kr.grad), rtol=6e-2, what="dk")
+    close(dv.float(), _back(vr.grad), rtol=6e-2, what="dv")
+
+
+@pytest.mark.parametrize("Lk", [256, 499])
+def test_attn7_rescale_path_with_growing_scores(Lk):
+    """Scores that grow along the keys (every 32-key half-tile exceeds the running maximum by far more than the
+    2^8 rescale threshold) exercise the slow path on every half-tile; scores that fall along the keys keep the first
+    half's reference. Both against float64."""
+    B, H, Lq = 2, 2, 128
+    D = H * 64
+    gen = torch.Generator().manual_seed(11)
+    u = torch.randn(64, generator=gen)
+    u = u / u.norm()
+    q = (u * 4.0).repeat(B, Lq, H) + 0.05 * torch.randn(B, Lq, D, generator=gen)
+    ramp = torch.linspace(0.0, 200.0, Lk)   # +6 to +13 scaled score units per 32-key half-tile
+    for sign in (1.0, -1.0):
+        k = (sign * ramp[None, :, None] * u.repeat(H)[None, None, :]).expand(B, Lk, D).contiguous()
+        k = k + 0.05 * torch.randn(B, Lk, D, generator=gen)
+        v = torch.randn(B, Lk, D, generator=gen)
+        od, lse, _ = _run(B, H, Lq, Lk, None, 0.1, q, k, v)
+        ref, rlse = _ref(_heads(q, B, H), _heads(k, B, H), _heads(v, B, H), None, 0.1, 5, 9)
+        close(od.float(), _back(ref), rtol=2e-2, what=f"out (sign {sign})")
+        close(lse.view(B, H, Lq), rlse, rtol=1e-4, atol=1e-3, what=f"lse (sign {sign})")
+
+
+def test_attn7_fully_masked_rows_give_nan_like_softmax():
+    """A batch whose keys are all padding: softmax over all -inf is NaN in the reference (torch), and so is every
+    output and LSE of that batch here; the other batch is unaffected."""
+    B, H, Lq, Lk = 2, 2, 96, 140
+    D = H * 64
+    gen = torch.Generator().manual_seed(3)
+    q, k, v = (torch.randn(B, L, D, generator=gen) for L in (Lq, Lk, Lk))
+    keep = torch.ones(B, Lk, dtype=torch.bool)
+    keep[1] = False
+    od, lse, _ = _run(B, H, Lq, Lk, keep, 0.1, q, k, v)
+    o = od.float().view(B, Lq, D)
+    assert torch.isnan(o[1]).all() and torch.isnan(lse.view(B, H, Lq)[1]).all()
+    ref, _ = _ref(_heads(q, B, H), _heads(k, B, H), _heads(v, B, H), keep, 0.1, 5, 9)
+    close(o[0], _back(ref)[: Lq].view(Lq, D), rtol=2e-2, what="unmasked batch")
+
+
+@pytest.mark.parametrize("B,H,Lq,Lk,masked,p", [SHAPES[0], SHAPES[2], SHAPES[5]])
+def test_attn7_agrees_with_round4_kernel(B, H, Lq, Lk, masked, p):
+    """The 32x32x16 forward and the round-4 16x16x32 forward (fwd6, keep words read the same way) on the same
+    inputs: both bf16 roundings of one float64 result, so within twice the per-kernel tolerance of each other."""
+    D = H * 64
+    gen = torch.Generator().manual_seed(99)
+    q, k, v = (torch.randn(B, L, D, generator=gen) for L in (Lq, Lk, Lk))
+    keep = None
+    if masked:
+        keep = torch.ones(B, Lk, dtype=torch.bool)
+        keep[0, Lk - 30:] = False
+    o7, l7, _ = _run(B, H, Lq, Lk, keep, p, q, k, v, family="auto")
+    o6, l6, _ = _run(B, H, Lq, Lk, keep, p, q, k, v, family="v6")
+    close(o7.float(), o6.float(), rtol=2e-2, what="fwd7 vs fwd6")
+    close(l7, l6, rtol=0, atol=1e-3, what="lse fwd7 vs fwd6")

@@ -47,13 +47,15 @@ def test_decoder_fp32_matches_reference_fixture():
         close(l2, g["logits_defmask"], rtol=1e-4, what="decoder default mask")
 
 
-@pytest.mark.parametrize("prec,tol,H", [("fp32", 1e-4, 2), ("bf16", 3e-2, 2), ("fp32", 1e-4, 4), ("bf16", 3e-2, 4),
-                                        ("fp32", 1e-4, 8)])
-def test_decoder_dropout_matches_oracle(prec, tol, H, monkeypatch):
+@pytest.mark.parametrize("prec,tol,H,d", [("fp32", 1e-4, 2, 128), ("bf16", 3e-2, 2, 128), ("fp32", 1e-4, 4, 128),
+                                          ("bf16", 3e-2, 4, 128), ("fp32", 1e-4, 8, 128), ("bf16", 3e-2, 4, 200)])
+def test_decoder_dropout_matches_oracle(prec, tol, H, d, monkeypatch):
     """Dropout 0.1 everywhere: masks follow the shared RNG contract, so GPU == oracle. H = 4 / 8 are head_dim
-    32 / 16 (C1's d_model 128 with 4 heads): the kernels run them on zero-padded 64-wide head slots."""
+    32 / 16 (C1's d_model 128 with 4 heads): the kernels run them on zero-padded 64-wide head slots. d = 200
+    (d % 16 == 8, head_dim 50): the bf16 LN3 -> next block RoPE hand-off is not taken (the fused kernel needs d % 16
+    == 0), the blocks run their own rope_fwd."""
     rt = _rt()
-    V, d, NL, FF, B, L, S = 304, 128, 2, 256, 2, 24, 30
+    V, NL, FF, B, L, S = 304, 2, 256, 2, 24, 30
     gen = torch.Generator().manual_seed(3)
     xt = torch.randint(1, V, (B, L), generator=gen)
     xt[1, 20:] = 0
