@@ -528,11 +528,14 @@ def main():
     torch.cuda.synchronize()
     tail_ev, T_.ALLREDUCE_TAIL = T_.ALLREDUCE_TAIL, None
     el = time.perf_counter() - t0
+    rank_ms = [1000.0 * el / args.steps]
     if world > 1:
         dist.barrier()
-        tt = torch.tensor([el], device=device)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        el = float(tt.item())
+        tt = torch.zeros(world, device=device)
+        tt[rank] = el
+        dist.all_reduce(tt, op=dist.ReduceOp.SUM)      # every rank's own time (the line reports min / max)
+        rank_ms = [1000.0 * float(x) / args.steps for x in tt.tolist()]
+        el = max(float(x) for x in tt.tolist())
     # decoder attention launches: HIP events on one extra, untimed step (an event pair around every attention
     # launch inside the timed steps would add its own stream gaps to ms_per_step)
     # the same step with the encoder not overlapped (FDDM_NO_ENC_PIPELINE) also times the dominant launch alone
@@ -553,7 +556,8 @@ def main():
         kms = sum(a.elapsed_time(b) for a, b in ev) / max(1, len(ev))
         kflops = dominant_flops(args)
         ncu = torch.cuda.get_device_properties(device).multi_processor_count
-        conv_cus = int(os.environ.get("FDDM_ENC_CUS_CONV", ncu // 2))
+        caps = T_.cu_caps(device)
+        conv_cus = caps["conv"]
         traffic, traffic_src = pmc_traffic(args)
         peak = BF16_PEAK_TFLOPS if args.precision == "bf16" else F32_PEAK_TFLOPS
         achieved = kflops / (kms * 1e-3) / 1e12
@@ -593,6 +597,10 @@ def main():
             "avg_loss": round(avg_loss, 4),
             "cpu_baseline": cpu,
         }
+        out["cu_caps"] = caps        # persistent encoder GEMM caps beside the decoder; coll = reserve under DP
+        if world > 1:
+            out["rank_ms_per_step"] = {"min": round(min(rank_ms), 3), "max": round(max(rank_ms), 3),
+                                       "per_rank": [round(x, 3) for x in rank_ms]}
         if tail_ev:
             # the part of the gradient all-reduce that outlasts the backward (DESIGN §5's overlap), per step
             tl = [a.elapsed_time(b) for a, b in tail_ev]

@@ -164,8 +164,6 @@ __device__ unsigned long long attn_stamps[8192 * 16];
 // rows repeat each other's draws (shifted) only if all three offset differences coincide (2^-20 per pair). The
 // forward kernel holds the three tables in LDS (24 KB, built once per workgroup): 3 ds_read_b64 + 2 64-bit XORs
 // per 4 keys, instead of a 64-bit splitmix64 hash per 4 keys.
-constexpr int ATTN_R = 4096;
-constexpr uint64_t ATTN_TAB0 = 1ull << 62, ATTN_OFF0 = 3ull << 62;
 __device__ __forceinline__ uint64_t attn_offsets(const AttnArgs& a, int bh, int q) {
   return mix64(eff_seed(a.seed, a.seed_off), a.stream, ATTN_OFF0 + (uint64_t)bh * a.Lq + q);
 }
@@ -2391,7 +2389,14 @@ static int run(int which, AttnArgs& a, hipStream_t s) {
       if (a.Lk <= 1024) {
         const int ntiles = LkP / 64, qw = 128;
         const int dm = !drop ? 0 : (a.bits_ready && a.dbits) ? 1 : 2;
-        if (dm != 2 && attn7_enabled()) return attn7_fwd(a, s);
+        if (attn7_enabled() && (dm != 2 || a.dbits)) {
+          if (dm == 2) {  // the caller's buffer gets this site's keep masks (layout v3) first; fwd7 reads them
+            const int e = attn7_drop_bits(a.dbits, 0, 1, a.B * a.H, a.Lq, a.Lk, a.seed, a.stream, 0, a.thr16,
+                                          a.seed_off, s);
+            if (e) return e;
+          }
+          return attn7_fwd(a, s);
+        }
         const size_t lds = (size_t)2 * 2 * 64 * 128 + (size_t)LkP * 4 +
                            (dm == 1 ? (size_t)ntiles * qw * 8 : dm == 2 ? (size_t)3 * ATTN_R * 2 : 0);
         dim3 g6((a.Lq + qw - 1) / qw, a.B * a.H);
@@ -2538,13 +2543,23 @@ FDDM_API int fddm_attn_fwd(int dtype, const void* Q, long sq, const void* K, lon
   return attn_dispatch(0, dtype, a, drop_p, hs);
 }
 
+// u64 words per site of the keep-bit buffer: room for either storage layout (the round-4 words [B*H][ntiles][Lq] or
+// layout v3's lane masks, attn7.hip); fddm_attn_drop_bits writes the one the selected kernel family reads
+FDDM_API long fddm_attn_drop_words(int B, int H, int Lq, int Lk) {
+  const long v2 = (long)B * H * Lq * ((Lk + 63) / 64), v3 = attn7_drop_words(B, H, Lq, Lk);
+  return v2 > v3 ? v2 : v3;
+}
+
 // Dropout keep bits of nsites attention sites with the same shape, rng streams stream0 + s * stream_step (site s at
 // out + s * site_words): the words fddm_attn_fwd(..., drop_bits_ready = 1) and fddm_attn_bwd read.
 FDDM_API int fddm_attn_drop_bits(unsigned long long* out, long site_words, int nsites, int B, int H, int Lq, int Lk,
                                  float drop_p, unsigned long long seed, unsigned long long stream0,
                                  unsigned long long stream_step, void* hs) {
   if (B <= 0 || H <= 0 || Lq <= 0 || Lk <= 0 || nsites <= 0) return 0;
-  if (!out || drop_p <= 0.f || site_words < (long)B * H * Lq * ((Lk + 63) / 64)) return (int)hipErrorInvalidValue;
+  if (!out || drop_p <= 0.f || site_words < fddm_attn_drop_words(B, H, Lq, Lk)) return (int)hipErrorInvalidValue;
+  if (attn7_enabled())  // storage layout v3 (lane masks) for the 32x32x16 kernels
+    return attn7_drop_bits((uint64_t*)out, site_words, nsites, B * H, Lq, Lk, seed, stream0, stream_step,
+                           (unsigned)llrintf(drop_p * 65536.f), g_seed_off, (hipStream_t)hs);
   DbArgs d{(uint64_t*)out, site_words, B * H, Lq, Lk, seed, stream0, stream_step, (unsigned)llrintf(drop_p * 65536.f),
            g_seed_off};
   hipLaunchKernelGGL(dbits_kernel, dim3(B * H, nsites), dim3(256), 0, (hipStream_t)hs, d);
@@ -2579,7 +2594,7 @@ FDDM_API int fddm_attn_bwd(int dtype, const void* Q, long sq, const void* K, lon
   a.sq = sq; a.sk = sk; a.sv = sv; a.so = so; a.sdo = sdo; a.sdq = sdq; a.sdk = sdk; a.sdv = sdv;
   a.key_keep = key_keep;
   a.B = B; a.H = H; a.Lq = Lq; a.Lk = Lk; a.scale = scale; a.seed = seed; a.stream = stream; a.seed_off = g_seed_off;
-  // bf16 with recorded or no dropout, Lk <= 1024: the 32x32x16 kernels (attn7.hip; delta_ws holds 2 * B*H*LqP)
+  // bf16 with recorded or no dropout, Lk <= 1024: the 32x32x16 kernels (attn7.hip; delta_ws holds 34 * B*H*LqP)
   if (dtype == FDDM_BF16 && attn7_enabled() && Lk <= 1024 && (drop_p <= 0.f || drop_bits))
     return attn_dispatch(4, dtype, a, drop_p, hs);
   // self-attention shapes (Lq == Lk <= 256, bf16, no rehashed dropout): dQ, dK and dV in one fused launch

@@ -31,6 +31,15 @@ namespace attn {
 
 typedef __attribute__((ext_vector_type(16))) float f32x16_t;
 
+// compile-time loop: f(integral_constant<int, I>) for I in [B, E)
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
 __device__ __forceinline__ f32x16_t mfma32(const uint4& a, const uint4& b, const f32x16_t& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
                                                  0, 0, 0);
@@ -68,18 +77,140 @@ __device__ __forceinline__ s16x4_t tr_read(const unsigned char* p) {
 
 constexpr int A7_TB = 64 * 128;  // one K or V tile in LDS: 64 rows x 128 B
 
+// ------------------------------------------------------------------ dropout keep bits, storage layout v3 (lane masks)
+// The keep decisions of RNG contract v2 (oracle attn_dropout_keep; attention.hip attn_keep4) stored so that one 64-bit
+// word is the lane mask of one accumulator register of the 32x32x16 score MFMA with the query on the lane: for (b, h),
+// 32-query group qg and 64-key tile t, slot j = 16 kb + r (kb = 32-key half, r = accumulator register), bit l =
+// keep(query 32 qg + (l & 31), key 64 t + 32 kb + 8 (r >> 2) + 4 (l >> 5) + (r & 3)). Word index
+// ((bh * nqg + qg) * ntiles + t) * 32 + j, nqg = ceil(Lq / 32). The forward and dQ kernels load a half-tile's 16
+// words into SGPRs with scalar loads and drop a probability with one v_cndmask (inverse ballot); the dK / dV kernel
+// (key on the lane) reads the one word of its key per 32-query half and extracts bits.
+__device__ __forceinline__ long lm_word(int bh, int nqg, int ntiles, int qg, int t) {
+  return (((long)bh * nqg + qg) * ntiles + t) * 32;
+}
+// The same bits per lane ("v4" part of the site buffer, after the lane masks): for (b, h, qg, t) 64 dwords, dword l =
+// the 32 keep bits of lane l of the query-lane kernels, bit 16 kb + r = the lane's accumulator register r of half kb.
+// The forward and dQ kernels stream one 256-B piece per wave and tile into LDS and test bits (bfe + and): a scalar
+// load of the lane masks per half-tile, waited for right before the select, cost more than the two VALU per score.
+__device__ __forceinline__ long lb_dword(int bh, int nqg, int ntiles, int qg, int t) {
+  return (((long)bh * nqg + qg) * ntiles + t) * 64;
+}
+typedef __attribute__((address_space(4))) const uint64_t* cu64p;
+// v_writelane_b32 through the LLVM intrinsic (this clang has no builtin for it), so the hazard recognizer inserts the
+// wait states a VALU-written SGPR needs before v_writelane reads it (an inline-asm writelane got none: stale ballots)
+__device__ int amdgcn_writelane_i32(int v, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
+// lane L of x := the wave-uniform value v (the ballot of one slot goes to the lane that stores it)
+template <int L>
+__device__ __forceinline__ void writelane(unsigned& x, unsigned v) {
+  x = (unsigned)amdgcn_writelane_i32((int)v, L, (int)x);
+}
+
+struct DmArgs {
+  uint64_t* out;
+  long site_words;  // words per site
+  int BH, Lq, Lk;
+  uint64_t seed, stream0, stream_step;
+  unsigned thr16;
+  const uint64_t* seed_off;
+};
+
+// One workgroup per (b, h, site): the site's three 4096-entry draw tables in LDS (one splitmix64 per 4 entries, as
+// dbits_kernel), then each wave takes 32-query groups; per group and key tile, lane l draws the 4 keys 64 t + 32 kb + 8 m
+// + 4 (l >> 5) + 0..3 of query 32 qg + (l & 31) from one 8-byte entry of each table, and the wave's compare of draw e
+// IS the word of slot 16 kb + 4 m + e (a ballot), gathered into lane j by v_writelane and stored as 256 B.
+__global__ void __launch_bounds__(256) dmask_kernel(DmArgs d) {
+  __shared__ __attribute__((aligned(16))) uint64_t tab[3 * ATTN_R / 4];
+  const int bh = blockIdx.x, site = blockIdx.y, tid = threadIdx.x;
+  const uint64_t stream = d.stream0 + (uint64_t)site * d.stream_step;
+  const uint64_t seed = eff_seed(d.seed, d.seed_off);
+  for (int wi = tid; wi < 3 * ATTN_R / 4; wi += 256) {
+    const int tau = wi / (ATTN_R / 4), jw = wi % (ATTN_R / 4);
+    tab[wi] = mix64(seed, stream, ATTN_TAB0 + ((uint64_t)bh * 3 + tau) * (ATTN_R / 4) + jw);
+  }
+  __syncthreads();
+  const int ntiles = (d.Lk + 63) >> 6, nqg = (d.Lq + 31) >> 5;
+  const int lane = tid & 63, w = tid >> 6, qi = lane & 31, hh = lane >> 5;
+  uint64_t* out = d.out + (long)site * d.site_words;
+  const unsigned char* tb = (const unsigned char*)tab;
+  unsigned* lbits = (unsigned*)(out + (long)d.BH * nqg * ntiles * 32);  // the per-lane dwords after the lane masks
+  for (int qg = w; qg < nqg; qg += 4) {
+    const uint64_t off = mix64(seed, stream, ATTN_OFF0 + (uint64_t)bh * d.Lq + 32 * qg + qi);
+    const unsigned o0 = (unsigned)(off & 0xFFCu), o1 = (unsigned)((off >> 16) & 0xFFCu),
+                   o2 = (unsigned)((off >> 32) & 0xFFCu);
+    for (int t = 0; t < ntiles; ++t) {
+      unsigned lo = 0, hi = 0, lw = 0;
+      static_for<0, 2>([&](auto kbc) {
+        constexpr int kb = decltype(kbc)::value;
+        static_for<0, 4>([&](auto mc) {
+          constexpr int m = decltype(mc)::value;
+          const unsigned kq = 64 * t + 32 * kb + 8 * m + 4 * hh;
+          const uint64_t wd = *(const uint64_t*)(tb + (((o0 + kq) & (ATTN_R - 1)) << 1)) ^
+                              *(const uint64_t*)(tb + ATTN_R * 2 + (((o1 + kq) & (ATTN_R - 1)) << 1)) ^
+                              *(const uint64_t*)(tb + ATTN_R * 4 + (((o2 + kq) & (ATTN_R - 1)) << 1));
+          static_for<0, 4>([&](auto ec) {
+            constexpr int e = decltype(ec)::value;
+            const bool keep = ((unsigned)(wd >> (16 * e)) & 0xFFFFu) >= d.thr16;
+            const unsigned long long bm = __ballot(keep);
+            writelane<16 * kb + 4 * m + e>(lo, (unsigned)bm);
+            writelane<16 * kb + 4 * m + e>(hi, (unsigned)(bm >> 32));
+            lw |= (keep ? 1u : 0u) << (16 * kb + 4 * m + e);
+          });
+        });
+      });
+      if (lane < 32) out[lm_word(bh, nqg, ntiles, qg, t) + lane] = ((uint64_t)hi << 32) | lo;
+      lbits[lb_dword(bh, nqg, ntiles, qg, t) + lane] = lw;
+    }
+  }
+}
+
+int attn7_drop_bits(uint64_t* out, long site_words, int nsites, int BH, int Lq, int Lk, uint64_t seed,
+                    uint64_t stream0, uint64_t stream_step, unsigned thr16, const uint64_t* seed_off, hipStream_t s) {
+  DmArgs d{out, site_words, BH, Lq, Lk, seed, stream0, stream_step, thr16, seed_off};
+  hipLaunchKernelGGL(dmask_kernel, dim3(BH, nsites), dim3(256), 0, s, d);
+  return (int)hipGetLastError();
+}
+long attn7_drop_words(int B, int H, int Lq, int Lk) {  // lane masks + per-lane dwords
+  return (long)B * H * ((Lq + 31) / 32) * ((Lk + 63) / 64) * 64;
+}
+
+// Images that serve both row reads (ds_read_b128, A = rows) and transposed reads (ds_read_b64_tr_b16, A = columns):
+// chunk c of row r at c ^ dsw(r), dsw(r) = a ^ ((a & 1) << 2) with a = (r >> 1) & 7. A row-read lane group's 16 rows
+// have distinct (r & 1, a), and a transposed read's rows 4j and 4j + 2 land 5 chunks apart (opposite 64-B halves).
+__device__ __forceinline__ int dsw(int r) {
+  const int a = (r >> 1) & 7;
+  return a ^ ((a & 1) << 2);
+}
+// the register-resident operand of the backward's score MFMA (Q in dq7, K in dkv7) pre-scaled by sl2 = scale *
+// log2(e) and rounded to bf16 once, so the product is the exponent in log2 units: 8 bf16 of one 16-B fragment
+__device__ __forceinline__ uint4 scale_frag(const uint4& x, float c) {
+  const u32x4v_t w = __builtin_bit_cast(u32x4v_t, x);
+  u32x4v_t o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    o[j] = pk_bf16(__uint_as_float(w[j] << 16) * c, __uint_as_float(w[j] & 0xFFFF0000u) * c);
+  return __builtin_bit_cast(uint4, o);
+}
+// -x as a bf16 pair (hi, lo) with hi + lo = -x to ~2^-16 relative: the exact-constant fifth k-step of a score MFMA
+__device__ __forceinline__ unsigned neg_split(float x) {
+  const float hi = __uint_as_float(((unsigned)pk_bf16(-x, 0.f)) << 16);
+  return pk_bf16(hi, -x - hi);
+}
+
 // DM: 0 no dropout, 1 keep bits from the words fddm_attn_drop_bits wrote (word (bh, t, q), bit = key - 64 t).
 // MK: 0 no mask, 1 the ragged last tile only (Lk % 64 != 0, no key-padding mask), 2 key-padding mask on every tile.
+#ifndef A7_FWD_WPS
+#define A7_FWD_WPS 3  // waves per SIMD the forward's register allocation targets
+#endif
 template <int DM, int MK>
-__global__ void __launch_bounds__(256, 3) fwd7_kernel(AttnArgs a) {
+__global__ void __launch_bounds__(256, A7_FWD_WPS) fwd7_kernel(AttnArgs a) {
   constexpr bool DROP = DM != 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char sm7[];
   const int ntiles = (a.Lk + 63) >> 6, LkP = ntiles * 64;
-  unsigned char* kst = sm7;                      // [2][64 rows][128 B] K, KC swizzle
-  unsigned char* vst = sm7 + 2 * A7_TB;          // [2][64 rows][128 B] V, vsw swizzle
-  unsigned char* kwl = sm7 + 4 * A7_TB;          // [2][128 queries][8 B] keep words of the tile
-  unsigned* tact = (unsigned*)(kwl + 2048);      // [4] active-tile nibbles per wave (MK 2)
-  float* mfull = (float*)(kwl + 2048 + 16);      // [LkP] 0 / -inf
+  unsigned char* kst = sm7;                             // [2][64 rows][128 B] K, KC swizzle
+  unsigned char* vst = sm7 + 2 * A7_TB;                 // [2][64 rows][128 B] V, vsw swizzle
+  unsigned* kbl = (unsigned*)(sm7 + 4 * A7_TB);         // [2][4 waves][64 lanes] keep bits of the tile (v4 dwords)
+  unsigned* tact = (unsigned*)(sm7 + 4 * A7_TB + 2048);  // [4] active-tile nibbles per wave (MK 2)
+  unsigned* mpk = (unsigned*)(sm7 + 4 * A7_TB + 2064);   // [LkP] bf16 pair (1, mask): the key's fifth-k-step operand
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hh = lane >> 5, qi = lane & 31;
   int bxi, bh;
@@ -93,11 +224,14 @@ __global__ void __launch_bounds__(256, 3) fwd7_kernel(AttnArgs a) {
   const bf16_t* Vb = (const bf16_t*)a.V + (long)b * a.Lk * a.sv + h * DH;
 
   // one tile's stream: wave w brings rows 16 w .. 16 w + 15 of K and V (2 + 2 KB pieces, XOR swizzles applied to the
-  // per-lane source addresses) and the keep words of its own 32 queries (one 256-B piece)
-  // byte offsets from the (b, h) bases: row * stride * 2 < 2^31 for every shape the dispatch admits (Lk <= 1024)
+  // per-lane source addresses); byte offsets from the (b, h) bases (row * stride * 2 < 2^31 for Lk <= 1024)
   const unsigned sk2 = (unsigned)a.sk * 2u, sv2 = (unsigned)a.sv * 2u;
-  const uint64_t* kwb = a.dbits + (long)bh * ntiles * a.Lq;
+  const int nqg = (a.Lq + 31) >> 5, qg = 4 * bxi + w;  // the wave's 32-query group (keep bits)
+  const unsigned* lbits = (const unsigned*)(a.dbits + (long)a.B * a.H * nqg * ntiles * 32);
   auto fill = [&](int tt, int st) {
+#ifdef A7_ABL_NODMA  // timing-only ablation (tools/probe): no K / V stream after the first tile, results wrong
+    if (tt > 0) return;
+#endif
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int R = 16 * w + 8 * u;
@@ -106,33 +240,39 @@ __global__ void __launch_bounds__(256, 3) fwd7_kernel(AttnArgs a) {
       dma16_sv(Kb, rr * sk2 + (unsigned)((pch ^ ((r >> 1) & 7)) << 4), kst + st * A7_TB + R * 128);
       dma16_sv(Vb, rr * sv2 + (unsigned)((pch ^ vsw(r)) << 4), vst + st * A7_TB + R * 128);
     }
-    if constexpr (DM == 1) {
-      const unsigned qq = (unsigned)min(qw0 + (lane >> 1), a.Lq - 1);
-      dma4_sv(kwb, ((unsigned)tt * (unsigned)a.Lq + qq) * 8u + 4u * (lane & 1), kwl + st * 1024 + w * 256);
-    }
+    if constexpr (DROP)
+      dma4_sv(lbits, (unsigned)(lb_dword(bh, nqg, ntiles, min(qg, nqg - 1), tt) + lane) * 4u,
+              (const unsigned char*)(kbl + st * 256 + w * 64));
   };
 
-  // ---- prologue: tile 0's stream, the Q fragments and the key mask in flight together
+  // ---- prologue: tile 0's stream, the Q fragments (pre-scaled by sl2: scores come out in log2 units) and the key
+  // mask in flight together; rows past Lq read row Lq - 1 and are zeroed (never stored)
   fill(0, 0);
+  const float sl2 = a.scale * 1.4426950408889634f;
   uint4 qf[4];
+  {
+    const long qc = min(q, a.Lq - 1);
+    const unsigned zm = qv ? 0xFFFFFFFFu : 0u;
 #pragma unroll
-  for (int ks = 0; ks < 4; ++ks)
-    qf[ks] = qv ? *(const uint4*)(Qb + (long)q * a.sq + 16 * ks + 8 * hh) : make_uint4(0, 0, 0, 0);
+    for (int ks = 0; ks < 4; ++ks) {
+      const uint4 x = *(const uint4*)(Qb + qc * a.sq + 16 * ks + 8 * hh);
+      qf[ks] = scale_frag(make_uint4(x.x & zm, x.y & zm, x.z & zm, x.w & zm), sl2);
+    }
+  }
   unsigned tmask = ntiles >= 32 ? 0xFFFFFFFFu : ((1u << ntiles) - 1u);
   if constexpr (MK != 0) {
     // thread tid owns keys 4 tid .. 4 tid + 3 (LkP <= 1024)
     bool any = false;
     if (4 * tid < LkP) {
-      float4 mv;
-      float* mp = (float*)&mv;
+      unsigned mv[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int k = 4 * tid + j;
         const bool ok = k < a.Lk && (MK == 1 || a.key_keep[(long)b * a.Lk + k] != 0);
-        mp[j] = ok ? 0.f : -INFINITY;
+        mv[j] = pk_bf16(1.f, ok ? 0.f : -INFINITY);
         any |= ok;
       }
-      *(float4*)(mfull + 4 * tid) = mv;
+      *(uint4*)(mpk + 4 * tid) = make_uint4(mv[0], mv[1], mv[2], mv[3]);
     }
     if constexpr (MK == 2) {
       const unsigned long long bal = __ballot(any);  // lanes 16 j .. 16 j + 15 of wave w: the keys of tile 4 w + j
@@ -161,47 +301,36 @@ __global__ void __launch_bounds__(256, 3) fwd7_kernel(AttnArgs a) {
   for (int db = 0; db < 2; ++db)
     voff[db] = vrow * 128 + (((8 * db + 4 * ((lane >> 4) & 1) + (vi & 3)) ^ ((vrow & 2) << 2)) << 3);
 
-  const float sl2 = a.scale * 1.4426950408889634f;  // p = 2^(s sl2 - m sl2), m in raw score units
-  float m = -INFINITY, l = 0.f;
+  // online softmax in log2 units: m = running maximum (-inf until a finite score), rf = the reference subtracted
+  // inside the score MFMA (bf16-exact, 0 while m = -inf): p = 2^(s sl2 - rf); O and l are kept relative to rf
+  float m = -INFINITY, rf = 0.f, l = 0.f;
   f32x16_t o0 = {}, o1 = {};
   bool first = true;
+  // the query's fifth-k-step operand: (-rf, 1, 0, ...) on the lanes of the first 8 k positions
+  uint4 q5 = hh ? make_uint4(0, 0, 0, 0) : make_uint4(pk_bf16(0.f, 1.f), 0u, 0u, 0u);
 
   // one 64-key tile as two 32-key halves, each an online-softmax step of its own (S, exponentials, PV), so that only
   // one half's 16 scores and 8 packed probabilities are live next to O and Q
-  auto tile = [&](const int t, const int st, auto mc) {
-    constexpr bool MT = decltype(mc)::value;
+  auto tile = [&](const int t, const int st) {
+    const bool mt = MK == 2 || (MK == 1 && t == ntiles - 1);  // this tile's keys carry a mask
     const unsigned char* kimg = kst + st * A7_TB;
     const unsigned char* vimg = vst + st * A7_TB;
-    unsigned kw2[2] = {0u, 0u};
-    if constexpr (DROP) {
-      const uint64_t kw = *(const uint64_t*)(kwl + st * 1024 + (32 * w + qi) * 8);
-      kw2[0] = (unsigned)(kw >> (4 * hh));
-      kw2[1] = (unsigned)(kw >> (32 + 4 * hh));
-    }
+    unsigned kw = 0xFFFFFFFFu;
+    if constexpr (DROP) kw = kbl[st * 256 + w * 64 + lane];
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
-      f32x16_t sc;
-      // S^T of the half (the mask row as the accumulator's initial value); recomputed on the rare slow path instead
-      // of keeping the raw scores live across the exponentials
-      auto scores = [&]() {
-        if constexpr (MT) {
-          const f32x4_t* m4 = (const f32x4_t*)(mfull + 64 * t + 32 * kb + 4 * hh);  // keys 8 j + 4 hh .. + 3
-          sc = __builtin_shufflevector(__builtin_shufflevector(m4[0], m4[2], 0, 1, 2, 3, 4, 5, 6, 7),
-                                       __builtin_shufflevector(m4[4], m4[6], 0, 1, 2, 3, 4, 5, 6, 7), 0, 1, 2, 3, 4,
-                                       5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
-        } else {
-          sc = f32x16_t{};
-        }
+      // S''^T = K Q'^T + (1, mask) . (-rf, 1): the key's operand (1, mask) on the lanes of the first 8 k positions
+      unsigned mk = pk_bf16(1.f, 0.f);
+      if (MK != 0 && mt) mk = mpk[64 * t + 32 * kb + qi];
+      const uint4 k5 = hh ? make_uint4(0, 0, 0, 0) : make_uint4(mk, 0u, 0u, 0u);
+      f32x16_t sc = mfma32(k5, q5, f32x16_t{});
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks) sc = mfma32(*(const uint4*)(kimg + koff[ks] + kb * 32 * 128), qf[ks], sc);
-      };
-      scores();
-      // exponentials against the reference mref, the lane's row sum (before dropout), the keep-bit AND and the bf16
-      // pack into the PV operands bq[s]
+      for (int ks = 0; ks < 4; ++ks) sc = mfma32(*(const uint4*)(kimg + koff[ks] + kb * 32 * 128), qf[ks], sc);
+      // exponentials 2^(sc - d), the lane's row sum (before dropout), the keep-mask select and the bf16 pack into
+      // the PV operands bq[s]
       uint4 bq[2];
       float ls;
-      auto expall = [&](float mref) {
-        const float nb = -mref * sl2;
+      auto expall = [&](float d) {
         float la = 0.f, lb = 0.f;
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
@@ -209,14 +338,13 @@ __global__ void __launch_bounds__(256, 3) fwd7_kernel(AttnArgs a) {
 #pragma unroll
           for (int jj = 0; jj < 4; ++jj) {
             const int r = 8 * s + 2 * jj;
-            float x = __builtin_amdgcn_exp2f(fmaf(sc[r], sl2, nb));
-            float y = __builtin_amdgcn_exp2f(fmaf(sc[r + 1], sl2, nb));
+            float x = __builtin_amdgcn_exp2f(sc[r] - d);
+            float y = __builtin_amdgcn_exp2f(sc[r + 1] - d);
             la += x;
             lb += y;
-            if constexpr (DROP) {
-              const int pos = 8 * (r >> 2) + (r & 3);
-              x = __uint_as_float(__float_as_uint(x) & (unsigned)__builtin_amdgcn_sbfe((int)kw2[kb], pos, 1));
-              y = __uint_as_float(__float_as_uint(y) & (unsigned)__builtin_amdgcn_sbfe((int)kw2[kb], pos + 1, 1));
+            if constexpr (DROP) {  // keep bit 16 kb + r of the lane's dword as an AND mask (v_bfe_i32)
+              x = __uint_as_float(__float_as_uint(x) & (unsigned)__builtin_amdgcn_sbfe((int)kw, 16 * kb + r, 1));
+              y = __uint_as_float(__float_as_uint(y) & (unsigned)__builtin_amdgcn_sbfe((int)kw, 16 * kb + r + 1, 1));
             }
             bw[jj] = pk_bf16(x, y);
           }
@@ -224,29 +352,29 @@ __global__ void __launch_bounds__(256, 3) fwd7_kernel(AttnArgs a) {
         }
         ls = la + lb;
       };
-      // fast path: exponentials against the running reference m; slow path (a query block's first half-tile, or a
-      // lane sum above 2^8 / inf / NaN): the half's maximum from recomputed raw scores, rescale O and l, again
-      bool redo = first;
-      while (true) {
-        if (redo) {
-          float tm = fmaxf(sc[0], sc[1]);
+      // fast path: 2^sc against the current reference; slow path (a query block's first half-tile, or a lane sum
+      // above 2^8 / inf / NaN): the half's maximum, a new bf16 reference, O and l rescaled, 2^(sc - (rf' - rf))
+      bool slow = first;
+      if (!first) {
+        expall(0.f);
+        slow = __any(!(ls <= 256.f));
+      }
+      if (slow) {
+        float tm = fmaxf(sc[0], sc[1]);
 #pragma unroll
-          for (int r = 2; r < 16; r += 2) tm = fmaxf(tm, fmaxf(sc[r], sc[r + 1]));
-          tm = xmax32(tm);
-          const float mn = fmaxf(m, tm);
-          const float alpha = (mn == -INFINITY) ? 1.f : __builtin_amdgcn_exp2f((m - mn) * sl2);
-          l *= alpha;
-          o0 *= alpha;
-          o1 *= alpha;
-          m = mn;
-        }
-        const float mref = m == -INFINITY ? 0.f : m;
-        expall(mref);
-        if (redo) break;
-        m = mref;
-        if (!__any(!(ls <= 256.f))) break;
-        redo = true;
-        scores();
+        for (int r = 2; r < 16; r += 2) tm = fmaxf(tm, fmaxf(sc[r], sc[r + 1]));
+        tm = xmax32(tm) + rf;                       // absolute (log2 units)
+        const float mn = fmaxf(m, tm);
+        float rn = rf;
+        if (mn != -INFINITY) rn = __uint_as_float(((unsigned)pk_bf16(mn, 0.f)) << 16);
+        const float alpha = (m == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(rf - rn);
+        l *= alpha;
+        o0 *= alpha;
+        o1 *= alpha;
+        expall(rn - rf);
+        m = mn;
+        rf = rn;
+        q5 = hh ? make_uint4(0, 0, 0, 0) : make_uint4(pk_bf16(-rf, 1.f), 0u, 0u, 0u);
       }
       l += ls;
       first = false;
@@ -269,10 +397,9 @@ __global__ void __launch_bounds__(256, 3) fwd7_kernel(AttnArgs a) {
     const unsigned rest = t + 1 < 32 ? (tmask & ~((2u << t) - 1u)) : 0u;
     const int tn = rest ? __builtin_ctz(rest) : -1;
     if (tn >= 0) fill(tn, st ^ 1);
-    if (act) {
-      if (MK == 2 || (MK == 1 && t == ntiles - 1)) tile(t, st, std::true_type{});
-      else tile(t, st, std::false_type{});
-    }
+#ifndef A7_ABL_NOCOMPUTE  // timing-only ablation (tools/probe): the stream and barriers without the tile work
+    if (act) tile(t, st);
+#endif
     if (tn < 0) break;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of tile tn landed
     __builtin_amdgcn_s_barrier();                      // every wave's pieces landed; every wave finished tile t
@@ -298,7 +425,7 @@ __global__ void __launch_bounds__(256, 3) fwd7_kernel(AttnArgs a) {
     }
   }
   if (a.lse && hh == 0 && qv)
-    a.lse[(long)bh * a.Lq + q] = (lt > 0.f) ? (m * sl2 + __log2f(lt)) * 0.69314718055994531f : NAN;
+    a.lse[(long)bh * a.Lq + q] = (lt > 0.f) ? (rf + __log2f(lt)) * 0.69314718055994531f : NAN;
   bf16_t* Ob = (bf16_t*)a.Out + (long)b * a.Lq * a.so + h * DH;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -308,35 +435,12 @@ __global__ void __launch_bounds__(256, 3) fwd7_kernel(AttnArgs a) {
   }
 }
 
-// ---------------------------------------------------------------------------------------------- backward
-// Images that serve both row reads (ds_read_b128, A = rows) and transposed reads (ds_read_b64_tr_b16, A = columns):
-// chunk c of row r at c ^ dsw(r), dsw(r) = a ^ ((a & 1) << 2) with a = (r >> 1) & 7. A row-read lane group's 16 rows
-// have distinct (r & 1, a), and a transposed read's rows 4j and 4j + 2 land 5 chunks apart (opposite 64-B halves).
-__device__ __forceinline__ int dsw(int r) {
-  const int a = (r >> 1) & 7;
-  return a ^ ((a & 1) << 2);
-}
-// the register-resident operand of the backward's score MFMA (Q in dq7, K in dkv7) pre-scaled by sl2 = scale *
-// log2(e) and rounded to bf16 once, so the product is the exponent in log2 units: 8 bf16 of one 16-B fragment
-__device__ __forceinline__ uint4 scale_frag(const uint4& x, float c) {
-  const u32x4v_t w = __builtin_bit_cast(u32x4v_t, x);
-  u32x4v_t o;
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-    o[j] = pk_bf16(__uint_as_float(w[j] << 16) * c, __uint_as_float(w[j] & 0xFFFF0000u) * c);
-  return __builtin_bit_cast(uint4, o);
-}
-// -x as a bf16 pair (hi, lo) with hi + lo = -x to ~2^-16 relative: the exact-constant fifth k-step of a score MFMA
-__device__ __forceinline__ unsigned neg_split(float x) {
-  const float hi = __uint_as_float(((unsigned)pk_bf16(-x, 0.f)) << 16);
-  return pk_bf16(hi, -x - hi);
-}
-
 // dQ, query-owned (4 waves x 32 queries per workgroup, K / V tiles of 64 keys streamed through a 2-stage LDS-DMA
 // ring). Per 32-key half: S''^T = K Q'^T over 4 k-steps plus a fifth k-step that adds -LSE (log2 units, hi + lo bf16)
 // and the key mask, so p = exp2(S'') is one instruction; dP^T = V dO^T; dS = p (keep dscale dP - delta);
 // dQ^T += K^T dS^T (K^T by transposed reads of the same K image). Also writes the backward's per-query row terms for
-// dkv7: nlse2 = -LSE log2(e) (-inf past Lq) and delta = rowsum(dO O) (0 past Lq), both [B*H][LqP].
+// dkv7: nlse2 = -LSE log2(e) (-inf past Lq) and delta = rowsum(dO O) (0 past Lq), both [B*H][LqP], then the
+// pre-scaled Q' = bf16(Q scale log2(e)) (0 past Lq) as [B*H][LqP][64] bf16.
 template <int DM, int MK>
 __global__ void __launch_bounds__(256, 3) dq7_kernel(AttnArgs a) {
   constexpr bool DROP = DM != 0;
@@ -344,9 +448,9 @@ __global__ void __launch_bounds__(256, 3) dq7_kernel(AttnArgs a) {
   const int ntiles = (a.Lk + 63) >> 6, LkP = ntiles * 64, LqP = (a.Lq + 63) & ~63;
   unsigned char* kst = smq7;                      // [2][64 rows][128 B] K, dsw swizzle (row + transposed reads)
   unsigned char* vst = smq7 + 2 * A7_TB;          // [2][64 rows][128 B] V, KC swizzle (row reads)
-  unsigned char* kwl = smq7 + 4 * A7_TB;          // [2][128 queries][8 B] keep words of the tile
-  unsigned* tact = (unsigned*)(kwl + 2048);       // [4] active-tile nibbles per wave (MK 2)
-  unsigned* mpk = (unsigned*)(kwl + 2048 + 16);   // [LkP] bf16 pair (mask, 0): the key's fifth-k-step operand
+  unsigned* kbl = (unsigned*)(smq7 + 4 * A7_TB);         // [2][4 waves][64 lanes] keep bits of the tile (v4 dwords)
+  unsigned* tact = (unsigned*)(smq7 + 4 * A7_TB + 2048);  // [4] active-tile nibbles per wave (MK 2)
+  unsigned* mpk = (unsigned*)(smq7 + 4 * A7_TB + 2064);   // [LkP] bf16 pair (mask, 0): the key's fifth-k-step operand
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hh = lane >> 5, qi = lane & 31;
   int bxi, bh;
@@ -361,7 +465,8 @@ __global__ void __launch_bounds__(256, 3) dq7_kernel(AttnArgs a) {
   const bf16_t* Kb = (const bf16_t*)a.K + (long)b * a.Lk * a.sk + h * DH;
   const bf16_t* Vb = (const bf16_t*)a.V + (long)b * a.Lk * a.sv + h * DH;
   const unsigned sk2 = (unsigned)a.sk * 2u, sv2 = (unsigned)a.sv * 2u;
-  const uint64_t* kwb = a.dbits + (long)bh * ntiles * a.Lq;
+  const int nqg = (a.Lq + 31) >> 5, qg = 4 * bxi + w;
+  const unsigned* lbits = (const unsigned*)(a.dbits + (long)a.B * a.H * nqg * ntiles * 32);
   auto fill = [&](int tt, int st) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -371,10 +476,9 @@ __global__ void __launch_bounds__(256, 3) dq7_kernel(AttnArgs a) {
       dma16_sv(Kb, rr * sk2 + (unsigned)((pch ^ dsw(r)) << 4), kst + st * A7_TB + R * 128);
       dma16_sv(Vb, rr * sv2 + (unsigned)((pch ^ ((r >> 1) & 7)) << 4), vst + st * A7_TB + R * 128);
     }
-    if constexpr (DM == 1) {
-      const unsigned qq = (unsigned)min(qw0 + (lane >> 1), a.Lq - 1);
-      dma4_sv(kwb, ((unsigned)tt * (unsigned)a.Lq + qq) * 8u + 4u * (lane & 1), kwl + st * 1024 + w * 256);
-    }
+    if constexpr (DROP)
+      dma4_sv(lbits, (unsigned)(lb_dword(bh, nqg, ntiles, min(qg, nqg - 1), tt) + lane) * 4u,
+              (const unsigned char*)(kbl + st * 256 + w * 64));
   };
 
   // ---- prologue: tile 0's stream; Q (pre-scaled), dO, O fragments; the key mask; delta and the row terms
@@ -464,12 +568,8 @@ __global__ void __launch_bounds__(256, 3) dq7_kernel(AttnArgs a) {
     const bool mt = MK == 2 || (MK == 1 && t == ntiles - 1);  // this tile's keys carry a mask
     const unsigned char* kimg = kst + st * A7_TB;
     const unsigned char* vimg = vst + st * A7_TB;
-    unsigned kw2[2] = {0u, 0u};
-    if constexpr (DROP) {
-      const uint64_t kw = *(const uint64_t*)(kwl + st * 1024 + (32 * w + qi) * 8);
-      kw2[0] = (unsigned)(kw >> (4 * hh));
-      kw2[1] = (unsigned)(kw >> (32 + 4 * hh));
-    }
+    unsigned kw = 0xFFFFFFFFu;
+    if constexpr (DROP) kw = kbl[st * 256 + w * 64 + lane];
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
       // the key's fifth-k-step operand: (1, 1, mask, 0, ...) on the lanes of the first 8 k positions
@@ -491,11 +591,10 @@ __global__ void __launch_bounds__(256, 3) dq7_kernel(AttnArgs a) {
         for (int jj = 0; jj < 4; ++jj) {
           const int r = 8 * s + 2 * jj;
           float d0 = dp[r], d1 = dp[r + 1];
-          if constexpr (DROP) {
-            const int pos = 8 * (r >> 2) + (r & 3);
-            d0 = fmaf(__uint_as_float(__float_as_uint(d0) & (unsigned)__builtin_amdgcn_sbfe((int)kw2[kb], pos, 1)),
+          if constexpr (DROP) {  // keep ? dscale dP - delta : -delta (keep bit 16 kb + r as an AND mask)
+            d0 = fmaf(__uint_as_float(__float_as_uint(d0) & (unsigned)__builtin_amdgcn_sbfe((int)kw, 16 * kb + r, 1)),
                       a.drop_scale, -dl);
-            d1 = fmaf(__uint_as_float(__float_as_uint(d1) & (unsigned)__builtin_amdgcn_sbfe((int)kw2[kb], pos + 1, 1)),
+            d1 = fmaf(__uint_as_float(__float_as_uint(d1) & (unsigned)__builtin_amdgcn_sbfe((int)kw, 16 * kb + r + 1, 1)),
                       a.drop_scale, -dl);
           } else {
             d0 -= dl;
@@ -531,6 +630,11 @@ __global__ void __launch_bounds__(256, 3) dq7_kernel(AttnArgs a) {
     act = true;
   }
 
+  if (q < LqP) {  // the pre-scaled Q dkv7 streams: the same bf16 scores as the forward and this kernel
+    uint4* qs = (uint4*)(a.delta + 2L * a.B * a.H * LqP) + ((long)bh * LqP + q) * 8 + hh;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) qs[2 * ks] = qf[ks];
+  }
   // ---- epilogue: dQ = scale * dQ^T, staged per wave in LDS (K ring, free after the barrier), stored as rows
   __syncthreads();
   unsigned char* ost = kst + w * 4096;
@@ -556,10 +660,12 @@ __global__ void __launch_bounds__(256, 3) dq7_kernel(AttnArgs a) {
 
 // dK / dV, key-owned (4 waves x 32 keys per workgroup, Q / dO tiles of 64 queries streamed through a 2-stage LDS-DMA
 // ring with the tiles' row terms nlse2 / delta from dq7 and the forward's keep words). Per 32-query half:
-// S'' = Q K'^T over 4 k-steps (K' = K pre-scaled by sl2, registers) plus a fifth k-step that adds the row's -LSE
-// (log2 units, hi + lo bf16), p = exp2(S''); dP = dO V^T; dS = p (keep dscale dP - delta); dV^T += dO^T (p keep) and
-// dK^T += Q^T dS with the key on the MFMA lane: the score accumulators are the B operands (no LDS round trip), and the
-// Q / dO images serve both the row reads and the transposed reads. Keys that are padding get zero gradients.
+// S'' = Q' K^T over 4 k-steps (Q' = the pre-scaled Q dq7 wrote, bf16-identical to the forward's and dq7's register
+// operand, so p is the forward's probability; K in registers) plus a fifth k-step that adds the row's -LSE (log2
+// units, hi + lo bf16), p = exp2(S''); dP = dO V^T; dS = p (keep dscale dP - delta); dV^T += dO^T (p keep) and
+// dK^T += Q'^T dS (x ln 2 = scale / sl2 at the end) with the key on the MFMA lane: the score accumulators are the B
+// operands (no LDS round trip), and the Q' / dO images serve both the row reads and the transposed reads. Keys that
+// are padding get zero gradients.
 template <int DM, bool MASK>
 __global__ void __launch_bounds__(256, 2) dkv7_kernel(AttnArgs a) {
   constexpr bool DROP = DM != 0;
@@ -568,7 +674,7 @@ __global__ void __launch_bounds__(256, 2) dkv7_kernel(AttnArgs a) {
   unsigned char* qst = smk7;                      // [2][64 rows][128 B] Q, dsw swizzle
   unsigned char* dost = smk7 + 2 * A7_TB;         // [2][64 rows][128 B] dO, dsw swizzle
   float* rowt = (float*)(smk7 + 4 * A7_TB);       // [2][nlse2 64 | delta 64]
-  unsigned* kwd = (unsigned*)(smk7 + 4 * A7_TB + 1024);  // [2][4 waves][64 queries] keep dwords of the wave's keys
+  unsigned* kwd = (unsigned*)(smk7 + 4 * A7_TB + 1024);  // [2][4 waves][2 query groups][16 words] keep masks
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hh = lane >> 5, qi = lane & 31;
   int bxi, bh;
@@ -577,16 +683,17 @@ __global__ void __launch_bounds__(256, 2) dkv7_kernel(AttnArgs a) {
   const int kw0 = bxi * 128 + 32 * w;
   const int kk = kw0 + qi;
   const bool kv = kk < a.Lk && (!MASK || a.key_keep[(long)b * a.Lk + min(kk, a.Lk - 1)] != 0);
-  const bf16_t* Qb = (const bf16_t*)a.Q + (long)b * a.Lq * a.sq + h * DH;
+  const bf16_t* Qb = (const bf16_t*)(a.delta + 2L * a.B * a.H * LqP) + (long)bh * LqP * DH;  // Q' rows, 128 B
   const bf16_t* dOb = (const bf16_t*)a.dO + (long)b * a.Lq * a.sdo + h * DH;
   const bf16_t* Kb = (const bf16_t*)a.K + (long)b * a.Lk * a.sk + h * DH;
   const bf16_t* Vb = (const bf16_t*)a.V + (long)b * a.Lk * a.sv + h * DH;
   const float* nlse_g = a.delta + (long)a.B * a.H * LqP + (long)bh * LqP;
   const float* dlt_g = a.delta + (long)bh * LqP;
-  const unsigned sq2 = (unsigned)a.sq * 2u, sdo2 = (unsigned)a.sdo * 2u;
-  // the wave's keep dwords: word (bh, t, q) of key tile t = kw0 / 64, half (kw0 / 32) & 1
-  const int tw = kw0 >> 6;
-  const uint64_t* kwb = a.dbits + ((long)bh * ntiles + min(tw, ntiles - 1)) * a.Lq;
+  const unsigned sq2 = (unsigned)DH * 2u, sdo2 = (unsigned)a.sdo * 2u;
+  // the keep masks (layout v3) of the wave's 32 keys: slots 16 kbw .. 16 kbw + 15 of key tile tw, for both 32-query
+  // groups of a 64-query tile (one 256-B piece per wave and tile); the lane's word is slot rpk of its key
+  const int nqg = (a.Lq + 31) >> 5, tw = min(kw0 >> 6, ntiles - 1), kbw = (kw0 >> 5) & 1;
+  const int kt = kk & 63, rpk = 4 * ((kt >> 3) & 3) + (kt & 3), ksh = 4 * hh + 32 * ((kt >> 2) & 1);
   auto fill = [&](int uu, int st) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -599,19 +706,19 @@ __global__ void __launch_bounds__(256, 2) dkv7_kernel(AttnArgs a) {
     if (w == 0) dma4_sv(nlse_g, (unsigned)(64 * uu + lane) * 4u, (const unsigned char*)(rowt + st * 128));
     if (w == 1) dma4_sv(dlt_g, (unsigned)(64 * uu + lane) * 4u, (const unsigned char*)(rowt + st * 128 + 64));
     if constexpr (DROP) {
-      const unsigned qq = (unsigned)min(64 * uu + lane, a.Lq - 1);
-      dma4_sv(kwb, qq * 8u + 4u * ((kw0 >> 5) & 1), (const unsigned char*)(kwd + st * 256 + w * 64));
+      const int qgl = min(2 * uu + (lane >> 5), nqg - 1);
+      dma4_sv(a.dbits, (unsigned)((lm_word(bh, nqg, ntiles, qgl, tw) + 16 * kbw) * 8 + (lane & 31) * 4),
+              (const unsigned char*)(kwd + st * 256 + w * 64));
     }
   };
 
   fill(0, 0);
-  const float sl2 = a.scale * 1.4426950408889634f;
   const int kc = min(kk, a.Lk - 1);
   uint4 kf[4], vf[4];
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
     const long c = 16 * ks + 8 * hh;
-    kf[ks] = scale_frag(*(const uint4*)(Kb + (long)kc * a.sk + c), sl2);
+    kf[ks] = *(const uint4*)(Kb + (long)kc * a.sk + c);
     vf[ks] = *(const uint4*)(Vb + (long)kc * a.sv + c);
   }
   // the key's fifth-k-step operand (1, 1, 0, ...) on the lanes of the first 8 k positions
@@ -648,6 +755,9 @@ __global__ void __launch_bounds__(256, 2) dkv7_kernel(AttnArgs a) {
     const unsigned* kd = kwd + st * 256 + w * 64;
 #pragma unroll
     for (int qb = 0; qb < 2; ++qb) {
+      // register r of this half is query 32 qb + 8 (r >> 2) + 4 hh + (r & 3): bit 8 (r >> 2) + (r & 3) of kbits
+      unsigned kbits = 0xFFFFFFFFu;
+      if constexpr (DROP) kbits = (unsigned)(*(const uint64_t*)(kd + 32 * qb + 2 * rpk) >> ksh);
       // the query row's fifth-k-step operand (-LSE log2(e) as hi + lo bf16) on the lanes of the first 8 k positions
       const float x = nl[32 * qb + qi];
       const float xh = __uint_as_float(((unsigned)pk_bf16(x, 0.f)) << 16);
@@ -669,15 +779,13 @@ __global__ void __launch_bounds__(256, 2) dkv7_kernel(AttnArgs a) {
           // registers r = 8 s + 4 mh .. + 3: queries 32 qb + 8 (2 s + mh) + 4 hh + 0 .. 3
           const int r0 = 8 * s + 4 * mh, qr = 32 * qb + 8 * (2 * s + mh) + 4 * hh;
           const f32x4_t d4 = *(const f32x4_t*)(dl + qr);
-          u32x4v_t k4 = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
-          if constexpr (DROP) k4 = *(const u32x4v_t*)(kd + qr);
           float pv[4], dv[4];
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const float pr = __builtin_amdgcn_exp2f(sc[r0 + e]);
             float dd = dp[r0 + e];
             if constexpr (DROP) {
-              const unsigned m = (unsigned)__builtin_amdgcn_sbfe((int)k4[e], qi, 1);
+              const unsigned m = (unsigned)__builtin_amdgcn_sbfe((int)kbits, 8 * (2 * s + mh) + e, 1);
               pv[e] = __uint_as_float(__float_as_uint(pr) & m);
               dd = fmaf(__uint_as_float(__float_as_uint(dd) & m), a.drop_scale, -d4[e]);
             } else {
@@ -720,10 +828,11 @@ __global__ void __launch_bounds__(256, 2) dkv7_kernel(AttnArgs a) {
     }
   }
 
-  // ---- epilogue: dV = dscale dV^T, dK = scale dK^T (zero for padding keys), staged per wave in LDS, stored as rows
+  // ---- epilogue: dV = dscale dV^T, dK = scale dK^T = ln 2 (Q'^T dS) (zero for padding keys), staged per wave in
+  // LDS, stored as rows
   __syncthreads();
   unsigned char* ost = qst + w * 4096;
-  const float fv = kv ? (DROP ? a.drop_scale : 1.f) : 0.f, fk = kv ? a.scale : 0.f;
+  const float fv = kv ? (DROP ? a.drop_scale : 1.f) : 0.f, fk = kv ? 0.6931471805599453f : 0.f;
 #pragma unroll
   for (int which = 0; which < 2; ++which) {
     const float f = which ? fk : fv;
@@ -753,7 +862,7 @@ int attn7_fwd(AttnArgs& a, hipStream_t s) {
   const int dm = a.thr16 == 0 ? 0 : 1;
   const int mk = a.key_keep != nullptr ? 2 : (a.Lk % 64) != 0 ? 1 : 0;
   const int ntiles = (a.Lk + 63) / 64;
-  const size_t lds = (size_t)4 * A7_TB + 2048 + 16 + (size_t)ntiles * 64 * 4;
+  const size_t lds = (size_t)4 * A7_TB + 2064 + (size_t)ntiles * 64 * 4;
   dim3 grid((a.Lq + 127) / 128, a.B * a.H);
 #define FWD7(D, M) hipLaunchKernelGGL((fwd7_kernel<D, M>), grid, dim3(256), lds, s, a)
   if (dm) { if (mk == 2) FWD7(1, 2); else if (mk == 1) FWD7(1, 1); else FWD7(1, 0); }
@@ -766,7 +875,7 @@ int attn7_dq(AttnArgs& a, hipStream_t s) {
   const int dm = a.thr16 == 0 ? 0 : 1;
   const int mk = a.key_keep != nullptr ? 2 : (a.Lk % 64) != 0 ? 1 : 0;
   const int ntiles = (a.Lk + 63) / 64;
-  const size_t lds = (size_t)4 * A7_TB + 2048 + 16 + (size_t)ntiles * 64 * 4;
+  const size_t lds = (size_t)4 * A7_TB + 2064 + (size_t)ntiles * 64 * 4;
   dim3 grid((a.Lq + 127) / 128, a.B * a.H);
 #define DQ7(D, M) hipLaunchKernelGGL((dq7_kernel<D, M>), grid, dim3(256), lds, s, a)
   if (dm) { if (mk == 2) DQ7(1, 2); else if (mk == 1) DQ7(1, 1); else DQ7(1, 0); }

@@ -4,6 +4,8 @@
 #pragma once
 #include "common.h"
 
+FDDM_API long fddm_attn_drop_words(int B, int H, int Lq, int Lk);
+
 namespace fddm {
 namespace attn {
 
@@ -52,6 +54,11 @@ __device__ __forceinline__ unsigned xor32(unsigned x) {
   return r[0] | r[1];
 }
 
+// Attention-probability dropout, RNG contract v2 (oracle/fddm_oracle.py attn_dropout_keep): per (b, h) three tables of
+// R = 4096 16-bit draws from splitmix64 at TAB0 + ..., per query row three offsets from splitmix64 at OFF0 + ...
+constexpr int ATTN_R = 4096;
+constexpr uint64_t ATTN_TAB0 = 1ull << 62, ATTN_OFF0 = 3ull << 62;
+
 struct AttnArgs {
   const void *Q, *K, *V, *O, *dO;
   void *Out, *dQ, *dK, *dV;
@@ -95,9 +102,14 @@ __device__ __forceinline__ void pin16(uint4& x) {
 // csrc/attn7.hip: the 32x32x16-MFMA decoder forward (bf16, head_dim 64, Lk <= 1024, no dropout or keep bits already
 // written by fddm_attn_drop_bits)
 int attn7_fwd(AttnArgs& a, hipStream_t s);
-// the backward pair: dq7 (dQ; writes delta and -LSE log2(e) as [2][B*H][LqP] into a.delta) and dkv7 (dK, dV)
+// the backward pair: dq7 (dQ; writes delta and -LSE log2(e) as [2][B*H][LqP] and the pre-scaled Q as
+// [B*H][LqP][64] bf16 into a.delta) and dkv7 (dK, dV)
 int attn7_dq(AttnArgs& a, hipStream_t s);
 int attn7_dkv(AttnArgs& a, hipStream_t s);
+// the keep-bit producer of storage layout v3 (lane masks) and its words per site
+int attn7_drop_bits(uint64_t* out, long site_words, int nsites, int BH, int Lq, int Lk, uint64_t seed,
+                    uint64_t stream0, uint64_t stream_step, unsigned thr16, const uint64_t* seed_off, hipStream_t s);
+long attn7_drop_words(int B, int H, int Lq, int Lk);
 
 }  // namespace attn
 }  // namespace fddm

@@ -51,9 +51,9 @@ def parse_header(path: str | None = None) -> dict:
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     src = re.sub(r"//[^\n]*", "", src)
     decls = {}
-    for m in re.finditer(r"(const\s+char\s*\*|int)\s+(fddm_\w+)\s*\(([^)]*)\)\s*;", src):
+    for m in re.finditer(r"(const\s+char\s*\*|int|long)\s+(fddm_\w+)\s*\(([^)]*)\)\s*;", src):
         ret, name, args = m.group(1), m.group(2), m.group(3).strip()
-        restype = ctypes.c_char_p if "char" in ret else ctypes.c_int
+        restype = ctypes.c_char_p if "char" in ret else ctypes.c_long if ret == "long" else ctypes.c_int
         argtypes = []
         if args and args != "void":
             for a in args.split(","):

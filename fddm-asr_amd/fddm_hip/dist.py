@@ -22,8 +22,9 @@ class OverlapReducer:
     async all-reduce of that slice. RCCL orders the collective after the kernels already on the compute
     stream and runs it on its own stream, so it proceeds under the remaining blocks' backward. `finish()`
     (from allreduce_grads, after backward) launches the tail, makes the compute stream wait for every slice
-    and averages. All ranks run the same backward sequence, so they issue identical collectives in the same
-    order."""
+    and averages. Slices are cut at fixed multiples of the bucket (not at the prefix's growth points), so the
+    collective sequence is the same on every rank whatever grouping the ranks' grads_ready calls came in
+    (tests/test_cpu_dist.py::test_overlap_reducer_gloo_world2 records and compares it)."""
 
     def __init__(self, arena, bucket_bytes: int = OVERLAP_BUCKET_BYTES):
         self.arena = arena
@@ -48,8 +49,8 @@ class OverlapReducer:
         while self.next < len(self.ready) and self.ready[self.next]:
             self.next += 1
         hi = a.offs[self.next]
-        if hi - self.launched >= self.bucket:
-            self._launch(hi)
+        while hi - self.launched >= self.bucket:      # fixed bucket-sized slices: the cut points do not depend
+            self._launch(self.launched + self.bucket)  # on how each rank grouped its grads_ready calls
 
     def _launch(self, hi):
         lo = self.launched

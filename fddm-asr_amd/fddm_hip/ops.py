@@ -246,9 +246,16 @@ def wavlm_gate(x2d, W, bias, cst, B, S, H):
 
 
 # ------------------------------------------------------------------------------------- attention
+def drop_words(B, H, Lq, Lk):
+    """u64 words per site of a keep-bit buffer (fddm_attn_drop_words: room for either storage layout)."""
+    from ._lib import lib
+    return int(lib().fddm_attn_drop_words(B, H, Lq, Lk))
+
+
 def drop_bits(B, H, Lq, Lk, device):
-    """Buffer for the forward's dropout keep bits ([B*H][ceil(Lk/64)][Lq] u64), read by the backward."""
-    return torch.empty(B * H * Lq * ((Lk + 63) // 64), device=device, dtype=torch.int64)
+    """Buffer for one attention site's dropout keep bits (written by attn_drop_bits or by the forward, read by the
+    backward; the layout is the selected kernel family's: csrc/attn7.hip layout v3 by default)."""
+    return torch.empty(drop_words(B, H, Lq, Lk), device=device, dtype=torch.int64)
 
 
 def _heads(x, rows, H, dh):
@@ -332,7 +339,7 @@ def attn_bwd(q, k, v, o, do, lse, dq, dk, dv, B, H, Lq, Lk, *, key_keep=None, dr
         return
     # row-term workspace: delta = rowsum(dO O) and -LSE log2(e) per query, [2][B*H][Lq rounded up to 64] (the
     # 32x32x16 backward's layout; the other kernels use the first B*H*Lq floats)
-    delta = torch.empty(2 * B * H * ((Lq + 63) // 64 * 64), device=q.device, dtype=torch.float32)
+    delta = torch.empty(34 * B * H * ((Lq + 63) // 64 * 64), device=q.device, dtype=torch.float32)   # + Q' bf16
     call("fddm_attn_bwd", code(q), ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(o),
          o.stride(0), ptr(do), do.stride(0), ptr(lse), ptr(dq), dq.stride(0), ptr(dk), dk.stride(0), ptr(dv),
          dv.stride(0), ptr(delta), ptr(key_keep), B, H, Lq, Lk, float(sc), float(drop_p), seed, rng_stream,

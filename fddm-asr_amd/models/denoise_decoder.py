@@ -21,6 +21,7 @@ import torch.nn.functional as F
 from fddm_hip import functions as FN
 from fddm_hip import runtime as rt
 from fddm_hip.ops import attn_drop_bits as ops_attn_drop_bits
+from fddm_hip.ops import drop_words
 from fddm_hip.ops import linear as ops_linear
 from fddm_hip.ops import rows_mean as ops_rows_mean
 
@@ -206,15 +207,15 @@ class DenoisingTransformerDecoder(nn.Module):
     @torch.no_grad()
     def _drop_bits(self, B, L, S, seed, dev):
         """The attention-probability dropout keep bits of every block's two attention sites (rng streams 6i+1 self,
-        6i+3 cross; RNG contract v2, oracle.attn_dropout_keep), written by two launches ahead of the blocks: the
-        attention forward kernels then read one word per (query, 64-key tile) instead of drawing them, and the
-        backward reads the same words. bf16 training only (the fp32 parity kernels draw their own)."""
+        6i+3 cross; RNG contract v2, oracle.attn_dropout_keep), written by two launches ahead of the blocks in the
+        storage layout the attention kernels read (fddm_attn_drop_words: layout v3, one lane mask per score-MFMA
+        register), so the forward and backward read them instead of drawing them. bf16 training only (the fp32 parity kernels draw their own)."""
         p = self.blocks[0].p if (self.training and len(self.blocks)) else 0.0
         if p <= 0 or rt.compute_dtype() != torch.bfloat16:
             return None
         H, nb = self.nhead, len(self.blocks)
-        ws = B * H * L * ((L + 63) // 64)
-        wc = B * H * L * ((S + 63) // 64)
+        ws = drop_words(B, H, L, L)
+        wc = drop_words(B, H, L, S)
         bs = torch.empty(nb, ws, device=dev, dtype=torch.int64)
         bc = torch.empty(nb, wc, device=dev, dtype=torch.int64)
         ops_attn_drop_bits(bs, nb, B, H, L, L, p, seed, 1, 6)

@@ -102,6 +102,24 @@ def align_speech(z_speech: torch.Tensor, L: int) -> torch.Tensor:
     return torch.cat([z_speech, z_speech[:, -1:, :].repeat(1, L - S, 1)], dim=1)
 
 
+def cu_caps(dev) -> dict:
+    """CU caps of the encoder's persistent GEMMs while they run beside the decoder (_encoded): "enc" for the
+    transformer layers (FDDM_ENC_CUS, default 3/4 of the chip), "conv" / "conv_rest" for conv layer 1 / layers 2-6
+    (FDDM_ENC_CUS_CONV / _CONV2, default half). Under data parallelism (world > 1) every cap is lowered by "coll"
+    (FDDM_COLL_CUS, default 8 = one per XCD): the CUs handed back stay free of persistent workgroups for RCCL's
+    all-reduce kernels, which run on their own stream under the backward (fddm_hip.dist.OverlapReducer) and would
+    otherwise compete for the CUs the decoder leaves between its launches while a persistent GEMM holds its share
+    for its whole launch. Single-GPU runs keep the measured caps (coll 0)."""
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    world = fdist.world()
+    coll = int(os.environ.get("FDDM_COLL_CUS", 8 if world > 1 else 0))
+    enc = int(os.environ.get("FDDM_ENC_CUS", ncu * 3 // 4))
+    conv = int(os.environ.get("FDDM_ENC_CUS_CONV", ncu // 2))
+    conv_rest = int(os.environ.get("FDDM_ENC_CUS_CONV2", conv))
+    low = lambda c: max(8, c - coll)  # noqa: E731
+    return {"enc": low(enc), "conv": low(conv), "conv_rest": low(conv_rest), "coll": coll, "ncu": ncu}
+
+
 def _encoded(encoder, loader, device, optimizer):
     """Yields (c, c_mask, x0) per batch. The encoder is frozen (eval mode, none of its parameters in the
     optimizer; train.py:543), so its output for batch i+1 does not depend on step i: on a GPU it is computed
@@ -127,13 +145,12 @@ def _encoded(encoder, loader, device, optimizer):
     # feature extractor's on half (it runs beside the decoder forward; bench.py C2 step, tools/cap_sweep.sh: conv
     # cap 128 -> 10.85-10.91 ms, 112 / 120 / 136 / 144 / 160 -> 11.0-11.06, 192 (= the rest) 11.02-11.11, 256
     # 11.17, 64 12.4)
-    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-    enc_cus = int(os.environ.get("FDDM_ENC_CUS", ncu * 3 // 4))
-    conv_cus = int(os.environ.get("FDDM_ENC_CUS_CONV", ncu // 2))
+    caps = cu_caps(dev)
+    enc_cus, conv_cus = caps["enc"], caps["conv"]
     bb = getattr(encoder, "backbone", None)
     if bb is not None and hasattr(bb, "stage_rest"):
         bb.conv_cus = conv_cus
-        bb.conv_cus_rest = int(os.environ.get("FDDM_ENC_CUS_CONV2", conv_cus))   # conv layers 2..6
+        bb.conv_cus_rest = caps["conv_rest"]   # conv layers 2..6
     # HIP-graph replay of the encoder forward (fddm_hip.graphs): the host launch path, not the GPU, bounded the step
     graphs = None
     if os.environ.get("FDDM_ENC_GRAPH", "1") != "0" and GraphedEncoder.supported(encoder):

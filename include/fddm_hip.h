@@ -82,10 +82,11 @@ int fddm_wavlm_gate(int dtype, const void* x, const float* W, const float* bias,
 
 /* ---- attention (head_dim 64). Element (b,pos,h,d) at base + (b*L+pos)*stride + h*64 + d.
  *      nn.MultiheadAttention (models/denoise_decoder.py:129-130,164,169-174) with key_padding_mask
- *      (key_keep[b][k] != 0 keeps) and attention-prob dropout (drop_bits, optional: the keep bits as
- *      [B*H][ceil(Lk/64)][Lq] u64 words, bit kk of word (bh, t, q) = keep(q, key 64t + kk); the backward reads them
- *      instead of rehashing); drop_bits_ready != 0: fddm_attn_drop_bits already wrote this site's words (the forward
- *      only reads them), else the forward produces them itself;
+ *      (key_keep[b][k] != 0 keeps) and attention-prob dropout (drop_bits, optional: a buffer of
+ *      fddm_attn_drop_words u64 holding the keep bits — round-4 layout: [B*H][ceil(Lk/64)][Lq] words, bit kk of word
+ *      (bh, t, q) = keep(q, key 64t + kk); layout v3: see fddm_attn_drop_words — the backward reads them instead of
+ *      rehashing); drop_bits_ready != 0: fddm_attn_drop_bits already wrote this site's words (the forward only reads
+ *      them), else the forward produces them itself;
  *      WavLM relative-bias attention
  *      (HF modeling_wavlm.py:152-200) via gate [B*H][Lq] and table [H][2*Lk-1]. lse: [B*H][Lq].
  *      fddm_attn_drop_bits: the keep-bit words of nsites sites of one shape at once (rng streams stream0 +
@@ -98,6 +99,12 @@ int fddm_attn_fwd(int dtype, const void* Q, long sq, const void* K, long sk, con
 int fddm_attn_drop_bits(unsigned long long* out, long site_words, int nsites, int B, int H, int Lq, int Lk,
                         float drop_p, unsigned long long seed, unsigned long long stream0,
                         unsigned long long stream_step, void* hip_stream);
+/* u64 words per site of a keep-bit buffer (room for either storage layout; site_words must be at least this).
+ * fddm_attn_drop_bits writes the layout of the selected kernel family: by default layout v3 of csrc/attn7.hip (one
+ * 64-bit lane mask per score-MFMA accumulator register: word ((bh*ceil(Lq/32) + qg)*ceil(Lk/64) + t)*32 + 16*kb + r,
+ * bit l = keep(query 32*qg + (l&31), key 64*t + 32*kb + 8*(r>>2) + 4*(l>>5) + (r&3))); under
+ * fddm_attn_set_kernels(1) the round-4 words above. The keep decisions are the same (RNG contract v2). */
+long fddm_attn_drop_words(int B, int H, int Lq, int Lk);
 /* WavLM variant (bf16): the gate is computed in the kernel from the 8 gru_rel_pos_linear pre-activations per
  * (token, head) stored at graw + (b*Lq+q)*sgr + h*8 (bf16, appended to the Q|K|V projection's output) and
  * gconst [H] (gru_rel_pos_const) — HF modeling_wavlm.py:177-186. */
@@ -106,8 +113,8 @@ int fddm_attn_fwd_relgate(const void* Q, long sq, const void* K, long sk, const 
                           int Lk, float scale, void* hip_stream);
 /* Backward: dQ, dK, dV. bf16 with recorded or no dropout and Lk <= 1024: the 32x32x16-MFMA pair (a query-owned dQ
  * launch that also writes the per-query row terms delta = rowsum(dO O) and -LSE log2(e) into delta_ws, laid out
- * [2][B*H][LqP] with LqP = Lq rounded up to 64, then a key-owned dK/dV launch that reads them); delta_ws must hold
- * 2 * B*H*LqP floats. Otherwise (fp32, rehashed dropout, longer keys, or fddm_attn_set_kernels(1)): bf16 self-
+ * [2][B*H][LqP] with LqP = Lq rounded up to 64, and Q pre-scaled by scale*log2(e) in bf16 as [B*H][LqP][64] after
+ * them, then a key-owned dK/dV launch that reads them); delta_ws must hold 34 * B*H*LqP floats. Otherwise (fp32, rehashed dropout, longer keys, or fddm_attn_set_kernels(1)): bf16 self-
  * attention shapes Lq == Lk <= 256 as one fused launch, else a dQ launch writing delta_ws [B*H][Lq] and a dK/dV
  * launch. */
 int fddm_attn_bwd(int dtype, const void* Q, long sq, const void* K, long sk, const void* V, long sv, const void* O,

@@ -125,3 +125,38 @@ def jumpy_case_inputs(i, B, L, K):
     boost = torch.from_numpy(r.uniform(-10.0, 6.0, size=(B, L)).astype(np.float32))
     logits.scatter_add_(-1, xt[..., None], boost[..., None])
     return logits, xt
+
+
+class CollectiveLog:
+    """Records every torch.distributed collective issued inside the context (name, shape, dtype, reduce op), in
+    issue order: DP ranks must issue the identical sequence (fddm_hip.dist, train.train_one_epoch)."""
+
+    NAMES = ("all_reduce", "broadcast", "all_gather", "all_gather_into_tensor", "reduce_scatter_tensor",
+             "all_gather_object", "barrier")
+
+    def __init__(self):
+        self.log = []
+        self._orig = {}
+
+    def __enter__(self):
+        import torch.distributed as dist
+        for n in self.NAMES:
+            f = getattr(dist, n, None)
+            if f is None:
+                continue
+            self._orig[n] = f
+
+            def wrap(*a, _n=n, _f=f, **k):
+                t = a[0] if a and hasattr(a[0], "shape") else None
+                op = k.get("op", a[1] if _n == "all_reduce" and len(a) > 1 else None)
+                self.log.append((_n, tuple(t.shape) if t is not None else None, str(t.dtype) if t is not None
+                                 else None, str(op) if op is not None else None))
+                return _f(*a, **k)
+            setattr(dist, n, wrap)
+        return self
+
+    def __exit__(self, *exc):
+        import torch.distributed as dist
+        for n, f in self._orig.items():
+            setattr(dist, n, f)
+        return False

@@ -67,15 +67,19 @@ def _overlap_worker(rank, world, port, q):
         arena = rt.GradArena(params, order)
         red = fdist.OverlapReducer(arena, bucket_bytes=256)   # tiny buckets: slices launch mid-"backward"
         inflight = []
+        from helpers import CollectiveLog
         for step in range(2):
             arena.zero_()
-            for i, p in enumerate(order):
-                g = torch.Generator().manual_seed(1000 * step + 100 * rank + i)
-                p.grad.add_(torch.randn(p.shape, generator=g))
-                rt.grads_ready([p])
-                inflight.append(len(red.works))
-            fdist.allreduce_grads(params, average=(step == 0))     # step 1: the SUM (fused AdamW applies 1/W)
-            q.put((rank, step, [p.grad.numpy().copy() for p in order], max(inflight)))   # by value
+            with CollectiveLog() as cl:
+                for i, p in enumerate(order):
+                    g = torch.Generator().manual_seed(1000 * step + 100 * rank + i)
+                    p.grad.add_(torch.randn(p.shape, generator=g))
+                    if rank == 1 and i % 2 == 0:
+                        continue                   # rank 1 reports some params late (in pairs): same collectives
+                    rt.grads_ready([p] if rank == 0 else order[max(0, i - 1):i + 1])
+                    inflight.append(len(red.works))
+                fdist.allreduce_grads(params, average=(step == 0))     # step 1: the SUM (fused AdamW applies 1/W)
+            q.put((rank, step, [p.grad.numpy().copy() for p in order], max(inflight), cl.log))   # by value
     finally:
         dist.destroy_process_group()
 
@@ -83,18 +87,22 @@ def _overlap_worker(rank, world, port, q):
 def test_overlap_reducer_gloo_world2():
     """Arena laid out in backward order; slices all-reduced asynchronously as soon as a bucket's worth of
     slots is final (fddm_hip.dist.OverlapReducer), the tail at allreduce_grads; two steps (reset between), the
-    second leaving the ranks' sum (average=False, the fused AdamW's grad_scale path)."""
+    second leaving the ranks' sum (average=False, the fused AdamW's grad_scale path). Rank 1 reports its
+    gradients ready in a different grouping (late, in pairs); both ranks still issue the same collectives."""
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = [ctx.Process(target=_overlap_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got = {}
+    got, logs = {}, {}
     for _ in range(2 * world):
-        r, step, gs, nin = q.get(timeout=120)
+        r, step, gs, nin, log = q.get(timeout=120)
         got[(r, step)] = gs
+        logs[(r, step)] = log
         assert nin > 0, "no slice was in flight before allreduce_grads"
+    for step in range(2):   # identical collective sequences on both ranks, although rank 1 reported grads late
+        assert logs[(0, step)] == logs[(1, step)] and len(logs[(0, step)]) > 2, (logs[(0, step)], logs[(1, step)])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0

@@ -3,7 +3,10 @@ oracle's dropout mask (contract v2), at the shapes the decoder runs (keep bits w
 fddm_attn_drop_bits, as models/denoise_decoder.py does) and at ragged / masked / extreme-score edge cases.
 
 Tolerance: bf16 inputs and outputs, fp32 softmax statistics -> 2e-2 of the reference's max magnitude (tests/
-test_gpu_kernels.py TOL for bf16); the LSE within 1e-3 absolute (natural-log units) where the row is finite.
+test_gpu_kernels.py TOL for bf16); the LSE within LSE_ATOL absolute (natural-log units) where the row is finite.
+fwd7 multiplies Q by scale*log2(e) once and rounds that to bf16 (one rounding of 2^-9 relative per element instead
+of rounding the scores), so a score of magnitude |s| carries up to ~|s|*2^-9 of extra error; over randn inputs at
+d=64 the LSE moves by up to ~2e-3, hence 4e-3 (the outputs stay within the bf16 2e-2 bar).
 Reference: models/denoise_decoder.py:129-130,164,169-176 (nn.MultiheadAttention, key_padding_mask, dropout on
 the probabilities).
 """
@@ -14,6 +17,7 @@ from helpers import close
 from oracle import fddm_oracle as O
 
 pytestmark = pytest.mark.gpu
+LSE_ATOL = 4e-3
 
 dev = torch.device("cuda:0")
 bf = torch.bfloat16
@@ -48,12 +52,12 @@ def _run(B, H, Lq, Lk, keep, p, q, k, v, do=None, seed=5, stream=9, family="auto
     lse = torch.empty(B * H, Lq, device=dev)
     kk = keep.to(dev).to(torch.uint8) if keep is not None else None
     db = None
-    if p > 0:
-        db = o.drop_bits(B, H, Lq, Lk, dev).view(1, -1)
-        o.attn_drop_bits(db, 1, B, H, Lq, Lk, p, seed, stream, 0)
-        db = db.view(-1)
-    old = o.attn_force_kernels(family)
+    old = o.attn_force_kernels(family)    # the producer writes the selected family's storage layout
     try:
+        if p > 0:
+            db = o.drop_bits(B, H, Lq, Lk, dev).view(1, -1)
+            o.attn_drop_bits(db, 1, B, H, Lq, Lk, p, seed, stream, 0)
+            db = db.view(-1)
         o.attn_fwd(qd, kd, vd, od, lse, B, H, Lq, Lk, key_keep=kk, drop_p=p, seed=seed, rng_stream=stream, dbits=db,
                    bits_ready=db is not None)
         grads = None
@@ -105,7 +109,7 @@ def test_attn7_forward_matches_float64(B, H, Lq, Lk, masked, p):
     od, lse, _ = _run(B, H, Lq, Lk, keep, p, q, k, v)
     ref, rlse = _ref(_heads(q, B, H), _heads(k, B, H), _heads(v, B, H), keep, p, 5, 9)
     close(od.float(), _back(ref), rtol=2e-2, what="attn7 out")
-    close(lse.view(B, H, Lq), rlse, rtol=0, atol=1e-3, what="attn7 lse")
+    close(lse.view(B, H, Lq), rlse, rtol=0, atol=LSE_ATOL, what="attn7 lse")
 
 
 @pytest.mark.parametrize("B,H,Lq,Lk,masked,p", [SHAPES[0], SHAPES[1], SHAPES[4], SHAPES[6]])
@@ -132,7 +136,10 @@ def test_attn7_forward_then_backward_matches_float64(B, H, Lq, Lk, masked, p):
 def test_attn7_rescale_path_with_growing_scores(Lk):
     """Scores that grow along the keys (every 32-key half-tile exceeds the running maximum by far more than the
     2^8 rescale threshold) exercise the slow path on every half-tile; scores that fall along the keys keep the first
-    half's reference. Both against float64."""
+    half's reference. Forward against float64. The gradients at these scores (up to ~100, |K| up to ~25 per element)
+    are bf16-limited in any kernel (dQ = scale sum_k dS K amplifies the bf16 rounding of P and dS by |K|): measured
+    ~0.2-0.36 of max|dQ| for both families, so the backward is held to the round-4 family's error on the same inputs
+    (within 1.5x) instead of to float64."""
     B, H, Lq = 2, 2, 128
     D = H * 64
     gen = torch.Generator().manual_seed(11)
@@ -144,10 +151,23 @@ def test_attn7_rescale_path_with_growing_scores(Lk):
         k = (sign * ramp[None, :, None] * u.repeat(H)[None, None, :]).expand(B, Lk, D).contiguous()
         k = k + 0.05 * torch.randn(B, Lk, D, generator=gen)
         v = torch.randn(B, Lk, D, generator=gen)
-        od, lse, _ = _run(B, H, Lq, Lk, None, 0.1, q, k, v)
-        ref, rlse = _ref(_heads(q, B, H), _heads(k, B, H), _heads(v, B, H), None, 0.1, 5, 9)
-        close(od.float(), _back(ref), rtol=2e-2, what=f"out (sign {sign})")
-        close(lse.view(B, H, Lq), rlse, rtol=1e-4, atol=1e-3, what=f"lse (sign {sign})")
+        do = torch.randn(B, Lq, D, generator=gen)
+        qr, kr, vr = (_heads(x, B, H).requires_grad_(True) for x in (q, k, v))
+        ref, rlse = _ref(qr, kr, vr, None, 0.1, 5, 9)
+        ref.backward(_heads(do, B, H))
+        rg = [_back(x.grad) for x in (qr, kr, vr)]
+        err = {}
+        for fam in ("auto", "v6"):
+            od, lse, grads = _run(B, H, Lq, Lk, None, 0.1, q, k, v, do, family=fam)
+            if fam == "auto":
+                close(od.float(), _back(ref.detach()), rtol=2e-2, what=f"out (sign {sign})")
+                # the bf16 rounding of the pre-scaled Q moves scores by up to ~|s| 2^-9, as a bf16 rounding of the
+                # scores themselves would (torch's bf16 bmm): a tolerance relative to the LSE
+                close(lse.view(B, H, Lq), rlse.detach(), rtol=2.0 ** -9, atol=LSE_ATOL, what=f"lse (sign {sign})")
+            err[fam] = [(g.float().cpu().double() - r).abs().max().item() / r.abs().max().item()
+                        for g, r in zip(grads, rg)]
+        for n, a_, b_ in zip(("dq", "dk", "dv"), err["auto"], err["v6"]):
+            assert a_ <= 1.5 * b_ + 2e-2, f"{n} (sign {sign}): attn7 rel err {a_:.3g} vs round-4 family {b_:.3g}"
 
 
 def test_attn7_fully_masked_rows_give_nan_like_softmax():
@@ -180,4 +200,28 @@ def test_attn7_agrees_with_round4_kernel(B, H, Lq, Lk, masked, p):
     o7, l7, _ = _run(B, H, Lq, Lk, keep, p, q, k, v, family="auto")
     o6, l6, _ = _run(B, H, Lq, Lk, keep, p, q, k, v, family="v6")
     close(o7.float(), o6.float(), rtol=2e-2, what="fwd7 vs fwd6")
-    close(l7, l6, rtol=0, atol=1e-3, what="lse fwd7 vs fwd6")
+    close(l7, l6, rtol=0, atol=LSE_ATOL, what="lse fwd7 vs fwd6")
+
+
+def test_attn7_forward_records_bits_when_not_ready():
+    """attn_fwd with a keep-bit buffer that the producer has not filled (a standalone call, not the decoder's path):
+    the 32x32x16 family writes the site's masks itself first, and the backward reads them."""
+    o = ops()
+    B, H, Lq, Lk, p = 2, 2, 96, 140, 0.1
+    D = H * 64
+    gen = torch.Generator().manual_seed(5)
+    q, k, v, do = (torch.randn(B, L, D, generator=gen) for L in (Lq, Lk, Lk, Lq))
+    to = lambda x: x.to(dev, bf).reshape(-1, D).contiguous()  # noqa: E731
+    od = torch.empty(B * Lq, D, device=dev, dtype=bf)
+    lse = torch.empty(B * H, Lq, device=dev)
+    db = o.drop_bits(B, H, Lq, Lk, dev)
+    o.attn_fwd(to(q), to(k), to(v), od, lse, B, H, Lq, Lk, drop_p=p, seed=5, rng_stream=9, dbits=db)
+    dq, dk, dv = (torch.empty(B * L, D, device=dev, dtype=bf) for L in (Lq, Lk, Lk))
+    o.attn_bwd(to(q), to(k), to(v), od, to(do), lse, dq, dk, dv, B, H, Lq, Lk, drop_p=p, seed=5, rng_stream=9,
+               dbits=db)
+    torch.cuda.synchronize()
+    qr, kr, vr = (_heads(x, B, H).requires_grad_(True) for x in (q, k, v))
+    ref, _ = _ref(qr, kr, vr, None, p, 5, 9)
+    ref.backward(_heads(do, B, H))
+    close(od.float(), _back(ref.detach()), rtol=2e-2, what="out")
+    close(dk.float(), _back(kr.grad), rtol=6e-2, what="dk")

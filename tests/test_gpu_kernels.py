@@ -442,24 +442,51 @@ def test_attention_fwd_bwd(dtype, Lq, Lk, masked, p, bits):
     close(dv.float(), back(vr.grad), rtol=3 * tol, what="dv")
 
 
+def _decode_v3(w, BH, Lq, Lk):
+    """Storage layout v3 (csrc/attn7.hip lane masks) -> keep [BH, Lq, Lk]: word ((bh*nqg + qg)*nt + t)*32 + 16kb + r,
+    bit l = keep(query 32qg + (l&31), key 64t + 32kb + 8(r>>2) + 4(l>>5) + (r&3))."""
+    nqg, nt = (Lq + 31) // 32, (Lk + 63) // 64
+    bits = ((w.view(BH, nqg, nt, 2, 16, 1) >> torch.arange(64, dtype=torch.int64)) & 1).bool()  # [BH,nqg,nt,kb,r,l]
+    r = torch.arange(16)[:, None]
+    l = torch.arange(64)[None, :]
+    q_of = (l & 31).expand(16, 64)                                  # query within the group
+    k_of = (8 * (r >> 2) + 4 * (l >> 5) + (r & 3)).expand(16, 64)   # key within the 32-key half
+    out = torch.zeros(BH, nqg * 32, nt * 64, dtype=torch.bool)
+    for g in range(nqg):
+        for t in range(nt):
+            for kb in range(2):
+                out[:, 32 * g + q_of, 64 * t + 32 * kb + k_of] = bits[:, g, t, kb]
+    return out[:, :Lq, :Lk]
+
+
+@pytest.mark.parametrize("family", ["auto", "v6"])
 @pytest.mark.parametrize("Lq,Lk", [(256, 256), (40, 499), (129, 70)])
-def test_attention_drop_bits_producer_matches_oracle(Lq, Lk):
+def test_attention_drop_bits_producer_matches_oracle(Lq, Lk, family):
     """fddm_attn_drop_bits (the decoder writes every block's attention-dropout keep bits in two launches ahead of the
     forward): 3 sites of one shape, rng streams 7, 13, 19, against the oracle's contract-v2 mask bit for bit, in the
-    word layout the forward / backward kernels read (bit kk of word (bh, t, q) = keep(q, key 64t + kk))."""
+    storage layout the selected kernel family reads: layout v3 lane masks (default, csrc/attn7.hip) or the round-4
+    words (bit kk of word (bh, t, q) = keep(q, key 64t + kk))."""
     o = ops()
     B, H, p, seed = 2, 3, 0.1, 77
     nt = (Lk + 63) // 64
-    words = B * H * nt * Lq
+    words = o.drop_words(B, H, Lq, Lk)
     out = torch.zeros(3, words + 5, device=dev, dtype=torch.int64)
-    o.attn_drop_bits(out, 3, B, H, Lq, Lk, p, seed, 7, 6)
+    old = o.attn_force_kernels(family)
+    try:
+        o.attn_drop_bits(out, 3, B, H, Lq, Lk, p, seed, 7, 6)
+    finally:
+        o.attn_force_kernels(old)
     torch.cuda.synchronize()
     assert (out[:, words:] == 0).all(), "wrote past the site's words"
     bitpos = torch.arange(64, dtype=torch.int64)
     for s_ in range(3):
-        w = out[s_, :words].cpu().view(B * H, nt, Lq)
-        bits = ((w[..., None] >> bitpos) & 1).bool()                       # [BH, nt, Lq, 64]
-        got = bits.permute(0, 2, 1, 3).reshape(B * H, Lq, nt * 64)[:, :, :Lk]
+        if family == "v6":
+            w = out[s_, :B * H * nt * Lq].cpu().view(B * H, nt, Lq)
+            bits = ((w[..., None] >> bitpos) & 1).bool()                       # [BH, nt, Lq, 64]
+            got = bits.permute(0, 2, 1, 3).reshape(B * H, Lq, nt * 64)[:, :, :Lk]
+        else:
+            n3 = B * H * ((Lq + 31) // 32) * nt * 32
+            got = _decode_v3(out[s_, :n3].cpu(), B * H, Lq, Lk)
         ref = O.attn_dropout_keep(seed, 7 + 6 * s_, B, H, Lq, Lk, p).reshape(B * H, Lq, Lk)
         assert torch.equal(got, ref), f"site {s_}: {(got != ref).sum().item()} bits differ"
 

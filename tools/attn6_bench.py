@@ -30,6 +30,7 @@ def timeit(fn, iters=20):
 
 
 def main():
+    ops.attn_force_kernels("v6")    # this tool times the round-4 family (keep bits in its word layout)
     cases = [("C2 self  L256 B32 H8 kpm", 32, 8, 256, 256, True),
              ("C2 cross 256x499 B32 H8", 32, 8, 256, 499, False),
              ("C4 self  L512 B16 H12 kpm", 16, 12, 512, 512, True),

@@ -48,11 +48,12 @@ def main():
             keep = (torch.arange(Lk, device=dev)[None] < lens[:, None]).to(torch.uint8).contiguous()
         fl = 4.0 * B * H * Lq * Lk * 64
         db = ops.drop_bits(B, H, Lq, Lk, dev)
-        ops.attn_drop_bits(db.view(1, -1), 1, B, H, Lq, Lk, 0.1, 1, 1, 0)
         res, outs = [], {}
         for fam in ("v6", "auto"):
             old = ops.attn_force_kernels(fam)
             try:
+                ops.attn_drop_bits(db.view(1, -1), 1, B, H, Lq, Lk, 0.1, 1, 1, 0)   # the family's storage layout
+                tp = timeit(lambda: ops.attn_drop_bits(db.view(1, -1), 1, B, H, Lq, Lk, 0.1, 1, 1, 0), iters)
                 o = torch.empty(B * Lq, H * 64, device=dev, dtype=bf)
                 lse = torch.empty(B * H, Lq, device=dev)
                 tf = timeit(lambda: ops.attn_fwd(q, k, v, o, lse, B, H, Lq, Lk, key_keep=keep, drop_p=0.1, seed=1,
@@ -66,7 +67,7 @@ def main():
             finally:
                 ops.attn_force_kernels(old)
             res.append(f"{fam}: fwd {tf*1e3:6.1f} us {fl/tf/1e12*1e3/PEAK:5.3f}  bwd {tb*1e3:6.1f} us "
-                       f"{2.5*fl/tb/1e12*1e3/PEAK:5.3f}")
+                       f"{2.5*fl/tb/1e12*1e3/PEAK:5.3f}  bits {tp*1e3:5.1f} us")
         diff = [(a_ - b_).abs().max().item() for a_, b_ in zip(outs["v6"], outs["auto"])]
         print(f"{name:28s} " + " | ".join(res) + " | max|diff| o/dq/dk/dv " + " ".join(f"{d:.3g}" for d in diff),
               flush=True)

@@ -26,12 +26,12 @@ if kpm:
     lens = torch.randint(Lk // 2, Lk + 1, (B,), device=dev, generator=g)
     keep = (torch.arange(Lk, device=dev)[None] < lens[:, None]).to(torch.uint8).contiguous()
 db = ops.drop_bits(B, H, Lq, Lk, dev)
-ops.attn_drop_bits(db.view(1, -1), 1, B, H, Lq, Lk, 0.1, 1, 1, 0)
 o = torch.empty(B * Lq, H * 64, device=dev, dtype=bf)
 lse = torch.empty(B * H, Lq, device=dev)
 dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
 for fam in ("v6", "auto"):
     old = ops.attn_force_kernels(fam)
+    ops.attn_drop_bits(db.view(1, -1), 1, B, H, Lq, Lk, 0.1, 1, 1, 0)
     for _ in range(5):
         ops.attn_fwd(q, k, v, o, lse, B, H, Lq, Lk, key_keep=keep, drop_p=0.1, seed=1, rng_stream=1, dbits=db,
                      bits_ready=True)
