@@ -104,25 +104,26 @@ NOISE_ONLY = ("s_proj.proj.net.0.bias", "t_proj.proj.net.0.bias")
 def _step_batches():
     g = torch.Generator().manual_seed(21)
     out = []
-    for i in range(2):
+    for i in range(3):
         wave = 0.1 * torch.randn(4, 16000, generator=g)
         x0 = torch.randint(1, SV, (4, SL), generator=g)
         x0[1, 14:] = 0
         x0[2, 9:] = 0
         xt = torch.randint(1, SV, (4, SL), generator=g)
-        t = torch.tensor([1, 3, 7, 10]) if i == 0 else torch.tensor([10, 2, 5, 1])
+        t = (torch.tensor([1, 3, 7, 10]), torch.tensor([10, 2, 5, 1]), torch.tensor([4, 9, 2, 6]))[i]
         out.append((wave, x0, xt, t))
     return out
 
 
 def _train_two_steps(rank, world, sync):
-    """train_one_epoch over global steps 4 (L_fd) and 5 on this rank's rows (all 4 when world == 1), encoder on
-    its side stream, decoder gradients all-reduced by the overlapped reducer; returns final params and L_fd."""
+    """train_one_epoch over global steps 3 (KL), 4 (L_fd) and 5 (KL) on this rank's rows (all 4 when world == 1),
+    encoder on its side stream, decoder gradients all-reduced by the overlapped reducer; returns final params, L_fd
+    and the torch.distributed collectives the three steps issued (helpers.CollectiveLog)."""
     import train as T_
     from fddm.sched.diffusion_scheduler import DiscreteDiffusionScheduler
     from fddm_hip import runtime as rt
     from fddm_hip.optim import FusedAdamW
-    from helpers import SMALL_WAVLM, _step_params
+    from helpers import SMALL_WAVLM, CollectiveLog, _step_params
     from models.projection import SpeechProjector, TextEmbedding, TextProjector
     from test_gpu_models import _encoder, make_decoder
     dev = torch.device("cuda:0")
@@ -160,15 +161,16 @@ def _train_two_steps(rank, world, sync):
                             lfd={"n_step_fd": 4, "tau": 1.0, "lambda_offdiag": 5e-3, "sync_batch_stats": sync},
                             log={"log_every": 1000})
             sch = TF(DiscreteDiffusionScheduler(K=SV, T=ST, device=dev))
-            T_.train_one_epoch(enc, dec, sp, te, tp, sch, [(b[0], b[1]) for b in data], opt, dev, cfg, 4, None, 1,
-                               False, draw_t=lambda B: next(tq))
-            torch.cuda.synchronize()
+            with CollectiveLog() as cl:
+                T_.train_one_epoch(enc, dec, sp, te, tp, sch, [(b[0], b[1]) for b in data], opt, dev, cfg, 3, None,
+                                   1, False, draw_t=lambda B: next(tq))
+                torch.cuda.synchronize()
         finally:
             T_.lfd_loss = orig
     final = {("decoder." + n): p.detach().cpu().clone() for n, p in dec.named_parameters()}
     for pre, m in (("s_proj.", sp), ("t_embed.", te), ("t_proj.", tp)):
         final.update({pre + n: p.detach().cpu().clone() for n, p in m.named_parameters()})
-    return final, rec, params
+    return final, rec, params, cl.log
 
 
 def _step_worker(rank, world, port, q):
@@ -177,31 +179,36 @@ def _step_worker(rank, world, port, q):
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=120))
     try:
-        final, rec, _ = _train_two_steps(rank, world, True)
-        q.put((rank, {n: v.numpy() for n, v in final.items()}, rec))
+        final, rec, _, log = _train_two_steps(rank, world, True)
+        q.put((rank, {n: v.numpy() for n, v in final.items()}, rec, log))
     finally:
         dist.destroy_process_group()
 
 
 def test_dp_train_step_global_batch_lfd_matches_full_batch():
-    """Two ranks x 2 utterances through train_one_epoch (L_fd step, then a KL-only step whose projector grads
-    are None on both ranks), encoder side stream on, lfd.sync_batch_stats: the global-batch L_fd, w_t mean and
+    """Two ranks x 2 utterances through train_one_epoch (KL step, L_fd step, KL step; the projectors' grads are None
+    on the KL steps on both ranks), encoder side stream on, lfd.sync_batch_stats: the global-batch L_fd, w_t mean and
     the averaged gradients make every rank's parameters equal those of one process on all 4 utterances
-    (reference losses/fddm_losses.py:18-58, train.py:390 over the whole batch)."""
+    (reference losses/fddm_losses.py:18-58, train.py:390 over the whole batch), and both ranks issue the identical
+    collective sequence (names, shapes, dtypes, ops), the L_fd step's statistics reductions included."""
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = [ctx.Process(target=_step_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got = {}
+    got, logs = {}, {}
     for _ in range(world):
-        r, fin, rec = q.get(timeout=240)
+        r, fin, rec, log = q.get(timeout=240)
         got[r] = (fin, rec)
+        logs[r] = log
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    ref, ref_rec, init = _train_two_steps(0, 1, False)
+    assert logs[0] == logs[1], "ranks issued different collective sequences"
+    names = [e[0] for e in logs[0]]
+    assert names.count("all_reduce") >= 3, logs[0]
+    ref, ref_rec, init, _ = _train_two_steps(0, 1, False)
     assert len(ref_rec) == 1
     for r in range(world):
         assert len(got[r][1]) == 1
