@@ -156,3 +156,13 @@ __device__ __forceinline__ float block_max(float v, float* red) {
 }  // namespace fddm
 
 #define FDDM_LAUNCH_CHECK() return (int)hipGetLastError()
+
+// Host-floor diagnostic build only (tools/build_stub.sh, -DFDDM_STUB_KERNELS): every launch enqueues one empty
+// 64-thread kernel on the same stream instead of its kernel, so a train step keeps its host work and launch count
+// while the GPU does (almost) nothing; bench.py's host_ms_per_step then measures the host floor.
+#ifdef FDDM_STUB_KERNELS
+static __global__ void fddm_stub_kernel() {}
+static inline void fddm_stub_launch(hipStream_t s) { hipLaunchKernelGGL(fddm_stub_kernel, dim3(1), dim3(64), 0, s); }
+#undef hipLaunchKernelGGL
+#define hipLaunchKernelGGL(k, g, b, l, s, ...) fddm_stub_launch(s)
+#endif
