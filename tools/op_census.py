@@ -44,7 +44,8 @@ class Census(TorchFunctionMode):
 
 def main():
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 4
-    sys.argv = [sys.argv[0], "--steps", str(steps), "--warmup", "4", "--no-cpu-baseline"]
+    sys.argv = [sys.argv[0], "--steps", str(steps), "--warmup", "4", "--no-cpu-baseline"] + \
+        os.environ.get("CENSUS_ARGS", "").split()   # e.g. CENSUS_ARGS="--config c4"
     args = bench.parse()
     device = torch.device("cuda", 0)
     torch.manual_seed(1337)
