@@ -48,6 +48,20 @@ def main():
     t = timeit(lambda: ops.ln_bwd(dout, s, m, r, g, b, dres=dres, dy_t=dy, dgamma=dg, dbeta=db, drop_p=0.1, seed=1,
                                   rng_stream=2))
     print(f"decoder LN bwd (no FiLM)        {t:6.1f} us  {byt / t / 1e3:6.0f} GB/s", flush=True)
+    N4, d4, L4 = 8192, 768, 512   # C4 decoder LN (d 768): FiLM form and the plain f32 -> f32 + bf16 form
+    x4 = torch.randn(N4, d4, device=dev)
+    y4 = torch.randn(N4, d4, device=dev, dtype=bf)
+    g4, b4 = torch.ones(d4, device=dev), torch.zeros(d4, device=dev)
+    fs4, fh4 = torch.zeros(N4 // L4, d4, device=dev), torch.zeros(N4 // L4, d4, device=dev)
+    s4, o4, m4, r4 = torch.empty_like(x4), torch.empty_like(x4), torch.empty(N4, device=dev), torch.empty(N4, device=dev)
+    ot4 = torch.empty(N4, d4, device=dev, dtype=bf)
+    t = timeit(lambda: ops.ln_fwd(x4, y4, g4, b4, out_f32=o4, out_t=ot4, save_s=s4, mean=m4, rstd=r4,
+                                  film=(fs4, fh4), rows_per_batch=L4, drop_p=0.1, seed=1, rng_stream=2))
+    byt = N4 * d4 * (4 + 2 + 4 + 4 + 2)
+    print(f"C4 decoder LN fwd (FiLM, drop)  {t:6.1f} us  {byt / t / 1e3:6.0f} GB/s", flush=True)
+    t = timeit(lambda: ops.ln_fwd(x4, y4, g4, b4, out_f32=o4, out_t=ot4, save_s=s4, mean=m4, rstd=r4,
+                                  drop_p=0.1, seed=1, rng_stream=2))
+    print(f"C4 decoder LN fwd (drop)        {t:6.1f} us  {byt / t / 1e3:6.0f} GB/s", flush=True)
     N2, d2 = 15968, 768
     xb = torch.randn(N2, d2, device=dev, dtype=bf)
     yb = torch.randn(N2, d2, device=dev, dtype=bf)
