@@ -97,3 +97,52 @@ def test_c5_sampler_matches_oracle(prec, enc_tol, mtol, monkeypatch):
     else:   # only near-ties differ (asserted above): each differing id moves the CER by at most one edit
         ndiff = int((x_gpu != x_ref).sum())
         assert abs(cer(x_gpu) - cer(x_ref)) <= ndiff / 100.0
+
+
+def test_c5_full_batch_graph_replay_and_rows(monkeypatch):
+    """C5 at its benchmark batch (B = 64, bf16): the HIP-graph replay of the whole denoise loop (the `bench.py
+    --config c5` path) equals the eager loop on all 64 utterances, and two rows (first, last) of every jump agree
+    with the oracle's decoder forward + exact posterior argmax on the GPU's own inputs beyond the bf16 margin."""
+    import bench
+    from fddm_hip import runtime as rt
+    from sampler import jumpy_sampler as JS
+
+    args = SimpleNamespace(config="c5", batch=64, seconds=10.0, seq_len=256, layers=6, d_model=512, heads=8,
+                           precision="bf16")
+    B, L, V, mtol = args.batch, args.seq_len, 8000, 5e-2
+    gen = torch.Generator().manual_seed(23)
+    wave = 0.1 * torch.randn(B, 160000, generator=gen)
+    xT = torch.randint(0, V, (B, L), generator=gen)
+    with rt.use_precision("bf16"):
+        torch.manual_seed(7)
+        _, _, models, _ = bench.build(args, dev)
+        smp = bench.c5_sampler(models, dev)
+        enc, dec = models[0], models[1]
+        with torch.no_grad():
+            cond = enc(wave.to(dev))[0]
+        xs, x0hs = [xT.to(dev)], []
+        plan = smp._plan(B)
+        with torch.no_grad():
+            for t, delta, coef in plan:
+                nx, x0h, _ = smp._step(xs[-1], t, delta, cond, coef)
+                xs.append(nx)
+                x0hs.append(x0h)
+        monkeypatch.setattr(JS.torch, "randint", lambda low, high, size, device=None: xT.to(dev))
+        x0_graph, _ = smp.sample(cond, seq_len=L, graph=True, return_probs=False)
+        torch.cuda.synchronize()
+        sd = {k: v.detach().float().cpu() for k, v in dec.state_dict().items()}
+        del models, smp, enc, dec
+    assert torch.equal(x0_graph.cpu(), x0hs[-1].cpu()), "graph replay of the denoise loop differs from the eager loop"
+    rows = [0, B - 1]
+    c_cpu = cond.detach().float().cpu()[rows]
+    betas, _ = O.sched_tables(200)
+    bad = 0
+    for j, (t, delta, _) in enumerate(plan):
+        x_in = xs[j].cpu()[rows]
+        tv = torch.full((len(rows),), t, dtype=torch.long)
+        with torch.no_grad():
+            logits = O.decoder_forward(sd, x_in, tv, c_cpu, None, H=args.heads, num_layers=args.layers)
+        nx_ref, margin = O.jump_argmax(logits, x_in, tv, delta, betas.numpy(), V, 200)
+        ok = margin.abs() >= mtol
+        bad += int((xs[j + 1].cpu()[rows] != nx_ref)[ok].sum())
+    assert bad == 0
