@@ -225,18 +225,20 @@ def test_dp_train_step_global_batch_lfd_matches_full_batch():
 
 
 # ------------------------------------------------------- the N > 1 benchmark path and the C2 geometry under DP
-def test_bench_two_ranks_run_real_c2_steps():
-    """`bench.py --gpus 2` at C2 (not a dry run): two ranks (gloo, both on this box's GPU; the 8-GPU node runs the
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_ranks_run_real_c2_steps(world):
+    """`bench.py --gpus N` at C2 (not a dry run): N ranks (gloo, all on this box's GPU; the 8-GPU node runs the
     same code over RCCL, one GPU per rank) run warm-up and timed train steps with the overlapped gradient
-    all-reduce, the HIP-graph encoder on its side stream and the CU caps; the line reports n_gpus 2 / dp2 and a
-    finite loss, and both replicas end with bit-identical parameters (BASELINE configs[2])."""
+    all-reduce, the HIP-graph encoder on its side stream and the CU caps lowered by the collective reserve; the
+    line reports n_gpus N / dpN, per-rank ms/step and the caps in force, a finite loss, and every replica ends with
+    bit-identical parameters (BASELINE configs[2])."""
     import json
     import math
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, FDDM_DIST_BACKEND="gloo", FDDM_DIST_TIMEOUT_S="300")
-    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "3", "--warmup", "1",
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", str(world), "--steps", "3", "--warmup", "1",
                         "--no-cpu-baseline", "--checksum"], cwd=root, env=env, capture_output=True, text=True,
                        timeout=900)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
@@ -244,10 +246,13 @@ def test_bench_two_ranks_run_real_c2_steps():
     assert len(lines) == 1, r.stdout[-2000:]
     out = json.loads(lines[0])
     print(json.dumps({k: out[k] for k in ("value", "ms_per_step", "n_gpus", "avg_loss", "param_checksums")}))
-    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 64
+    assert out["n_gpus"] == world and out["config"]["parallelism"] == f"dp{world}"
+    assert out["config"]["global_batch"] == 32 * world
     assert math.isfinite(out["avg_loss"]) and out["value"] > 0
+    assert len(out["rank_ms_per_step"]["per_rank"]) == world and out["cu_caps"]["coll"] == 8
+    assert out["cu_caps"]["enc"] == out["cu_caps"]["ncu"] * 3 // 4 - 8
     cs = out["param_checksums"]
-    assert len(cs) == 2 and cs[0] == cs[1], cs
+    assert len(cs) == world and all(c == cs[0] for c in cs), cs
 
 
 def _c2_dp_grads(rank, world):
