@@ -2550,6 +2550,13 @@ FDDM_API long fddm_attn_drop_words(int B, int H, int Lq, int Lk) {
   return v2 > v3 ? v2 : v3;
 }
 
+// floats of fddm_attn_bwd's delta_ws for this shape (the larger of the two families' needs: the 32x32x16 pair's
+// [2][B*H][LqP] row terms plus the pre-scaled Q' [B*H][LqP][64] bf16, the round-4 kernels' [B*H][Lq])
+FDDM_API long fddm_attn_bwd_ws_floats(int B, int H, int Lq, int Lk) {
+  (void)Lk;
+  return 34L * B * H * ((Lq + 63) / 64 * 64);
+}
+
 // Dropout keep bits of nsites attention sites with the same shape, rng streams stream0 + s * stream_step (site s at
 // out + s * site_words): the words fddm_attn_fwd(..., drop_bits_ready = 1) and fddm_attn_bwd read.
 FDDM_API int fddm_attn_drop_bits(unsigned long long* out, long site_words, int nsites, int B, int H, int Lq, int Lk,

@@ -339,7 +339,7 @@ def attn_bwd(q, k, v, o, do, lse, dq, dk, dv, B, H, Lq, Lk, *, key_keep=None, dr
         return
     # row-term workspace: delta = rowsum(dO O) and -LSE log2(e) per query, [2][B*H][Lq rounded up to 64] (the
     # 32x32x16 backward's layout; the other kernels use the first B*H*Lq floats)
-    delta = torch.empty(34 * B * H * ((Lq + 63) // 64 * 64), device=q.device, dtype=torch.float32)   # + Q' bf16
+    delta = torch.empty(int(lib().fddm_attn_bwd_ws_floats(B, H, Lq, Lk)), device=q.device, dtype=torch.float32)
     call("fddm_attn_bwd", code(q), ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(o),
          o.stride(0), ptr(do), do.stride(0), ptr(lse), ptr(dq), dq.stride(0), ptr(dk), dk.stride(0), ptr(dv),
          dv.stride(0), ptr(delta), ptr(key_keep), B, H, Lq, Lk, float(sc), float(drop_p), seed, rng_stream,

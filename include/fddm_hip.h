@@ -114,9 +114,12 @@ int fddm_attn_fwd_relgate(const void* Q, long sq, const void* K, long sk, const 
 /* Backward: dQ, dK, dV. bf16 with recorded or no dropout and Lk <= 1024: the 32x32x16-MFMA pair (a query-owned dQ
  * launch that also writes the per-query row terms delta = rowsum(dO O) and -LSE log2(e) into delta_ws, laid out
  * [2][B*H][LqP] with LqP = Lq rounded up to 64, and Q pre-scaled by scale*log2(e) in bf16 as [B*H][LqP][64] after
- * them, then a key-owned dK/dV launch that reads them); delta_ws must hold 34 * B*H*LqP floats. Otherwise (fp32, rehashed dropout, longer keys, or fddm_attn_set_kernels(1)): bf16 self-
+ * them, then a key-owned dK/dV launch that reads them); delta_ws must hold fddm_attn_bwd_ws_floats(B, H, Lq, Lk)
+ * = 34 * B*H*LqP floats (ABI 5; ABI 4 needed B*H*Lq). Otherwise (fp32, rehashed dropout, longer keys, or
+ * fddm_attn_set_kernels(1)): bf16 self-
  * attention shapes Lq == Lk <= 256 as one fused launch, else a dQ launch writing delta_ws [B*H][Lq] and a dK/dV
  * launch. */
+long fddm_attn_bwd_ws_floats(int B, int H, int Lq, int Lk);
 int fddm_attn_bwd(int dtype, const void* Q, long sq, const void* K, long sk, const void* V, long sv, const void* O,
                   long so, const void* dO, long sdo, const float* lse, void* dQ, long sdq, void* dK, long sdk,
                   void* dV, long sdv, float* delta_ws, const unsigned char* key_keep, int B, int H, int Lq, int Lk,
