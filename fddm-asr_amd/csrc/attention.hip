@@ -2564,7 +2564,9 @@ FDDM_API int fddm_attn_drop_bits(unsigned long long* out, long site_words, int n
                                  unsigned long long stream_step, void* hs) {
   if (B <= 0 || H <= 0 || Lq <= 0 || Lk <= 0 || nsites <= 0) return 0;
   if (!out || drop_p <= 0.f || site_words < fddm_attn_drop_words(B, H, Lq, Lk)) return (int)hipErrorInvalidValue;
-  if (attn7_enabled())  // storage layout v3 (lane masks) for the 32x32x16 kernels
+  // storage layout v3 (lane masks) where the 32x32x16 kernels read the bits (bf16, Lk <= 1024); the round-4 words
+  // for the kernels that take longer key ranges (fwd2 draws its own, dq2 / dkv2 read these)
+  if (attn7_enabled() && Lk <= 1024)
     return attn7_drop_bits((uint64_t*)out, site_words, nsites, B * H, Lq, Lk, seed, stream0, stream_step,
                            (unsigned)llrintf(drop_p * 65536.f), g_seed_off, (hipStream_t)hs);
   DbArgs d{(uint64_t*)out, site_words, B * H, Lq, Lk, seed, stream0, stream_step, (unsigned)llrintf(drop_p * 65536.f),

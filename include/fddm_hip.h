@@ -100,10 +100,12 @@ int fddm_attn_drop_bits(unsigned long long* out, long site_words, int nsites, in
                         float drop_p, unsigned long long seed, unsigned long long stream0,
                         unsigned long long stream_step, void* hip_stream);
 /* u64 words per site of a keep-bit buffer (room for either storage layout; site_words must be at least this).
- * fddm_attn_drop_bits writes the layout of the selected kernel family: by default layout v3 of csrc/attn7.hip (one
+ * fddm_attn_drop_bits writes the layout of the kernels that will read it: for Lk <= 1024 under the default family
+ * (the bf16 32x32x16 kernels) layout v3 of csrc/attn7.hip (one
  * 64-bit lane mask per score-MFMA accumulator register: word ((bh*ceil(Lq/32) + qg)*ceil(Lk/64) + t)*32 + 16*kb + r,
- * bit l = keep(query 32*qg + (l&31), key 64*t + 32*kb + 8*(r>>2) + 4*(l>>5) + (r&3))); under
- * fddm_attn_set_kernels(1) the round-4 words above. The keep decisions are the same (RNG contract v2). */
+ * bit l = keep(query 32*qg + (l&31), key 64*t + 32*kb + 8*(r>>2) + 4*(l>>5) + (r&3))); for Lk > 1024 or under
+ * fddm_attn_set_kernels(1) the round-4 words above. Recorded bits are for bf16 attention (the fp32 kernels draw
+ * their own). The keep decisions are the same (RNG contract v2). */
 long fddm_attn_drop_words(int B, int H, int Lq, int Lk);
 /* WavLM variant (bf16): the gate is computed in the kernel from the 8 gru_rel_pos_linear pre-activations per
  * (token, head) stored at graw + (b*Lq+q)*sgr + h*8 (bf16, appended to the Q|K|V projection's output) and

@@ -91,6 +91,10 @@ SHAPES = [  # (B, H, Lq, Lk, key-padding mask, dropout p)
     (2, 3, 129, 257, True, 0.1),
     (3, 1, 64, 64, False, 0.0),
     (2, 2, 200, 200, True, 0.1),
+    (1, 1, 1, 1, False, 0.1),        # one query, one key
+    (2, 2, 33, 5, True, 0.1),        # a partial 32-query group, five keys
+    (1, 2, 96, 1024, True, 0.1),     # the longest key range of the 32x32x16 family (16 tiles, mask on every one)
+    (1, 2, 96, 1025, False, 0.1),    # one key past it: the round-4 family takes the launch
 ]
 
 
@@ -102,17 +106,21 @@ def test_attn7_forward_matches_float64(B, H, Lq, Lk, masked, p):
     keep = None
     if masked:
         keep = torch.ones(B, Lk, dtype=torch.bool)
-        keep[1, Lk - 9:] = False
-        keep[0, 3] = False
+        keep[B - 1, max(1, Lk - 9):] = False
+        if Lk > 3:
+            keep[0, 3] = False
         if Lk > 130:
-            keep[1, 64:128] = False      # a whole 64-key tile of padding inside the range (skipped tile)
+            keep[B - 1, 64:128] = False  # a whole 64-key tile of padding inside the range (skipped tile)
     od, lse, _ = _run(B, H, Lq, Lk, keep, p, q, k, v)
     ref, rlse = _ref(_heads(q, B, H), _heads(k, B, H), _heads(v, B, H), keep, p, 5, 9)
     close(od.float(), _back(ref), rtol=2e-2, what="attn7 out")
-    close(lse.view(B, H, Lq), rlse, rtol=0, atol=LSE_ATOL, what="attn7 lse")
+    # with few keys the LSE is close to one score, whose error is the bf16 rounding of Q' (|s| 2^-9), not averaged
+    smax = (_heads(q, B, H) @ _heads(k, B, H).transpose(-1, -2)).abs().max().item() / 8.0
+    close(lse.view(B, H, Lq), rlse, rtol=0, atol=max(LSE_ATOL, 2.0 ** -8 * smax), what="attn7 lse")
 
 
-@pytest.mark.parametrize("B,H,Lq,Lk,masked,p", [SHAPES[0], SHAPES[1], SHAPES[4], SHAPES[6]])
+@pytest.mark.parametrize("B,H,Lq,Lk,masked,p", [SHAPES[0], SHAPES[1], SHAPES[4], SHAPES[6], SHAPES[9], SHAPES[10],
+                                                SHAPES[11], SHAPES[12]])
 def test_attn7_forward_then_backward_matches_float64(B, H, Lq, Lk, masked, p):
     """The backward kernels read the forward's LSE and the same keep words: gradients vs float64 autograd."""
     D = H * 64
@@ -121,15 +129,17 @@ def test_attn7_forward_then_backward_matches_float64(B, H, Lq, Lk, masked, p):
     keep = None
     if masked:
         keep = torch.ones(B, Lk, dtype=torch.bool)
-        keep[1, Lk - 9:] = False
+        keep[B - 1, max(1, Lk - 9):] = False
     od, lse, (dq, dk, dv) = _run(B, H, Lq, Lk, keep, p, q, k, v, do)
     qr, kr, vr = (_heads(x, B, H).requires_grad_(True) for x in (q, k, v))
     ref, _ = _ref(qr, kr, vr, keep, p, 5, 9)
     ref.backward(_heads(do, B, H))
     close(od.float(), _back(ref.detach()), rtol=2e-2, what="out")
-    close(dq.float(), _back(qr.grad), rtol=6e-2, what="dq")
-    close(dk.float(), _back(kr.grad), rtol=6e-2, what="dk")
-    close(dv.float(), _back(vr.grad), rtol=6e-2, what="dv")
+    # delta = rowsum(dO O) comes from the stored bf16 O: dS carries ~2^-9 |dO| |O| absolute error even where the
+    # exact gradient vanishes (one key: softmax = 1, dQ = dK = 0 exactly), hence an absolute floor of 1e-2
+    close(dq.float(), _back(qr.grad), rtol=6e-2, atol=1e-2, what="dq")
+    close(dk.float(), _back(kr.grad), rtol=6e-2, atol=1e-2, what="dk")
+    close(dv.float(), _back(vr.grad), rtol=6e-2, atol=1e-2, what="dv")
 
 
 @pytest.mark.parametrize("Lk", [256, 499])
