@@ -235,3 +235,40 @@ def test_attn7_forward_records_bits_when_not_ready():
     ref.backward(_heads(do, B, H))
     close(od.float(), _back(ref.detach()), rtol=2e-2, what="out")
     close(dk.float(), _back(kr.grad), rtol=6e-2, what="dk")
+
+
+def test_decoder_long_audio_families_agree():
+    """The whole bf16 decoder (training mode, dropout 0.1, keep bits written ahead by the producer for every block's
+    two attention sites) with a condition longer than the 32x32x16 family takes (S = 1100 frames: the cross sites run
+    on the round-4 kernels and read the round-4 words, the self sites on attn7 with layout v3): logits and every
+    parameter gradient agree with the all-round-4 run on the same inputs and seeds (bf16 roundings of one result)."""
+    from fddm_hip import runtime as rt
+    from test_gpu_models import make_decoder
+    o = ops()
+    B, L, S, V, d, H, NL, FF = 2, 64, 1100, 300, 128, 2, 2, 256
+    gen = torch.Generator().manual_seed(41)
+    xt = torch.randint(1, V, (B, L), generator=gen)
+    xt[1, 50:] = 0
+    t = torch.tensor([3, 17])
+    cond = torch.randn(B, S, d, generator=gen)
+    R = torch.randn(B, L, V, generator=gen)
+    res = {}
+    for fam in ("auto", "v6"):
+        old = o.attn_force_kernels(fam)
+        try:
+            with rt.use_precision("bf16"):
+                torch.manual_seed(3)
+                dec = make_decoder(V, d, H, NL, FF, dropout=0.1)
+                dec.train()
+                rt.reseed(11)
+                logits = dec(xt.to(dev), t.to(dev), cond.to(dev), x_mask=(xt != 0).to(dev))
+                (logits.float() * R.to(dev)).sum().backward()
+                torch.cuda.synchronize()
+                res[fam] = (logits.float().cpu(), {n: p.grad.float().cpu() for n, p in dec.named_parameters()
+                                                   if p.grad is not None})
+        finally:
+            o.attn_force_kernels(old)
+    close(res["auto"][0], res["v6"][0], rtol=3e-2, what="logits auto vs round-4")
+    assert res["auto"][1].keys() == res["v6"][1].keys()
+    for n in res["auto"][1]:
+        close(res["auto"][1][n], res["v6"][1][n], rtol=6e-2, atol=1e-3, what=f"grad {n}")
