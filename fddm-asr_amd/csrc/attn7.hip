@@ -229,9 +229,6 @@ __global__ void __launch_bounds__(256, A7_FWD_WPS) fwd7_kernel(AttnArgs a) {
   const int nqg = (a.Lq + 31) >> 5, qg = 4 * bxi + w;  // the wave's 32-query group (keep bits)
   const unsigned* lbits = (const unsigned*)(a.dbits + (long)a.B * a.H * nqg * ntiles * 32);
   auto fill = [&](int tt, int st) {
-#ifdef A7_ABL_NODMA  // timing-only ablation (tools/probe): no K / V stream after the first tile, results wrong
-    if (tt > 0) return;
-#endif
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int R = 16 * w + 8 * u;
@@ -397,9 +394,7 @@ __global__ void __launch_bounds__(256, A7_FWD_WPS) fwd7_kernel(AttnArgs a) {
     const unsigned rest = t + 1 < 32 ? (tmask & ~((2u << t) - 1u)) : 0u;
     const int tn = rest ? __builtin_ctz(rest) : -1;
     if (tn >= 0) fill(tn, st ^ 1);
-#ifndef A7_ABL_NOCOMPUTE  // timing-only ablation (tools/probe): the stream and barriers without the tile work
     if (act) tile(t, st);
-#endif
     if (tn < 0) break;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of tile tn landed
     __builtin_amdgcn_s_barrier();                      // every wave's pieces landed; every wave finished tile t
