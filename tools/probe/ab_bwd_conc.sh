@@ -1,0 +1,6 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_attn7.py tests/test_gpu_kernels.py -k "attn or attention" > gpurun_out/ab1_tests.log 2>&1 || { tail -30 gpurun_out/ab1_tests.log; exit 1; }
+tail -2 gpurun_out/ab1_tests.log
+timeout -k 10 120 python -u tools/attn7_bench.py 50 > gpurun_out/ab1_new.txt 2>&1 && FDDM_HIP_LIB=vlib/base.so timeout -k 10 120 python -u tools/attn7_bench.py 50 > gpurun_out/ab1_base.txt 2>&1 && timeout -k 10 120 python -u tools/attn7_bench.py 50 > gpurun_out/ab1_new2.txt 2>&1
+cat gpurun_out/ab1_new.txt gpurun_out/ab1_base.txt gpurun_out/ab1_new2.txt
