@@ -2366,9 +2366,10 @@ __global__ void __launch_bounds__(1024, 1) bwd3s_kernel(AttnArgs a) {
 //           else dq4 + dkv4 (streamed rings) for L <= 1024 with recorded bits or no dropout; dq2 + dkv2 otherwise
 //           (keep bits rehashed when the forward recorded none, or longer sequences).
 // fddm_attn_set_kernels (tests / tools only): 1 selects the round-4 16x16x32 kernels (fwd6 / dq4 / dkv4 / bwd3s)
-// where the 32x32x16 family (attn7.hip) would run; 0 (default) the 32x32x16 family
+// where the 32x32x16 family (attn7.hip) would run; 0 (default) the 32x32x16 family; 2 the same without the fused
+// backward (dq7 + dkv7 at every Lk)
 static int g_attn_v6 = 0;
-static bool attn7_enabled() { return g_attn_v6 == 0; }
+static bool attn7_enabled() { return g_attn_v6 != 1; }
 
 template <typename T>
 static int run(int which, AttnArgs& a, hipStream_t s) {
@@ -2452,7 +2453,9 @@ static int run(int which, AttnArgs& a, hipStream_t s) {
       else hipLaunchKernelGGL((dkv2_kernel<0>), grid, dim3(256), 0, s, a);
       return (int)hipGetLastError();
     }
-    if (which == 4) {  // the 32x32x16 family: dq7 (also writes dkv7's row terms), then dkv7
+    if (which == 4) {  // the 32x32x16 family: the fused launch for Lk <= 256, else dq7 (also writes dkv7's row
+                       // terms), then dkv7
+      if (a.Lk <= 256 && g_attn_v6 == 0) return attn7_bwdf(a, s);
       const int e = attn7_dq(a, s);
       return e ? e : attn7_dkv(a, s);
     }
@@ -2524,7 +2527,7 @@ FDDM_API int fddm_attn_stamps_clear() {
 
 FDDM_API int fddm_attn_set_kernels(int v6) {
   const int old = g_attn_v6;
-  g_attn_v6 = v6 ? 1 : 0;
+  g_attn_v6 = (v6 == 1 || v6 == 2) ? v6 : 0;
   return old;
 }
 

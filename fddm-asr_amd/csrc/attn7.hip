@@ -853,6 +853,261 @@ __global__ void __launch_bounds__(256, 2) dkv7_kernel(AttnArgs a) {
   }
 }
 
+// Fused backward for Lk <= 256: one workgroup of 8 waves x 32 keys holds the whole key range of one (b, h), so dQ of
+// a query tile is complete inside it and P, dP are computed once (dq7 + dkv7 compute them twice). Per 64-query tile:
+// dkv7's body (S'' = Q' K^T with the key on the lane, dP, dS; dV^T and dK^T accumulated), each wave writing its dS^T
+// slice into an LDS image ([256 keys][64 queries] bf16, dsw swizzle, zero for padding keys); after the tile's barrier
+// the 4 waves of the tile's parity compute dQ^T = K^T dS^T over all keys (one 32x32 block each; K^T and dS^T by
+// transposed reads of the K image and the dS^T image, dq7's addressing) and store it. The row terms come one tile
+// ahead from the waves themselves: each thread loads 16 B of the next tile's Q, dO and O (8 lanes per query row),
+// writes Q' = bf16(Q scale log2 e) (the forward's operand, bit for bit) and dO into the ring, and the row's
+// delta = rowsum(dO O) (8-lane reduction) and -LSE log2 e into the row-term slots. No workspace is read or written.
+template <int DM, bool MASK>
+__global__ void __launch_bounds__(512, 1) bwdf7_kernel(AttnArgs a) {
+  constexpr bool DROP = DM != 0;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smf7[];
+  const int ntiles = (a.Lk + 63) >> 6, nqt = (a.Lq + 63) >> 6;
+  unsigned char* qst = smf7;                              // [2][64 rows][128 B] Q', dsw swizzle
+  unsigned char* dost = smf7 + 2 * A7_TB;                 // [2][64 rows][128 B] dO, dsw swizzle
+  unsigned char* kim = smf7 + 4 * A7_TB;                  // [256 keys][128 B] K, dsw swizzle
+  unsigned char* dsi = smf7 + 8 * A7_TB;                  // [2][256 keys][128 B] dS^T (64 queries), dsw swizzle
+  float* rowt = (float*)(smf7 + 16 * A7_TB);              // [2][nlse2 64 | delta 64]
+  unsigned* kwd = (unsigned*)(smf7 + 16 * A7_TB + 1024);  // [2][8 waves][64 dwords] keep masks
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hh = lane >> 5, qi = lane & 31;
+  const int bh = blockIdx.x, b = bh / a.H, h = bh - b * a.H;
+  const int kw0 = 32 * w, kk = kw0 + qi;
+  const bool kv = kk < a.Lk && (!MASK || a.key_keep[(long)b * a.Lk + min(kk, a.Lk - 1)] != 0);
+  const unsigned kvm = kv ? 0xFFFFFFFFu : 0u;
+  const bf16_t* Kb = (const bf16_t*)a.K + (long)b * a.Lk * a.sk + h * DH;
+  const bf16_t* Vb = (const bf16_t*)a.V + (long)b * a.Lk * a.sv + h * DH;
+  const int nqg = (a.Lq + 31) >> 5, tw = min(kw0 >> 6, ntiles - 1), kbw = (kw0 >> 5) & 1;
+  const int kt = kk & 63, rpk = 4 * ((kt >> 3) & 3) + (kt & 3), ksh = 4 * hh + 32 * ((kt >> 2) & 1);
+
+  // ---- row terms of query tile uu into stage st: thread = (row tid >> 3, 16-B chunk tid & 7)
+  const int pr_r = tid >> 3, pr_c = tid & 7;
+  const float sl2 = a.scale * 1.4426950408889634f;
+  uint4 nx, nxo, ny;
+  float nlse = 0.f;
+  auto pload = [&](int uu) {
+    const long qc = min(64 * uu + pr_r, a.Lq - 1);
+    const long c = h * DH + pr_c * 8;
+    nx = *(const uint4*)((const bf16_t*)a.Q + ((long)b * a.Lq + qc) * a.sq + c);
+    nxo = *(const uint4*)((const bf16_t*)a.dO + ((long)b * a.Lq + qc) * a.sdo + c);
+    ny = *(const uint4*)((const bf16_t*)a.O + ((long)b * a.Lq + qc) * a.so + c);
+    nlse = a.lse[(long)bh * a.Lq + qc];
+  };
+  auto pstore = [&](int uu, int st) {
+    const bool qv = 64 * uu + pr_r < a.Lq;
+    const unsigned zm = qv ? 0xFFFFFFFFu : 0u;
+    const uint4 xd = make_uint4(nxo.x & zm, nxo.y & zm, nxo.z & zm, nxo.w & zm);
+    const u32x4v_t xv = __builtin_bit_cast(u32x4v_t, xd), yv = __builtin_bit_cast(u32x4v_t, ny);
+    float dl = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      dl += __uint_as_float(xv[j] << 16) * __uint_as_float(yv[j] << 16) +
+            __uint_as_float(xv[j] & 0xFFFF0000u) * __uint_as_float(yv[j] & 0xFFFF0000u);
+    dl += __shfl_xor(dl, 1);
+    dl += __shfl_xor(dl, 2);
+    dl += __shfl_xor(dl, 4);
+    const int off = st * A7_TB + pr_r * 128 + ((pr_c ^ dsw(pr_r)) << 4);
+    *(uint4*)(qst + off) = scale_frag(make_uint4(nx.x & zm, nx.y & zm, nx.z & zm, nx.w & zm), sl2);
+    *(uint4*)(dost + off) = xd;
+    if (pr_c == 0) {
+      rowt[st * 128 + pr_r] = qv ? -(nlse * 1.4426950408889634f) : -INFINITY;
+      rowt[st * 128 + 64 + pr_r] = qv ? dl : 0.f;
+    }
+  };
+  auto kmask = [&](int uu, int st) {  // the keep masks of the wave's 32 keys for query tile uu (as dkv7)
+    if constexpr (DROP) {
+      const int qgl = min(2 * uu + (lane >> 5), nqg - 1);
+      dma4_sv(a.dbits, (unsigned)((lm_word(bh, nqg, ntiles, qgl, tw) + 16 * kbw) * 8 + (lane & 31) * 4),
+              (const unsigned char*)(kwd + st * 512 + w * 64));
+    }
+  };
+
+  // ---- prologue: the lane's K / V rows (registers) and the K image; tile 0's row terms and keep masks
+  const int kc = min(kk, a.Lk - 1);
+  uint4 kf[4], vf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const long c = 16 * ks + 8 * hh;
+    kf[ks] = *(const uint4*)(Kb + (long)kc * a.sk + c);
+    vf[ks] = *(const uint4*)(Vb + (long)kc * a.sv + c);
+  }
+  kmask(0, 0);
+  pload(0);
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) *(uint4*)(kim + kk * 128 + (((2 * ks + hh) ^ dsw(kk)) << 4)) = kf[ks];
+  pstore(0, 0);
+  const uint4 b5 = hh ? make_uint4(0, 0, 0, 0) : make_uint4(pk_bf16(1.f, 1.f), 0u, 0u, 0u);
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    pin16(kf[ks]);
+    pin16(vf[ks]);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  int qoff[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) qoff[ks] = qi * 128 + (((2 * ks + hh) ^ dsw(qi)) << 4);
+  const int vi = lane & 15;
+  int ttr[2][2];
+#pragma unroll
+  for (int hi = 0; hi < 2; ++hi) {
+    const int row = 4 * hh + 8 * hi + (vi >> 2);
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+      const int u = 8 * db + 4 * ((lane >> 4) & 1) + (vi & 3);
+      ttr[hi][db] = row * 128 + ((((u >> 1) ^ dsw(row)) << 1 | (u & 1)) << 3);
+    }
+  }
+  // the dQ block of this wave (when its parity group runs dQ): d-block w & 1, query half (w >> 1) & 1
+  const int dqd = w & 1, dqq = (w >> 1) & 1;
+  const int ka0 = dqd ? ttr[0][1] : ttr[0][0], ka1 = dqd ? ttr[1][1] : ttr[1][0];
+  const int sb0 = dqq ? ttr[0][1] : ttr[0][0], sb1 = dqq ? ttr[1][1] : ttr[1][0];
+  const int nks = (a.Lk + 15) >> 4;  // 16-key steps holding a key < Lk
+  f32x16_t gk0 = {}, gk1 = {}, gv0 = {}, gv1 = {};  // dK^T, dV^T, d-blocks 0 / 1
+
+  auto tile = [&](const int st) {
+    const unsigned char* qimg = qst + st * A7_TB;
+    const unsigned char* doimg = dost + st * A7_TB;
+    unsigned char* dsimg = dsi + st * 4 * A7_TB + kk * 128;
+    const float* nl = rowt + st * 128;
+    const float* dl = nl + 64;
+    const unsigned* kd = kwd + st * 512 + w * 64;
+    const int dsw_k = dsw(kk);
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      unsigned kbits = 0xFFFFFFFFu;
+      if constexpr (DROP) kbits = (unsigned)(*(const uint64_t*)(kd + 32 * qb + 2 * rpk) >> ksh);
+      const float x = nl[32 * qb + qi];
+      const float xh = __uint_as_float(((unsigned)pk_bf16(x, 0.f)) << 16);
+      const float xl = (x == -INFINITY) ? 0.f : x - xh;
+      const uint4 a5 = hh ? make_uint4(0, 0, 0, 0) : make_uint4(pk_bf16(xh, xl), 0u, 0u, 0u);
+      f32x16_t sc = mfma32(a5, b5, f32x16_t{});
+      f32x16_t dp = {};
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        sc = mfma32(*(const uint4*)(qimg + qoff[ks] + qb * 32 * 128), kf[ks], sc);
+        dp = mfma32(*(const uint4*)(doimg + qoff[ks] + qb * 32 * 128), vf[ks], dp);
+      }
+      uint4 bp[2], bs[2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        unsigned pw[4], sw[4];
+#pragma unroll
+        for (int mh = 0; mh < 2; ++mh) {
+          const int r0 = 8 * s + 4 * mh, qr = 32 * qb + 8 * (2 * s + mh) + 4 * hh;
+          const f32x4_t d4 = *(const f32x4_t*)(dl + qr);
+          float pv[4], dv[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float pr = __builtin_amdgcn_exp2f(sc[r0 + e]);
+            float dd = dp[r0 + e];
+            if constexpr (DROP) {
+              const unsigned m = (unsigned)__builtin_amdgcn_sbfe((int)kbits, 8 * (2 * s + mh) + e, 1);
+              pv[e] = __uint_as_float(__float_as_uint(pr) & m);
+              dd = fmaf(__uint_as_float(__float_as_uint(dd) & m), a.drop_scale, -d4[e]);
+            } else {
+              pv[e] = pr;
+              dd -= d4[e];
+            }
+            dv[e] = pr * dd;
+          }
+          pw[2 * mh] = pk_bf16(pv[0], pv[1]);
+          pw[2 * mh + 1] = pk_bf16(pv[2], pv[3]);
+          sw[2 * mh] = pk_bf16(dv[0], dv[1]);
+          sw[2 * mh + 1] = pk_bf16(dv[2], dv[3]);
+          // dS^T for dQ: queries 32 qb + 16 s + 8 mh + 4 hh + 0..3 of the key's row (zero for padding keys)
+          *(uint2*)(dsimg + (((4 * qb + 2 * s + mh) ^ dsw_k) << 4) + 8 * hh) =
+              make_uint2(sw[2 * mh] & kvm, sw[2 * mh + 1] & kvm);
+        }
+        bp[s] = make_uint4(pw[0], pw[1], pw[2], pw[3]);
+        bs[s] = make_uint4(sw[0], sw[1], sw[2], sw[3]);
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int rb = (32 * qb + 16 * s) * 128;
+        const uint4 o0 = join_tr(tr_read(doimg + ttr[0][0] + rb), tr_read(doimg + ttr[1][0] + rb));
+        const uint4 o1 = join_tr(tr_read(doimg + ttr[0][1] + rb), tr_read(doimg + ttr[1][1] + rb));
+        gv0 = mfma32(o0, bp[s], gv0);
+        gv1 = mfma32(o1, bp[s], gv1);
+        const uint4 q0 = join_tr(tr_read(qimg + ttr[0][0] + rb), tr_read(qimg + ttr[1][0] + rb));
+        const uint4 q1 = join_tr(tr_read(qimg + ttr[0][1] + rb), tr_read(qimg + ttr[1][1] + rb));
+        gk0 = mfma32(q0, bs[s], gk0);
+        gk1 = mfma32(q1, bs[s], gk1);
+      }
+    }
+  };
+  // dQ of query tile uu (dS^T image st): this wave's 32x32 block over every 16-key step, scaled and stored
+  bf16_t* dQb = (bf16_t*)a.dQ + (long)b * a.Lq * a.sdq + h * DH;
+  auto dq_tile = [&](const int uu, const int st) {
+    const unsigned char* ds = dsi + st * 4 * A7_TB;
+    f32x16_t g = {};
+#pragma unroll 4
+    for (int j = 0; j < nks; ++j) {
+      const int rb = j * 16 * 128;
+      const uint4 ka = join_tr(tr_read(kim + ka0 + rb), tr_read(kim + ka1 + rb));
+      const uint4 sb = join_tr(tr_read(ds + sb0 + rb), tr_read(ds + sb1 + rb));
+      g = mfma32(ka, sb, g);
+    }
+    // register r: d = 32 dqd + 8 (r >> 2) + 4 hh + (r & 3), query 64 uu + 32 dqq + qi
+    const int q = 64 * uu + 32 * dqq + qi;
+    if (q < a.Lq) {
+      bf16_t* row = dQb + (long)q * a.sdq + 32 * dqd + 4 * hh;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+        *(uint2*)(row + 8 * rr) = make_uint2(pk_bf16(g[4 * rr] * a.scale, g[4 * rr + 1] * a.scale),
+                                             pk_bf16(g[4 * rr + 2] * a.scale, g[4 * rr + 3] * a.scale));
+    }
+  };
+
+  for (int uu = 0; uu < nqt; ++uu) {
+    const int st = uu & 1;
+    const bool more = uu + 1 < nqt;
+    if (more) {
+      kmask(uu + 1, st ^ 1);
+      pload(uu + 1);
+    }
+    tile(st);
+    if (more) pstore(uu + 1, st ^ 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // tile uu's dS^T image complete; tile uu + 1's ring stage and row terms in place
+    if ((w >> 2) == st) dq_tile(uu, st);
+  }
+
+  // ---- epilogue: dV = dscale dV^T, dK = ln 2 (Q'^T dS) (zero for padding keys), staged per wave in the Q' / dO
+  // ring (every wave is past its last ring read after the barrier), stored as rows
+  __syncthreads();
+  unsigned char* ost = qst + w * 4096;
+  const float fv = kv ? (DROP ? a.drop_scale : 1.f) : 0.f, fk = kv ? 0.6931471805599453f : 0.f;
+#pragma unroll
+  for (int which = 0; which < 2; ++which) {
+    const float f = which ? fk : fv;
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+#pragma unroll
+      for (int mm = 0; mm < 4; ++mm) {
+        const f32x16_t& gg = which ? (db ? gk1 : gk0) : (db ? gv1 : gv0);
+        uint2 u2;
+        u2.x = pk_bf16(gg[4 * mm] * f, gg[4 * mm + 1] * f);
+        u2.y = pk_bf16(gg[4 * mm + 2] * f, gg[4 * mm + 3] * f);
+        *(uint2*)(ost + qi * 128 + (((4 * db + mm) ^ (qi & 7)) << 4) + 8 * hh) = u2;
+      }
+    }
+    bf16_t* Gb = which ? (bf16_t*)a.dK + (long)b * a.Lk * a.sdk + h * DH : (bf16_t*)a.dV + (long)b * a.Lk * a.sdv + h * DH;
+    const long sg = which ? a.sdk : a.sdv;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = (lane >> 3) + 8 * i, c = lane & 7;
+      const uint4 v = *(const uint4*)(ost + row * 128 + ((c ^ (row & 7)) << 4));
+      if (kw0 + row < a.Lk) *(uint4*)(Gb + (long)(kw0 + row) * sg + c * 8) = v;
+    }
+  }
+}
+
 int attn7_fwd(AttnArgs& a, hipStream_t s) {
   const int dm = a.thr16 == 0 ? 0 : 1;
   const int mk = a.key_keep != nullptr ? 2 : (a.Lk % 64) != 0 ? 1 : 0;
@@ -887,6 +1142,18 @@ int attn7_dkv(AttnArgs& a, hipStream_t s) {
   if (dm) { if (a.key_keep) DKV7(1, true); else DKV7(1, false); }
   else { if (a.key_keep) DKV7(0, true); else DKV7(0, false); }
 #undef DKV7
+  return (int)hipGetLastError();
+}
+
+int attn7_bwdf(AttnArgs& a, hipStream_t s) {
+  if (a.Lk > 256) return (int)hipErrorInvalidValue;
+  const int dm = a.thr16 == 0 ? 0 : 1;
+  const size_t lds = (size_t)16 * A7_TB + 1024 + 4096;
+  dim3 grid(a.B * a.H);
+#define BWF7(D, M) hipLaunchKernelGGL((bwdf7_kernel<D, M>), grid, dim3(512), lds, s, a)
+  if (dm) { if (a.key_keep) BWF7(1, true); else BWF7(1, false); }
+  else { if (a.key_keep) BWF7(0, true); else BWF7(0, false); }
+#undef BWF7
   return (int)hipGetLastError();
 }
 

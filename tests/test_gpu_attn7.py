@@ -142,6 +142,32 @@ def test_attn7_forward_then_backward_matches_float64(B, H, Lq, Lk, masked, p):
     close(dv.float(), _back(vr.grad), rtol=6e-2, atol=1e-2, what="dv")
 
 
+@pytest.mark.parametrize("B,H,Lq,Lk,masked,p", [(2, 3, 256, 256, True, 0.1), (2, 2, 300, 200, True, 0.1),
+                                                (1, 2, 1, 256, False, 0.0), (2, 1, 65, 17, True, 0.1),
+                                                (1, 1, 200, 240, False, 0.1)])
+def test_attn7_fused_backward_matches_float64_and_split_pair(B, H, Lq, Lk, masked, p):
+    """Lk <= 256: the fused backward (bwdf7, one launch per (b, h) computing P and dP once, dQ from the dS^T image
+    in LDS; the default) against float64 autograd, and against the split pair (dq7 + dkv7, family "nofused") on the
+    same forward — two bf16 roundings of one float64 result (P, dS rounded to bf16 in both, sums in other orders)."""
+    D = H * 64
+    gen = torch.Generator().manual_seed(17 + Lq + Lk)
+    q, k, v, do = (torch.randn(B, L, D, generator=gen) for L in (Lq, Lk, Lk, Lq))
+    keep = None
+    if masked:
+        keep = torch.ones(B, Lk, dtype=torch.bool)
+        keep[B - 1, max(1, Lk - 9):] = False
+        if Lk > 130:
+            keep[0, 64:128] = False  # a padded 64-key tile inside the range: two waves with no valid key
+    _, _, gf = _run(B, H, Lq, Lk, keep, p, q, k, v, do, family="auto")
+    _, _, gs = _run(B, H, Lq, Lk, keep, p, q, k, v, do, family="nofused")
+    qr, kr, vr = (_heads(x, B, H).requires_grad_(True) for x in (q, k, v))
+    ref, _ = _ref(qr, kr, vr, keep, p, 5, 9)
+    ref.backward(_heads(do, B, H))
+    for n, a_, b_, r in zip(("dq", "dk", "dv"), gf, gs, (qr.grad, kr.grad, vr.grad)):
+        close(a_.float(), _back(r), rtol=6e-2, atol=1e-2, what=f"fused {n}")
+        close(a_.float(), b_.float(), rtol=2e-2, atol=1e-2, what=f"fused vs split {n}")
+
+
 @pytest.mark.parametrize("Lk", [256, 499])
 def test_attn7_rescale_path_with_growing_scores(Lk):
     """Scores that grow along the keys (every 32-key half-tile exceeds the running maximum by far more than the
