@@ -2369,6 +2369,9 @@ __global__ void __launch_bounds__(1024, 1) bwd3s_kernel(AttnArgs a) {
 // where the 32x32x16 family (attn7.hip) would run; 0 (default) the 32x32x16 family; 2 the same without the fused
 // backward (dq7 + dkv7 at every Lk)
 static int g_attn_v6 = 0;
+#ifndef A7_FUSED_MAXLQ
+#define A7_FUSED_MAXLQ 256  // two-pass fused backward up to this many queries (more: per-(b, h) workgroups run long)
+#endif
 static bool attn7_enabled() { return g_attn_v6 != 1; }
 
 template <typename T>
@@ -2453,9 +2456,9 @@ static int run(int which, AttnArgs& a, hipStream_t s) {
       else hipLaunchKernelGGL((dkv2_kernel<0>), grid, dim3(256), 0, s, a);
       return (int)hipGetLastError();
     }
-    if (which == 4) {  // the 32x32x16 family: the fused launch for Lk <= 256, else dq7 (also writes dkv7's row
-                       // terms), then dkv7
-      if (a.Lk <= 256 && g_attn_v6 == 0) return attn7_bwdf(a, s);
+    if (which == 4) {  // the 32x32x16 family: the fused launch for Lk <= 256 (one key pass) or Lq <= 256, Lk <= 512
+                       // (two), else dq7 (also writes dkv7's row terms), then dkv7
+      if (g_attn_v6 == 0 && (a.Lk <= 256 || (a.Lk <= 512 && a.Lq <= A7_FUSED_MAXLQ))) return attn7_bwdf(a, s);
       const int e = attn7_dq(a, s);
       return e ? e : attn7_dkv(a, s);
     }
@@ -2553,11 +2556,12 @@ FDDM_API long fddm_attn_drop_words(int B, int H, int Lq, int Lk) {
   return v2 > v3 ? v2 : v3;
 }
 
-// floats of fddm_attn_bwd's delta_ws for this shape (the larger of the two families' needs: the 32x32x16 pair's
-// [2][B*H][LqP] row terms plus the pre-scaled Q' [B*H][LqP][64] bf16, the round-4 kernels' [B*H][Lq])
+// floats of fddm_attn_bwd's delta_ws for this shape (the largest need: the two-pass fused launch's f32 dQ partials,
+// 64 per query row; the 32x32x16 pair's [2][B*H][LqP] row terms plus the pre-scaled Q' [B*H][LqP][64] bf16 take 34,
+// the round-4 kernels' [B*H][Lq] 1)
 FDDM_API long fddm_attn_bwd_ws_floats(int B, int H, int Lq, int Lk) {
   (void)Lk;
-  return 34L * B * H * ((Lq + 63) / 64 * 64);
+  return 64L * B * H * ((Lq + 63) / 64 * 64);
 }
 
 // Dropout keep bits of nsites attention sites with the same shape, rng streams stream0 + s * stream_step (site s at

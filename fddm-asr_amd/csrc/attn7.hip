@@ -853,36 +853,37 @@ __global__ void __launch_bounds__(256, 2) dkv7_kernel(AttnArgs a) {
   }
 }
 
-// Fused backward for Lk <= 256: one workgroup of 8 waves x 32 keys holds the whole key range of one (b, h), so dQ of
-// a query tile is complete inside it and P, dP are computed once (dq7 + dkv7 compute them twice). Per 64-query tile:
-// dkv7's body (S'' = Q' K^T with the key on the lane, dP, dS; dV^T and dK^T accumulated), each wave writing its dS^T
-// slice into an LDS image ([256 keys][64 queries] bf16, dsw swizzle, zero for padding keys); after the tile's barrier
-// the 4 waves of the tile's parity compute dQ^T = K^T dS^T over all keys (one 32x32 block each; K^T and dS^T by
-// transposed reads of the K image and the dS^T image, dq7's addressing) and store it. The row terms come one tile
-// ahead from the waves themselves: each thread loads 16 B of the next tile's Q, dO and O (8 lanes per query row),
-// writes Q' = bf16(Q scale log2 e) (the forward's operand, bit for bit) and dO into the ring, and the row's
-// delta = rowsum(dO O) (8-lane reduction) and -LSE log2 e into the row-term slots. No workspace is read or written.
-template <int DM, bool MASK>
+// Fused backward for Lk <= 512: one workgroup of 8 waves x 32 keys holds 256 keys of one (b, h) at a time (one pass
+// per 256 keys), so P and dP are computed once (dq7 + dkv7 compute them twice). Per 64-query tile: dkv7's body
+// (S'' = Q' K^T with the key on the lane, dP, dS; dV^T and dK^T accumulated), each wave writing its dS^T slice into
+// an LDS image ([256 keys][64 queries] bf16, dsw swizzle, zero for padding keys); after the tile's barrier the 4
+// waves of the tile's parity compute dQ^T = K^T dS^T over the pass's keys (one 32x32 block each; K^T and dS^T by
+// transposed reads of the K image and the dS^T image, dq7's addressing). With one pass dQ is stored at once; with two,
+// the first pass leaves each block's f32 partial in the workspace (written and read back by the same lane, no
+// synchronisation) and the second adds it. The row terms come one tile ahead from the waves themselves: each thread
+// loads 16 B of the next tile's Q, dO and O (8 lanes per query row), writes Q' = bf16(Q scale log2 e) (the forward's
+// operand, bit for bit) and dO into the ring, and the row's delta = rowsum(dO O) (8-lane reduction) and -LSE log2 e
+// into the row-term slots.
+template <int DM, bool MASK, int NP>
 __global__ void __launch_bounds__(512, 1) bwdf7_kernel(AttnArgs a) {
   constexpr bool DROP = DM != 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char smf7[];
-  const int ntiles = (a.Lk + 63) >> 6, nqt = (a.Lq + 63) >> 6;
+  const int ntiles = (a.Lk + 63) >> 6, nqt = (a.Lq + 63) >> 6;  // NP = (Lk + 255) / 256 key passes
   unsigned char* qst = smf7;                              // [2][64 rows][128 B] Q', dsw swizzle
   unsigned char* dost = smf7 + 2 * A7_TB;                 // [2][64 rows][128 B] dO, dsw swizzle
-  unsigned char* kim = smf7 + 4 * A7_TB;                  // [256 keys][128 B] K, dsw swizzle
+  unsigned char* kim = smf7 + 4 * A7_TB;                  // [256 keys][128 B] K of the pass, dsw swizzle
   unsigned char* dsi = smf7 + 8 * A7_TB;                  // [2][256 keys][128 B] dS^T (64 queries), dsw swizzle
   float* rowt = (float*)(smf7 + 16 * A7_TB);              // [2][nlse2 64 | delta 64]
   unsigned* kwd = (unsigned*)(smf7 + 16 * A7_TB + 1024);  // [2][8 waves][64 dwords] keep masks
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hh = lane >> 5, qi = lane & 31;
   const int bh = blockIdx.x, b = bh / a.H, h = bh - b * a.H;
-  const int kw0 = 32 * w, kk = kw0 + qi;
-  const bool kv = kk < a.Lk && (!MASK || a.key_keep[(long)b * a.Lk + min(kk, a.Lk - 1)] != 0);
-  const unsigned kvm = kv ? 0xFFFFFFFFu : 0u;
+  const int kr = 32 * w + qi;  // the lane's key within a pass (and its LDS row)
   const bf16_t* Kb = (const bf16_t*)a.K + (long)b * a.Lk * a.sk + h * DH;
   const bf16_t* Vb = (const bf16_t*)a.V + (long)b * a.Lk * a.sv + h * DH;
-  const int nqg = (a.Lq + 31) >> 5, tw = min(kw0 >> 6, ntiles - 1), kbw = (kw0 >> 5) & 1;
-  const int kt = kk & 63, rpk = 4 * ((kt >> 3) & 3) + (kt & 3), ksh = 4 * hh + 32 * ((kt >> 2) & 1);
+  const int nqg = (a.Lq + 31) >> 5, kbw = (kr >> 5) & 1;
+  const int kt = kr & 63, rpk = 4 * ((kt >> 3) & 3) + (kt & 3), ksh = 4 * hh + 32 * ((kt >> 2) & 1);
+  int kk = kr, tw = 0;  // the pass's key of the lane and the wave's 64-key tile
 
   // ---- row terms of query tile uu into stage st: thread = (row tid >> 3, 16-B chunk tid & 7)
   const int pr_r = tid >> 3, pr_c = tid & 7;
@@ -926,29 +927,6 @@ __global__ void __launch_bounds__(512, 1) bwdf7_kernel(AttnArgs a) {
     }
   };
 
-  // ---- prologue: the lane's K / V rows (registers) and the K image; tile 0's row terms and keep masks
-  const int kc = min(kk, a.Lk - 1);
-  uint4 kf[4], vf[4];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    const long c = 16 * ks + 8 * hh;
-    kf[ks] = *(const uint4*)(Kb + (long)kc * a.sk + c);
-    vf[ks] = *(const uint4*)(Vb + (long)kc * a.sv + c);
-  }
-  kmask(0, 0);
-  pload(0);
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) *(uint4*)(kim + kk * 128 + (((2 * ks + hh) ^ dsw(kk)) << 4)) = kf[ks];
-  pstore(0, 0);
-  const uint4 b5 = hh ? make_uint4(0, 0, 0, 0) : make_uint4(pk_bf16(1.f, 1.f), 0u, 0u, 0u);
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    pin16(kf[ks]);
-    pin16(vf[ks]);
-  }
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __syncthreads();
-
   int qoff[4];
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) qoff[ks] = qi * 128 + (((2 * ks + hh) ^ dsw(qi)) << 4);
@@ -967,143 +945,197 @@ __global__ void __launch_bounds__(512, 1) bwdf7_kernel(AttnArgs a) {
   const int dqd = w & 1, dqq = (w >> 1) & 1;
   const int ka0 = dqd ? ttr[0][1] : ttr[0][0], ka1 = dqd ? ttr[1][1] : ttr[1][0];
   const int sb0 = dqq ? ttr[0][1] : ttr[0][0], sb1 = dqq ? ttr[1][1] : ttr[1][0];
-  const int nks = (a.Lk + 15) >> 4;  // 16-key steps holding a key < Lk
-  f32x16_t gk0 = {}, gk1 = {}, gv0 = {}, gv1 = {};  // dK^T, dV^T, d-blocks 0 / 1
-
-  auto tile = [&](const int st) {
-    const unsigned char* qimg = qst + st * A7_TB;
-    const unsigned char* doimg = dost + st * A7_TB;
-    unsigned char* dsimg = dsi + st * 4 * A7_TB + kk * 128;
-    const float* nl = rowt + st * 128;
-    const float* dl = nl + 64;
-    const unsigned* kd = kwd + st * 512 + w * 64;
-    const int dsw_k = dsw(kk);
-#pragma unroll
-    for (int qb = 0; qb < 2; ++qb) {
-      unsigned kbits = 0xFFFFFFFFu;
-      if constexpr (DROP) kbits = (unsigned)(*(const uint64_t*)(kd + 32 * qb + 2 * rpk) >> ksh);
-      const float x = nl[32 * qb + qi];
-      const float xh = __uint_as_float(((unsigned)pk_bf16(x, 0.f)) << 16);
-      const float xl = (x == -INFINITY) ? 0.f : x - xh;
-      const uint4 a5 = hh ? make_uint4(0, 0, 0, 0) : make_uint4(pk_bf16(xh, xl), 0u, 0u, 0u);
-      f32x16_t sc = mfma32(a5, b5, f32x16_t{});
-      f32x16_t dp = {};
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        sc = mfma32(*(const uint4*)(qimg + qoff[ks] + qb * 32 * 128), kf[ks], sc);
-        dp = mfma32(*(const uint4*)(doimg + qoff[ks] + qb * 32 * 128), vf[ks], dp);
-      }
-      uint4 bp[2], bs[2];
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        unsigned pw[4], sw[4];
-#pragma unroll
-        for (int mh = 0; mh < 2; ++mh) {
-          const int r0 = 8 * s + 4 * mh, qr = 32 * qb + 8 * (2 * s + mh) + 4 * hh;
-          const f32x4_t d4 = *(const f32x4_t*)(dl + qr);
-          float pv[4], dv[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float pr = __builtin_amdgcn_exp2f(sc[r0 + e]);
-            float dd = dp[r0 + e];
-            if constexpr (DROP) {
-              const unsigned m = (unsigned)__builtin_amdgcn_sbfe((int)kbits, 8 * (2 * s + mh) + e, 1);
-              pv[e] = __uint_as_float(__float_as_uint(pr) & m);
-              dd = fmaf(__uint_as_float(__float_as_uint(dd) & m), a.drop_scale, -d4[e]);
-            } else {
-              pv[e] = pr;
-              dd -= d4[e];
-            }
-            dv[e] = pr * dd;
-          }
-          pw[2 * mh] = pk_bf16(pv[0], pv[1]);
-          pw[2 * mh + 1] = pk_bf16(pv[2], pv[3]);
-          sw[2 * mh] = pk_bf16(dv[0], dv[1]);
-          sw[2 * mh + 1] = pk_bf16(dv[2], dv[3]);
-          // dS^T for dQ: queries 32 qb + 16 s + 8 mh + 4 hh + 0..3 of the key's row (zero for padding keys)
-          *(uint2*)(dsimg + (((4 * qb + 2 * s + mh) ^ dsw_k) << 4) + 8 * hh) =
-              make_uint2(sw[2 * mh] & kvm, sw[2 * mh + 1] & kvm);
-        }
-        bp[s] = make_uint4(pw[0], pw[1], pw[2], pw[3]);
-        bs[s] = make_uint4(sw[0], sw[1], sw[2], sw[3]);
-      }
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int rb = (32 * qb + 16 * s) * 128;
-        const uint4 o0 = join_tr(tr_read(doimg + ttr[0][0] + rb), tr_read(doimg + ttr[1][0] + rb));
-        const uint4 o1 = join_tr(tr_read(doimg + ttr[0][1] + rb), tr_read(doimg + ttr[1][1] + rb));
-        gv0 = mfma32(o0, bp[s], gv0);
-        gv1 = mfma32(o1, bp[s], gv1);
-        const uint4 q0 = join_tr(tr_read(qimg + ttr[0][0] + rb), tr_read(qimg + ttr[1][0] + rb));
-        const uint4 q1 = join_tr(tr_read(qimg + ttr[0][1] + rb), tr_read(qimg + ttr[1][1] + rb));
-        gk0 = mfma32(q0, bs[s], gk0);
-        gk1 = mfma32(q1, bs[s], gk1);
-      }
-    }
-  };
-  // dQ of query tile uu (dS^T image st): this wave's 32x32 block over every 16-key step, scaled and stored
+  const uint4 b5 = hh ? make_uint4(0, 0, 0, 0) : make_uint4(pk_bf16(1.f, 1.f), 0u, 0u, 0u);
   bf16_t* dQb = (bf16_t*)a.dQ + (long)b * a.Lq * a.sdq + h * DH;
-  auto dq_tile = [&](const int uu, const int st) {
-    const unsigned char* ds = dsi + st * 4 * A7_TB;
-    f32x16_t g = {};
+  const int dsw_k = dsw(kr);
+
+#pragma unroll
+  for (int pass = 0; pass < NP; ++pass) {
+    kk = 256 * pass + kr;
+    tw = min(kk >> 6, ntiles - 1);
+    const bool kv = kk < a.Lk && (!MASK || a.key_keep[(long)b * a.Lk + min(kk, a.Lk - 1)] != 0);
+    const unsigned kvm = kv ? 0xFFFFFFFFu : 0u;
+    const int nks = (min(256, a.Lk - 256 * pass) + 15) >> 4;  // 16-key steps holding a key < Lk
+    const bool first = NP == 1 || pass == 0, last = NP == 1 || pass == NP - 1;
+
+    // ---- prologue: the lane's K / V rows (registers) and the K image; tile 0's row terms and keep masks
+    const int kc = min(kk, a.Lk - 1);
+    uint4 kf[4], vf[4];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const long c = 16 * ks + 8 * hh;
+      kf[ks] = *(const uint4*)(Kb + (long)kc * a.sk + c);
+      vf[ks] = *(const uint4*)(Vb + (long)kc * a.sv + c);
+    }
+    kmask(0, 0);
+    pload(0);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) *(uint4*)(kim + kr * 128 + (((2 * ks + hh) ^ dsw_k) << 4)) = kf[ks];
+    pstore(0, 0);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      pin16(kf[ks]);
+      pin16(vf[ks]);
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    f32x16_t gk0 = {}, gk1 = {}, gv0 = {}, gv1 = {};  // dK^T, dV^T, d-blocks 0 / 1
+
+    auto tile = [&](const int st) {
+      const unsigned char* qimg = qst + st * A7_TB;
+      const unsigned char* doimg = dost + st * A7_TB;
+      unsigned char* dsimg = dsi + st * 4 * A7_TB + kr * 128;
+      const float* nl = rowt + st * 128;
+      const float* dl = nl + 64;
+      const unsigned* kd = kwd + st * 512 + w * 64;
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        unsigned kbits = 0xFFFFFFFFu;
+        if constexpr (DROP) kbits = (unsigned)(*(const uint64_t*)(kd + 32 * qb + 2 * rpk) >> ksh);
+        const float x = nl[32 * qb + qi];
+        const float xh = __uint_as_float(((unsigned)pk_bf16(x, 0.f)) << 16);
+        const float xl = (x == -INFINITY) ? 0.f : x - xh;
+        const uint4 a5 = hh ? make_uint4(0, 0, 0, 0) : make_uint4(pk_bf16(xh, xl), 0u, 0u, 0u);
+        f32x16_t sc = mfma32(a5, b5, f32x16_t{});
+        f32x16_t dp = {};
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          sc = mfma32(*(const uint4*)(qimg + qoff[ks] + qb * 32 * 128), kf[ks], sc);
+          dp = mfma32(*(const uint4*)(doimg + qoff[ks] + qb * 32 * 128), vf[ks], dp);
+        }
+        uint4 bp[2], bs[2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          unsigned pw[4], sw[4];
+#pragma unroll
+          for (int mh = 0; mh < 2; ++mh) {
+            const int r0 = 8 * s + 4 * mh, qr = 32 * qb + 8 * (2 * s + mh) + 4 * hh;
+            const f32x4_t d4 = *(const f32x4_t*)(dl + qr);
+            float pv[4], dv[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float pr = __builtin_amdgcn_exp2f(sc[r0 + e]);
+              float dd = dp[r0 + e];
+              if constexpr (DROP) {
+                const unsigned m = (unsigned)__builtin_amdgcn_sbfe((int)kbits, 8 * (2 * s + mh) + e, 1);
+                pv[e] = __uint_as_float(__float_as_uint(pr) & m);
+                dd = fmaf(__uint_as_float(__float_as_uint(dd) & m), a.drop_scale, -d4[e]);
+              } else {
+                pv[e] = pr;
+                dd -= d4[e];
+              }
+              dv[e] = pr * dd;
+            }
+            pw[2 * mh] = pk_bf16(pv[0], pv[1]);
+            pw[2 * mh + 1] = pk_bf16(pv[2], pv[3]);
+            sw[2 * mh] = pk_bf16(dv[0], dv[1]);
+            sw[2 * mh + 1] = pk_bf16(dv[2], dv[3]);
+            // dS^T for dQ: queries 32 qb + 16 s + 8 mh + 4 hh + 0..3 of the key's row (zero for padding keys)
+            *(uint2*)(dsimg + (((4 * qb + 2 * s + mh) ^ dsw_k) << 4) + 8 * hh) =
+                make_uint2(sw[2 * mh] & kvm, sw[2 * mh + 1] & kvm);
+          }
+          bp[s] = make_uint4(pw[0], pw[1], pw[2], pw[3]);
+          bs[s] = make_uint4(sw[0], sw[1], sw[2], sw[3]);
+        }
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const int rb = (32 * qb + 16 * s) * 128;
+          const uint4 o0 = join_tr(tr_read(doimg + ttr[0][0] + rb), tr_read(doimg + ttr[1][0] + rb));
+          const uint4 o1 = join_tr(tr_read(doimg + ttr[0][1] + rb), tr_read(doimg + ttr[1][1] + rb));
+          gv0 = mfma32(o0, bp[s], gv0);
+          gv1 = mfma32(o1, bp[s], gv1);
+          const uint4 q0 = join_tr(tr_read(qimg + ttr[0][0] + rb), tr_read(qimg + ttr[1][0] + rb));
+          const uint4 q1 = join_tr(tr_read(qimg + ttr[0][1] + rb), tr_read(qimg + ttr[1][1] + rb));
+          gk0 = mfma32(q0, bs[s], gk0);
+          gk1 = mfma32(q1, bs[s], gk1);
+        }
+      }
+    };
+    // dQ of query tile uu (dS^T image st): this wave's 32x32 block over the pass's 16-key steps; the f32 partial of
+    // an earlier pass comes back from the workspace (this lane wrote it), the last pass stores bf16 dQ
+    auto dq_tile = [&](const int uu, const int st) {
+      const unsigned char* ds = dsi + st * 4 * A7_TB;
+      float4* part = (float4*)(a.delta + (((long)bh * nqt + uu) * 4 + 2 * dqq + dqd) * 1024) + lane * 4;
+      f32x16_t g = {};
+      if (!first) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float4 v = part[i];
+          g[4 * i] = v.x;
+          g[4 * i + 1] = v.y;
+          g[4 * i + 2] = v.z;
+          g[4 * i + 3] = v.w;
+        }
+      }
 #pragma unroll 4
-    for (int j = 0; j < nks; ++j) {
-      const int rb = j * 16 * 128;
-      const uint4 ka = join_tr(tr_read(kim + ka0 + rb), tr_read(kim + ka1 + rb));
-      const uint4 sb = join_tr(tr_read(ds + sb0 + rb), tr_read(ds + sb1 + rb));
-      g = mfma32(ka, sb, g);
-    }
-    // register r: d = 32 dqd + 8 (r >> 2) + 4 hh + (r & 3), query 64 uu + 32 dqq + qi
-    const int q = 64 * uu + 32 * dqq + qi;
-    if (q < a.Lq) {
-      bf16_t* row = dQb + (long)q * a.sdq + 32 * dqd + 4 * hh;
+      for (int j = 0; j < nks; ++j) {
+        const int rb = j * 16 * 128;
+        const uint4 ka = join_tr(tr_read(kim + ka0 + rb), tr_read(kim + ka1 + rb));
+        const uint4 sb = join_tr(tr_read(ds + sb0 + rb), tr_read(ds + sb1 + rb));
+        g = mfma32(ka, sb, g);
+      }
+      if (!last) {
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr)
-        *(uint2*)(row + 8 * rr) = make_uint2(pk_bf16(g[4 * rr] * a.scale, g[4 * rr + 1] * a.scale),
-                                             pk_bf16(g[4 * rr + 2] * a.scale, g[4 * rr + 3] * a.scale));
-    }
-  };
+        for (int i = 0; i < 4; ++i) part[i] = make_float4(g[4 * i], g[4 * i + 1], g[4 * i + 2], g[4 * i + 3]);
+        return;
+      }
+      // register r: d = 32 dqd + 8 (r >> 2) + 4 hh + (r & 3), query 64 uu + 32 dqq + qi
+      const int q = 64 * uu + 32 * dqq + qi;
+      if (q < a.Lq) {
+        bf16_t* row = dQb + (long)q * a.sdq + 32 * dqd + 4 * hh;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+          *(uint2*)(row + 8 * rr) = make_uint2(pk_bf16(g[4 * rr] * a.scale, g[4 * rr + 1] * a.scale),
+                                               pk_bf16(g[4 * rr + 2] * a.scale, g[4 * rr + 3] * a.scale));
+      }
+    };
 
-  for (int uu = 0; uu < nqt; ++uu) {
-    const int st = uu & 1;
-    const bool more = uu + 1 < nqt;
-    if (more) {
-      kmask(uu + 1, st ^ 1);
-      pload(uu + 1);
+    for (int uu = 0; uu < nqt; ++uu) {
+      const int st = uu & 1;
+      const bool more = uu + 1 < nqt;
+      if (more) {
+        kmask(uu + 1, st ^ 1);
+        pload(uu + 1);
+      }
+      tile(st);
+      if (more) pstore(uu + 1, st ^ 1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();  // tile uu's dS^T image complete; tile uu + 1's ring stage and row terms in place
+      if ((w >> 2) == st) dq_tile(uu, st);
     }
-    tile(st);
-    if (more) pstore(uu + 1, st ^ 1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // tile uu's dS^T image complete; tile uu + 1's ring stage and row terms in place
-    if ((w >> 2) == st) dq_tile(uu, st);
-  }
 
-  // ---- epilogue: dV = dscale dV^T, dK = ln 2 (Q'^T dS) (zero for padding keys), staged per wave in the Q' / dO
-  // ring (every wave is past its last ring read after the barrier), stored as rows
-  __syncthreads();
-  unsigned char* ost = qst + w * 4096;
-  const float fv = kv ? (DROP ? a.drop_scale : 1.f) : 0.f, fk = kv ? 0.6931471805599453f : 0.f;
+    // ---- the pass's keys: dV = dscale dV^T, dK = ln 2 (Q'^T dS) (zero for padding keys), staged per wave in the
+    // Q' / dO ring (every wave is past its last ring read after the barrier), stored as rows
+    __syncthreads();
+    unsigned char* ost = qst + w * 4096;
+    const float fv = kv ? (DROP ? a.drop_scale : 1.f) : 0.f, fk = kv ? 0.6931471805599453f : 0.f;
+    const int kw0 = 256 * pass + 32 * w;
 #pragma unroll
-  for (int which = 0; which < 2; ++which) {
-    const float f = which ? fk : fv;
+    for (int which = 0; which < 2; ++which) {
+      const float f = which ? fk : fv;
 #pragma unroll
-    for (int db = 0; db < 2; ++db) {
+      for (int db = 0; db < 2; ++db) {
 #pragma unroll
-      for (int mm = 0; mm < 4; ++mm) {
-        const f32x16_t& gg = which ? (db ? gk1 : gk0) : (db ? gv1 : gv0);
-        uint2 u2;
-        u2.x = pk_bf16(gg[4 * mm] * f, gg[4 * mm + 1] * f);
-        u2.y = pk_bf16(gg[4 * mm + 2] * f, gg[4 * mm + 3] * f);
-        *(uint2*)(ost + qi * 128 + (((4 * db + mm) ^ (qi & 7)) << 4) + 8 * hh) = u2;
+        for (int mm = 0; mm < 4; ++mm) {
+          const f32x16_t& gg = which ? (db ? gk1 : gk0) : (db ? gv1 : gv0);
+          uint2 u2;
+          u2.x = pk_bf16(gg[4 * mm] * f, gg[4 * mm + 1] * f);
+          u2.y = pk_bf16(gg[4 * mm + 2] * f, gg[4 * mm + 3] * f);
+          *(uint2*)(ost + qi * 128 + (((4 * db + mm) ^ (qi & 7)) << 4) + 8 * hh) = u2;
+        }
+      }
+      bf16_t* Gb = which ? (bf16_t*)a.dK + (long)b * a.Lk * a.sdk + h * DH : (bf16_t*)a.dV + (long)b * a.Lk * a.sdv + h * DH;
+      const long sg = which ? a.sdk : a.sdv;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = (lane >> 3) + 8 * i, c = lane & 7;
+        const uint4 v = *(const uint4*)(ost + row * 128 + ((c ^ (row & 7)) << 4));
+        if (kw0 + row < a.Lk) *(uint4*)(Gb + (long)(kw0 + row) * sg + c * 8) = v;
       }
     }
-    bf16_t* Gb = which ? (bf16_t*)a.dK + (long)b * a.Lk * a.sdk + h * DH : (bf16_t*)a.dV + (long)b * a.Lk * a.sdv + h * DH;
-    const long sg = which ? a.sdk : a.sdv;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = (lane >> 3) + 8 * i, c = lane & 7;
-      const uint4 v = *(const uint4*)(ost + row * 128 + ((c ^ (row & 7)) << 4));
-      if (kw0 + row < a.Lk) *(uint4*)(Gb + (long)(kw0 + row) * sg + c * 8) = v;
+    if (!last) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __syncthreads();  // the staging reads are done before the next pass's K image and ring stage 0 are written
     }
   }
 }
@@ -1146,13 +1178,19 @@ int attn7_dkv(AttnArgs& a, hipStream_t s) {
 }
 
 int attn7_bwdf(AttnArgs& a, hipStream_t s) {
-  if (a.Lk > 256) return (int)hipErrorInvalidValue;
+  // two key passes keep a per-lane f32 dQ partial of 64 floats per query row in the workspace (fddm_attn_bwd_ws_floats)
+  if (a.Lk > 512 || (a.Lk > 256 && a.delta == nullptr)) return (int)hipErrorInvalidValue;
   const int dm = a.thr16 == 0 ? 0 : 1;
   const size_t lds = (size_t)16 * A7_TB + 1024 + 4096;
   dim3 grid(a.B * a.H);
-#define BWF7(D, M) hipLaunchKernelGGL((bwdf7_kernel<D, M>), grid, dim3(512), lds, s, a)
-  if (dm) { if (a.key_keep) BWF7(1, true); else BWF7(1, false); }
-  else { if (a.key_keep) BWF7(0, true); else BWF7(0, false); }
+#define BWF7(D, M, P) hipLaunchKernelGGL((bwdf7_kernel<D, M, P>), grid, dim3(512), lds, s, a)
+  if (a.Lk <= 256) {
+    if (dm) { if (a.key_keep) BWF7(1, true, 1); else BWF7(1, false, 1); }
+    else { if (a.key_keep) BWF7(0, true, 1); else BWF7(0, false, 1); }
+  } else {
+    if (dm) { if (a.key_keep) BWF7(1, true, 2); else BWF7(1, false, 2); }
+    else { if (a.key_keep) BWF7(0, true, 2); else BWF7(0, false, 2); }
+  }
 #undef BWF7
   return (int)hipGetLastError();
 }

@@ -106,7 +106,8 @@ int attn7_fwd(AttnArgs& a, hipStream_t s);
 // [B*H][LqP][64] bf16 into a.delta) and dkv7 (dK, dV)
 int attn7_dq(AttnArgs& a, hipStream_t s);
 int attn7_dkv(AttnArgs& a, hipStream_t s);
-// the fused backward for Lk <= 256 (dQ, dK, dV in one launch of one workgroup per (b, h); reads no workspace)
+// the fused backward for Lk <= 512 (dQ, dK, dV in one launch of one workgroup per (b, h), one pass per 256 keys;
+// with two passes a.delta holds the f32 dQ partials, 64 floats per query row)
 int attn7_bwdf(AttnArgs& a, hipStream_t s);
 // the keep-bit producer of storage layout v3 (lane masks) and its words per site
 int attn7_drop_bits(uint64_t* out, long site_words, int nsites, int BH, int Lq, int Lk, uint64_t seed,

@@ -113,13 +113,14 @@ long fddm_attn_drop_words(int B, int H, int Lq, int Lk);
 int fddm_attn_fwd_relgate(const void* Q, long sq, const void* K, long sk, const void* V, long sv, void* O, long so,
                           const void* graw, long sgr, const float* gconst, const float* table, int B, int H, int Lq,
                           int Lk, float scale, void* hip_stream);
-/* Backward: dQ, dK, dV. bf16 with recorded or no dropout and Lk <= 256: one fused 32x32x16-MFMA launch per (b, h)
- * (csrc/attn7.hip bwdf7: P and dP computed once, dQ of each query tile from all keys in LDS; delta_ws not touched).
- * bf16 with recorded or no dropout and 256 < Lk <= 1024 (or fddm_attn_set_kernels(2)): the 32x32x16-MFMA pair (a
- * query-owned dQ launch that also writes the per-query row terms delta = rowsum(dO O) and -LSE log2(e) into delta_ws,
- * laid out [2][B*H][LqP] with LqP = Lq rounded up to 64, and Q pre-scaled by scale*log2(e) in bf16 as [B*H][LqP][64]
- * after them, then a key-owned dK/dV launch that reads them). delta_ws must hold fddm_attn_bwd_ws_floats(B, H, Lq,
- * Lk) = 34 * B*H*LqP floats whichever kernels run (ABI 5; ABI 4 needed B*H*Lq). Otherwise (fp32, rehashed dropout,
+/* Backward: dQ, dK, dV. bf16 with recorded or no dropout and Lk <= 256, or Lq <= 256 and Lk <= 512: one fused
+ * 32x32x16-MFMA launch per (b, h) (csrc/attn7.hip bwdf7: P and dP computed once, dQ of each query tile from the keys
+ * in LDS; with Lk > 256 two key passes, the first leaving f32 dQ partials in delta_ws, 64 floats per query row).
+ * Other bf16 shapes with Lk <= 1024 (or fddm_attn_set_kernels(2)): the 32x32x16-MFMA pair (a query-owned dQ launch
+ * that also writes the per-query row terms delta = rowsum(dO O) and -LSE log2(e) into delta_ws, laid out
+ * [2][B*H][LqP] with LqP = Lq rounded up to 64, and Q pre-scaled by scale*log2(e) in bf16 as [B*H][LqP][64] after
+ * them, then a key-owned dK/dV launch that reads them). delta_ws must hold fddm_attn_bwd_ws_floats(B, H, Lq, Lk)
+ * = 64 * B*H*LqP floats whichever kernels run (round 5; ABI 4 needed B*H*Lq). Otherwise (fp32, rehashed dropout,
  * longer keys, or fddm_attn_set_kernels(1)): bf16 self-attention shapes Lq == Lk <= 256 as one fused launch, else a
  * dQ launch writing delta_ws [B*H][Lq] and a dK/dV launch. */
 long fddm_attn_bwd_ws_floats(int B, int H, int Lq, int Lk);

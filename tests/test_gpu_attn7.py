@@ -144,11 +144,14 @@ def test_attn7_forward_then_backward_matches_float64(B, H, Lq, Lk, masked, p):
 
 @pytest.mark.parametrize("B,H,Lq,Lk,masked,p", [(2, 3, 256, 256, True, 0.1), (2, 2, 300, 200, True, 0.1),
                                                 (1, 2, 1, 256, False, 0.0), (2, 1, 65, 17, True, 0.1),
-                                                (1, 1, 200, 240, False, 0.1)])
+                                                (1, 1, 200, 240, False, 0.1), (2, 3, 256, 499, False, 0.1),
+                                                (2, 2, 100, 300, True, 0.1), (1, 2, 256, 512, True, 0.0),
+                                                (2, 1, 64, 257, False, 0.1)])
 def test_attn7_fused_backward_matches_float64_and_split_pair(B, H, Lq, Lk, masked, p):
-    """Lk <= 256: the fused backward (bwdf7, one launch per (b, h) computing P and dP once, dQ from the dS^T image
-    in LDS; the default) against float64 autograd, and against the split pair (dq7 + dkv7, family "nofused") on the
-    same forward — two bf16 roundings of one float64 result (P, dS rounded to bf16 in both, sums in other orders)."""
+    """Lk <= 256, or Lq <= 256 and Lk <= 512 (two key passes, the dQ partial kept in the workspace between them): the
+    fused backward (bwdf7, one launch per (b, h) computing P and dP once, dQ from the dS^T image in LDS; the default)
+    against float64 autograd, and against the split pair (dq7 + dkv7, family "nofused") on the same forward — two
+    bf16 roundings of one float64 result (P, dS rounded to bf16 in both, sums in other orders)."""
     D = H * 64
     gen = torch.Generator().manual_seed(17 + Lq + Lk)
     q, k, v, do = (torch.randn(B, L, D, generator=gen) for L in (Lq, Lk, Lk, Lq))
