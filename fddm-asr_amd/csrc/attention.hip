@@ -587,6 +587,35 @@ __global__ void __launch_bounds__(256, NG == 1 ? 4 : 2) fwd5_kernel(AttnArgs a) 
       gate[gq] = ga * (gb * a.gconst[h] - 1.f) + 2.f;
     }
   }
+  if (a.gx) {
+    // gate from the attention input x (HF modeling_wavlm.py:177-186 with the 4 + 4 pre-activations summed through
+    // the folded weights): the 4 lanes of a query (groups g) each take 16 of the head's 64 inputs, then 2 lane swaps
+    const float4* wa = (const float4*)(a.gw + 16 * g);
+    const float4* wb = (const float4*)(a.gw + 64 + 16 * g);
+#pragma unroll
+    for (int gq = 0; gq < NG; ++gq) {
+      float sa = 0.f, sb = 0.f;
+      if (qv[gq]) {
+        const bf16_t* xr = (const bf16_t*)a.gx + ((long)b * a.Lq + q[gq]) * a.sgx + h * DH + 16 * g;
+        const uint4 x0 = *(const uint4*)xr, x1 = *(const uint4*)(xr + 8);
+        const unsigned xs[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float4 A = wa[j], Bw = wb[j];
+          const float e0 = __uint_as_float(xs[2 * j] << 16), e1 = __uint_as_float(xs[2 * j] & 0xFFFF0000u);
+          const float e2 = __uint_as_float(xs[2 * j + 1] << 16), e3 = __uint_as_float(xs[2 * j + 1] & 0xFFFF0000u);
+          sa = fmaf(e0, A.x, fmaf(e1, A.y, fmaf(e2, A.z, fmaf(e3, A.w, sa))));
+          sb = fmaf(e0, Bw.x, fmaf(e1, Bw.y, fmaf(e2, Bw.z, fmaf(e3, Bw.w, sb))));
+        }
+      }
+      sa = xsum32(xsum16(sa)) + a.gw[128];
+      sb = xsum32(xsum16(sb)) + a.gw[129];
+      if (qv[gq]) {
+        const float ga = 1.f / (1.f + __expf(-sa)), gb = 1.f / (1.f + __expf(-sb));
+        gate[gq] = ga * (gb * a.gconst[h] - 1.f) + 2.f;
+      }
+    }
+  }
   for (int k = tid; k < LkP; k += 256) mfull[k] = (MASK && !key_ok(a, b, k)) ? -INFINITY : 0.f;
   {
     const float* tabh = a.table + (long)h * (2 * a.Lk - 1);
@@ -2380,7 +2409,7 @@ static int run(int which, AttnArgs& a, hipStream_t s) {
   const bool drop = a.thr16 != 0, mask = a.key_keep != nullptr || (a.Lk % 64) != 0;
   if constexpr (sizeof(T) == 2) {
     if (which == 0) {
-      const bool rel = a.table != nullptr && (a.gate != nullptr || a.graw != nullptr);
+      const bool rel = a.table != nullptr && (a.gate != nullptr || a.graw != nullptr || a.gx != nullptr);
       const int LkP = (a.Lk + 63) / 64 * 64;
       if (rel) {
         if (drop) return (int)hipErrorInvalidValue;    // WavLM attention has no dropout in the frozen encoder
@@ -2592,6 +2621,22 @@ FDDM_API int fddm_attn_fwd_relgate(const void* Q, long sq, const void* K, long s
   a.Q = Q; a.K = K; a.V = V; a.Out = O;
   a.sq = sq; a.sk = sk; a.sv = sv; a.so = so;
   a.graw = graw; a.sgr = sgr; a.gconst = gconst; a.table = table;
+  a.B = B; a.H = H; a.Lq = Lq; a.Lk = Lk; a.scale = scale;
+  return attn_dispatch(0, FDDM_BF16, a, 0.f, hs);
+}
+
+// WavLM forward with the gate computed in the kernel from the attention input x itself (bf16 rows, stride sx; the
+// head's 64 inputs against gw = [sum of gru_rel_pos_linear rows 0-3 | rows 4-7 | their bias sums], 130 floats): the
+// Q|K|V projection needs no extra gate columns and no separate gate pass runs.
+FDDM_API int fddm_attn_fwd_relgate_x(const void* Q, long sq, const void* K, long sk, const void* V, long sv, void* O,
+                                     long so, const void* x, long sx, const float* gw, const float* gconst,
+                                     const float* table, int B, int H, int Lq, int Lk, float scale, void* hs) {
+  if (!x || !gw || !gconst || !table || (((uintptr_t)x) & 15) || (((uintptr_t)gw) & 15) || sx % 8)
+    return (int)hipErrorInvalidValue;
+  AttnArgs a{};
+  a.Q = Q; a.K = K; a.V = V; a.Out = O;
+  a.sq = sq; a.sk = sk; a.sv = sv; a.so = so;
+  a.gx = x; a.sgx = sx; a.gw = gw; a.gconst = gconst; a.table = table;
   a.B = B; a.H = H; a.Lq = Lq; a.Lk = Lk; a.scale = scale;
   return attn_dispatch(0, FDDM_BF16, a, 0.f, hs);
 }

@@ -72,6 +72,9 @@ struct AttnArgs {
   const void* graw;               // WavLM gate pre-activations (bf16) at graw + (b*Lq + q)*sgr + h*8 + o, or null
   long sgr;
   const float* gconst;            // [H] gru_rel_pos_const
+  const void* gx;                 // WavLM gate from the attention input: x rows (bf16) at gx + (b*Lq + q)*sgx + h*64,
+  long sgx;                       // folded weights gw = [sum of gru rows 0-3 (64) | rows 4-7 (64) | bias sums a, b]
+  const float* gw;
   int B, H, Lq, Lk;
   float scale;
   uint64_t seed, stream;

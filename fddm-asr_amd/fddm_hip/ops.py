@@ -309,6 +309,20 @@ def attn_fwd(q, k, v, out, lse, B, H, Lq, Lk, *, key_keep=None, gate=None, table
     return out
 
 
+def attn_fwd_relgate_x(q, k, v, out, x, gw, gconst, table, B, H, L, scale=None):
+    """WavLM attention (bf16) with the gate computed in the kernel from the attention input x [B*L, H*64] (bf16, row
+    stride x.stride(0)) and the folded gru_rel_pos_linear weights gw (130 floats: sum of weight rows 0-3, rows 4-7,
+    the two bias sums; models/wavlm.py)."""
+    _chk(q.dtype == k.dtype == v.dtype == out.dtype == x.dtype == torch.bfloat16, "relgate attention is bf16")
+    _chk(x.stride(-1) == 1 and x.shape[1] >= H * 64 and x.data_ptr() % 16 == 0, "gate input layout")
+    _chk(gw.dtype == torch.float32 and gw.numel() >= 130 and gw.is_contiguous() and gw.data_ptr() % 16 == 0,
+         "folded gate weights")
+    sc = 1.0 / math.sqrt(64) if scale is None else scale
+    call("fddm_attn_fwd_relgate_x", ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out),
+         out.stride(0), ptr(x), x.stride(0), ptr(gw), ptr(gconst), ptr(table), B, H, L, L, float(sc), stream())
+    return out
+
+
 def attn_fwd_relgate(q, k, v, out, graw, gconst, table, B, H, L, scale=None):
     """WavLM attention (bf16) with the gate computed in the kernel from graw [B*L, >= H*8] (row stride
     graw.stride(0)): 8 gru_rel_pos_linear pre-activations per (token, head)."""

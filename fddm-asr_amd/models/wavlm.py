@@ -20,6 +20,19 @@ import torch.nn as nn
 from fddm_hip import ops
 from fddm_hip import runtime as rt
 
+# where the bf16 encoder's attention gate comes from (HF modeling_wavlm.py:177-186): "x" (default) the attention
+# kernel computes it from the attention input with the folded gru_rel_pos_linear weights; "cols" 8*H extra Q|K|V
+# output columns (round 2-5; at the 192-CU encoder cap 2400 columns take 4 tile rounds instead of 3); "separate" the
+# fddm_wavlm_gate pass (the fp32 path's)
+GATE_MODE = os.environ.get("FDDM_WAVLM_GATE", "x")
+
+
+def _fold_gate(lin):
+    """gru_rel_pos_linear (8 x 64) folded for the in-kernel gate: the reference sums pre-activations 0-3 and 4-7
+    (HF modeling_wavlm.py:181-183), so [sum of weight rows 0-3 | rows 4-7 | bias sum 0-3, 4-7] (130 floats)."""
+    w, b = lin.weight.detach().float(), lin.bias.detach().float()
+    return torch.cat([w[:4].sum(0), w[4:].sum(0), b[:4].sum().reshape(1), b[4:].sum().reshape(1)]).contiguous()
+
 WAVLM_BASE = dict(hidden_size=768, num_hidden_layers=12, num_attention_heads=12, intermediate_size=3072,
                   conv_dim=(512,) * 7, conv_kernel=(10, 3, 3, 3, 3, 2, 2), conv_stride=(5, 2, 2, 2, 2, 2, 2),
                   conv_bias=False, num_conv_pos_embeddings=128, num_conv_pos_embedding_groups=16, num_buckets=320,
@@ -139,7 +152,7 @@ class WavLMModel(nn.Module):
                 a = L.attention
                 qkv_w = [a.q_proj.weight, a.k_proj.weight, a.v_proj.weight]
                 qkv_b = [a.q_proj.bias, a.k_proj.bias, a.v_proj.bias]
-                if cd == torch.bfloat16:
+                if cd == torch.bfloat16 and GATE_MODE == "cols":
                     # gate pre-activations of every head as 8*H extra output columns (block-diagonal copies of
                     # gru_rel_pos_linear), consumed by the attention kernel (no separate gate pass)
                     gw = a.gru_rel_pos_linear.weight.detach().float()
@@ -155,6 +168,7 @@ class WavLMModel(nn.Module):
                     gru=(a.gru_rel_pos_linear.weight.detach().float().contiguous(),
                          a.gru_rel_pos_linear.bias.detach().float().contiguous(),
                          a.gru_rel_pos_const.detach().float().reshape(-1).contiguous()),
+                    gw=_fold_gate(a.gru_rel_pos_linear),
                     ln1=(L.layer_norm.weight.detach().float(), L.layer_norm.bias.detach().float()),
                     f1=(T(L.feed_forward.intermediate_dense.weight), L.feed_forward.intermediate_dense.bias.detach().float()),
                     f2=(T(L.feed_forward.output_dense.weight), L.feed_forward.output_dense.bias.detach().float()),
@@ -252,7 +266,9 @@ class WavLMModel(nn.Module):
         for Lp in P["layers"]:
             qkv = ops.linear(x, Lp["qkv"], Lp["bqkv"], out_dtype=cd)
             o = torch.empty(B * S, E, device=dev, dtype=cd)
-            if cd == torch.bfloat16:
+            if cd == torch.bfloat16 and GATE_MODE == "x":
+                ops.attn_fwd_relgate_x(qkv, qkv[:, E:], qkv[:, 2 * E:], o, x, Lp["gw"], Lp["gru"][2], table, B, H, S)
+            elif cd == torch.bfloat16 and GATE_MODE == "cols":
                 ops.attn_fwd_relgate(qkv, qkv[:, E:], qkv[:, 2 * E:], o, qkv[:, 3 * E:], Lp["gru"][2], table, B, H, S)
             else:
                 gate = ops.wavlm_gate(x, Lp["gru"][0], Lp["gru"][1], Lp["gru"][2], B, S, H)

@@ -113,6 +113,13 @@ long fddm_attn_drop_words(int B, int H, int Lq, int Lk);
 int fddm_attn_fwd_relgate(const void* Q, long sq, const void* K, long sk, const void* V, long sv, void* O, long so,
                           const void* graw, long sgr, const float* gconst, const float* table, int B, int H, int Lq,
                           int Lk, float scale, void* hip_stream);
+/* WavLM variant (bf16) with the gate computed in the kernel from the attention input x (bf16 rows at x + (b*Lq+q)*sx,
+ * head h's 64 inputs at + h*64) and the folded gru_rel_pos_linear weights gw = [sum of weight rows 0-3 (64 floats) |
+ * rows 4-7 (64) | sum of bias 0-3 | sum of bias 4-7] (the reference sums the 4 + 4 pre-activations, so the sums of
+ * the rows give the same gate): no extra Q|K|V columns and no gate pass — HF modeling_wavlm.py:177-186. */
+int fddm_attn_fwd_relgate_x(const void* Q, long sq, const void* K, long sk, const void* V, long sv, void* O, long so,
+                            const void* x, long sx, const float* gw, const float* gconst, const float* table, int B,
+                            int H, int Lq, int Lk, float scale, void* hip_stream);
 /* Backward: dQ, dK, dV. bf16 with recorded or no dropout and Lk <= 256, or Lq <= 256 and Lk <= 512: one fused
  * 32x32x16-MFMA launch per (b, h) (csrc/attn7.hip bwdf7: P and dP computed once, dQ of each query tile from the keys
  * in LDS; with Lk > 256 two key passes, the first leaving f32 dQ partials in delta_ws, 64 floats per query row).

@@ -588,6 +588,44 @@ def test_attention_relgate_matches_gate_kernel_path(S):
     close(out.float(), ref.transpose(1, 2).reshape(B * S, E), rtol=2e-2, what="relgate vs float64")
 
 
+@pytest.mark.parametrize("S", [499, 70])
+def test_attention_relgate_x_matches_gate_kernel_path(S):
+    """WavLM attention with the gate computed in the kernel from the attention input x and the folded
+    gru_rel_pos_linear weights (fddm_attn_fwd_relgate_x, models/wavlm.py _fold_gate) vs the two-pass path
+    (fddm_wavlm_gate + fddm_attn_fwd) and vs float64 torch (per-row pre-activations summed as HF does) on the same
+    bf16 inputs; x given with a padded row stride."""
+    o = ops()
+    from models.wavlm import _fold_gate
+    B, H, E = 2, 12, 768
+    gen = torch.Generator(device=dev).manual_seed(41)
+    xb = torch.randn(B * S, E + 64, device=dev, generator=gen).bfloat16()
+    x = xb[:, :E]
+    qkv = torch.randn(B * S, 3 * E, device=dev, generator=gen).bfloat16()
+    lin = torch.nn.Linear(64, 8).to(dev)
+    with torch.no_grad():
+        lin.weight.copy_(torch.randn(8, 64, device=dev, generator=gen) * 0.2)
+        lin.bias.copy_(torch.randn(8, device=dev, generator=gen) * 0.1)
+    cst = torch.rand(H, device=dev, generator=gen) + 0.5
+    table = torch.randn(H, 2 * S - 1, device=dev, generator=gen)
+    out = torch.empty(B * S, E, device=dev, dtype=torch.bfloat16)
+    o.attn_fwd_relgate_x(qkv, qkv[:, E:], qkv[:, 2 * E:], out, x, _fold_gate(lin), cst, table, B, H, S)
+    gate = o.wavlm_gate(x.contiguous(), lin.weight.detach(), lin.bias.detach(), cst, B, S, H)
+    out2 = torch.empty_like(out)
+    o.attn_fwd(qkv, qkv[:, E:], qkv[:, 2 * E:], out2, None, B, H, S, S, gate=gate, table=table)
+    close(out.float(), out2.float(), rtol=2e-2, what="relgate_x vs gate kernel")
+    r = torch.einsum("nhd,od->nho", x.double().view(B * S, H, 64), lin.weight.detach().double()) + \
+        lin.bias.detach().double()
+    r = r.view(B, S, H, 8)
+    ga, gb = torch.sigmoid(r[..., :4].sum(-1)), torch.sigmoid(r[..., 4:].sum(-1))
+    gref = (ga * (gb * cst.double() - 1) + 2).permute(0, 2, 1)                      # [B, H, S]
+    hv = lambda t: t.double().view(B, S, H, 64).transpose(1, 2)  # noqa: E731
+    q_, k_, v_ = hv(qkv[:, :E]), hv(qkv[:, E:2 * E]), hv(qkv[:, 2 * E:])
+    rel = torch.arange(S, device=dev)[None, :] - torch.arange(S, device=dev)[:, None] + S - 1   # key - query + S-1
+    sc = q_ @ k_.transpose(-1, -2) / 8.0 + gref[..., None] * table.double()[:, rel][None]
+    ref = torch.softmax(sc, -1) @ v_
+    close(out.float(), ref.transpose(1, 2).reshape(B * S, E), rtol=2e-2, what="relgate_x vs float64")
+
+
 # ----------------------------------------------------------------------------- LN / RoPE / embed
 @pytest.mark.parametrize("fold", [False, True])
 @pytest.mark.parametrize("film", [False, True])
