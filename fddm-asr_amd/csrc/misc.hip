@@ -337,7 +337,7 @@ FDDM_API int fddm_cast(int src_dtype, int dst_dtype, const void* x, void* y, lon
 
 FDDM_API const char* fddm_error_string(int code) { return hipGetErrorString((hipError_t)code); }
 
-FDDM_API int fddm_abi_version() { return 5; }
+FDDM_API int fddm_abi_version() { return 6; }  // 6: fddm_attn_bwd workspace 64 B*H*LqP floats (fused backward)
 
 // HIP-graph replays of the train step (fddm_hip.graphs.StepGraphs): launches enqueued while `off` is set read their
 // dropout seed as seed + *off (common.h eff_seed); null restores plain seeds. Returns the previous setting's state

@@ -127,7 +127,7 @@ int fddm_attn_fwd_relgate_x(const void* Q, long sq, const void* K, long sk, cons
  * that also writes the per-query row terms delta = rowsum(dO O) and -LSE log2(e) into delta_ws, laid out
  * [2][B*H][LqP] with LqP = Lq rounded up to 64, and Q pre-scaled by scale*log2(e) in bf16 as [B*H][LqP][64] after
  * them, then a key-owned dK/dV launch that reads them). delta_ws must hold fddm_attn_bwd_ws_floats(B, H, Lq, Lk)
- * = 64 * B*H*LqP floats whichever kernels run (round 5; ABI 4 needed B*H*Lq). Otherwise (fp32, rehashed dropout,
+ * = 64 * B*H*LqP floats whichever kernels run (ABI 6; ABI 5 needed 34, ABI 4 B*H*Lq). Otherwise (fp32, rehashed dropout,
  * longer keys, or fddm_attn_set_kernels(1)): bf16 self-attention shapes Lq == Lk <= 256 as one fused launch, else a
  * dQ launch writing delta_ws [B*H][Lq] and a dK/dV launch. */
 long fddm_attn_bwd_ws_floats(int B, int H, int Lq, int Lk);

@@ -17,7 +17,7 @@ def test_library_exports_every_declared_symbol():
     assert len(names) >= 25
     for n in names:
         assert hasattr(L, n), n
-    assert L.fddm_abi_version() == 5
+    assert L.fddm_abi_version() == 6
     assert b"no error" in L.fddm_error_string(0).lower()
 
 
