@@ -2389,11 +2389,12 @@ __global__ void __launch_bounds__(1024, 1) bwd3s_kernel(AttnArgs a) {
 }
 
 // Kernel choice per launch shape (bf16; the fp32 parity mode runs the generic kernels):
-//  forward  WavLM gated rel-pos bias: fwd5 (streamed ring, bias slice staged); decoder, Lk <= 1024: fwd6 (streamed ring;
-//           dropout keep bits precomputed (bits_ready) or drawn from LDS tables and recorded); Lk > 1024: fwd2.
-//  backward Lq == Lk <= 256 with recorded bits or no dropout: bwd3s (one fused launch per (b, h));
-//           else dq4 + dkv4 (streamed rings) for L <= 1024 with recorded bits or no dropout; dq2 + dkv2 otherwise
-//           (keep bits rehashed when the forward recorded none, or longer sequences).
+//  forward  WavLM gated rel-pos bias: fwd5 (streamed ring, bias slice staged; gate from a precomputed row, from the
+//           projection's extra columns, or from the attention input); decoder, Lk <= 1024: fwd7 (attn7.hip, 32x32x16;
+//           keep bits from the producer); Lk > 1024: fwd2.
+//  backward decoder, recorded bits or no dropout: Lk <= 256, or Lq <= 256 and Lk <= 512: bwdf7 (attn7.hip, one
+//           fused launch per (b, h), one pass per 256 keys); other Lk <= 1024: dq7 + dkv7; longer or rehashed:
+//           dq2 + dkv2. Under fddm_attn_set_kernels(1) the round-4 kernels: bwd3s (Lq == Lk <= 256), dq4 + dkv4.
 // fddm_attn_set_kernels (tests / tools only): 1 selects the round-4 16x16x32 kernels (fwd6 / dq4 / dkv4 / bwd3s)
 // where the 32x32x16 family (attn7.hip) would run; 0 (default) the 32x32x16 family; 2 the same without the fused
 // backward (dq7 + dkv7 at every Lk)
