@@ -105,14 +105,14 @@ def align_speech(z_speech: torch.Tensor, L: int) -> torch.Tensor:
 def cu_caps(dev) -> dict:
     """CU caps of the encoder's persistent GEMMs while they run beside the decoder (_encoded): "enc" for the
     transformer layers (FDDM_ENC_CUS, default 3/4 of the chip), "conv" / "conv_rest" for conv layer 1 / layers 2-6
-    (FDDM_ENC_CUS_CONV / _CONV2, default half). Under data parallelism (world > 1) every cap is lowered by "coll"
-    (FDDM_COLL_CUS, default 8 = one per XCD): the CUs handed back stay free of persistent workgroups for RCCL's
-    all-reduce kernels, which run on their own stream under the backward (fddm_hip.dist.OverlapReducer) and would
-    otherwise compete for the CUs the decoder leaves between its launches while a persistent GEMM holds its share
-    for its whole launch. Single-GPU runs keep the measured caps (coll 0)."""
+    (FDDM_ENC_CUS_CONV / _CONV2, default half). FDDM_COLL_CUS (default 0) lowers every cap by that many CUs, left
+    free of persistent workgroups for RCCL's all-reduce kernels under data parallelism. It stays 0 by default: the
+    caps sit on tile-round boundaries — the WavLM projections have 189 / 567 / 756 tiles of 256^2, 1 / 3 / 4 rounds
+    at 192 CUs; at 184 the 189-tile launches take 2 rounds — and on one GPU the caps a reserve of 8 leaves (184 /
+    120) made the C2 step 12 % slower (9.70 -> 10.88 ms, tools/probe/dpcaps.sh), against an unmeasured gain for the
+    collectives, which run on their own stream beside the decoder's short launches."""
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-    world = fdist.world()
-    coll = int(os.environ.get("FDDM_COLL_CUS", 8 if world > 1 else 0))
+    coll = int(os.environ.get("FDDM_COLL_CUS", 0))
     enc = int(os.environ.get("FDDM_ENC_CUS", ncu * 3 // 4))
     conv = int(os.environ.get("FDDM_ENC_CUS_CONV", ncu // 2))
     conv_rest = int(os.environ.get("FDDM_ENC_CUS_CONV2", conv))
