@@ -217,3 +217,34 @@ def test_attention_dropout_contract_v2():
     # pairwise independence of neighbouring keys: P(both kept) ~ 0.81
     both = (k[..., 1:] & k[..., :-1]).float().mean().item()
     assert abs(both - 0.81) < 0.015
+
+
+def test_attention_workspace_size_query():
+    """fddm_attn_bwd_ws_floats (ABI 6): 64 floats per (b, h, query row) with Lq rounded up to 64 — the fused
+    backward's f32 dQ partials for two key passes (csrc/attn7.hip bwdf7), the largest need of any backward kernel."""
+    import ctypes
+    from fddm_hip import _lib
+    f = _lib.lib().fddm_attn_bwd_ws_floats
+    f.restype = ctypes.c_long
+    for B, H, Lq, Lk in ((32, 8, 256, 256), (32, 8, 256, 499), (16, 12, 512, 512), (1, 1, 1, 1), (2, 3, 65, 300)):
+        assert f(B, H, Lq, Lk) == 64 * B * H * ((Lq + 63) // 64 * 64)
+
+
+def test_wavlm_folded_gate_weights_match_summed_preactivations():
+    """models/wavlm.py _fold_gate: the in-kernel WavLM gate (fddm_attn_fwd_relgate_x) uses the sums of
+    gru_rel_pos_linear's rows 0-3 / 4-7 and of their biases; by linearity that equals summing the 8 pre-activations
+    as HF modeling_wavlm.py:181-183 does (float64 check on random inputs)."""
+    from models.wavlm import _fold_gate
+    g = torch.Generator().manual_seed(5)
+    lin = torch.nn.Linear(64, 8).double()
+    with torch.no_grad():
+        lin.weight.copy_(torch.randn(8, 64, generator=g, dtype=torch.float64))
+        lin.bias.copy_(torch.randn(8, generator=g, dtype=torch.float64))
+    x = torch.randn(100, 64, generator=g, dtype=torch.float64)
+    pre = lin(x).detach()
+    gw = _fold_gate(lin).double()
+    assert gw.shape == (130,)
+    ra = x @ gw[:64] + gw[128]
+    rb = x @ gw[64:128] + gw[129]
+    assert torch.allclose(ra, pre[:, :4].sum(-1), rtol=1e-6, atol=1e-5)
+    assert torch.allclose(rb, pre[:, 4:].sum(-1), rtol=1e-6, atol=1e-5)
