@@ -1,5 +1,5 @@
 """One decoder-attention shape, both kernel families, a few launches each (for rocprofv3 counter passes).
-  python tools/probe/attn7_one.py [c2self|c2cross|c4self|c4cross] [fwd|bwd|both]"""
+  python tools/probe/attn7_one.py [c2self|c2cross|c4self|c4cross] [fwd|bwd|both] [families, default v6,auto]"""
 import os
 import sys
 
@@ -29,7 +29,7 @@ db = ops.drop_bits(B, H, Lq, Lk, dev)
 o = torch.empty(B * Lq, H * 64, device=dev, dtype=bf)
 lse = torch.empty(B * H, Lq, device=dev)
 dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
-for fam in ("v6", "auto"):
+for fam in (sys.argv[3] if len(sys.argv) > 3 else "v6,auto").split(","):
     old = ops.attn_force_kernels(fam)
     ops.attn_drop_bits(db.view(1, -1), 1, B, H, Lq, Lk, 0.1, 1, 1, 0)
     for _ in range(5):
