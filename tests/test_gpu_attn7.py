@@ -146,7 +146,8 @@ def test_attn7_forward_then_backward_matches_float64(B, H, Lq, Lk, masked, p):
                                                 (1, 2, 1, 256, False, 0.0), (2, 1, 65, 17, True, 0.1),
                                                 (1, 1, 200, 240, False, 0.1), (2, 3, 256, 499, False, 0.1),
                                                 (2, 2, 100, 300, True, 0.1), (1, 2, 256, 512, True, 0.0),
-                                                (2, 1, 64, 257, False, 0.1)])
+                                                (2, 1, 64, 257, False, 0.1), (2, 2, 200, 512, True, 0.1),
+                                                (2, 2, 300, 400, True, 0.1)])  # the last: Lq > 256 -> the pair
 def test_attn7_fused_backward_matches_float64_and_split_pair(B, H, Lq, Lk, masked, p):
     """Lk <= 256, or Lq <= 256 and Lk <= 512 (two key passes, the dQ partial kept in the workspace between them): the
     fused backward (bwdf7, one launch per (b, h) computing P and dP once, dQ from the dS^T image in LDS; the default)
