@@ -2392,15 +2392,16 @@ __global__ void __launch_bounds__(1024, 1) bwd3s_kernel(AttnArgs a) {
 //  forward  WavLM gated rel-pos bias: fwd5 (streamed ring, bias slice staged; gate from a precomputed row, from the
 //           projection's extra columns, or from the attention input); decoder, Lk <= 1024: fwd7 (attn7.hip, 32x32x16;
 //           keep bits from the producer); Lk > 1024: fwd2.
-//  backward decoder, recorded bits or no dropout: Lk <= 256, or Lq <= 256 and Lk <= 512: bwdf7 (attn7.hip, one
-//           fused launch per (b, h), one pass per 256 keys); other Lk <= 1024: dq7 + dkv7; longer or rehashed:
+//  backward decoder, recorded bits or no dropout: Lq <= 256 and Lk <= 512: bwdf7 (attn7.hip, one fused launch per
+//           (b, h), one pass per 256 keys); other Lk <= 1024: dq7 + dkv7; longer or rehashed:
 //           dq2 + dkv2. Under fddm_attn_set_kernels(1) the round-4 kernels: bwd3s (Lq == Lk <= 256), dq4 + dkv4.
 // fddm_attn_set_kernels (tests / tools only): 1 selects the round-4 16x16x32 kernels (fwd6 / dq4 / dkv4 / bwd3s)
 // where the 32x32x16 family (attn7.hip) would run; 0 (default) the 32x32x16 family; 2 the same without the fused
 // backward (dq7 + dkv7 at every Lk)
 static int g_attn_v6 = 0;
 #ifndef A7_FUSED_MAXLQ
-#define A7_FUSED_MAXLQ 256  // two-pass fused backward up to this many queries (more: per-(b, h) workgroups run long)
+#define A7_FUSED_MAXLQ 256  // fused backward up to this many queries, one or two key passes (more: one workgroup per
+                            // (b, h) walks every 64-query tile, measured slower than dq7 + dkv7 at Lq 512)
 #endif
 static bool attn7_enabled() { return g_attn_v6 != 1; }
 
@@ -2486,9 +2487,9 @@ static int run(int which, AttnArgs& a, hipStream_t s) {
       else hipLaunchKernelGGL((dkv2_kernel<0>), grid, dim3(256), 0, s, a);
       return (int)hipGetLastError();
     }
-    if (which == 4) {  // the 32x32x16 family: the fused launch for Lk <= 256 (one key pass) or Lq <= 256, Lk <= 512
-                       // (two), else dq7 (also writes dkv7's row terms), then dkv7
-      if (g_attn_v6 == 0 && (a.Lk <= 256 || (a.Lk <= 512 && a.Lq <= A7_FUSED_MAXLQ))) return attn7_bwdf(a, s);
+    if (which == 4) {  // the 32x32x16 family: the fused launch for Lq <= 256 and Lk <= 512 (one or two key passes),
+                       // else dq7 (also writes dkv7's row terms), then dkv7
+      if (g_attn_v6 == 0 && a.Lk <= 512 && a.Lq <= A7_FUSED_MAXLQ) return attn7_bwdf(a, s);
       const int e = attn7_dq(a, s);
       return e ? e : attn7_dkv(a, s);
     }
@@ -2656,7 +2657,8 @@ FDDM_API int fddm_attn_bwd(int dtype, const void* Q, long sq, const void* K, lon
   a.sq = sq; a.sk = sk; a.sv = sv; a.so = so; a.sdo = sdo; a.sdq = sdq; a.sdk = sdk; a.sdv = sdv;
   a.key_keep = key_keep;
   a.B = B; a.H = H; a.Lq = Lq; a.Lk = Lk; a.scale = scale; a.seed = seed; a.stream = stream; a.seed_off = g_seed_off;
-  // bf16 with recorded or no dropout, Lk <= 1024: the 32x32x16 kernels (attn7.hip; delta_ws holds 34 * B*H*LqP)
+  // bf16 with recorded or no dropout, Lk <= 1024: the 32x32x16 kernels (attn7.hip; delta_ws holds
+  // fddm_attn_bwd_ws_floats = 64 * B*H*LqP floats)
   if (dtype == FDDM_BF16 && attn7_enabled() && Lk <= 1024 && (drop_p <= 0.f || drop_bits))
     return attn_dispatch(4, dtype, a, drop_p, hs);
   // self-attention shapes (Lq == Lk <= 256, bf16, no rehashed dropout): dQ, dK and dV in one fused launch

@@ -351,10 +351,12 @@ __global__ void __launch_bounds__(256, A7_FWD_WPS) fwd7_kernel(AttnArgs a) {
       };
       // fast path: 2^sc against the current reference; slow path (a query block's first half-tile, or a lane sum
       // above 2^8 / inf / NaN): the half's maximum, a new bf16 reference, O and l rescaled, 2^(sc - (rf' - rf))
+      // (also while a row has no finite reference yet, m = -inf: the fast path bounds the sum only from above, so a
+      // row whose first keys were all masked and whose later scores sit below 2^-126 of rf = 0 would sum to 0)
       bool slow = first;
       if (!first) {
         expall(0.f);
-        slow = __any(!(ls <= 256.f));
+        slow = __any(!(ls <= 256.f) || m == -INFINITY);
       }
       if (slow) {
         float tm = fmaxf(sc[0], sc[1]);

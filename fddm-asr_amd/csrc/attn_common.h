@@ -63,8 +63,10 @@ struct AttnArgs {
   const void *Q, *K, *V, *O, *dO;
   void *Out, *dQ, *dK, *dV;
   float* lse;
-  float* delta;  // [B*H][Lq] workspace: rowsum(dO*O), written by dq_kernel
-  uint64_t* dbits;  // [B*H][ceil(Lk/64)][Lq] dropout keep bits: written by the forward, read by the backward
+  float* delta;  // backward workspace, fddm_attn_bwd_ws_floats = 64 * B*H*LqP floats: the round-4 kernels' rowsum(dO*O)
+                 // [B*H][Lq]; dq7's row terms [2][B*H][LqP] + pre-scaled Q' [B*H][LqP][64] bf16; bwdf7's f32 dQ partials
+  uint64_t* dbits;  // dropout keep bits, fddm_attn_drop_words per site: layout v3 lane masks + v4 per-lane dwords
+                    // (attn7.hip lm_word / lb_dword) for the 32x32x16 family, else round-4 words [B*H][ntiles][Lq]
   long sq, sk, sv, so, sdo, sdq, sdk, sdv;
   const unsigned char* key_keep;  // [B][Lk] or null
   const float* gate;              // [B*H][Lq] or null (WavLM)

@@ -77,6 +77,23 @@ def world() -> int:
     return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
 
 
+_FORCE_DP = False
+
+
+def force_dp(on: bool) -> bool:
+    """Tests only: run the DP exchange (rank-0 broadcast, overlapped all-reduce, global-batch L_fd statistics) even in
+    a world-size-1 process group, so the collective path (e.g. RCCL's) executes on a one-GPU box. Returns the previous
+    setting."""
+    global _FORCE_DP
+    old, _FORCE_DP = _FORCE_DP, bool(on)
+    return old
+
+
+def dp_active() -> bool:
+    """True when the train step exchanges gradients: more than one rank, or a forced world-size-1 group."""
+    return world() > 1 or (_FORCE_DP and dist.is_available() and dist.is_initialized())
+
+
 def default_group():
     return dist.group.WORLD
 
@@ -96,7 +113,7 @@ def broadcast_params(tensors, src: int = 0, bucket_bytes: int = BUCKET_BYTES) ->
     (what DistributedDataParallel's constructor does): replicas that start from different random inits would
     otherwise drift apart under the averaged gradients. The copies back go through Tensor.copy_ so each tensor's
     version counter moves and every cached low-precision / permuted copy of it is rebuilt."""
-    if world() <= 1:
+    if not dp_active():
         return
     by_dtype = {}
     for t in tensors:
@@ -124,7 +141,7 @@ def allreduce_grads(params, bucket_bytes: int = BUCKET_BYTES, average: bool = Tr
     average=False leaves the SUM, for a consumer that applies 1/W itself (the fused AdamW's grad_scale), which saves
     a pass over every gradient."""
     W = world()
-    if W <= 1:
+    if not dp_active():
         return
     params = list(params)
     arena = next((a for a in (getattr(p, "_fddm_arena", None) for p in params) if a is not None), None)

@@ -112,8 +112,9 @@ class StepGraphs:
     Validity: a graph reads parameters, cached bf16 weights, optimizer moments / chunk tables and gradient-arena views
     by address. It is dropped (and the step runs eagerly, then recaptures) when the runtime cache epoch changes
     (clear_cache), when any trainable parameter is replaced or changed by a torch op (data_ptr / _version), when
-    the optimizer rebuilt its tables (FusedAdamW.table_epoch) or when an optimizer hyperparameter the AdamW launch
-    takes by value changed (lr, weight decay, betas, eps: `_hparams`). The two kinds share one memory pool (they
+    the optimizer rebuilt its tables (FusedAdamW.table_epoch), when an optimizer hyperparameter the AdamW launch
+    takes by value changed (lr, weight decay, betas, eps: `_hparams`) or when the clip_and_step arguments the step
+    passes changed (max_norm, grad_scale: the caller's `step_args`). The two kinds share one memory pool (they
     replay on one stream, never concurrently; their outputs stay live).
 
     Fixed shapes only: the graphs are keyed by the step's input shapes, and a batch of another shape drops both kinds
@@ -136,29 +137,29 @@ class StepGraphs:
     @staticmethod
     def _hparams(optimizer):
         """The optimizer hyperparameters a captured AdamW launch bakes in as kernel arguments (lr, weight decay,
-        betas, eps per param group; max_norm / grad_scale where the optimizer keeps them): a change (e.g. an lr
-        schedule writing param_groups[i]['lr']) must recapture, or replays would keep the captured values."""
-        groups = tuple((float(g.get("lr", 0.0)), float(g.get("weight_decay", 0.0)),
-                        tuple(float(b) for b in g.get("betas", ())), float(g.get("eps", 0.0)))
-                       for g in getattr(optimizer, "param_groups", ()))
-        extra = tuple(getattr(optimizer, k, None) for k in ("max_norm", "grad_scale"))
-        return groups, extra
+        betas, eps per param group): a change (e.g. an lr schedule writing param_groups[i]['lr']) must recapture, or
+        replays would keep the captured values. max_norm / grad_scale are clip_and_step() arguments, not optimizer
+        state: the caller passes the values its step uses as `step_args`, and they join the token too."""
+        return tuple((float(g.get("lr", 0.0)), float(g.get("weight_decay", 0.0)),
+                      tuple(float(b) for b in g.get("betas", ())), float(g.get("eps", 0.0)))
+                     for g in getattr(optimizer, "param_groups", ()))
 
-    def _token(self, params, optimizer):
-        return (rt.cache_epoch(), getattr(optimizer, "table_epoch", 0), self._hparams(optimizer),
+    def _token(self, params, optimizer, step_args):
+        return (rt.cache_epoch(), getattr(optimizer, "table_epoch", 0), self._hparams(optimizer), tuple(step_args),
                 tuple((p.data_ptr(), p._version) for p in params))
 
-    def get(self, kind, params, optimizer, shapes):
+    def get(self, kind, params, optimizer, shapes, step_args=()):
         s = self.graphs.get(kind)
         if s is None:
             return None
-        if s.shapes != shapes or s.token != self._token(params, optimizer):
+        if s.shapes != shapes or s.token != self._token(params, optimizer, step_args):
             self.reset()             # stale addresses: recapture both kinds
             return None
         return s
 
-    def capture(self, kind, fn, inputs: dict, params, optimizer):
-        """Capture fn(**static inputs) -> tuple of output tensors as step kind `kind`."""
+    def capture(self, kind, fn, inputs: dict, params, optimizer, step_args=()):
+        """Capture fn(**static inputs) -> tuple of output tensors as step kind `kind`; step_args: the by-value
+        arguments fn passes to the optimizer step (clip_and_step's max_norm, grad_scale)."""
         from ._lib import lib
         shapes = tuple((k, tuple(v.shape), v.dtype) for k, v in sorted(inputs.items()))
         if any(self.static.get(k) is None or self.static[k].shape != v.shape or self.static[k].dtype != v.dtype
@@ -181,7 +182,7 @@ class StepGraphs:
         if self.pool is None:
             self.pool = g.pool()
         self.graphs[kind] = SimpleNamespace(g=g, outs=outs, c0=c0, nseeds=nseeds, keep=keep, shapes=shapes,
-                                            token=self._token(params, optimizer))
+                                            token=self._token(params, optimizer, step_args))
 
     def replay(self, kind, inputs: dict):
         s = self.graphs[kind]

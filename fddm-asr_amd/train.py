@@ -195,6 +195,7 @@ def _encoded(encoder, loader, device, optimizer):
 
 
 LAST_ENQUEUE_DONE = 0.0
+CLIP_MAX_NORM = 5.0     # clip_grad_norm_ max_norm of the reference step (train.py:411,422)
 _STEP_GRAPHS = weakref.WeakKeyDictionary()    # decoder -> StepGraphs (HIP-graph replay of the decoder step)
 # DP all-reduce tail (bench.py --gpus N): HIP events on the compute stream at the end of backward and after
 # allreduce_grads (the stream has waited for every gradient slice); ALLREDUCE_TAIL collects the event pairs
@@ -232,7 +233,7 @@ def _step_graph_ok(device, scaler, optimizer, arena) -> bool:
     if os.environ.get("DEBUG_HIP_FORCE_GRAPH_QUEUES", None) == "0":
         return False
     return (torch.device(device).type == "cuda" and rt.compute_dtype() == torch.bfloat16 and scaler is None and
-            arena is not None and hasattr(optimizer, "clip_and_step") and fdist.world() == 1 and
+            arena is not None and hasattr(optimizer, "clip_and_step") and not fdist.dp_active() and
             os.environ.get("FDDM_STEP_GRAPH", "0") == "1")
 
 
@@ -268,18 +269,18 @@ def train_one_epoch(encoder, decoder, s_proj, t_embed, t_proj, scheduler, loader
         if all(id(p) in opt_ids for p in dparams):
             order = decoder.grad_ready_order() if hasattr(decoder, "grad_ready_order") else None
             optimizer.use_grad_arena(dparams, order)
-    if fdist.world() > 1 and not getattr(optimizer, "_fddm_replicas_synced", False):
+    if fdist.dp_active() and not getattr(optimizer, "_fddm_replicas_synced", False):
         # DP replicas start from rank 0's weights (DDP's constructor broadcast): the trainable parameters and the
         # frozen encoder's parameters / buffers (a random-init encoder differs per rank otherwise)
         fdist.broadcast_params(trainable + list(encoder.parameters()) + list(encoder.buffers()) +
                                [b for m in (decoder, s_proj, t_embed, t_proj) for b in m.buffers()])
         optimizer._fddm_replicas_synced = True
     arena = getattr(optimizer, "arena", None)
-    if arena is not None and fdist.world() > 1 and arena.reducer is None:
+    if arena is not None and fdist.dp_active() and arena.reducer is None:
         fdist.OverlapReducer(arena)     # gradient all-reduce overlapped with backward
     # DP: L_fd's batch-dim statistics and w_t's batch mean over the GLOBAL batch (additive lfd.sync_batch_stats,
     # SURVEY §8(e)); default: each rank's own batch (documented "local-batch L_fd")
-    lfd_group = fdist.default_group() if (fdist.world() > 1 and cfg.lfd.get("sync_batch_stats", False)) else None
+    lfd_group = fdist.default_group() if (fdist.dp_active() and cfg.lfd.get("sync_batch_stats", False)) else None
     pbar = loader
     if tqdm is not None and print_epoch_summary:
         pbar = tqdm(loader, desc=f"Epoch {epoch} [train]", leave=False)
@@ -315,7 +316,7 @@ def train_one_epoch(encoder, decoder, s_proj, t_embed, t_proj, scheduler, loader
             scaler.scale(loss).backward()
             fdist.allreduce_grads(trainable)    # before unscale_: overlapped slices may still be in flight
             scaler.unscale_(optimizer)
-            torch.nn.utils.clip_grad_norm_([p for p in trainable if p.grad is not None], max_norm=5.0)
+            torch.nn.utils.clip_grad_norm_([p for p in trainable if p.grad is not None], max_norm=CLIP_MAX_NORM)
             scaler.step(optimizer)
             scaler.update()
         else:
@@ -327,9 +328,9 @@ def train_one_epoch(encoder, decoder, s_proj, t_embed, t_proj, scheduler, loader
             _mark_allreduce_tail(t_bwd)
             if fused:
                 # the step zeroes the gradients it reads (the next zero_grad's 156 MB arena fill folded into AdamW)
-                optimizer.clip_and_step(max_norm=5.0, zero_grads=True, grad_scale=1.0 / fdist.world())
+                optimizer.clip_and_step(max_norm=CLIP_MAX_NORM, zero_grads=True, grad_scale=1.0 / fdist.world())
             else:
-                torch.nn.utils.clip_grad_norm_([p for p in trainable if p.grad is not None], max_norm=5.0)
+                torch.nn.utils.clip_grad_norm_([p for p in trainable if p.grad is not None], max_norm=CLIP_MAX_NORM)
                 optimizer.step()
         return loss, loss_diff, loss_fd
 
@@ -347,13 +348,15 @@ def train_one_epoch(encoder, decoder, s_proj, t_embed, t_proj, scheduler, loader
         if graphs is not None and c_mask is None and not rt.probing_any("decoder."):
             inputs = {"c": c, "x0": x0, "t": t, "xt": xt}
             shapes = tuple((k, tuple(v.shape), v.dtype) for k, v in sorted(inputs.items()))
-            if graphs.get(fd, trainable, optimizer, shapes) is not None:
+            step_args = (CLIP_MAX_NORM, 1.0 / fdist.world())    # the clip_and_step values a capture bakes in
+            if graphs.get(fd, trainable, optimizer, shapes, step_args) is not None:
                 loss, loss_diff, loss_fd = graphs.replay(fd, inputs)
             else:
                 # the first step of this kind runs eagerly (creating every cache / table it reads), then the kind is
                 # captured for the next one (a capture executes nothing)
                 loss, loss_diff, loss_fd = step(c, None, x0, t, xt, fd)
-                graphs.capture(fd, lambda c, x0, t, xt: step(c, None, x0, t, xt, fd), inputs, trainable, optimizer)
+                graphs.capture(fd, lambda c, x0, t, xt: step(c, None, x0, t, xt, fd), inputs, trainable, optimizer,
+                               step_args)
         else:
             loss, loss_diff, loss_fd = step(c, c_mask, x0, t, xt, fd)
         loss_sum += loss.detach()

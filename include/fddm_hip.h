@@ -120,7 +120,7 @@ int fddm_attn_fwd_relgate(const void* Q, long sq, const void* K, long sk, const 
 int fddm_attn_fwd_relgate_x(const void* Q, long sq, const void* K, long sk, const void* V, long sv, void* O, long so,
                             const void* x, long sx, const float* gw, const float* gconst, const float* table, int B,
                             int H, int Lq, int Lk, float scale, void* hip_stream);
-/* Backward: dQ, dK, dV. bf16 with recorded or no dropout and Lk <= 256, or Lq <= 256 and Lk <= 512: one fused
+/* Backward: dQ, dK, dV. bf16 with recorded or no dropout, Lq <= 256 and Lk <= 512: one fused
  * 32x32x16-MFMA launch per (b, h) (csrc/attn7.hip bwdf7: P and dP computed once, dQ of each query tile from the keys
  * in LDS; with Lk > 256 two key passes, the first leaving f32 dQ partials in delta_ws, 64 floats per query row).
  * Other bf16 shapes with Lk <= 1024 (or fddm_attn_set_kernels(2)): the 32x32x16-MFMA pair (a query-owned dQ launch

@@ -302,3 +302,26 @@ def test_decoder_long_audio_families_agree():
     assert res["auto"][1].keys() == res["v6"][1].keys()
     for n in res["auto"][1]:
         close(res["auto"][1][n], res["v6"][1][n], rtol=6e-2, atol=1e-3, what=f"grad {n}")
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_attn7_first_half_tile_masked_with_very_negative_scores(p):
+    """a query whose first 32 keys are all padding keeps m = -inf after its first half-tile; with every
+    valid score far below the running reference (here ~ -130 in log2 units) the fast path's exponentials underflow
+    to 0 and the row sum stays 0 unless the slow path runs while no finite reference exists. Output and LSE must be
+    finite and match float64 (torch's softmax is finite there)."""
+    B, H, Lq, Lk = 1, 2, 64, 160
+    D = H * 64
+    gen = torch.Generator().manual_seed(13)
+    u = torch.randn(64, generator=gen)
+    u = u / u.norm()
+    q = (u * 30.0).repeat(B, Lq, H) + 0.05 * torch.randn(B, Lq, D, generator=gen)
+    k = (-u * 30.0).repeat(B, Lk, H) + 0.05 * torch.randn(B, Lk, D, generator=gen)   # q.k / 8 ~ -112
+    v = torch.randn(B, Lk, D, generator=gen)
+    keep = torch.ones(B, Lk, dtype=torch.bool)
+    keep[:, :32] = False
+    od, lse, _ = _run(B, H, Lq, Lk, keep, p, q, k, v)
+    assert torch.isfinite(od.float()).all() and torch.isfinite(lse).all()
+    ref, rlse = _ref(_heads(q, B, H), _heads(k, B, H), _heads(v, B, H), keep, p, 5, 9)
+    close(od.float(), _back(ref), rtol=2e-2, what="out")
+    close(lse.view(B, H, Lq), rlse, rtol=2.0 ** -8, atol=LSE_ATOL, what="lse")

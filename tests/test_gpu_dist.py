@@ -255,7 +255,7 @@ def test_bench_ranks_run_real_c2_steps(world):
     assert len(cs) == world and all(c == cs[0] for c in cs), cs
 
 
-def _c2_dp_grads(rank, world):
+def _c2_dp_grads(rank, world, params_out=None):
     """Two teacher-forced train_one_epoch steps (global steps 3: KL, 4: L_fd with global-batch statistics) at the C2
     decoder geometry (6 layers, d_model 512, 8 heads, ff 2048, L 256, V 8000) over WavLM-base on 10 s audio, encoder
     graph-replayed on its side stream with the CU caps, on this rank's rows (all 4 when world == 1); returns the
@@ -318,6 +318,8 @@ def _c2_dp_grads(rank, world):
         T_.train_one_epoch(enc, dec, sp, te, tp, sch, [(b[0], b[1]) for b in data], opt, dev, cfg, 3, None, 1, False,
                            draw_t=lambda B: next(tq))
         torch.cuda.synchronize()
+    if params_out is not None:
+        params_out.update({n: p.detach().cpu().clone() for n, p in named})
     return grads
 
 
@@ -363,3 +365,77 @@ def test_dp_c2_geometry_matches_full_batch():
                 worst = max(worst, e / max(float(v.double().norm()), 1e-3 * G))
             print(f"step {i} rank {r}: worst grad rel err {worst:.2e}")
             assert worst < 1e-4
+
+
+# ------------------------------------------------- RCCL on hardware: a world-size-1 "nccl" group with the DP path forced
+def _rccl_worker(backend, port, q):
+    """One process: (backend None) the plain single-GPU step, or a world-size-1 process group of `backend` with the DP
+    exchange forced on (fddm_hip.dist.force_dp): rank-0 broadcast, the overlapped all-reduce issued from the backward's
+    grads_ready callbacks, the global-batch L_fd statistics, 1/W in AdamW. Returns the gradients at both steps, the
+    final parameters and the collectives issued."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import datetime
+    import torch.distributed as dist
+    from fddm_hip import dist as fdist
+    from helpers import CollectiveLog
+    if backend is not None:
+        kw = {"device_id": torch.device("cuda", 0)} if backend == "nccl" else {}
+        dist.init_process_group(backend, rank=0, world_size=1, timeout=datetime.timedelta(seconds=120), **kw)
+        fdist.force_dp(True)
+    try:
+        final = {}
+        with CollectiveLog() as cl:
+            grads = _c2_dp_grads(0, 1, params_out=final)
+        q.put(([{n: (None if v is None else v.numpy()) for n, v in gr.items()} for gr in grads],
+               {n: v.numpy() for n, v in final.items()}, cl.log))
+    finally:
+        if backend is not None:
+            dist.destroy_process_group()
+
+
+def _spawn_one(backend):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(backend, _free_port(), q))
+    p.start()
+    out = q.get(timeout=400)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    return out
+
+
+def test_rccl_world1_forced_dp_step_matches_single_gpu():
+    """RCCL executes this code's DP path on hardware before any multi-GPU node does (verdict r5 item 5): a world-size-1
+    `nccl` group (init with device_id, as bench.py does), the DP exchange forced on, one KL step and one L_fd step with
+    sync_batch_stats at the C2 decoder geometry beside the graph-replayed encoder stream. The same run over a world-1
+    gloo group is the reference for the collective path (the all-reduce of one rank is the identity, so both must
+    give the single-GPU result): gradients and parameters equal bit for bit where the kernels are deterministic, and
+    in any case within the fp32 run-to-run spread (1e-6 norm-wise); against the plain single-GPU step (whose L_fd
+    statistics take the local kernels instead of the all-reduced column sums) within 1e-5. Not a scaling number:
+    SCALE runs on the driver's 8-GPU node."""
+    ref_g, ref_p, ref_log = _spawn_one(None)
+    glo_g, glo_p, glo_log = _spawn_one("gloo")
+    rc_g, rc_p, rc_log = _spawn_one("nccl")
+    assert ref_log == [] and rc_log == glo_log, (rc_log[:8], glo_log[:8])
+    names = [e[0] for e in rc_log]
+    # rank-0 broadcasts, one overlapped slice per 16 MB of the 155.8 MB arena on each step, the L_fd statistics
+    assert names.count("broadcast") >= 1 and names.count("all_reduce") >= 2 * 9, names
+    exact, w_gloo, w_ref = 0, 0.0, 0.0
+
+    def rel(x, y):
+        return float((x - y).norm()) / max(float(y.norm()), 1e-12)
+
+    for i in range(2):
+        for n, v in ref_g[i].items():
+            assert (rc_g[i][n] is None) == (v is None) == (glo_g[i][n] is None), n
+            if v is None:
+                continue
+            a, g, r = (torch.from_numpy(x).double() for x in (rc_g[i][n], glo_g[i][n], v))
+            exact += int(torch.equal(a, g))
+            w_gloo, w_ref = max(w_gloo, rel(a, g)), max(w_ref, rel(a, r))
+    for n, v in ref_p.items():
+        a, g, r = (torch.from_numpy(x).double() for x in (rc_p[n], glo_p[n], v))
+        w_gloo, w_ref = max(w_gloo, rel(a, g)), max(w_ref, rel(a, r))
+    print(f"RCCL world-1: {exact} gradient tensors bit-identical to the gloo run; worst rel diff vs gloo {w_gloo:.2e}, "
+          f"vs the single-GPU step (local L_fd statistics path) {w_ref:.2e}")
+    assert w_gloo < 1e-6 and w_ref < 1e-5
