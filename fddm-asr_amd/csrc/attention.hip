@@ -2390,14 +2390,14 @@ __global__ void __launch_bounds__(1024, 1) bwd3s_kernel(AttnArgs a) {
 
 // Kernel choice per launch shape (bf16; the fp32 parity mode runs the generic kernels):
 //  forward  WavLM gated rel-pos bias: fwd5 (streamed ring, bias slice staged; gate from a precomputed row, from the
-//           projection's extra columns, or from the attention input); decoder, Lk <= 1024: fwd7 (attn7.hip, 32x32x16;
-//           keep bits from the producer); Lk > 1024: fwd2.
+//           projection's extra columns, or from the attention input); decoder, Lk <= 1024: fwd8 (attn8.hip, two
+//           32-query chains per wave on 32x32x16 MFMAs; keep bits from the producer); Lk > 1024: fwd2.
 //  backward decoder, recorded bits or no dropout: Lq <= 256 and Lk <= 512: bwdf7 (attn7.hip, one fused launch per
 //           (b, h), one pass per 256 keys); other Lk <= 1024: dq7 + dkv7; longer or rehashed:
 //           dq2 + dkv2. Under fddm_attn_set_kernels(1) the round-4 kernels: bwd3s (Lq == Lk <= 256), dq4 + dkv4.
 // fddm_attn_set_kernels (tests / tools only): 1 selects the round-4 16x16x32 kernels (fwd6 / dq4 / dkv4 / bwd3s)
-// where the 32x32x16 family (attn7.hip) would run; 0 (default) the 32x32x16 family; 2 the same without the fused
-// backward (dq7 + dkv7 at every Lk)
+// where the 32x32x16 family (attn7.hip) would run; 0 (default) the 32x32x16 family with the two-chain forward fwd8
+// (attn8.hip); 2 the same without the fused backward (dq7 + dkv7 at every Lk); 3 the default with fwd7 as the forward
 static int g_attn_v6 = 0;
 #ifndef A7_FUSED_MAXLQ
 #define A7_FUSED_MAXLQ 256  // fused backward up to this many queries, one or two key passes (more: one workgroup per
@@ -2430,7 +2430,7 @@ static int run(int which, AttnArgs& a, hipStream_t s) {
                                           a.seed_off, s);
             if (e) return e;
           }
-          return attn7_fwd(a, s);
+          return g_attn_v6 == 3 ? attn7_fwd(a, s) : attn8_fwd(a, s);
         }
         const size_t lds = (size_t)2 * 2 * 64 * 128 + (size_t)LkP * 4 +
                            (dm == 1 ? (size_t)ntiles * qw * 8 : dm == 2 ? (size_t)3 * ATTN_R * 2 : 0);
@@ -2489,7 +2489,7 @@ static int run(int which, AttnArgs& a, hipStream_t s) {
     }
     if (which == 4) {  // the 32x32x16 family: the fused launch for Lq <= 256 and Lk <= 512 (one or two key passes),
                        // else dq7 (also writes dkv7's row terms), then dkv7
-      if (g_attn_v6 == 0 && a.Lk <= 512 && a.Lq <= A7_FUSED_MAXLQ) return attn7_bwdf(a, s);
+      if ((g_attn_v6 == 0 || g_attn_v6 == 3) && a.Lk <= 512 && a.Lq <= A7_FUSED_MAXLQ) return attn7_bwdf(a, s);
       const int e = attn7_dq(a, s);
       return e ? e : attn7_dkv(a, s);
     }
@@ -2561,7 +2561,7 @@ FDDM_API int fddm_attn_stamps_clear() {
 
 FDDM_API int fddm_attn_set_kernels(int v6) {
   const int old = g_attn_v6;
-  g_attn_v6 = (v6 == 1 || v6 == 2) ? v6 : 0;
+  g_attn_v6 = (v6 >= 1 && v6 <= 3) ? v6 : 0;
   return old;
 }
 

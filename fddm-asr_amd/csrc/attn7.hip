@@ -22,79 +22,11 @@
 //   A = V^T from two ds_read_b64_tr_b16 of 4 keys each (V image swizzle vsw: the 4 rows a 32-lane half reads are
 //   conflict-free).
 // The key mask (0 / -inf per key) is the S accumulator's initial value (no add per score).
-#include <type_traits>
-
-#include "attn_common.h"
+#include "attn7_common.h"
 
 namespace fddm {
 namespace attn {
 
-typedef __attribute__((ext_vector_type(16))) float f32x16_t;
-
-// compile-time loop: f(integral_constant<int, I>) for I in [B, E)
-template <int B, int E, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (B < E) {
-    f(std::integral_constant<int, B>{});
-    static_for<B + 1, E>(f);
-  }
-}
-
-__device__ __forceinline__ f32x16_t mfma32(const uint4& a, const uint4& b, const f32x16_t& c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
-                                                 0, 0, 0);
-}
-
-// V image: 16-B chunk c of row r is stored at chunk c ^ vsw(r). A transposed read of a 32-lane half covers 4
-// consecutive rows (4j .. 4j + 3) x 64 B; rows 4j and 4j + 2 share a 256-B bank window and land in opposite 64-B
-// halves of it.
-__device__ __forceinline__ int vsw(int r) { return (r & 2) << 1; }
-
-// 4-B-per-lane LDS-DMA piece (256 B per wave-instruction into lds + 4 * lane)
-__device__ __forceinline__ void dma4_asm(const void* src, const unsigned char* lds) {
-  typedef __attribute__((address_space(3))) const void* lcp_t;
-  const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lcp_t)(const void*)lds);
-  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" ::"v"(src), "s"(la) : "memory", "m0");
-}
-
-// LDS-DMA piece from a wave-uniform 64-bit base (SGPRs) + a 32-bit per-lane byte offset: no 64-bit address math per
-// lane and piece
-__device__ __forceinline__ void dma16_sv(const void* sbase, unsigned voff, const unsigned char* lds) {
-  typedef __attribute__((address_space(3))) const void* lcp_t;
-  const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lcp_t)(const void*)lds);
-  asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(la) : "memory", "m0");
-}
-__device__ __forceinline__ void dma4_sv(const void* sbase, unsigned voff, const unsigned char* lds) {
-  typedef __attribute__((address_space(3))) const void* lcp_t;
-  const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lcp_t)(const void*)lds);
-  asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dword %0, %1" ::"v"(voff), "s"(sbase), "s"(la) : "memory", "m0");
-}
-
-__device__ __forceinline__ s16x4_t tr_read(const unsigned char* p) {
-  typedef __attribute__((address_space(3))) s16x4_t* lp;
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(p));
-}
-
-constexpr int A7_TB = 64 * 128;  // one K or V tile in LDS: 64 rows x 128 B
-
-// ------------------------------------------------------------------ dropout keep bits, storage layout v3 (lane masks)
-// The keep decisions of RNG contract v2 (oracle attn_dropout_keep; attention.hip attn_keep4) stored so that one 64-bit
-// word is the lane mask of one accumulator register of the 32x32x16 score MFMA with the query on the lane: for (b, h),
-// 32-query group qg and 64-key tile t, slot j = 16 kb + r (kb = 32-key half, r = accumulator register), bit l =
-// keep(query 32 qg + (l & 31), key 64 t + 32 kb + 8 (r >> 2) + 4 (l >> 5) + (r & 3)). Word index
-// ((bh * nqg + qg) * ntiles + t) * 32 + j, nqg = ceil(Lq / 32). The forward and dQ kernels load a half-tile's 16
-// words into SGPRs with scalar loads and drop a probability with one v_cndmask (inverse ballot); the dK / dV kernel
-// (key on the lane) reads the one word of its key per 32-query half and extracts bits.
-__device__ __forceinline__ long lm_word(int bh, int nqg, int ntiles, int qg, int t) {
-  return (((long)bh * nqg + qg) * ntiles + t) * 32;
-}
-// The same bits per lane ("v4" part of the site buffer, after the lane masks): for (b, h, qg, t) 64 dwords, dword l =
-// the 32 keep bits of lane l of the query-lane kernels, bit 16 kb + r = the lane's accumulator register r of half kb.
-// The forward and dQ kernels stream one 256-B piece per wave and tile into LDS and test bits (bfe + and): a scalar
-// load of the lane masks per half-tile, waited for right before the select, cost more than the two VALU per score.
-__device__ __forceinline__ long lb_dword(int bh, int nqg, int ntiles, int qg, int t) {
-  return (((long)bh * nqg + qg) * ntiles + t) * 64;
-}
 typedef __attribute__((address_space(4))) const uint64_t* cu64p;
 // v_writelane_b32 through the LLVM intrinsic (this clang has no builtin for it), so the hazard recognizer inserts the
 // wait states a VALU-written SGPR needs before v_writelane reads it (an inline-asm writelane got none: stale ballots)
@@ -171,29 +103,6 @@ int attn7_drop_bits(uint64_t* out, long site_words, int nsites, int BH, int Lq, 
 }
 long attn7_drop_words(int B, int H, int Lq, int Lk) {  // lane masks + per-lane dwords
   return (long)B * H * ((Lq + 31) / 32) * ((Lk + 63) / 64) * 64;
-}
-
-// Images that serve both row reads (ds_read_b128, A = rows) and transposed reads (ds_read_b64_tr_b16, A = columns):
-// chunk c of row r at c ^ dsw(r), dsw(r) = a ^ ((a & 1) << 2) with a = (r >> 1) & 7. A row-read lane group's 16 rows
-// have distinct (r & 1, a), and a transposed read's rows 4j and 4j + 2 land 5 chunks apart (opposite 64-B halves).
-__device__ __forceinline__ int dsw(int r) {
-  const int a = (r >> 1) & 7;
-  return a ^ ((a & 1) << 2);
-}
-// the register-resident operand of the backward's score MFMA (Q in dq7, K in dkv7) pre-scaled by sl2 = scale *
-// log2(e) and rounded to bf16 once, so the product is the exponent in log2 units: 8 bf16 of one 16-B fragment
-__device__ __forceinline__ uint4 scale_frag(const uint4& x, float c) {
-  const u32x4v_t w = __builtin_bit_cast(u32x4v_t, x);
-  u32x4v_t o;
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-    o[j] = pk_bf16(__uint_as_float(w[j] << 16) * c, __uint_as_float(w[j] & 0xFFFF0000u) * c);
-  return __builtin_bit_cast(uint4, o);
-}
-// -x as a bf16 pair (hi, lo) with hi + lo = -x to ~2^-16 relative: the exact-constant fifth k-step of a score MFMA
-__device__ __forceinline__ unsigned neg_split(float x) {
-  const float hi = __uint_as_float(((unsigned)pk_bf16(-x, 0.f)) << 16);
-  return pk_bf16(hi, -x - hi);
 }
 
 // DM: 0 no dropout, 1 keep bits from the words fddm_attn_drop_bits wrote (word (bh, t, q), bit = key - 64 t).

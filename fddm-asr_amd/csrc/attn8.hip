@@ -1,0 +1,517 @@
+// Decoder attention forward with two query chains per wave (gfx950): fwd8.
+//
+// The decoder's self- and cross-attention (models/denoise_decoder.py:129-130,164,169-176 -> nn.MultiheadAttention:
+// key-padding mask, dropout p on the attention probabilities, head_dim 64), bf16 in / out, fp32 softmax statistics.
+// Same numerics as fwd7 (attn7.hip): pre-scaled Q' = bf16(Q scale log2 e), the softmax reference and the key mask
+// folded into the score MFMA as a fifth k-step, lazy rescale (slow path only when a half-tile's probabilities could
+// exceed 2^8 or no finite reference exists yet), keep bits of layout v4 tested per score, bf16 P into the PV MFMA.
+//
+// Why a new structure (profiles/r05e_pmc_attn7_c2.md): fwd7 runs one 32-query chain per wave, so
+// each half-tile is a serial chain — score MFMAs, then ~70 VALU + 16 v_exp on their results, then the PV MFMAs — and
+// its waves sat parked 34-44 % of their cycles with the matrix pipe busy 8-14 %. Here each wave owns TWO independent
+// 32-query chains A and B and software-pipelines them against each other: while the VALU works on one chain's
+// exponentials, the matrix pipe runs the other chain's PV MFMAs and next score MFMAs. One phase = 9 MFMAs:
+//   alpha_j: MFMA { S_B(j) [5], PV_B(j-1) [4] }   VALU { softmax_A(j) }   LDS { K fragments of half j + 1 }
+//   beta_j : MFMA { S_A(j+1) [5], PV_A(j) [4] }   VALU { softmax_B(j) }   LDS { V fragments of half j + 1 }
+// (j = 32-key half-tile). Each phase is written as 9 chunks {one MFMA, one score pair's softmax VALU, an LDS read}
+// fenced by sched_barrier, so the placement is ours, not the scheduler's. Both chains share every K / V fragment
+// (half the LDS reads per MFMA of fwd7).
+//
+// Layout: one workgroup = 4 waves x 64 queries = 256 queries of one (b, h) (C2's Lq 256: one workgroup per (b, h),
+// K / V read once). Register file per wave: 2 x (O 32 + Q' 16 + S 16 + P 8) + 2 K + 2 V fragment sets (64).
+// K / V tiles (64 keys) stream through a 4-stage LDS-DMA ring, two tiles ahead; one counted vmcnt + barrier per tile,
+// placed mid-tile (after the last read of the previous tile's stage, before the first read of the next tile).
+#include "attn7_common.h"
+
+namespace fddm {
+namespace attn {
+
+constexpr int A8_NS = 4;  // ring stages (tiles in flight: 2 ahead of the one being read)
+#ifndef A8_WPS
+#define A8_WPS 2  // waves per SIMD the register allocation targets (<= 256 registers: no accumulator-file split)
+#endif
+
+// one global_load_dwordx4 the compiler does not track (the prologue's Q rows: waited for by the counted vmcnt that
+// also covers the first K / V tiles, instead of a compiler vmcnt(0) that would drain the whole prefetch)
+__device__ __forceinline__ uint4 gload16_asm(const void* p) {
+  u32x4v_t v;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return __builtin_bit_cast(uint4, v);
+}
+
+// pin a value to this point of the instruction stream: its computation cannot sink past the chunk's sched_barrier
+__device__ __forceinline__ void pinv(float& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void pinv(unsigned& x) { asm volatile("" : "+v"(x)); }
+// a score pair's keep mask and bf16 pack in one statement: x & sext(bit b0 of kw), y & sext(bit b1 of kw), then
+// v_cvt_pk_bf16_f32 (low half = x). One asm statement, so hipcc pads no hazard state between the steps.
+template <int B0>
+__device__ __forceinline__ unsigned keep_pack(float x, float y, unsigned kw) {
+  unsigned r, t;
+  asm volatile(
+      "v_bfe_i32 %1, %3, %5, 1\n\t"
+      "v_and_b32 %1, %1, %2\n\t"
+      "v_bfe_i32 %0, %3, %6, 1\n\t"
+      "v_and_b32 %0, %0, %4\n\t"
+      "v_cvt_pk_bf16_f32 %0, %1, %0"
+      : "=&v"(r), "=&v"(t)
+      : "v"(x), "v"(kw), "v"(y), "i"(B0), "i"(B0 + 1));
+  return r;
+}
+
+template <int N>
+__device__ __forceinline__ void vmwait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+#define A8_FENCE() __builtin_amdgcn_sched_barrier(0)
+
+template <int DM, int MK>
+__global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
+  constexpr bool DROP = DM != 0;
+  constexpr int NP = DROP ? 6 : 4;  // LDS-DMA instructions per wave and tile (K 2, V 2, keep dwords 2)
+  extern __shared__ __attribute__((aligned(16))) unsigned char sm8[];
+  const int ntiles = (a.Lk + 63) >> 6, LkP = ntiles * 64;
+  unsigned char* kst = sm8;                                     // [NS][64 rows][128 B] K, KC swizzle
+  unsigned char* vst = sm8 + A8_NS * A7_TB;                     // [NS][64 rows][128 B] V, vsw swizzle
+  unsigned* kbl = (unsigned*)(sm8 + 2 * A8_NS * A7_TB);         // [NS][4 waves][2 chains][64 lanes] keep dwords
+  unsigned* tact = kbl + A8_NS * 512;                           // [4] active-tile nibbles per wave (MK 2)
+  unsigned* mpk = tact + 4;                                     // [LkP] bf16 pair (1, mask): the key's fifth k-step
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hh = lane >> 5, qi = lane & 31;
+  int bxi, bh;
+  xcd_tile(bxi, bh);
+  const int b = bh / a.H, h = bh - b * a.H;
+  const int qw0 = bxi * 256 + 64 * w;  // chain c: queries qw0 + 32 c + (lane & 31)
+  const bf16_t* Qb = (const bf16_t*)a.Q + (long)b * a.Lq * a.sq + h * DH;
+  const bf16_t* Kb = (const bf16_t*)a.K + (long)b * a.Lk * a.sk + h * DH;
+  const bf16_t* Vb = (const bf16_t*)a.V + (long)b * a.Lk * a.sv + h * DH;
+  const unsigned sk2 = (unsigned)a.sk * 2u, sv2 = (unsigned)a.sv * 2u;
+  const int nqg = (a.Lq + 31) >> 5, qg0 = 8 * bxi + 2 * w;  // the chains' 32-query groups qg0, qg0 + 1
+  const unsigned* lbits = (const unsigned*)(a.dbits + (long)a.B * a.H * nqg * ntiles * 32);
+
+  // ---- key mask (compiler-tracked loads, before any untracked one): thread tid owns keys 4 tid .. 4 tid + 3
+  unsigned tmask = ntiles >= 32 ? 0xFFFFFFFFu : ((1u << ntiles) - 1u);
+  if constexpr (MK != 0) {
+    bool any = false;
+    if (4 * tid < LkP) {
+      unsigned mv[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = 4 * tid + j;
+        const bool ok = k < a.Lk && (MK == 1 || a.key_keep[(long)b * a.Lk + k] != 0);
+        mv[j] = pk_bf16(1.f, ok ? 0.f : -INFINITY);
+        any |= ok;
+      }
+      *(uint4*)(mpk + 4 * tid) = make_uint4(mv[0], mv[1], mv[2], mv[3]);
+    }
+    if constexpr (MK == 2) {
+      const unsigned long long bal = __ballot(any);  // lanes 16 j .. 16 j + 15 of wave w: the keys of tile 4 w + j
+      if (lane == 0) {
+        unsigned nib = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) nib |= ((bal >> (16 * j)) & 0xFFFFull) ? (1u << j) : 0u;
+        tact[w] = nib;
+      }
+    }
+    __syncthreads();
+    if constexpr (MK == 2) tmask &= tact[0] | (tact[1] << 4) | (tact[2] << 8) | (tact[3] << 12);
+  }
+  const int nact = __builtin_popcount(tmask);
+
+  // ---- prologue: Q rows of both chains (untracked loads), then tiles 0 .. NS-1 of the active-tile list
+  const float sl2 = a.scale * 1.4426950408889634f;
+  uint4 qa[4], qb[4];
+  const int qA = qw0 + qi, qB = qw0 + 32 + qi;
+  {
+    const long ca = min(qA, a.Lq - 1), cb = min(qB, a.Lq - 1);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      qa[ks] = gload16_asm(Qb + ca * a.sq + 16 * ks + 8 * hh);
+      qb[ks] = gload16_asm(Qb + cb * a.sq + 16 * ks + 8 * hh);
+    }
+  }
+  auto fill = [&](int tt, int st) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int R = 16 * w + 8 * u;
+      const int r = 64 * tt + R + (lane >> 3), pch = lane & 7;
+      const unsigned rr = (unsigned)min(r, a.Lk - 1);
+      dma16_sv(Kb, rr * sk2 + (unsigned)((pch ^ ((r >> 1) & 7)) << 4), kst + st * A7_TB + R * 128);
+      dma16_sv(Vb, rr * sv2 + (unsigned)((pch ^ vsw(r)) << 4), vst + st * A7_TB + R * 128);
+    }
+    if constexpr (DROP) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+        dma4_sv(lbits, (unsigned)(lb_dword(bh, nqg, ntiles, min(qg0 + c, nqg - 1), tt) + lane) * 4u,
+                (const unsigned char*)(kbl + st * 512 + (2 * w + c) * 64));
+    }
+  };
+  // fill cursor: the active tiles still to be filled (ascending); active tile i goes to stage i % NS
+  unsigned fmask = tmask;
+  int fst = 0, nfilled = 0;
+  auto fill_next = [&]() {
+    const int tt = __builtin_ctz(fmask);
+    fmask &= fmask - 1u;
+    fill(tt, fst);
+    fst = fst == A8_NS - 1 ? 0 : fst + 1;
+    ++nfilled;
+  };
+  const int npro = min(nact, A8_NS - 1);
+  for (int i = 0; i < npro; ++i) fill_next();
+  // tile 0 landed (and with it the older Q rows): the other prologue fills stay in flight
+  if (npro == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NP) : "memory");
+  else if (npro == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NP) : "memory");
+  else vmwait<0>();
+  {
+    const unsigned zA = qA < a.Lq ? 0xFFFFFFFFu : 0u, zB = qB < a.Lq ? 0xFFFFFFFFu : 0u;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      u32x4v_t x = __builtin_bit_cast(u32x4v_t, qa[ks]), y = __builtin_bit_cast(u32x4v_t, qb[ks]);
+      asm volatile("" : "+v"(x), "+v"(y));  // uses after the counted wait above
+      qa[ks] = scale_frag(make_uint4(x[0] & zA, x[1] & zA, x[2] & zA, x[3] & zA), sl2);
+      qb[ks] = scale_frag(make_uint4(y[0] & zB, y[1] & zB, y[2] & zB, y[3] & zB), sl2);
+    }
+  }
+  __builtin_amdgcn_s_barrier();  // every wave's pieces of tile 0 landed
+
+  // per-lane LDS offsets: K row reads (row qi of a 32-key half, chunk 2 ks + hh), V transposed reads
+  int koff[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) koff[ks] = qi * 128 + (((2 * ks + hh) ^ ((qi >> 1) & 7)) << 4);
+  const int vi = lane & 15, vrow = 4 * hh + (vi >> 2);
+  int voff[2];
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+    voff[db] = vrow * 128 + (((8 * db + 4 * ((lane >> 4) & 1) + (vi & 3)) ^ ((vrow & 2) << 2)) << 3);
+
+  // chain state, softmax in log2 units: rf = the chain's bf16 reference, fixed after its first half-tile (the lane
+  // pair's row maximum there, 0 while that is -inf), subtracted inside the score MFMA; l = the lane's row sum
+  // relative to rf; O^T accumulators; q5 = the fifth-k-step operand (-rf, 1); p = packed probabilities.
+  // With a fixed reference the fast loop has no rescale branch (no phi copies of O); a guard flags any half-tile
+  // whose lane sum could overflow (> 2^64, inf, NaN), and a row sum that ends below 2^-40 (a first half-tile fully
+  // masked, then scores far below 0): such waves recompute their chains in the wave-local fallback (online softmax
+  // with rescaling, fwd7's algorithm), which is exact but slow — and does not occur for softmax inputs of sane range.
+  float rfA = 0.f, lA = 0.f, rfB = 0.f, lB = 0.f;
+  f32x16_t oA0 = {}, oA1 = {}, oB0 = {}, oB1 = {};
+  f32x16_t sA, sB;
+  uint4 pA[2], pB[2];
+  pB[0] = pB[1] = make_uint4(0, 0, 0, 0);
+  const uint4 q5init = hh ? make_uint4(0, 0, 0, 0) : make_uint4(pk_bf16(0.f, 1.f), 0u, 0u, 0u);
+  uint4 q5A = q5init, q5B = q5init;
+  unsigned kwA = 0xFFFFFFFFu, kwB = 0xFFFFFFFFu;
+  bool bad = false;
+  // fragments, one buffer each (reads are placed after the last MFMA that used the previous contents): K of a half
+  // (4 x ds_read_b128), its fifth-k-step operand k5, V of a half (2 steps x 2 d-blocks, each two tr reads)
+  uint4 kf[4], vf[2][2];
+  uint4 k5 = make_uint4(0, 0, 0, 0);
+  const unsigned lo32 = hh ? 0u : 0xFFFFFFFFu;  // lanes 0-31 hold the first 8 k positions of the fifth k-step
+  auto mk5 = [&](int key0) {
+    unsigned mk = pk_bf16(1.f, 0.f);
+    if constexpr (MK != 0) mk = mpk[key0 + qi];  // every lane reads (no exec-masked branch), lanes 32-63 drop it
+    return make_uint4(mk & lo32, 0u, 0u, 0u);
+  };
+  // in the phases the key operand's LDS read (chunk 1) and its use (chunk 8) are apart, so its wait finds it landed
+  unsigned mkr = 0;
+  auto mk5_read = [&](int key0) {
+    if constexpr (MK != 0) mkr = mpk[key0 + qi];
+  };
+  auto mk5_set = [&]() {
+    unsigned mk = pk_bf16(1.f, 0.f);
+    if constexpr (MK != 0) mk = mkr;
+    k5 = make_uint4(mk & lo32, 0u, 0u, 0u);
+  };
+  // V fragment c (= 2 s + db) of the half at vimg
+  auto rdv = [&](const unsigned char* vimg, int c) {
+    const int o = voff[c & 1] + 16 * (c >> 1) * 128;
+    vf[c >> 1][c & 1] = join_tr(tr_read(vimg + o), tr_read(vimg + o + 1024));
+  };
+
+  // softmax of one chain's half: pair i of registers (2 i, 2 i + 1) -> exponentials 2^(s - d), the lane's row sum, the
+  // keep mask (bits 2 i, 2 i + 1 of kwh) and the bf16 pack into p
+  auto sm_pair = [&](const f32x16_t& s, float d, unsigned kwh, uint4 (&p)[2], float& la, float& lb, auto ic) {
+    constexpr int i = decltype(ic)::value;
+    const float x = __builtin_amdgcn_exp2f(s[2 * i] - d);
+    const float y = __builtin_amdgcn_exp2f(s[2 * i + 1] - d);
+    if constexpr (i == 0) {
+      la = x;
+      lb = y;
+    } else {
+      la += x;
+      lb += y;
+    }
+    pinv(la);
+    pinv(lb);
+    unsigned v;
+    if constexpr (DROP) v = keep_pack<2 * i>(x, y, kwh);
+    else {
+      v = pk_bf16(x, y);
+      pinv(v);
+    }
+    if constexpr ((i & 3) == 0) p[i >> 2].x = v;
+    if constexpr ((i & 3) == 1) p[i >> 2].y = v;
+    if constexpr ((i & 3) == 2) p[i >> 2].z = v;
+    if constexpr ((i & 3) == 3) p[i >> 2].w = v;
+  };
+  // the reference of a chain's first half-tile (scores computed against 0): bf16 of the lane pair's row maximum
+  auto first_ref = [&](const f32x16_t& s, float& rf, uint4& q5) {
+    float tm = fmaxf(s[0], s[1]);
+#pragma unroll
+    for (int r = 2; r < 16; r += 2) tm = fmaxf(tm, fmaxf(s[r], s[r + 1]));
+    tm = xmax32(tm);
+    rf = (tm == -INFINITY) ? 0.f : __uint_as_float(((unsigned)pk_bf16(tm, 0.f)) << 16);
+    q5 = hh ? make_uint4(0, 0, 0, 0) : make_uint4(pk_bf16(-rf, 1.f), 0u, 0u, 0u);
+  };
+
+  // One phase: 9 chunks of {MFMA, softmax pair of the other chain, LDS read}, fenced. MFMA order: the score chain
+  // first (its result feeds the next phase's VALU), then the PV chain (its operand came from the previous phase).
+  //   SX: score accumulator (written) from qX / q5X and the current kf / k5
+  //   oY0 / oY1 += V^T pY with the current vf; sZ - dZ -> pZ, lZ: the softmax chain; rd(c): the LDS reads of chunk c
+  auto phase = [&](f32x16_t& SX, const uint4 (&qX)[4], const uint4& q5X, f32x16_t& oY0, f32x16_t& oY1,
+                   const uint4 (&pY)[2], const f32x16_t& sZ, float dZ, uint4 (&pZ)[2], float& lZ, unsigned kwZ,
+                   auto&& rd) {
+    float la, lb;
+    f32x16_t acc = mfma32(k5, q5X, f32x16_t{});
+    sm_pair(sZ, dZ, kwZ, pZ, la, lb, std::integral_constant<int, 0>{});
+    rd(std::integral_constant<int, 0>{});
+    A8_FENCE();
+    static_for<0, 4>([&](auto kc) {
+      constexpr int ks = decltype(kc)::value;
+      acc = mfma32(kf[ks], qX[ks], acc);
+      sm_pair(sZ, dZ, kwZ, pZ, la, lb, std::integral_constant<int, ks + 1>{});
+      rd(std::integral_constant<int, ks + 1>{});
+      A8_FENCE();
+    });
+    SX = acc;
+    static_for<0, 4>([&](auto pc) {
+      constexpr int pi = decltype(pc)::value;  // PV step s = pi >> 1, d-block pi & 1
+      if constexpr ((pi & 1) == 0) oY0 = mfma32(vf[pi >> 1][0], pY[pi >> 1], oY0);
+      else oY1 = mfma32(vf[pi >> 1][1], pY[pi >> 1], oY1);
+      if constexpr (pi < 3) sm_pair(sZ, dZ, kwZ, pZ, la, lb, std::integral_constant<int, 5 + pi>{});
+      if constexpr (pi == 3) {
+        const float ls = la + lb;
+        lZ += ls;
+        bad |= !(ls <= 0x1p64f);
+      }
+      rd(std::integral_constant<int, 5 + pi>{});
+      A8_FENCE();
+    });
+  };
+
+  // the stream of active tiles: active tile i = tile t in stage i % NS; half 0 = keys 64 t .. + 31, half 1 = + 32 ..
+  unsigned cmask = tmask;
+  int t = __builtin_ctz(cmask);
+  cmask &= cmask - 1u;
+  int st = 0;
+  if (nact == 0) goto epilogue;  // every key masked: NaN rows (torch's softmax over -inf)
+  {
+    // pipeline start: K (+ k5) of half 0 and S_A(half 0) against reference 0; V of half 0 for PV_B(-1), which runs
+    // with pB = 0 (finite data, zero contribution); keep bits of tile 0
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) kf[ks] = *(const uint4*)(kst + koff[ks]);
+    k5 = mk5(64 * t);
+    if constexpr (DROP) {
+      kwA = kbl[(2 * w) * 64 + lane];
+      kwB = kbl[(2 * w + 1) * 64 + lane];
+    }
+    f32x16_t acc = mfma32(k5, q5A, f32x16_t{});
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) acc = mfma32(kf[ks], qa[ks], acc);
+    sA = acc;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) rdv(vst, c);
+  }
+  // ---- tile 0, half 0: each chain's reference comes from this half's scores (computed against 0)
+  first_ref(sA, rfA, q5A);
+  phase(sB, qb, q5B, oB0, oB1, pB, sA, rfA, pA, lA, kwA, [&](auto cc) {  // alpha (see below)
+    constexpr int c = decltype(cc)::value;
+    if constexpr (c == 1) mk5_read(64 * t + 32);
+    if constexpr (c == 8) mk5_set();
+    if constexpr (c >= 5) kf[c - 5] = *(const uint4*)(kst + koff[c - 5] + 32 * 128);
+  });
+  first_ref(sB, rfB, q5B);
+  phase(sA, qa, q5A, oA0, oA1, pA, sB, rfB, pB, lB, kwB, [&](auto cc) {  // beta
+    constexpr int c = decltype(cc)::value;
+    if constexpr (c < 4) rdv(vst, c);
+  });
+  for (int i = 0;; ++i) {
+    const bool more = cmask != 0u;
+    // ---- mid-tile: the previous tile's stage is read out by every wave; the next active tile must have landed (own
+    // pieces, then every wave's by the barrier); then that stage takes the tile NS - 1 ahead
+    int tn = t, stn = st;
+    unsigned kwAn = 0xFFFFFFFFu, kwBn = 0xFFFFFFFFu;
+    if (more) {
+      tn = __builtin_ctz(cmask);
+      cmask &= cmask - 1u;
+      stn = st == A8_NS - 1 ? 0 : st + 1;
+      if (nfilled > i + 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NP) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (fmask) fill_next();
+      if constexpr (DROP) {
+        kwAn = kbl[stn * 512 + (2 * w) * 64 + lane];
+        kwBn = kbl[stn * 512 + (2 * w + 1) * 64 + lane];
+      }
+    }
+    {
+      const unsigned char* kimn = kst + stn * A7_TB;
+      const unsigned char* vimg = vst + st * A7_TB;
+      // ---- half 1. alpha: S_B(h1), PV_B(h0); softmax A(h1); reads: k5 and K of the next tile's h0
+      phase(sB, qb, q5B, oB0, oB1, pB, sA, 0.f, pA, lA, kwA >> 16, [&](auto cc) {
+        constexpr int c = decltype(cc)::value;
+        if constexpr (c == 1) mk5_read(64 * tn);
+        if constexpr (c == 8) mk5_set();
+        if constexpr (c >= 5) kf[c - 5] = *(const uint4*)(kimn + koff[c - 5]);
+      });
+      // beta: V of h1 (chunks 0-3, before its PV in chunks 5-8), S_A(next h0), PV_A(h1); softmax B(h1)
+      phase(sA, qa, q5A, oA0, oA1, pA, sB, 0.f, pB, lB, kwB >> 16, [&](auto cc) {
+        constexpr int c = decltype(cc)::value;
+        if constexpr (c < 4) rdv(vimg + 32 * 128, c);
+      });
+    }
+    if (!more) break;
+    t = tn;
+    st = stn;
+    kwA = kwAn;
+    kwB = kwBn;
+    {
+      const unsigned char* kimg = kst + st * A7_TB;
+      const unsigned char* vimg = vst + st * A7_TB;
+      // ---- half 0. alpha: S_B(h0), PV_B(previous h1); softmax A(h0); reads: k5 and K of h1 (after S_B's last K use)
+      phase(sB, qb, q5B, oB0, oB1, pB, sA, 0.f, pA, lA, kwA, [&](auto cc) {
+        constexpr int c = decltype(cc)::value;
+        if constexpr (c == 1) mk5_read(64 * t + 32);
+    if constexpr (c == 8) mk5_set();
+        if constexpr (c >= 5) kf[c - 5] = *(const uint4*)(kimg + koff[c - 5] + 32 * 128);
+      });
+      // beta: V of h0, S_A(h1), PV_A(h0); softmax B(h0)
+      phase(sA, qa, q5A, oA0, oA1, pA, sB, 0.f, pB, lB, kwB, [&](auto cc) {
+        constexpr int c = decltype(cc)::value;
+        if constexpr (c < 4) rdv(vimg, c);
+      });
+    }
+  }
+  // pipeline end: PV_B of the last half
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    oB0 = mfma32(vf[s][0], pB[s], oB0);
+    oB1 = mfma32(vf[s][1], pB[s], oB1);
+  }
+
+epilogue:
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();  // the ring is free: wave w owns bytes [16 KB w, 16 KB (w + 1)) for the fallback and the staging
+  unsigned char* own = sm8 + w * 16384;
+  if (nact > 0 && __any(bad || !(xsum32(lA) >= 0x1p-40f) || !(xsum32(lB) >= 0x1p-40f))) {
+    // ---- fallback (guard tripped): both chains again, online softmax with rescaling (fwd7's algorithm), each
+    // active tile staged by this wave alone into its own 16 KB (K image 8 KB, V image 8 KB), keep dwords from memory
+    unsigned char* kp = own;
+    unsigned char* vp = own + 8192;
+    auto redo = [&](int c, const uint4 (&qX)[4], f32x16_t& o0, f32x16_t& o1, float& l, float& rf) {
+      const int qg = min(qg0 + c, nqg - 1);
+      float m = -INFINITY;
+      rf = 0.f;
+      l = 0.f;
+      o0 = f32x16_t{};
+      o1 = f32x16_t{};
+      uint4 q5 = q5init;
+      unsigned tm_ = tmask;
+      while (tm_) {
+        const int tt = __builtin_ctz(tm_);
+        tm_ &= tm_ - 1u;
+        const int r = 64 * tt + lane, rr = min(r, a.Lk - 1);
+#pragma unroll
+        for (int ch = 0; ch < 8; ++ch) {
+          const uint4 kx = *(const uint4*)(Kb + (long)rr * a.sk + 8 * ch);
+          const uint4 vx = *(const uint4*)(Vb + (long)rr * a.sv + 8 * ch);
+          *(uint4*)(kp + lane * 128 + ((ch ^ ((lane >> 1) & 7)) << 4)) = kx;
+          *(uint4*)(vp + lane * 128 + ((ch ^ vsw(lane)) << 4)) = vx;
+        }
+        unsigned kw = 0xFFFFFFFFu;
+        if constexpr (DROP) kw = lbits[lb_dword(bh, nqg, ntiles, qg, tt) + lane];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+          const uint4 k5_ = mk5(64 * tt + 32 * kb);
+          f32x16_t sc = mfma32(k5_, q5, f32x16_t{});
+#pragma unroll
+          for (int ks = 0; ks < 4; ++ks) sc = mfma32(*(const uint4*)(kp + koff[ks] + kb * 32 * 128), qX[ks], sc);
+          float tmx = fmaxf(sc[0], sc[1]);
+#pragma unroll
+          for (int rr2 = 2; rr2 < 16; rr2 += 2) tmx = fmaxf(tmx, fmaxf(sc[rr2], sc[rr2 + 1]));
+          tmx = xmax32(tmx) + rf;
+          const float mn = fmaxf(m, tmx);
+          float rn = rf;
+          if (mn != -INFINITY) rn = __uint_as_float(((unsigned)pk_bf16(mn, 0.f)) << 16);
+          const float alpha = (m == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(rf - rn);
+          l *= alpha;
+          o0 *= alpha;
+          o1 *= alpha;
+          uint4 pp[2];
+          float la, lb;
+          static_for<0, 8>([&](auto ic) { sm_pair(sc, rn - rf, kw >> (16 * kb), pp, la, lb, ic); });
+          l += la + lb;
+          m = mn;
+          rf = rn;
+          q5 = hh ? make_uint4(0, 0, 0, 0) : make_uint4(pk_bf16(-rf, 1.f), 0u, 0u, 0u);
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            const int rb = (32 * kb + 16 * s) * 128;
+            o0 = mfma32(join_tr(tr_read(vp + voff[0] + rb), tr_read(vp + voff[0] + rb + 1024)), pp[s], o0);
+            o1 = mfma32(join_tr(tr_read(vp + voff[1] + rb), tr_read(vp + voff[1] + rb + 1024)), pp[s], o1);
+          }
+        }
+      }
+    };
+    redo(0, qa, oA0, oA1, lA, rfA);
+    redo(1, qb, oB0, oB1, lB, rfB);
+  }
+  // ---- normalise, stage the wave's 64 output rows in its own LDS bytes, store whole rows
+  bf16_t* Ob = (bf16_t*)a.Out + (long)b * a.Lq * a.so + h * DH;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const float lt = xsum32(c ? lB : lA);
+    const float rf = c ? rfB : rfA;
+    const float inv = (lt > 0.f) ? (DROP ? a.drop_scale : 1.f) / lt : NAN;
+    const int q = qw0 + 32 * c + qi;
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+#pragma unroll
+      for (int mm = 0; mm < 4; ++mm) {
+        const f32x16_t& oo = c ? (db ? oB1 : oB0) : (db ? oA1 : oA0);
+        uint2 u2;
+        u2.x = pk_bf16(oo[4 * mm] * inv, oo[4 * mm + 1] * inv);
+        u2.y = pk_bf16(oo[4 * mm + 2] * inv, oo[4 * mm + 3] * inv);
+        const int row = 32 * c + qi;
+        *(uint2*)(own + row * 128 + (((4 * db + mm) ^ (row & 7)) << 4) + 8 * hh) = u2;
+      }
+    }
+    if (a.lse && hh == 0 && q < a.Lq)
+      a.lse[(long)bh * a.Lq + q] = (lt > 0.f) ? (rf + __log2f(lt)) * 0.69314718055994531f : NAN;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row = (lane >> 3) + 8 * i, c = lane & 7;
+    const uint4 v = *(const uint4*)(own + row * 128 + ((c ^ (row & 7)) << 4));
+    if (qw0 + row < a.Lq) *(uint4*)(Ob + (long)(qw0 + row) * a.so + c * 8) = v;
+  }
+}
+
+size_t attn8_fwd_lds(int Lk) {
+  const int LkP = (Lk + 63) / 64 * 64;
+  return (size_t)2 * A8_NS * A7_TB + (size_t)A8_NS * 512 * 4 + 16 + (size_t)LkP * 4;
+}
+
+int attn8_fwd(AttnArgs& a, hipStream_t s) {
+  if (a.Lk > 1024 || a.Lk <= 0 || a.Lq <= 0) return (int)hipErrorInvalidValue;
+  const int dm = a.thr16 == 0 ? 0 : 1;
+  const int mk = a.key_keep != nullptr ? 2 : (a.Lk % 64) != 0 ? 1 : 0;
+  const size_t lds = attn8_fwd_lds(a.Lk);
+  dim3 grid((a.Lq + 255) / 256, a.B * a.H);
+#define FWD8(D, M) hipLaunchKernelGGL((fwd8_kernel<D, M>), grid, dim3(256), lds, s, a)
+  if (dm) { if (mk == 2) FWD8(1, 2); else if (mk == 1) FWD8(1, 1); else FWD8(1, 0); }
+  else { if (mk == 2) FWD8(0, 2); else if (mk == 1) FWD8(0, 1); else FWD8(0, 0); }
+#undef FWD8
+  return (int)hipGetLastError();
+}
+
+}  // namespace attn
+}  // namespace fddm

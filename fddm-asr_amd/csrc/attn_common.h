@@ -107,6 +107,8 @@ __device__ __forceinline__ void pin16(uint4& x) {
 // csrc/attn7.hip: the 32x32x16-MFMA decoder forward (bf16, head_dim 64, Lk <= 1024, no dropout or keep bits already
 // written by fddm_attn_drop_bits)
 int attn7_fwd(AttnArgs& a, hipStream_t s);
+// csrc/attn8.hip: the two-chain forward (same inputs, outputs and numerics contract as attn7_fwd)
+int attn8_fwd(AttnArgs& a, hipStream_t s);
 // the backward pair: dq7 (dQ; writes delta and -LSE log2(e) as [2][B*H][LqP] and the pre-scaled Q as
 // [B*H][LqP][64] bf16 into a.delta) and dkv7 (dK, dV)
 int attn7_dq(AttnArgs& a, hipStream_t s);

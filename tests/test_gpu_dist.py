@@ -409,10 +409,12 @@ def test_rccl_world1_forced_dp_step_matches_single_gpu():
     `nccl` group (init with device_id, as bench.py does), the DP exchange forced on, one KL step and one L_fd step with
     sync_batch_stats at the C2 decoder geometry beside the graph-replayed encoder stream. The same run over a world-1
     gloo group is the reference for the collective path (the all-reduce of one rank is the identity, so both must
-    give the single-GPU result): gradients and parameters equal bit for bit where the kernels are deterministic, and
-    in any case within the fp32 run-to-run spread (1e-6 norm-wise); against the plain single-GPU step (whose L_fd
-    statistics take the local kernels instead of the all-reduced column sums) within 1e-5. Not a scaling number:
-    SCALE runs on the driver's 8-GPU node."""
+    give the single-GPU result). The fp32 kernels' atomics make runs differ by ~1.5e-6 (KL step) and ~1e-5 (L_fd step)
+    norm-wise even between two plain runs (tools/probe/rccl_diag.py: gloo vs gloo-bulk 7.7e-6 on the L_fd step), so
+    the bar is that spread: gradients within 5e-5 of the gloo run and of the plain single-GPU step (whose L_fd
+    statistics take the local kernels), parameters after AdamW within 1e-5. The two projector biases whose true
+    gradient is zero (the L_fd standardisation removes them; NOISE_ONLY) are left out, as in the other DP tests.
+    Not a scaling number: SCALE runs on the driver's 8-GPU node."""
     ref_g, ref_p, ref_log = _spawn_one(None)
     glo_g, glo_p, glo_log = _spawn_one("gloo")
     rc_g, rc_p, rc_log = _spawn_one("nccl")
@@ -428,14 +430,17 @@ def test_rccl_world1_forced_dp_step_matches_single_gpu():
     for i in range(2):
         for n, v in ref_g[i].items():
             assert (rc_g[i][n] is None) == (v is None) == (glo_g[i][n] is None), n
-            if v is None:
+            if v is None or n in NOISE_ONLY:
                 continue
             a, g, r = (torch.from_numpy(x).double() for x in (rc_g[i][n], glo_g[i][n], v))
             exact += int(torch.equal(a, g))
             w_gloo, w_ref = max(w_gloo, rel(a, g)), max(w_ref, rel(a, r))
+    p_gloo, p_ref = 0.0, 0.0
     for n, v in ref_p.items():
+        if n in NOISE_ONLY:
+            continue
         a, g, r = (torch.from_numpy(x).double() for x in (rc_p[n], glo_p[n], v))
-        w_gloo, w_ref = max(w_gloo, rel(a, g)), max(w_ref, rel(a, r))
-    print(f"RCCL world-1: {exact} gradient tensors bit-identical to the gloo run; worst rel diff vs gloo {w_gloo:.2e}, "
-          f"vs the single-GPU step (local L_fd statistics path) {w_ref:.2e}")
-    assert w_gloo < 1e-6 and w_ref < 1e-5
+        p_gloo, p_ref = max(p_gloo, rel(a, g)), max(p_ref, rel(a, r))
+    print(f"RCCL world-1: {exact} gradient tensors bit-identical to the gloo run; worst gradient rel diff vs gloo "
+          f"{w_gloo:.2e}, vs the single-GPU step {w_ref:.2e}; worst parameter rel diff {p_gloo:.2e} / {p_ref:.2e}")
+    assert w_gloo < 5e-5 and w_ref < 5e-5 and p_gloo < 1e-5 and p_ref < 1e-5

@@ -3,7 +3,8 @@ the producer as the decoder does): "v6" = attention.hip's 16x16x32 kernels (fwd6
 default choice (attn7.hip's 32x32x16 kernels where they apply). Prints us per launch and the fraction of the dense
 bf16 MFMA peak (fwd 4 Lq Lk 64, bwd 10 Lq Lk 64 FLOP per (b, h)), and the max |difference| between the families'
 outputs (bf16 roundings of the same math).
-  python tools/attn7_bench.py [iters]"""
+  python tools/attn7_bench.py [iters] [family,family]   (default families: v6,auto; "fwd7" = the default with the
+  one-chain forward fwd7 instead of the two-chain fwd8)"""
 import os
 import sys
 
@@ -32,6 +33,7 @@ def timeit(fn, iters):
 
 def main():
     iters = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    fams = tuple(sys.argv[2].split(",")) if len(sys.argv) > 2 else ("v6", "auto")
     cases = [("C2 self  L256 B32 H8 kpm", 32, 8, 256, 256, True),
              ("C2 cross 256x499 B32 H8", 32, 8, 256, 499, False),
              ("C4 self  L512 B16 H12 kpm", 16, 12, 512, 512, True),
@@ -49,7 +51,7 @@ def main():
         fl = 4.0 * B * H * Lq * Lk * 64
         db = ops.drop_bits(B, H, Lq, Lk, dev)
         res, outs = [], {}
-        for fam in ("v6", "auto"):
+        for fam in fams:
             old = ops.attn_force_kernels(fam)
             try:
                 ops.attn_drop_bits(db.view(1, -1), 1, B, H, Lq, Lk, 0.1, 1, 1, 0)   # the family's storage layout
@@ -68,7 +70,7 @@ def main():
                 ops.attn_force_kernels(old)
             res.append(f"{fam}: fwd {tf*1e3:6.1f} us {fl/tf/1e12*1e3/PEAK:5.3f}  bwd {tb*1e3:6.1f} us "
                        f"{2.5*fl/tb/1e12*1e3/PEAK:5.3f}  bits {tp*1e3:5.1f} us")
-        diff = [(a_ - b_).abs().max().item() for a_, b_ in zip(outs["v6"], outs["auto"])]
+        diff = [(a_ - b_).abs().max().item() for a_, b_ in zip(outs[fams[0]], outs[fams[-1]])]
         print(f"{name:28s} " + " | ".join(res) + " | max|diff| o/dq/dk/dv " + " ".join(f"{d:.3g}" for d in diff),
               flush=True)
 
