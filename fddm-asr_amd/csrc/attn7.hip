@@ -85,7 +85,7 @@ __global__ void __launch_bounds__(256) dmask_kernel(DmArgs d) {
             const unsigned long long bm = __ballot(keep);
             writelane<16 * kb + 4 * m + e>(lo, (unsigned)bm);
             writelane<16 * kb + 4 * m + e>(hi, (unsigned)(bm >> 32));
-            lw |= (keep ? 1u : 0u) << (16 * kb + 4 * m + e);
+            lw |= (keep ? 1u : 0u) << lb_bit(kb, 4 * m + e);
           });
         });
       });
@@ -248,9 +248,9 @@ __global__ void __launch_bounds__(256, A7_FWD_WPS) fwd7_kernel(AttnArgs a) {
             float y = __builtin_amdgcn_exp2f(sc[r + 1] - d);
             la += x;
             lb += y;
-            if constexpr (DROP) {  // keep bit 16 kb + r of the lane's dword as an AND mask (v_bfe_i32)
-              x = __uint_as_float(__float_as_uint(x) & (unsigned)__builtin_amdgcn_sbfe((int)kw, 16 * kb + r, 1));
-              y = __uint_as_float(__float_as_uint(y) & (unsigned)__builtin_amdgcn_sbfe((int)kw, 16 * kb + r + 1, 1));
+            if constexpr (DROP) {  // keep bit lb_bit(kb, r) of the lane's dword as an AND mask (v_bfe_i32)
+              x = __uint_as_float(__float_as_uint(x) & (unsigned)__builtin_amdgcn_sbfe((int)kw, lb_bit(kb, r), 1));
+              y = __uint_as_float(__float_as_uint(y) & (unsigned)__builtin_amdgcn_sbfe((int)kw, lb_bit(kb, r + 1), 1));
             }
             bw[jj] = pk_bf16(x, y);
           }
@@ -497,10 +497,10 @@ __global__ void __launch_bounds__(256, 3) dq7_kernel(AttnArgs a) {
         for (int jj = 0; jj < 4; ++jj) {
           const int r = 8 * s + 2 * jj;
           float d0 = dp[r], d1 = dp[r + 1];
-          if constexpr (DROP) {  // keep ? dscale dP - delta : -delta (keep bit 16 kb + r as an AND mask)
-            d0 = fmaf(__uint_as_float(__float_as_uint(d0) & (unsigned)__builtin_amdgcn_sbfe((int)kw, 16 * kb + r, 1)),
+          if constexpr (DROP) {  // keep ? dscale dP - delta : -delta (keep bit lb_bit(kb, r) as an AND mask)
+            d0 = fmaf(__uint_as_float(__float_as_uint(d0) & (unsigned)__builtin_amdgcn_sbfe((int)kw, lb_bit(kb, r), 1)),
                       a.drop_scale, -dl);
-            d1 = fmaf(__uint_as_float(__float_as_uint(d1) & (unsigned)__builtin_amdgcn_sbfe((int)kw, 16 * kb + r + 1, 1)),
+            d1 = fmaf(__uint_as_float(__float_as_uint(d1) & (unsigned)__builtin_amdgcn_sbfe((int)kw, lb_bit(kb, r + 1), 1)),
                       a.drop_scale, -dl);
           } else {
             d0 -= dl;

@@ -68,10 +68,13 @@ constexpr int A7_TB = 64 * 128;  // one K or V tile in LDS: 64 rows x 128 B
 __device__ __forceinline__ long lm_word(int bh, int nqg, int ntiles, int qg, int t) {
   return (((long)bh * nqg + qg) * ntiles + t) * 32;
 }
-// The same bits per lane ("v4" part of the site buffer, after the lane masks): for (b, h, qg, t) 64 dwords, dword l =
-// the 32 keep bits of lane l of the query-lane kernels, bit 16 kb + r = the lane's accumulator register r of half kb.
-// The forward and dQ kernels stream one 256-B piece per wave and tile into LDS and test bits (bfe + and): a scalar
-// load of the lane masks per half-tile, waited for right before the select, cost more than the two VALU per score.
+// The same bits per lane (the "per-lane dword" part of the site buffer, after the lane masks; layout v5): for (b, h, qg,
+// t) 64 dwords, dword l = the 32 keep bits of lane l of the query-lane kernels. Register r of half kb (score pair
+// p = 8 kb + (r >> 1), registers 2 p' and 2 p' + 1 of the half) sits at bit 15 - p (r even) or 31 - p (r odd): shifted
+// left by p, the pair's two bits are bits 15 and 31, which one v_perm_b32 (selectors 8 / 9: the sign of byte 1 / 3)
+// turns into the pair's 32-bit bf16 mask (fwd8). fwd7 and dq7 test single bits (bfe + and). The forward and dQ kernels
+// stream one 256-B piece per wave and tile into LDS.
+__host__ __device__ constexpr int lb_bit(int kb, int r) { return ((r & 1) ? 31 : 15) - (8 * kb + (r >> 1)); }
 __device__ __forceinline__ long lb_dword(int bh, int nqg, int ntiles, int qg, int t) {
   return (((long)bh * nqg + qg) * ntiles + t) * 64;
 }

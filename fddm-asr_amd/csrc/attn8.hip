@@ -42,9 +42,9 @@ __device__ __forceinline__ uint4 gload16_asm(const void* p) {
 // pin a value to this point of the instruction stream: its computation cannot sink past the chunk's sched_barrier
 __device__ __forceinline__ void pinv(float& x) { asm volatile("" : "+v"(x)); }
 __device__ __forceinline__ void pinv(unsigned& x) { asm volatile("" : "+v"(x)); }
-// a score pair's keep mask and bf16 pack in one statement: x & sext(bit b0 of kw), y & sext(bit b1 of kw), then
-// v_cvt_pk_bf16_f32 (low half = x). One asm statement, so hipcc pads no hazard state between the steps.
-template <int B0>
+// a score pair's keep mask and bf16 pack in one statement (the fallback's f32 path): x & sext(bit B0 of kw),
+// y & sext(bit B1 of kw), then v_cvt_pk_bf16_f32 (low half = x); one asm statement, so hipcc pads no state between
+template <int B0, int B1>
 __device__ __forceinline__ unsigned keep_pack(float x, float y, unsigned kw) {
   unsigned r, t;
   asm volatile(
@@ -54,8 +54,29 @@ __device__ __forceinline__ unsigned keep_pack(float x, float y, unsigned kw) {
       "v_and_b32 %0, %0, %4\n\t"
       "v_cvt_pk_bf16_f32 %0, %1, %0"
       : "=&v"(r), "=&v"(t)
-      : "v"(x), "v"(kw), "v"(y), "i"(B0), "i"(B0 + 1));
+      : "v"(x), "v"(kw), "v"(y), "i"(B0), "i"(B1));
   return r;
+}
+// the 32-bit bf16 keep mask of score pair P (layout v5, attn7_common.h lb_bit): bits 15 - P and 31 - P of kw moved to
+// bits 15 and 31, then v_perm_b32 replicates their signs into the low and high halves
+template <int P>
+__device__ __forceinline__ unsigned pair_mask(unsigned kw) {
+  unsigned m;
+  if constexpr (P == 0) {
+    asm volatile("v_perm_b32 %0, %1, %1, %2" : "=v"(m) : "v"(kw), "s"(0x09090808u));
+  } else {
+    unsigned t;
+    asm volatile(
+        "v_lshlrev_b32 %1, %3, %2\n\t"
+        "v_perm_b32 %0, %1, %1, %4"
+        : "=&v"(m), "=&v"(t)
+        : "v"(kw), "i"(P), "s"(0x09090808u));
+  }
+  return m;
+}
+__device__ __forceinline__ f32x4_t mfma16(const uint4& a, const uint4& b, const f32x4_t& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
+                                                 0, 0, 0);
 }
 
 template <int N>
@@ -64,6 +85,19 @@ __device__ __forceinline__ void vmwait() {
 }
 
 #define A8_FENCE() __builtin_amdgcn_sched_barrier(0)
+
+// Diagnostic build only (-DA8_STAMPS, tools/probe/a8_stamps.py; outputs are overwritten): s_memtime of wave 0 at the
+// kernel's phase points, written over the first output row of the workgroup's query block (16 x 8 B = 128 B)
+#ifdef A8_STAMPS
+#define A8ST(k)                                                   \
+  do {                                                            \
+    if (threadIdx.x == 0) a8st_[k] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define A8ST(k) \
+  do {          \
+  } while (0)
+#endif
 
 template <int DM, int MK>
 __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
@@ -80,6 +114,10 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
   const int hh = lane >> 5, qi = lane & 31;
   int bxi, bh;
   xcd_tile(bxi, bh);
+#ifdef A8_STAMPS
+  unsigned long long a8st_[16] = {};
+#endif
+  A8ST(0);
   const int b = bh / a.H, h = bh - b * a.H;
   const int qw0 = bxi * 256 + 64 * w;  // chain c: queries qw0 + 32 c + (lane & 31)
   const bf16_t* Qb = (const bf16_t*)a.Q + (long)b * a.Lq * a.sq + h * DH;
@@ -173,6 +211,7 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
     }
   }
   __builtin_amdgcn_s_barrier();  // every wave's pieces of tile 0 landed
+  A8ST(1);
 
   // per-lane LDS offsets: K row reads (row qi of a 32-key half, chunk 2 ks + hh), V transposed reads
   int koff[4];
@@ -185,21 +224,26 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
     voff[db] = vrow * 128 + (((8 * db + 4 * ((lane >> 4) & 1) + (vi & 3)) ^ ((vrow & 2) << 2)) << 3);
 
   // chain state, softmax in log2 units: rf = the chain's bf16 reference, fixed after its first half-tile (the lane
-  // pair's row maximum there, 0 while that is -inf), subtracted inside the score MFMA; l = the lane's row sum
-  // relative to rf; O^T accumulators; q5 = the fifth-k-step operand (-rf, 1); p = packed probabilities.
-  // With a fixed reference the fast loop has no rescale branch (no phi copies of O); a guard flags any half-tile
-  // whose lane sum could overflow (> 2^64, inf, NaN), and a row sum that ends below 2^-40 (a first half-tile fully
-  // masked, then scores far below 0): such waves recompute their chains in the wave-local fallback (online softmax
-  // with rescaling, fwd7's algorithm), which is exact but slow — and does not occur for softmax inputs of sane range.
-  float rfA = 0.f, lA = 0.f, rfB = 0.f, lB = 0.f;
+  // pair's row maximum there, 0 while that is -inf), subtracted inside the score MFMA; O^T accumulators; q5 = the
+  // fifth-k-step operand (-rf, 1); p = packed probabilities; ls = the row sums, accumulated by a 16x16x32 MFMA from
+  // the undropped packed probabilities (ones-selector A operand: row m of the product = the sum of lane n + 16 m's 8
+  // values, so lane n < 16 ends with query n's sum in registers 0 + 2 and query n + 16's in 1 + 3): no VALU adds.
+  // With a fixed reference the fast loop has no rescale branch (no phi copies of O). A row sum that ends above 2^64
+  // (or inf / NaN) could have overflowed on the way, and one below 2^-40 (a first half-tile fully masked, then scores
+  // far below 0) lost its precision: such waves recompute their chains in the wave-local fallback (online softmax with
+  // rescaling, fwd7's algorithm), exact but slow — not reached by softmax inputs of sane range.
+  float rfA = 0.f, rfB = 0.f;
   f32x16_t oA0 = {}, oA1 = {}, oB0 = {}, oB1 = {};
+  f32x4_t lsA = {}, lsB = {};
   f32x16_t sA, sB;
   uint4 pA[2], pB[2];
   pB[0] = pB[1] = make_uint4(0, 0, 0, 0);
   const uint4 q5init = hh ? make_uint4(0, 0, 0, 0) : make_uint4(pk_bf16(0.f, 1.f), 0u, 0u, 0u);
   uint4 q5A = q5init, q5B = q5init;
+  // the row-sum MFMA's A operand: A[m][8 b + j] = (m == b), i.e. bf16 ones on lanes with (l & 15) == (l >> 4)
+  const unsigned one2 = ((lane & 15) == (lane >> 4)) ? 0x3F803F80u : 0u;
+  const uint4 onesel = make_uint4(one2, one2, one2, one2);
   unsigned kwA = 0xFFFFFFFFu, kwB = 0xFFFFFFFFu;
-  bool bad = false;
   // fragments, one buffer each (reads are placed after the last MFMA that used the previous contents): K of a half
   // (4 x ds_read_b128), its fifth-k-step operand k5, V of a half (2 steps x 2 d-blocks, each two tr reads)
   uint4 kf[4], vf[2][2];
@@ -225,32 +269,33 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
     const int o = voff[c & 1] + 16 * (c >> 1) * 128;
     vf[c >> 1][c & 1] = join_tr(tr_read(vimg + o), tr_read(vimg + o + 1024));
   };
-
-  // softmax of one chain's half: pair i of registers (2 i, 2 i + 1) -> exponentials 2^(s - d), the lane's row sum, the
-  // keep mask (bits 2 i, 2 i + 1 of kwh) and the bf16 pack into p
-  auto sm_pair = [&](const f32x16_t& s, float d, unsigned kwh, uint4 (&p)[2], float& la, float& lb, auto ic) {
+  auto pset = [&](uint4 (&p)[2], auto ic, unsigned v) {
     constexpr int i = decltype(ic)::value;
-    const float x = __builtin_amdgcn_exp2f(s[2 * i] - d);
-    const float y = __builtin_amdgcn_exp2f(s[2 * i + 1] - d);
-    if constexpr (i == 0) {
-      la = x;
-      lb = y;
-    } else {
-      la += x;
-      lb += y;
-    }
-    pinv(la);
-    pinv(lb);
-    unsigned v;
-    if constexpr (DROP) v = keep_pack<2 * i>(x, y, kwh);
-    else {
-      v = pk_bf16(x, y);
-      pinv(v);
-    }
     if constexpr ((i & 3) == 0) p[i >> 2].x = v;
     if constexpr ((i & 3) == 1) p[i >> 2].y = v;
     if constexpr ((i & 3) == 2) p[i >> 2].z = v;
     if constexpr ((i & 3) == 3) p[i >> 2].w = v;
+  };
+  auto pand = [&](uint4 (&p)[2], auto ic, unsigned m) {
+    constexpr int i = decltype(ic)::value;
+    if constexpr ((i & 3) == 0) p[i >> 2].x &= m;
+    if constexpr ((i & 3) == 1) p[i >> 2].y &= m;
+    if constexpr ((i & 3) == 2) p[i >> 2].z &= m;
+    if constexpr ((i & 3) == 3) p[i >> 2].w &= m;
+  };
+
+  // the fallback's softmax pair (f32 row sums, keep bits tested one by one): registers 2 i, 2 i + 1 of half kb
+  auto sm_pair_f32 = [&](const f32x16_t& s, float d, unsigned kw, uint4 (&p)[2], float& la, float& lb, auto kbc,
+                         auto ic) {
+    constexpr int kb = decltype(kbc)::value, i = decltype(ic)::value;
+    const float x = __builtin_amdgcn_exp2f(s[2 * i] - d);
+    const float y = __builtin_amdgcn_exp2f(s[2 * i + 1] - d);
+    la += x;
+    lb += y;
+    unsigned v;
+    if constexpr (DROP) v = keep_pack<lb_bit(kb, 2 * i), lb_bit(kb, 2 * i + 1)>(x, y, kw);
+    else v = pk_bf16(x, y);
+    pset(p, ic, v);
   };
   // the reference of a chain's first half-tile (scores computed against 0): bf16 of the lane pair's row maximum
   auto first_ref = [&](const f32x16_t& s, float& rf, uint4& q5) {
@@ -262,22 +307,52 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
     q5 = hh ? make_uint4(0, 0, 0, 0) : make_uint4(pk_bf16(-rf, 1.f), 0u, 0u, 0u);
   };
 
-  // One phase: 9 chunks of {MFMA, softmax pair of the other chain, LDS read}, fenced. MFMA order: the score chain
-  // first (its result feeds the next phase's VALU), then the PV chain (its operand came from the previous phase).
+  // One phase: 9 chunks {an MFMA, one score pair of the other chain's softmax, LDS reads}, fenced. MFMA order: the
+  // score chain first (its result feeds the next phase's VALU), then the PV chain (its operand came from the previous
+  // phase); two row-sum MFMAs (16x16x32) ride in chunks 3 and 7, after the 4 pairs they sum were packed.
+  // Per score pair: 2 v_exp, 1 v_cvt_pk, and with dropout the pair mask (shift + v_perm) and one v_and after the
+  // row-sum MFMA has read the undropped word.
   //   SX: score accumulator (written) from qX / q5X and the current kf / k5
-  //   oY0 / oY1 += V^T pY with the current vf; sZ - dZ -> pZ, lZ: the softmax chain; rd(c): the LDS reads of chunk c
+  //   oY0 / oY1 += V^T pY with the current vf; sZ - dZ -> pZ, lsZ: the softmax chain (half KB of the tile: keep bits of
+  //   kwZ at lb_bit(KB, .)); rd(c): the LDS reads of chunk c
   auto phase = [&](f32x16_t& SX, const uint4 (&qX)[4], const uint4& q5X, f32x16_t& oY0, f32x16_t& oY1,
-                   const uint4 (&pY)[2], const f32x16_t& sZ, float dZ, uint4 (&pZ)[2], float& lZ, unsigned kwZ,
-                   auto&& rd) {
-    float la, lb;
+                   const uint4 (&pY)[2], const f32x16_t& sZ, float dZ, uint4 (&pZ)[2], f32x4_t& lsZ, unsigned kwZ,
+                   auto kbc, auto&& rd) {
+    constexpr int KB = decltype(kbc)::value;
+    unsigned msk[8];
+    auto pair = [&](auto ic) {  // exponentials, undropped pack, and the pair's keep mask
+      constexpr int i = decltype(ic)::value;
+#ifndef A8_NOEXP  // timing-only ablation: no exponentials (wrong results)
+      const float x = __builtin_amdgcn_exp2f(sZ[2 * i] - dZ);
+      const float y = __builtin_amdgcn_exp2f(sZ[2 * i + 1] - dZ);
+#else
+      const float x = sZ[2 * i] - dZ, y = sZ[2 * i + 1] - dZ;
+#endif
+      unsigned v = pk_bf16(x, y);
+      pinv(v);
+      pset(pZ, ic, v);
+      if constexpr (DROP) msk[i] = pair_mask<8 * KB + i>(kwZ);
+    };
+    auto drop = [&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      if constexpr (DROP) pand(pZ, ic, msk[i]);
+    };
+    auto lsum = [&](auto hc) {  // the row-sum MFMA over pairs 4 h .. 4 h + 3
+      constexpr int h = decltype(hc)::value;
+      lsZ = mfma16(onesel, pZ[h], lsZ);
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
     f32x16_t acc = mfma32(k5, q5X, f32x16_t{});
-    sm_pair(sZ, dZ, kwZ, pZ, la, lb, std::integral_constant<int, 0>{});
-    rd(std::integral_constant<int, 0>{});
+    pair(I0{});
+    rd(I0{});
     A8_FENCE();
     static_for<0, 4>([&](auto kc) {
       constexpr int ks = decltype(kc)::value;
       acc = mfma32(kf[ks], qX[ks], acc);
-      sm_pair(sZ, dZ, kwZ, pZ, la, lb, std::integral_constant<int, ks + 1>{});
+      pair(std::integral_constant<int, ks + 1>{});
+      if constexpr (ks == 2) lsum(I0{});                       // pairs 0-3 packed (chunk 3)
+      if constexpr (ks == 3) drop(I0{});
       rd(std::integral_constant<int, ks + 1>{});
       A8_FENCE();
     });
@@ -286,12 +361,12 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
       constexpr int pi = decltype(pc)::value;  // PV step s = pi >> 1, d-block pi & 1
       if constexpr ((pi & 1) == 0) oY0 = mfma32(vf[pi >> 1][0], pY[pi >> 1], oY0);
       else oY1 = mfma32(vf[pi >> 1][1], pY[pi >> 1], oY1);
-      if constexpr (pi < 3) sm_pair(sZ, dZ, kwZ, pZ, la, lb, std::integral_constant<int, 5 + pi>{});
-      if constexpr (pi == 3) {
-        const float ls = la + lb;
-        lZ += ls;
-        bad |= !(ls <= 0x1p64f);
+      if constexpr (pi < 3) {
+        pair(std::integral_constant<int, 5 + pi>{});
+        drop(std::integral_constant<int, 1 + pi>{});
       }
+      if constexpr (pi == 2) lsum(I1{});                      // pairs 4-7 packed (chunk 7)
+      if constexpr (pi == 3) static_for<4, 8>([&](auto ic) { drop(ic); });
       rd(std::integral_constant<int, 5 + pi>{});
       A8_FENCE();
     });
@@ -322,17 +397,18 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
   }
   // ---- tile 0, half 0: each chain's reference comes from this half's scores (computed against 0)
   first_ref(sA, rfA, q5A);
-  phase(sB, qb, q5B, oB0, oB1, pB, sA, rfA, pA, lA, kwA, [&](auto cc) {  // alpha (see below)
+  phase(sB, qb, q5B, oB0, oB1, pB, sA, rfA, pA, lsA, kwA, std::integral_constant<int, 0>{}, [&](auto cc) {  // alpha (see below)
     constexpr int c = decltype(cc)::value;
     if constexpr (c == 1) mk5_read(64 * t + 32);
     if constexpr (c == 8) mk5_set();
     if constexpr (c >= 5) kf[c - 5] = *(const uint4*)(kst + koff[c - 5] + 32 * 128);
   });
   first_ref(sB, rfB, q5B);
-  phase(sA, qa, q5A, oA0, oA1, pA, sB, rfB, pB, lB, kwB, [&](auto cc) {  // beta
+  phase(sA, qa, q5A, oA0, oA1, pA, sB, rfB, pB, lsB, kwB, std::integral_constant<int, 0>{}, [&](auto cc) {  // beta
     constexpr int c = decltype(cc)::value;
     if constexpr (c < 4) rdv(vst, c);
   });
+  A8ST(2);
   for (int i = 0;; ++i) {
     const bool more = cmask != 0u;
     // ---- mid-tile: the previous tile's stage is read out by every wave; the next active tile must have landed (own
@@ -343,9 +419,14 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
       tn = __builtin_ctz(cmask);
       cmask &= cmask - 1u;
       stn = st == A8_NS - 1 ? 0 : st + 1;
+#ifndef A8_NOWAIT  // timing-only ablation: no wait for the next tile's DMA (wrong results)
       if (nfilled > i + 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NP) : "memory");
       else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#else
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
       __builtin_amdgcn_s_barrier();
+      A8ST(3 + (i < 8 ? i : 8));
       if (fmask) fill_next();
       if constexpr (DROP) {
         kwAn = kbl[stn * 512 + (2 * w) * 64 + lane];
@@ -356,14 +437,14 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
       const unsigned char* kimn = kst + stn * A7_TB;
       const unsigned char* vimg = vst + st * A7_TB;
       // ---- half 1. alpha: S_B(h1), PV_B(h0); softmax A(h1); reads: k5 and K of the next tile's h0
-      phase(sB, qb, q5B, oB0, oB1, pB, sA, 0.f, pA, lA, kwA >> 16, [&](auto cc) {
+      phase(sB, qb, q5B, oB0, oB1, pB, sA, 0.f, pA, lsA, kwA, std::integral_constant<int, 1>{}, [&](auto cc) {
         constexpr int c = decltype(cc)::value;
         if constexpr (c == 1) mk5_read(64 * tn);
         if constexpr (c == 8) mk5_set();
         if constexpr (c >= 5) kf[c - 5] = *(const uint4*)(kimn + koff[c - 5]);
       });
       // beta: V of h1 (chunks 0-3, before its PV in chunks 5-8), S_A(next h0), PV_A(h1); softmax B(h1)
-      phase(sA, qa, q5A, oA0, oA1, pA, sB, 0.f, pB, lB, kwB >> 16, [&](auto cc) {
+      phase(sA, qa, q5A, oA0, oA1, pA, sB, 0.f, pB, lsB, kwB, std::integral_constant<int, 1>{}, [&](auto cc) {
         constexpr int c = decltype(cc)::value;
         if constexpr (c < 4) rdv(vimg + 32 * 128, c);
       });
@@ -377,14 +458,14 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
       const unsigned char* kimg = kst + st * A7_TB;
       const unsigned char* vimg = vst + st * A7_TB;
       // ---- half 0. alpha: S_B(h0), PV_B(previous h1); softmax A(h0); reads: k5 and K of h1 (after S_B's last K use)
-      phase(sB, qb, q5B, oB0, oB1, pB, sA, 0.f, pA, lA, kwA, [&](auto cc) {
+      phase(sB, qb, q5B, oB0, oB1, pB, sA, 0.f, pA, lsA, kwA, std::integral_constant<int, 0>{}, [&](auto cc) {
         constexpr int c = decltype(cc)::value;
         if constexpr (c == 1) mk5_read(64 * t + 32);
     if constexpr (c == 8) mk5_set();
         if constexpr (c >= 5) kf[c - 5] = *(const uint4*)(kimg + koff[c - 5] + 32 * 128);
       });
       // beta: V of h0, S_A(h1), PV_A(h0); softmax B(h0)
-      phase(sA, qa, q5A, oA0, oA1, pA, sB, 0.f, pB, lB, kwB, [&](auto cc) {
+      phase(sA, qa, q5A, oA0, oA1, pA, sB, 0.f, pB, lsB, kwB, std::integral_constant<int, 0>{}, [&](auto cc) {
         constexpr int c = decltype(cc)::value;
         if constexpr (c < 4) rdv(vimg, c);
       });
@@ -398,10 +479,19 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
   }
 
 epilogue:
+  A8ST(12);
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __syncthreads();  // the ring is free: wave w owns bytes [16 KB w, 16 KB (w + 1)) for the fallback and the staging
+  __syncthreads();
+  A8ST(13);  // the ring is free: wave w owns bytes [16 KB w, 16 KB (w + 1)) for the fallback and the staging
   unsigned char* own = sm8 + w * 16384;
-  if (nact > 0 && __any(bad || !(xsum32(lA) >= 0x1p-40f) || !(xsum32(lB) >= 0x1p-40f))) {
+  // the row sums: lanes n < 16 of the row-sum accumulator hold query n's in registers 0 + 2, query n + 16's in 1 + 3
+  auto rowsum = [&](const f32x4_t& ls) {
+    const float slo = ls[0] + ls[2], shi = ls[1] + ls[3];
+    const float a0 = __shfl(slo, qi & 15), a1 = __shfl(shi, qi & 15);
+    return qi < 16 ? a0 : a1;
+  };
+  float ltA = rowsum(lsA), ltB = rowsum(lsB);
+  if (nact > 0 && __any(!(ltA <= 0x1p64f && ltA >= 0x1p-40f) || !(ltB <= 0x1p64f && ltB >= 0x1p-40f))) {
     // ---- fallback (guard tripped): both chains again, online softmax with rescaling (fwd7's algorithm), each
     // active tile staged by this wave alone into its own 16 KB (K image 8 KB, V image 8 KB), keep dwords from memory
     unsigned char* kp = own;
@@ -428,8 +518,8 @@ epilogue:
         }
         unsigned kw = 0xFFFFFFFFu;
         if constexpr (DROP) kw = lbits[lb_dword(bh, nqg, ntiles, qg, tt) + lane];
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb) {
+        static_for<0, 2>([&](auto kbc) {
+          constexpr int kb = decltype(kbc)::value;
           const uint4 k5_ = mk5(64 * tt + 32 * kb);
           f32x16_t sc = mfma32(k5_, q5, f32x16_t{});
 #pragma unroll
@@ -446,8 +536,8 @@ epilogue:
           o0 *= alpha;
           o1 *= alpha;
           uint4 pp[2];
-          float la, lb;
-          static_for<0, 8>([&](auto ic) { sm_pair(sc, rn - rf, kw >> (16 * kb), pp, la, lb, ic); });
+          float la = 0.f, lb = 0.f;
+          static_for<0, 8>([&](auto ic) { sm_pair_f32(sc, rn - rf, kw, pp, la, lb, kbc, ic); });
           l += la + lb;
           m = mn;
           rf = rn;
@@ -458,17 +548,18 @@ epilogue:
             o0 = mfma32(join_tr(tr_read(vp + voff[0] + rb), tr_read(vp + voff[0] + rb + 1024)), pp[s], o0);
             o1 = mfma32(join_tr(tr_read(vp + voff[1] + rb), tr_read(vp + voff[1] + rb + 1024)), pp[s], o1);
           }
-        }
+        });
       }
+      l = xsum32(l);
     };
-    redo(0, qa, oA0, oA1, lA, rfA);
-    redo(1, qb, oB0, oB1, lB, rfB);
+    redo(0, qa, oA0, oA1, ltA, rfA);
+    redo(1, qb, oB0, oB1, ltB, rfB);
   }
   // ---- normalise, stage the wave's 64 output rows in its own LDS bytes, store whole rows
   bf16_t* Ob = (bf16_t*)a.Out + (long)b * a.Lq * a.so + h * DH;
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
-    const float lt = xsum32(c ? lB : lA);
+    const float lt = c ? ltB : ltA;
     const float rf = c ? rfB : rfA;
     const float inv = (lt > 0.f) ? (DROP ? a.drop_scale : 1.f) / lt : NAN;
     const int q = qw0 + 32 * c + qi;
@@ -493,11 +584,24 @@ epilogue:
     const uint4 v = *(const uint4*)(own + row * 128 + ((c ^ (row & 7)) << 4));
     if (qw0 + row < a.Lq) *(uint4*)(Ob + (long)(qw0 + row) * a.so + c * 8) = v;
   }
+#ifdef A8_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  A8ST(14);
+  if (threadIdx.x == 0) {
+    unsigned long long* dst = (unsigned long long*)(Ob + (long)(bxi * 256) * a.so);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) dst[k] = a8st_[k];
+  }
+#endif
 }
 
+#ifndef A8_LDS_FLOOR
+#define A8_LDS_FLOOR 0  // timing probe: a larger LDS request limits the workgroups per CU (tools/build_variant.sh)
+#endif
 size_t attn8_fwd_lds(int Lk) {
   const int LkP = (Lk + 63) / 64 * 64;
-  return (size_t)2 * A8_NS * A7_TB + (size_t)A8_NS * 512 * 4 + 16 + (size_t)LkP * 4;
+  const size_t n = (size_t)2 * A8_NS * A7_TB + (size_t)A8_NS * 512 * 4 + 16 + (size_t)LkP * 4;
+  return n > (size_t)A8_LDS_FLOOR ? n : (size_t)A8_LDS_FLOOR;
 }
 
 int attn8_fwd(AttnArgs& a, hipStream_t s) {

@@ -501,12 +501,33 @@ def _decode_v3(w, BH, Lq, Lk):
     return out[:, :Lq, :Lk]
 
 
+def _decode_v5(w, BH, Lq, Lk):
+    """The per-lane dwords after the lane masks (layout v5, csrc/attn7_common.h lb_bit) -> keep [BH, Lq, Lk]: dword
+    ((bh*nqg + qg)*nt + t)*64 + l, register r of half kb at bit 15 - p (r even) or 31 - p (r odd), p = 8kb + (r>>1);
+    register r of lane l is query 32qg + (l&31), key 64t + 32kb + 8(r>>2) + 4(l>>5) + (r&3)."""
+    nqg, nt = (Lq + 31) // 32, (Lk + 63) // 64
+    d = (w & 0xFFFFFFFF).view(BH, nqg, nt, 64)
+    out = torch.zeros(BH, nqg * 32, nt * 64, dtype=torch.bool)
+    lanes = torch.arange(64)
+    for kb in range(2):
+        for r in range(16):
+            p_ = 8 * kb + (r >> 1)
+            bit = (31 if r & 1 else 15) - p_
+            v = ((d >> bit) & 1).bool()                                     # [BH, nqg, nt, 64 lanes]
+            key = 32 * kb + 8 * (r >> 2) + 4 * (lanes >> 5) + (r & 3)
+            for g in range(nqg):
+                for t in range(nt):
+                    out[:, 32 * g + (lanes & 31), 64 * t + key] = v[:, g, t]
+    return out[:, :Lq, :Lk]
+
+
 @pytest.mark.parametrize("family", ["auto", "v6"])
 @pytest.mark.parametrize("Lq,Lk", [(256, 256), (40, 499), (129, 70)])
 def test_attention_drop_bits_producer_matches_oracle(Lq, Lk, family):
     """fddm_attn_drop_bits (the decoder writes every block's attention-dropout keep bits in two launches ahead of the
     forward): 3 sites of one shape, rng streams 7, 13, 19, against the oracle's contract-v2 mask bit for bit, in the
-    storage layout the selected kernel family reads: layout v3 lane masks (default, csrc/attn7.hip) or the round-4
+    storage layout the selected kernel family reads: layout v3 lane masks and the v5 per-lane dwords after them
+    (default, csrc/attn7.hip, attn7_common.h) or the round-4
     words (bit kk of word (bh, t, q) = keep(q, key 64t + kk))."""
     o = ops()
     B, H, p, seed = 2, 3, 0.1, 77
@@ -529,6 +550,12 @@ def test_attention_drop_bits_producer_matches_oracle(Lq, Lk, family):
         else:
             n3 = B * H * ((Lq + 31) // 32) * nt * 32
             got = _decode_v3(out[s_, :n3].cpu(), B * H, Lq, Lk)
+            # the per-lane dwords (layout v5) that fwd7 / fwd8 / dq7 read: the same bits
+            lw = out[s_, n3:2 * n3].cpu()
+            dw = torch.stack([lw & 0xFFFFFFFF, (lw >> 32) & 0xFFFFFFFF], -1).reshape(-1)
+            ref0 = O.attn_dropout_keep(seed, 7 + 6 * s_, B, H, Lq, Lk, p).reshape(B * H, Lq, Lk)
+            got5 = _decode_v5(dw, B * H, Lq, Lk)
+            assert torch.equal(got5, ref0), f"site {s_} per-lane dwords: {(got5 != ref0).sum().item()} bits differ"
         ref = O.attn_dropout_keep(seed, 7 + 6 * s_, B, H, Lq, Lk, p).reshape(B * H, Lq, Lk)
         assert torch.equal(got, ref), f"site {s_}: {(got != ref).sum().item()} bits differ"
 
