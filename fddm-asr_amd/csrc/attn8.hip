@@ -57,26 +57,27 @@ __device__ __forceinline__ unsigned keep_pack(float x, float y, unsigned kw) {
       : "v"(x), "v"(kw), "v"(y), "i"(B0), "i"(B1));
   return r;
 }
-// the 32-bit bf16 keep mask of score pair P (layout v5, attn7_common.h lb_bit): bits 15 - P and 31 - P of kw moved to
-// bits 15 and 31, then v_perm_b32 replicates their signs into the low and high halves
+// score pair P's keep mask applied to its packed bf16 word v (layout v5, attn7_common.h lb_bit): bits 15 - P and 31 - P
+// of kw moved to bits 15 and 31, v_perm_b32 replicates their signs into the low and high halves, one v_and; a single
+// asm statement, so hipcc pads no hazard state between the steps
 template <int P>
-__device__ __forceinline__ unsigned pair_mask(unsigned kw) {
-  unsigned m;
+__device__ __forceinline__ unsigned keep_pair(unsigned v, unsigned kw) {
+  unsigned t;
   if constexpr (P == 0) {
-    asm volatile("v_perm_b32 %0, %1, %1, %2" : "=v"(m) : "v"(kw), "s"(0x09090808u));
-  } else {
-    unsigned t;
     asm volatile(
-        "v_lshlrev_b32 %1, %3, %2\n\t"
-        "v_perm_b32 %0, %1, %1, %4"
-        : "=&v"(m), "=&v"(t)
-        : "v"(kw), "i"(P), "s"(0x09090808u));
+        "v_perm_b32 %1, %2, %2, %3\n\t"
+        "v_and_b32 %0, %0, %1"
+        : "+v"(v), "=&v"(t)
+        : "v"(kw), "s"(0x09090808u));
+  } else {
+    asm volatile(
+        "v_lshlrev_b32 %1, %4, %2\n\t"
+        "v_perm_b32 %1, %1, %1, %3\n\t"
+        "v_and_b32 %0, %0, %1"
+        : "+v"(v), "=&v"(t)
+        : "v"(kw), "s"(0x09090808u), "i"(P));
   }
-  return m;
-}
-__device__ __forceinline__ f32x4_t mfma16(const uint4& a, const uint4& b, const f32x4_t& c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
-                                                 0, 0, 0);
+  return v;
 }
 
 template <int N>
@@ -89,9 +90,9 @@ __device__ __forceinline__ void vmwait() {
 // Diagnostic build only (-DA8_STAMPS, tools/probe/a8_stamps.py; outputs are overwritten): s_memtime of wave 0 at the
 // kernel's phase points, written over the first output row of the workgroup's query block (16 x 8 B = 128 B)
 #ifdef A8_STAMPS
-#define A8ST(k)                                                   \
-  do {                                                            \
-    if (threadIdx.x == 0) a8st_[k] = __builtin_amdgcn_s_memtime(); \
+#define A8ST(k)                                 \
+  do {                                          \
+    a8st_[k] = __builtin_amdgcn_s_memtime(); /* uniform: SGPRs */ \
   } while (0)
 #else
 #define A8ST(k) \
@@ -127,7 +128,22 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
   const int nqg = (a.Lq + 31) >> 5, qg0 = 8 * bxi + 2 * w;  // the chains' 32-query groups qg0, qg0 + 1
   const unsigned* lbits = (const unsigned*)(a.dbits + (long)a.B * a.H * nqg * ntiles * 32);
 
-  // ---- key mask (compiler-tracked loads, before any untracked one): thread tid owns keys 4 tid .. 4 tid + 3
+  // ---- prologue. The loads are issued in the order they are needed and the prologue fetches no more than the
+  // pipeline's start needs (Q and tiles 0, 1): with every workgroup issuing at once, an instruction that finds the
+  // memory queue full blocks its wave, so a deeper up-front prefetch only delays the first MFMA (stamps: issuing Q +
+  // three tiles took 3.9k-8.6k cycles). Later tiles are fetched one per mid-tile span, their pieces spread over the
+  // phases' chunks.
+  // Q rows of the wave's two chains by LDS-DMA into ring stages 2-3 (free until tile 2's fill): waves 0-1 in the K
+  // ring's stages 2-3, waves 2-3 in the V ring's; the wave's 64 rows (8 KB), chunk c of row r at c ^ (r & 7)
+  unsigned char* qst = sm8 + (w < 2 ? 2 * A7_TB + w * 8192 : 6 * A7_TB + (w - 2) * 8192);
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int r = 8 * u + (lane >> 3), pch = lane & 7;   // row within the wave's 64 queries
+    const unsigned qr = (unsigned)min(qw0 + r, a.Lq - 1);
+    dma16_sv(Qb, qr * (unsigned)a.sq * 2u + (unsigned)((pch ^ (r & 7)) << 4), qst + 8 * u * 128);
+  }
+  // key mask (compiler-tracked loads: hipcc's vmcnt(0) before their use also drains the Q pieces above, whose latency
+  // this overlaps): thread tid owns keys 4 tid .. 4 tid + 3
   unsigned tmask = ntiles >= 32 ? 0xFFFFFFFFu : ((1u << ntiles) - 1u);
   if constexpr (MK != 0) {
     bool any = false;
@@ -155,63 +171,63 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
     if constexpr (MK == 2) tmask &= tact[0] | (tact[1] << 4) | (tact[2] << 8) | (tact[3] << 12);
   }
   const int nact = __builtin_popcount(tmask);
+  A8ST(15);
 
-  // ---- prologue: Q rows of both chains (untracked loads), then tiles 0 .. NS-1 of the active-tile list
+  // tile fills by pieces (K rows 16 w .. + 7 and + 8 .. + 15, V the same, the chains' keep dwords): piece k of tile
+  // tt into stage st. Wave w brings rows 16 w .. 16 w + 15; XOR swizzles applied to the per-lane source addresses.
+  auto piece = [&](int tt, int st, int k) {
+    if (k < 4) {
+      const int u = k >> 1, R = 16 * w + 8 * u;
+      const int r = 64 * tt + R + (lane >> 3), pch = lane & 7;
+      const unsigned rr = (unsigned)min(r, a.Lk - 1);
+      if ((k & 1) == 0) dma16_sv(Kb, rr * sk2 + (unsigned)((pch ^ ((r >> 1) & 7)) << 4), kst + st * A7_TB + R * 128);
+      else dma16_sv(Vb, rr * sv2 + (unsigned)((pch ^ vsw(r)) << 4), vst + st * A7_TB + R * 128);
+    } else {
+      const int c = k - 4;
+      dma4_sv(lbits, (unsigned)(lb_dword(bh, nqg, ntiles, min(qg0 + c, nqg - 1), tt) + lane) * 4u,
+              (const unsigned char*)(kbl + st * 512 + (2 * w + c) * 64));
+    }
+  };
+  // fill cursor over the active tiles; active tile i goes to stage i % NS. Every span issues exactly NP pieces (past
+  // the last active tile: the last one again, into the stage nobody reads), so each wait below is vmcnt(NP).
+  unsigned fmask = tmask;
+  int flast = 0;
+  auto next_fill_tile = [&]() {
+    if (fmask) {
+      flast = __builtin_ctz(fmask);
+      fmask &= fmask - 1u;
+    }
+    return flast;
+  };
+  {
+    const int t0 = next_fill_tile(), t1 = next_fill_tile();
+#pragma unroll
+    for (int k = 0; k < NP; ++k) piece(t0, 0, k);
+#pragma unroll
+    for (int k = 0; k < NP; ++k) piece(t1, 1, k);
+  }
+  A8ST(11);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NP) : "memory");  // Q and tile 0 landed; tile 1 in flight
+  __builtin_amdgcn_s_barrier();                                 // every wave's pieces
+  A8ST(1);
+  // the chains' Q fragments (lane: row qi of chain c, chunk 2 ks + hh), pre-scaled by sl2 (scores in log2 units);
+  // rows past Lq are zeroed (never stored)
   const float sl2 = a.scale * 1.4426950408889634f;
   uint4 qa[4], qb[4];
   const int qA = qw0 + qi, qB = qw0 + 32 + qi;
   {
-    const long ca = min(qA, a.Lq - 1), cb = min(qB, a.Lq - 1);
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      qa[ks] = gload16_asm(Qb + ca * a.sq + 16 * ks + 8 * hh);
-      qb[ks] = gload16_asm(Qb + cb * a.sq + 16 * ks + 8 * hh);
-    }
-  }
-  auto fill = [&](int tt, int st) {
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int R = 16 * w + 8 * u;
-      const int r = 64 * tt + R + (lane >> 3), pch = lane & 7;
-      const unsigned rr = (unsigned)min(r, a.Lk - 1);
-      dma16_sv(Kb, rr * sk2 + (unsigned)((pch ^ ((r >> 1) & 7)) << 4), kst + st * A7_TB + R * 128);
-      dma16_sv(Vb, rr * sv2 + (unsigned)((pch ^ vsw(r)) << 4), vst + st * A7_TB + R * 128);
-    }
-    if constexpr (DROP) {
-#pragma unroll
-      for (int c = 0; c < 2; ++c)
-        dma4_sv(lbits, (unsigned)(lb_dword(bh, nqg, ntiles, min(qg0 + c, nqg - 1), tt) + lane) * 4u,
-                (const unsigned char*)(kbl + st * 512 + (2 * w + c) * 64));
-    }
-  };
-  // fill cursor: the active tiles still to be filled (ascending); active tile i goes to stage i % NS
-  unsigned fmask = tmask;
-  int fst = 0, nfilled = 0;
-  auto fill_next = [&]() {
-    const int tt = __builtin_ctz(fmask);
-    fmask &= fmask - 1u;
-    fill(tt, fst);
-    fst = fst == A8_NS - 1 ? 0 : fst + 1;
-    ++nfilled;
-  };
-  const int npro = min(nact, A8_NS - 1);
-  for (int i = 0; i < npro; ++i) fill_next();
-  // tile 0 landed (and with it the older Q rows): the other prologue fills stay in flight
-  if (npro == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NP) : "memory");
-  else if (npro == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NP) : "memory");
-  else vmwait<0>();
-  {
     const unsigned zA = qA < a.Lq ? 0xFFFFFFFFu : 0u, zB = qB < a.Lq ? 0xFFFFFFFFu : 0u;
+    const int rA = qi, rB = qi + 32;
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
-      u32x4v_t x = __builtin_bit_cast(u32x4v_t, qa[ks]), y = __builtin_bit_cast(u32x4v_t, qb[ks]);
-      asm volatile("" : "+v"(x), "+v"(y));  // uses after the counted wait above
-      qa[ks] = scale_frag(make_uint4(x[0] & zA, x[1] & zA, x[2] & zA, x[3] & zA), sl2);
-      qb[ks] = scale_frag(make_uint4(y[0] & zB, y[1] & zB, y[2] & zB, y[3] & zB), sl2);
+      const uint4 x = *(const uint4*)(qst + rA * 128 + (((2 * ks + hh) ^ (rA & 7)) << 4));
+      const uint4 y = *(const uint4*)(qst + rB * 128 + (((2 * ks + hh) ^ (rB & 7)) << 4));
+      qa[ks] = scale_frag(make_uint4(x.x & zA, x.y & zA, x.z & zA, x.w & zA), sl2);
+      qb[ks] = scale_frag(make_uint4(y.x & zB, y.y & zB, y.z & zB, y.w & zB), sl2);
     }
   }
-  __builtin_amdgcn_s_barrier();  // every wave's pieces of tile 0 landed
-  A8ST(1);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // every wave's Q reads done: stages 2-3 may be filled
 
   // per-lane LDS offsets: K row reads (row qi of a 32-key half, chunk 2 ks + hh), V transposed reads
   int koff[4];
@@ -225,24 +241,19 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
 
   // chain state, softmax in log2 units: rf = the chain's bf16 reference, fixed after its first half-tile (the lane
   // pair's row maximum there, 0 while that is -inf), subtracted inside the score MFMA; O^T accumulators; q5 = the
-  // fifth-k-step operand (-rf, 1); p = packed probabilities; ls = the row sums, accumulated by a 16x16x32 MFMA from
-  // the undropped packed probabilities (ones-selector A operand: row m of the product = the sum of lane n + 16 m's 8
-  // values, so lane n < 16 ends with query n's sum in registers 0 + 2 and query n + 16's in 1 + 3): no VALU adds.
+  // fifth-k-step operand (-rf, 1); p = packed probabilities; ls = the lane's row sum of its keys (f32 adds).
   // With a fixed reference the fast loop has no rescale branch (no phi copies of O). A row sum that ends above 2^64
   // (or inf / NaN) could have overflowed on the way, and one below 2^-40 (a first half-tile fully masked, then scores
   // far below 0) lost its precision: such waves recompute their chains in the wave-local fallback (online softmax with
   // rescaling, fwd7's algorithm), exact but slow — not reached by softmax inputs of sane range.
   float rfA = 0.f, rfB = 0.f;
   f32x16_t oA0 = {}, oA1 = {}, oB0 = {}, oB1 = {};
-  f32x4_t lsA = {}, lsB = {};
+  float lsA = 0.f, lsB = 0.f;  // the lanes' row sums (relative to rf)
   f32x16_t sA, sB;
   uint4 pA[2], pB[2];
   pB[0] = pB[1] = make_uint4(0, 0, 0, 0);
   const uint4 q5init = hh ? make_uint4(0, 0, 0, 0) : make_uint4(pk_bf16(0.f, 1.f), 0u, 0u, 0u);
   uint4 q5A = q5init, q5B = q5init;
-  // the row-sum MFMA's A operand: A[m][8 b + j] = (m == b), i.e. bf16 ones on lanes with (l & 15) == (l >> 4)
-  const unsigned one2 = ((lane & 15) == (lane >> 4)) ? 0x3F803F80u : 0u;
-  const uint4 onesel = make_uint4(one2, one2, one2, one2);
   unsigned kwA = 0xFFFFFFFFu, kwB = 0xFFFFFFFFu;
   // fragments, one buffer each (reads are placed after the last MFMA that used the previous contents): K of a half
   // (4 x ds_read_b128), its fifth-k-step operand k5, V of a half (2 steps x 2 d-blocks, each two tr reads)
@@ -309,51 +320,65 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
 
   // One phase: 9 chunks {an MFMA, one score pair of the other chain's softmax, LDS reads}, fenced. MFMA order: the
   // score chain first (its result feeds the next phase's VALU), then the PV chain (its operand came from the previous
-  // phase); two row-sum MFMAs (16x16x32) ride in chunks 3 and 7, after the 4 pairs they sum were packed.
-  // Per score pair: 2 v_exp, 1 v_cvt_pk, and with dropout the pair mask (shift + v_perm) and one v_and after the
-  // row-sum MFMA has read the undropped word.
+  // phase). A score pair's work is pipelined over two chunks so a chunk's VALU instructions do not wait on each other:
+  // chunk i issues pair i's two v_exp, chunk i + 1 its two row-sum adds, the v_cvt_pk and (dropout) the pair mask
+  // (shift + v_perm) and one v_and. Measured against an MFMA row sum (a 16x16x32 ones-selector product of the packed
+  // probabilities): that cost 3.4 us at C2 cross in stalls around the 16x16 MFMAs (profiles/r06_attn8_ablations.md).
   //   SX: score accumulator (written) from qX / q5X and the current kf / k5
   //   oY0 / oY1 += V^T pY with the current vf; sZ - dZ -> pZ, lsZ: the softmax chain (half KB of the tile: keep bits of
-  //   kwZ at lb_bit(KB, .)); rd(c): the LDS reads of chunk c
+  //   kwZ at lb_bit(KB, .)); rd(c): the LDS reads of chunk c; dm(c): its LDS-DMA pieces of the span's tile fill
   auto phase = [&](f32x16_t& SX, const uint4 (&qX)[4], const uint4& q5X, f32x16_t& oY0, f32x16_t& oY1,
-                   const uint4 (&pY)[2], const f32x16_t& sZ, float dZ, uint4 (&pZ)[2], f32x4_t& lsZ, unsigned kwZ,
-                   auto kbc, auto&& rd) {
+                   const uint4 (&pY)[2], const f32x16_t& sZ, float dZ, uint4 (&pZ)[2], float& lZ, unsigned kwZ,
+                   auto kbc, auto&& rd, auto&& dm) {
     constexpr int KB = decltype(kbc)::value;
-    unsigned msk[8];
-    auto pair = [&](auto ic) {  // exponentials, undropped pack, and the pair's keep mask
+    float ex[8], ey[8], la, lb;
+    // stage 1 of score pair i (chunk i): the two exponentials
+    auto expo = [&](auto ic) {
       constexpr int i = decltype(ic)::value;
 #ifndef A8_NOEXP  // timing-only ablation: no exponentials (wrong results)
-      const float x = __builtin_amdgcn_exp2f(sZ[2 * i] - dZ);
-      const float y = __builtin_amdgcn_exp2f(sZ[2 * i + 1] - dZ);
+      ex[i] = __builtin_amdgcn_exp2f(sZ[2 * i] - dZ);
+      ey[i] = __builtin_amdgcn_exp2f(sZ[2 * i + 1] - dZ);
 #else
-      const float x = sZ[2 * i] - dZ, y = sZ[2 * i + 1] - dZ;
+      ex[i] = sZ[2 * i] - dZ;
+      ey[i] = sZ[2 * i + 1] - dZ;
 #endif
-      unsigned v = pk_bf16(x, y);
-      pinv(v);
-      pset(pZ, ic, v);
-      if constexpr (DROP) msk[i] = pair_mask<8 * KB + i>(kwZ);
+      pinv(ex[i]);
+      pinv(ey[i]);
     };
-    auto drop = [&](auto ic) {
+    // stage 2 (chunk i + 1, so the exponentials have landed and the chunk's VALU work is independent): the row sums,
+    // the bf16 pack and the keep mask
+    auto fin = [&](auto ic) {
       constexpr int i = decltype(ic)::value;
-      if constexpr (DROP) pand(pZ, ic, msk[i]);
+      if constexpr (i == 0) {
+        la = ex[0];
+        lb = ey[0];
+      } else {
+        la += ex[i];
+        lb += ey[i];
+      }
+      pinv(la);
+      pinv(lb);
+      unsigned v = pk_bf16(ex[i], ey[i]);
+#ifndef A8_NODROPMASK
+      if constexpr (DROP) v = keep_pair<8 * KB + i>(v, kwZ);
+      else pinv(v);
+#else
+      pinv(v);
+#endif
+      pset(pZ, ic, v);
     };
-    auto lsum = [&](auto hc) {  // the row-sum MFMA over pairs 4 h .. 4 h + 3
-      constexpr int h = decltype(hc)::value;
-      lsZ = mfma16(onesel, pZ[h], lsZ);
-    };
-    using I0 = std::integral_constant<int, 0>;
-    using I1 = std::integral_constant<int, 1>;
     f32x16_t acc = mfma32(k5, q5X, f32x16_t{});
-    pair(I0{});
-    rd(I0{});
+    expo(std::integral_constant<int, 0>{});
+    rd(std::integral_constant<int, 0>{});
+    dm(std::integral_constant<int, 0>{});
     A8_FENCE();
     static_for<0, 4>([&](auto kc) {
       constexpr int ks = decltype(kc)::value;
       acc = mfma32(kf[ks], qX[ks], acc);
-      pair(std::integral_constant<int, ks + 1>{});
-      if constexpr (ks == 2) lsum(I0{});                       // pairs 0-3 packed (chunk 3)
-      if constexpr (ks == 3) drop(I0{});
+      expo(std::integral_constant<int, ks + 1>{});
+      fin(std::integral_constant<int, ks>{});
       rd(std::integral_constant<int, ks + 1>{});
+      dm(std::integral_constant<int, ks + 1>{});
       A8_FENCE();
     });
     SX = acc;
@@ -361,13 +386,11 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
       constexpr int pi = decltype(pc)::value;  // PV step s = pi >> 1, d-block pi & 1
       if constexpr ((pi & 1) == 0) oY0 = mfma32(vf[pi >> 1][0], pY[pi >> 1], oY0);
       else oY1 = mfma32(vf[pi >> 1][1], pY[pi >> 1], oY1);
-      if constexpr (pi < 3) {
-        pair(std::integral_constant<int, 5 + pi>{});
-        drop(std::integral_constant<int, 1 + pi>{});
-      }
-      if constexpr (pi == 2) lsum(I1{});                      // pairs 4-7 packed (chunk 7)
-      if constexpr (pi == 3) static_for<4, 8>([&](auto ic) { drop(ic); });
+      if constexpr (pi < 3) expo(std::integral_constant<int, 5 + pi>{});
+      fin(std::integral_constant<int, 4 + pi>{});
+      if constexpr (pi == 3) lZ += la + lb;
       rd(std::integral_constant<int, 5 + pi>{});
+      dm(std::integral_constant<int, 5 + pi>{});
       A8_FENCE();
     });
   };
@@ -377,7 +400,7 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
   int t = __builtin_ctz(cmask);
   cmask &= cmask - 1u;
   int st = 0;
-  if (nact == 0) goto epilogue;  // every key masked: NaN rows (torch's softmax over -inf)
+  if (nact > 0) {  // (every key masked: NaN rows, torch's softmax over -inf)
   {
     // pipeline start: K (+ k5) of half 0 and S_A(half 0) against reference 0; V of half 0 for PV_B(-1), which runs
     // with pB = 0 (finite data, zero contribution); keep bits of tile 0
@@ -395,24 +418,41 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) rdv(vst, c);
   }
-  // ---- tile 0, half 0: each chain's reference comes from this half's scores (computed against 0)
+  // ---- tile 0, half 0: each chain's reference comes from this half's scores (computed against 0). This span fills
+  // active tile 2 (stage 2, after the Q reads' barrier): pieces in chunks 1, 4, 7 of both phases
+  int fidx = 2, ftile = next_fill_tile();
+  auto dm_first = [&](auto base, auto cc) {
+    constexpr int c = decltype(cc)::value, k = decltype(base)::value + c / 3;
+    if constexpr (c % 3 == 1 && k < NP) piece(ftile, fidx & 3, k);
+  };
+  auto dm_none = [&](auto) {};
   first_ref(sA, rfA, q5A);
-  phase(sB, qb, q5B, oB0, oB1, pB, sA, rfA, pA, lsA, kwA, std::integral_constant<int, 0>{}, [&](auto cc) {  // alpha (see below)
-    constexpr int c = decltype(cc)::value;
-    if constexpr (c == 1) mk5_read(64 * t + 32);
-    if constexpr (c == 8) mk5_set();
-    if constexpr (c >= 5) kf[c - 5] = *(const uint4*)(kst + koff[c - 5] + 32 * 128);
-  });
+  phase(sB, qb, q5B, oB0, oB1, pB, sA, rfA, pA, lsA, kwA, std::integral_constant<int, 0>{},
+        [&](auto cc) {  // alpha (see below)
+          constexpr int c = decltype(cc)::value;
+          if constexpr (c == 1) mk5_read(64 * t + 32);
+          if constexpr (c == 8) mk5_set();
+          if constexpr (c >= 5) kf[c - 5] = *(const uint4*)(kst + koff[c - 5] + 32 * 128);
+        },
+        [&](auto cc) { dm_first(std::integral_constant<int, 0>{}, cc); });
   first_ref(sB, rfB, q5B);
-  phase(sA, qa, q5A, oA0, oA1, pA, sB, rfB, pB, lsB, kwB, std::integral_constant<int, 0>{}, [&](auto cc) {  // beta
-    constexpr int c = decltype(cc)::value;
-    if constexpr (c < 4) rdv(vst, c);
-  });
+  phase(sA, qa, q5A, oA0, oA1, pA, sB, rfB, pB, lsB, kwB, std::integral_constant<int, 0>{},
+        [&](auto cc) {  // beta
+          constexpr int c = decltype(cc)::value;
+          if constexpr (c < 4) rdv(vst, c);
+        },
+        [&](auto cc) { dm_first(std::integral_constant<int, 3>{}, cc); });
   A8ST(2);
+  // the other spans (mid-tile i to mid-tile i + 1: the current tile's half 1, the next tile's half 0) fill active tile
+  // i + 3 into the stage of tile i - 1 (read out before mid-tile i): pieces in chunks 2 and 6 of the first 3 phases
+  auto dm_span = [&](auto base, auto cc) {
+    constexpr int c = decltype(cc)::value, k = decltype(base)::value + (c == 6 ? 1 : 0);
+    if constexpr ((c == 2 || c == 6) && k < NP) piece(ftile, fidx & 3, k);
+  };
   for (int i = 0;; ++i) {
     const bool more = cmask != 0u;
     // ---- mid-tile: the previous tile's stage is read out by every wave; the next active tile must have landed (own
-    // pieces, then every wave's by the barrier); then that stage takes the tile NS - 1 ahead
+    // pieces, then every wave's by the barrier; the span's fill of the tile after it stays in flight)
     int tn = t, stn = st;
     unsigned kwAn = 0xFFFFFFFFu, kwBn = 0xFFFFFFFFu;
     if (more) {
@@ -420,34 +460,47 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
       cmask &= cmask - 1u;
       stn = st == A8_NS - 1 ? 0 : st + 1;
 #ifndef A8_NOWAIT  // timing-only ablation: no wait for the next tile's DMA (wrong results)
-      if (nfilled > i + 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NP) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NP) : "memory");
 #else
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #endif
       __builtin_amdgcn_s_barrier();
-      A8ST(3 + (i < 8 ? i : 8));
-      if (fmask) fill_next();
+#ifdef A8_STAMPS  // constant indices only (a register array indexed at run time would go to scratch)
+      if (i == 0) A8ST(3);
+      if (i == 1) A8ST(4);
+      if (i == 2) A8ST(5);
+      if (i == 3) A8ST(6);
+      if (i == 4) A8ST(7);
+      if (i == 5) A8ST(8);
+      if (i == 6) A8ST(9);
+      if (i == 7) A8ST(10);
+#endif
       if constexpr (DROP) {
         kwAn = kbl[stn * 512 + (2 * w) * 64 + lane];
         kwBn = kbl[stn * 512 + (2 * w + 1) * 64 + lane];
       }
     }
+    ++fidx;
+    ftile = next_fill_tile();
     {
       const unsigned char* kimn = kst + stn * A7_TB;
       const unsigned char* vimg = vst + st * A7_TB;
       // ---- half 1. alpha: S_B(h1), PV_B(h0); softmax A(h1); reads: k5 and K of the next tile's h0
-      phase(sB, qb, q5B, oB0, oB1, pB, sA, 0.f, pA, lsA, kwA, std::integral_constant<int, 1>{}, [&](auto cc) {
-        constexpr int c = decltype(cc)::value;
-        if constexpr (c == 1) mk5_read(64 * tn);
-        if constexpr (c == 8) mk5_set();
-        if constexpr (c >= 5) kf[c - 5] = *(const uint4*)(kimn + koff[c - 5]);
-      });
+      phase(sB, qb, q5B, oB0, oB1, pB, sA, 0.f, pA, lsA, kwA, std::integral_constant<int, 1>{},
+            [&](auto cc) {
+              constexpr int c = decltype(cc)::value;
+              if constexpr (c == 1) mk5_read(64 * tn);
+              if constexpr (c == 8) mk5_set();
+              if constexpr (c >= 5) kf[c - 5] = *(const uint4*)(kimn + koff[c - 5]);
+            },
+            [&](auto cc) { dm_span(std::integral_constant<int, 0>{}, cc); });
       // beta: V of h1 (chunks 0-3, before its PV in chunks 5-8), S_A(next h0), PV_A(h1); softmax B(h1)
-      phase(sA, qa, q5A, oA0, oA1, pA, sB, 0.f, pB, lsB, kwB, std::integral_constant<int, 1>{}, [&](auto cc) {
-        constexpr int c = decltype(cc)::value;
-        if constexpr (c < 4) rdv(vimg + 32 * 128, c);
-      });
+      phase(sA, qa, q5A, oA0, oA1, pA, sB, 0.f, pB, lsB, kwB, std::integral_constant<int, 1>{},
+            [&](auto cc) {
+              constexpr int c = decltype(cc)::value;
+              if constexpr (c < 4) rdv(vimg + 32 * 128, c);
+            },
+            [&](auto cc) { dm_span(std::integral_constant<int, 2>{}, cc); });
     }
     if (!more) break;
     t = tn;
@@ -458,17 +511,21 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
       const unsigned char* kimg = kst + st * A7_TB;
       const unsigned char* vimg = vst + st * A7_TB;
       // ---- half 0. alpha: S_B(h0), PV_B(previous h1); softmax A(h0); reads: k5 and K of h1 (after S_B's last K use)
-      phase(sB, qb, q5B, oB0, oB1, pB, sA, 0.f, pA, lsA, kwA, std::integral_constant<int, 0>{}, [&](auto cc) {
-        constexpr int c = decltype(cc)::value;
-        if constexpr (c == 1) mk5_read(64 * t + 32);
-    if constexpr (c == 8) mk5_set();
-        if constexpr (c >= 5) kf[c - 5] = *(const uint4*)(kimg + koff[c - 5] + 32 * 128);
-      });
+      phase(sB, qb, q5B, oB0, oB1, pB, sA, 0.f, pA, lsA, kwA, std::integral_constant<int, 0>{},
+            [&](auto cc) {
+              constexpr int c = decltype(cc)::value;
+              if constexpr (c == 1) mk5_read(64 * t + 32);
+              if constexpr (c == 8) mk5_set();
+              if constexpr (c >= 5) kf[c - 5] = *(const uint4*)(kimg + koff[c - 5] + 32 * 128);
+            },
+            [&](auto cc) { dm_span(std::integral_constant<int, 4>{}, cc); });
       // beta: V of h0, S_A(h1), PV_A(h0); softmax B(h0)
-      phase(sA, qa, q5A, oA0, oA1, pA, sB, 0.f, pB, lsB, kwB, std::integral_constant<int, 0>{}, [&](auto cc) {
-        constexpr int c = decltype(cc)::value;
-        if constexpr (c < 4) rdv(vimg, c);
-      });
+      phase(sA, qa, q5A, oA0, oA1, pA, sB, 0.f, pB, lsB, kwB, std::integral_constant<int, 0>{},
+            [&](auto cc) {
+              constexpr int c = decltype(cc)::value;
+              if constexpr (c < 4) rdv(vimg, c);
+            },
+            dm_none);
     }
   }
   // pipeline end: PV_B of the last half
@@ -477,21 +534,19 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
     oB0 = mfma32(vf[s][0], pB[s], oB0);
     oB1 = mfma32(vf[s][1], pB[s], oB1);
   }
+  }  // nact > 0
 
-epilogue:
   A8ST(12);
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
   A8ST(13);  // the ring is free: wave w owns bytes [16 KB w, 16 KB (w + 1)) for the fallback and the staging
   unsigned char* own = sm8 + w * 16384;
-  // the row sums: lanes n < 16 of the row-sum accumulator hold query n's in registers 0 + 2, query n + 16's in 1 + 3
-  auto rowsum = [&](const f32x4_t& ls) {
-    const float slo = ls[0] + ls[2], shi = ls[1] + ls[3];
-    const float a0 = __shfl(slo, qi & 15), a1 = __shfl(shi, qi & 15);
-    return qi < 16 ? a0 : a1;
-  };
-  float ltA = rowsum(lsA), ltB = rowsum(lsB);
+  float ltA = xsum32(lsA), ltB = xsum32(lsB);  // the row sums (the query's keys sit in lanes l and l ^ 32)
+#ifdef A8_NOFALLBACK  // timing-only ablations below skip the fallback (their sums are not softmax sums)
+  if (false) {
+#else
   if (nact > 0 && __any(!(ltA <= 0x1p64f && ltA >= 0x1p-40f) || !(ltB <= 0x1p64f && ltB >= 0x1p-40f))) {
+#endif
     // ---- fallback (guard tripped): both chains again, online softmax with rescaling (fwd7's algorithm), each
     // active tile staged by this wave alone into its own 16 KB (K image 8 KB, V image 8 KB), keep dwords from memory
     unsigned char* kp = own;

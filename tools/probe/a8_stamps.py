@@ -1,7 +1,8 @@
 """Phase timing of fwd8 from in-kernel s_memtime stamps (timing-only build: tools/build_variant.sh a8st attn8
 -fno-slp-vectorize -DA8_STAMPS, then FDDM_HIP_LIB=abl/a8st.so python tools/probe/a8_stamps.py). Stamps of wave 0 of
 every workgroup overwrite the first output row of its query block: 0 start, 1 tile 0 landed (after the prologue's
-barrier), 2 first half-tile done, 3.. mid-tile barriers, 12 loop end, 13 epilogue barrier, 14 stores drained.
+barrier), 2 first half-tile done, 3..10 mid-tile barriers, 12 loop end, 13 epilogue barrier, 14 stores drained;
+15 key mask done (before the Q loads), 11 prologue fills issued.
 Prints, per shape, the median cycles between consecutive stamps over the workgroups and the spread of start times."""
 import os
 import sys
@@ -46,7 +47,8 @@ def main():
         t0 = st[:, 0].min()
         print(f"{name}: {st.shape[0]} WGs, start spread {float(st[:, 0].max() - t0):.0f} cyc, "
               f"end spread {float(st[:, 14].max() - st[:, 14].min()):.0f}, kernel span {float(st[:, 14].max() - t0):.0f}")
-        pts = [0, 1, 2] + [i for i in range(3, 12) if (st[:, i] > 0).all()] + [12, 13, 14]
+        pro = [0, 15, 11, 1] if (st[:, 15] > 0).all() else [0, 11, 1]
+        pts = pro + [2] + [i for i in range(3, 11) if (st[:, i] > 0).all()] + [12, 13, 14]
         seg = []
         for a_, b_ in zip(pts[:-1], pts[1:]):
             seg.append(f"{a_}->{b_} {float((st[:, b_] - st[:, a_]).median()):.0f}")

@@ -11,3 +11,5 @@ for v in nowait noexp; do
   FDDM_HIP_LIB=$PWD/abl/$v.so timeout -k 10 120 python -u tools/attn7_bench.py 20 fwd7,auto > gpurun_out/r06_t5_bench_$v.log 2>&1 || exit 1
 done
 echo done
+FDDM_HIP_LIB=$PWD/abl/a8st.so timeout -k 10 120 python -u tools/probe/a8_stamps.py > gpurun_out/r06_t5_stamps.log 2>&1 || exit 1
+echo done2
