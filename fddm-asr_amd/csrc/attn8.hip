@@ -109,8 +109,7 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
   unsigned char* kst = sm8;                                     // [NS][64 rows][128 B] K, KC swizzle
   unsigned char* vst = sm8 + A8_NS * A7_TB;                     // [NS][64 rows][128 B] V, vsw swizzle
   unsigned* kbl = (unsigned*)(sm8 + 2 * A8_NS * A7_TB);         // [NS][4 waves][2 chains][64 lanes] keep dwords
-  unsigned* tact = kbl + A8_NS * 512;                           // [4] active-tile nibbles per wave (MK 2)
-  unsigned* mpk = tact + 4;                                     // [LkP] bf16 pair (1, mask): the key's fifth k-step
+  unsigned* mpk = kbl + A8_NS * 512 + 4;                        // [LkP] bf16 pair (1, mask): the key's fifth k-step
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hh = lane >> 5, qi = lane & 31;
   int bxi, bh;
@@ -129,10 +128,21 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
   const unsigned* lbits = (const unsigned*)(a.dbits + (long)a.B * a.H * nqg * ntiles * 32);
 
   // ---- prologue. The loads are issued in the order they are needed and the prologue fetches no more than the
-  // pipeline's start needs (Q and tiles 0, 1): with every workgroup issuing at once, an instruction that finds the
-  // memory queue full blocks its wave, so a deeper up-front prefetch only delays the first MFMA (stamps: issuing Q +
-  // three tiles took 3.9k-8.6k cycles). Later tiles are fetched one per mid-tile span, their pieces spread over the
-  // phases' chunks.
+  // pipeline's start needs (key mask, Q, tiles 0 and 1), all untracked by hipcc and waited for by ONE counted vmcnt:
+  // with every workgroup issuing at once, an instruction that finds the memory queue full blocks its wave, so a deeper
+  // up-front prefetch only delays the first MFMA (stamps: issuing Q + three tiles took 3.9k-8.6k cycles). Later tiles
+  // are fetched one per mid-tile span, their pieces spread over the phases' chunks. Every key tile is computed (no
+  // skipping of fully masked tiles: with one workgroup per (b, h) and CU, the kernel lasts as long as its longest
+  // workgroup anyway, and the key mask need not be known before the first fills).
+  // key-padding bytes (MK 2): thread tid's keys 4 tid .. 4 tid + 3, one global_load_ubyte each
+  unsigned kb8[4] = {1u, 1u, 1u, 1u};
+  if constexpr (MK == 2) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = min(4 * tid + j, a.Lk - 1);
+      asm volatile("global_load_ubyte %0, %1, off" : "=v"(kb8[j]) : "v"(a.key_keep + (long)b * a.Lk + k) : "memory");
+    }
+  }
   // Q rows of the wave's two chains by LDS-DMA into ring stages 2-3 (free until tile 2's fill): waves 0-1 in the K
   // ring's stages 2-3, waves 2-3 in the V ring's; the wave's 64 rows (8 KB), chunk c of row r at c ^ (r & 7)
   unsigned char* qst = sm8 + (w < 2 ? 2 * A7_TB + w * 8192 : 6 * A7_TB + (w - 2) * 8192);
@@ -142,35 +152,8 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
     const unsigned qr = (unsigned)min(qw0 + r, a.Lq - 1);
     dma16_sv(Qb, qr * (unsigned)a.sq * 2u + (unsigned)((pch ^ (r & 7)) << 4), qst + 8 * u * 128);
   }
-  // key mask (compiler-tracked loads: hipcc's vmcnt(0) before their use also drains the Q pieces above, whose latency
-  // this overlaps): thread tid owns keys 4 tid .. 4 tid + 3
-  unsigned tmask = ntiles >= 32 ? 0xFFFFFFFFu : ((1u << ntiles) - 1u);
-  if constexpr (MK != 0) {
-    bool any = false;
-    if (4 * tid < LkP) {
-      unsigned mv[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int k = 4 * tid + j;
-        const bool ok = k < a.Lk && (MK == 1 || a.key_keep[(long)b * a.Lk + k] != 0);
-        mv[j] = pk_bf16(1.f, ok ? 0.f : -INFINITY);
-        any |= ok;
-      }
-      *(uint4*)(mpk + 4 * tid) = make_uint4(mv[0], mv[1], mv[2], mv[3]);
-    }
-    if constexpr (MK == 2) {
-      const unsigned long long bal = __ballot(any);  // lanes 16 j .. 16 j + 15 of wave w: the keys of tile 4 w + j
-      if (lane == 0) {
-        unsigned nib = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) nib |= ((bal >> (16 * j)) & 0xFFFFull) ? (1u << j) : 0u;
-        tact[w] = nib;
-      }
-    }
-    __syncthreads();
-    if constexpr (MK == 2) tmask &= tact[0] | (tact[1] << 4) | (tact[2] << 8) | (tact[3] << 12);
-  }
-  const int nact = __builtin_popcount(tmask);
+  const unsigned tmask = ntiles >= 32 ? 0xFFFFFFFFu : ((1u << ntiles) - 1u);
+  const int nact = ntiles;
   A8ST(15);
 
   // tile fills by pieces (K rows 16 w .. + 7 and + 8 .. + 15, V the same, the chains' keep dwords): piece k of tile
@@ -207,8 +190,21 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
     for (int k = 0; k < NP; ++k) piece(t1, 1, k);
   }
   A8ST(11);
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NP) : "memory");  // Q and tile 0 landed; tile 1 in flight
-  __builtin_amdgcn_s_barrier();                                 // every wave's pieces
+  // key bytes, Q and tile 0 landed; tile 1 in flight (the key bytes' registers named, so no use moves above the wait)
+  asm volatile("s_waitcnt vmcnt(%4)" : "+v"(kb8[0]), "+v"(kb8[1]), "+v"(kb8[2]), "+v"(kb8[3]) : "n"(NP) : "memory");
+  // the keys' fifth-k-step operands (1, 0 or -inf)
+  if constexpr (MK != 0) {
+    if (4 * tid < LkP) {
+      unsigned mv[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bool ok = 4 * tid + j < a.Lk && (MK == 1 || (kb8[j] & 0xFFu) != 0);
+        mv[j] = pk_bf16(1.f, ok ? 0.f : -INFINITY);
+      }
+      *(uint4*)(mpk + 4 * tid) = make_uint4(mv[0], mv[1], mv[2], mv[3]);
+    }
+  }
+  __builtin_amdgcn_s_barrier();                                 // every wave's pieces; the key operands in LDS
   A8ST(1);
   // the chains' Q fragments (lane: row qi of chain c, chunk 2 ks + hh), pre-scaled by sl2 (scores in log2 units);
   // rows past Lq are zeroed (never stored)
@@ -332,7 +328,9 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
                    auto kbc, auto&& rd, auto&& dm) {
     constexpr int KB = decltype(kbc)::value;
     float ex[8], ey[8], la, lb;
-    // stage 1 of score pair i (chunk i): the two exponentials
+    unsigned sh[8], u[8], mk[8];
+    // stage 1 of score pair i (chunk i): the two exponentials and the keep word shifted to the pair's bits (layout
+    // v5, attn7_common.h lb_bit: bits 15 - P and 31 - P, P = 8 KB + i, moved to bits 15 and 31)
     auto expo = [&](auto ic) {
       constexpr int i = decltype(ic)::value;
 #ifndef A8_NOEXP  // timing-only ablation: no exponentials (wrong results)
@@ -344,9 +342,13 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
 #endif
       pinv(ex[i]);
       pinv(ey[i]);
+      if constexpr (DROP) {
+        sh[i] = kwZ << (8 * KB + i);
+        pinv(sh[i]);
+      }
     };
-    // stage 2 (chunk i + 1, so the exponentials have landed and the chunk's VALU work is independent): the row sums,
-    // the bf16 pack and the keep mask
+    // stage 2 (chunk i + 1): the row sums, the bf16 pack, the pair's 32-bit keep mask (v_perm: the signs of bits 15 and
+    // 31 replicated into the low and high halves)
     auto fin = [&](auto ic) {
       constexpr int i = decltype(ic)::value;
       if constexpr (i == 0) {
@@ -358,25 +360,49 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
       }
       pinv(la);
       pinv(lb);
-      unsigned v = pk_bf16(ex[i], ey[i]);
+      u[i] = pk_bf16(ex[i], ey[i]);
+      pinv(u[i]);
+      if constexpr (DROP) {
 #ifndef A8_NODROPMASK
-      if constexpr (DROP) v = keep_pair<8 * KB + i>(v, kwZ);
-      else pinv(v);
+        mk[i] = __builtin_amdgcn_perm(sh[i], sh[i], 0x09090808u);
 #else
-      pinv(v);
+        mk[i] = 0xFFFFFFFFu;
 #endif
-      pset(pZ, ic, v);
+        pinv(mk[i]);
+      } else {
+        pset(pZ, ic, u[i]);
+      }
+    };
+    // stage 3 (chunk i + 2): the mask applied -> the PV operand
+    auto apply = [&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      if constexpr (DROP) {
+        unsigned v = u[i] & mk[i];
+        pinv(v);
+        pset(pZ, ic, v);
+      }
+    };
+    // chunk c: stage 1 of pair c, stage 2 of pair c - 1, stage 3 of pair c - 2 (pair 7's stage 3 in chunk 8 as well):
+    // the chunk's VALU instructions are independent of each other
+    auto stages = [&](auto cc) {
+      constexpr int c = decltype(cc)::value;
+      if constexpr (c < 8) expo(std::integral_constant<int, c>{});
+      if constexpr (c >= 1) fin(std::integral_constant<int, c - 1>{});
+      if constexpr (c >= 2) apply(std::integral_constant<int, c - 2>{});
+      if constexpr (c == 8) {
+        apply(std::integral_constant<int, 7>{});
+        lZ += la + lb;
+      }
     };
     f32x16_t acc = mfma32(k5, q5X, f32x16_t{});
-    expo(std::integral_constant<int, 0>{});
+    stages(std::integral_constant<int, 0>{});
     rd(std::integral_constant<int, 0>{});
     dm(std::integral_constant<int, 0>{});
     A8_FENCE();
     static_for<0, 4>([&](auto kc) {
       constexpr int ks = decltype(kc)::value;
       acc = mfma32(kf[ks], qX[ks], acc);
-      expo(std::integral_constant<int, ks + 1>{});
-      fin(std::integral_constant<int, ks>{});
+      stages(std::integral_constant<int, ks + 1>{});
       rd(std::integral_constant<int, ks + 1>{});
       dm(std::integral_constant<int, ks + 1>{});
       A8_FENCE();
@@ -386,9 +412,7 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
       constexpr int pi = decltype(pc)::value;  // PV step s = pi >> 1, d-block pi & 1
       if constexpr ((pi & 1) == 0) oY0 = mfma32(vf[pi >> 1][0], pY[pi >> 1], oY0);
       else oY1 = mfma32(vf[pi >> 1][1], pY[pi >> 1], oY1);
-      if constexpr (pi < 3) expo(std::integral_constant<int, 5 + pi>{});
-      fin(std::integral_constant<int, 4 + pi>{});
-      if constexpr (pi == 3) lZ += la + lb;
+      stages(std::integral_constant<int, 5 + pi>{});
       rd(std::integral_constant<int, 5 + pi>{});
       dm(std::integral_constant<int, 5 + pi>{});
       A8_FENCE();
