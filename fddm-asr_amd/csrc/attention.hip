@@ -2404,6 +2404,19 @@ static int g_attn_v6 = 0;
                             // (b, h) walks every 64-query tile, measured slower than dq7 + dkv7 at Lq 512)
 #endif
 static bool attn7_enabled() { return g_attn_v6 != 1; }
+// compute units of the current device (cached; one process drives one GPU)
+static long attn_cu_count() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) ==
+                                                 hipSuccess && v > 0)
+      n = v;
+    else
+      n = 256;
+  }
+  return n;
+}
 
 template <typename T>
 static int run(int which, AttnArgs& a, hipStream_t s) {
@@ -2430,7 +2443,14 @@ static int run(int which, AttnArgs& a, hipStream_t s) {
                                           a.seed_off, s);
             if (e) return e;
           }
-          return g_attn_v6 == 3 ? attn7_fwd(a, s) : attn8_fwd(a, s);
+          // fwd8 (256 queries per workgroup, two chains per wave) unless its grid loads the busiest CU with more
+          // queries than fwd7's (128 per workgroup) does: C2 (256 workgroups, one per CU) takes fwd8; C4 (B16 H12
+          // Lq 512: 384 fwd8 workgroups -> 512 queries on half the CUs, vs 768 fwd7 workgroups -> 384 on every CU)
+          // takes fwd7 (measured 24.5 vs 25.1-25.7 us)
+          const long nh = (long)a.B * a.H, ncu = attn_cu_count();
+          const long load8 = (nh * ((a.Lq + 255) / 256) + ncu - 1) / ncu * 256;
+          const long load7 = (nh * ((a.Lq + 127) / 128) + ncu - 1) / ncu * 128;
+          return (g_attn_v6 == 3 || (g_attn_v6 != 4 && load8 > load7)) ? attn7_fwd(a, s) : attn8_fwd(a, s);
         }
         const size_t lds = (size_t)2 * 2 * 64 * 128 + (size_t)LkP * 4 +
                            (dm == 1 ? (size_t)ntiles * qw * 8 : dm == 2 ? (size_t)3 * ATTN_R * 2 : 0);
@@ -2489,7 +2509,7 @@ static int run(int which, AttnArgs& a, hipStream_t s) {
     }
     if (which == 4) {  // the 32x32x16 family: the fused launch for Lq <= 256 and Lk <= 512 (one or two key passes),
                        // else dq7 (also writes dkv7's row terms), then dkv7
-      if ((g_attn_v6 == 0 || g_attn_v6 == 3) && a.Lk <= 512 && a.Lq <= A7_FUSED_MAXLQ) return attn7_bwdf(a, s);
+      if ((g_attn_v6 == 0 || g_attn_v6 >= 3) && a.Lk <= 512 && a.Lq <= A7_FUSED_MAXLQ) return attn7_bwdf(a, s);
       const int e = attn7_dq(a, s);
       return e ? e : attn7_dkv(a, s);
     }
@@ -2561,7 +2581,7 @@ FDDM_API int fddm_attn_stamps_clear() {
 
 FDDM_API int fddm_attn_set_kernels(int v6) {
   const int old = g_attn_v6;
-  g_attn_v6 = (v6 >= 1 && v6 <= 3) ? v6 : 0;
+  g_attn_v6 = (v6 >= 1 && v6 <= 4) ? v6 : 0;
   return old;
 }
 

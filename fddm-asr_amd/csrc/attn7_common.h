@@ -50,6 +50,19 @@ __device__ __forceinline__ void dma4_sv(const void* sbase, unsigned voff, const 
   asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dword %0, %1" ::"v"(voff), "s"(sbase), "s"(la) : "memory", "m0");
 }
 
+// the same with the LDS destination as a byte address (wave-uniform integer): no generic->LDS pointer conversion (and
+// its null-pointer select) per piece
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  typedef __attribute__((address_space(3))) const void* lcp_t;
+  return (unsigned)(size_t)(lcp_t)p;
+}
+__device__ __forceinline__ void dma16_so(const void* sbase, unsigned voff, unsigned la) {
+  asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(la) : "memory", "m0");
+}
+__device__ __forceinline__ void dma4_so(const void* sbase, unsigned voff, unsigned la) {
+  asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dword %0, %1" ::"v"(voff), "s"(sbase), "s"(la) : "memory", "m0");
+}
+
 __device__ __forceinline__ s16x4_t tr_read(const unsigned char* p) {
   typedef __attribute__((address_space(3))) s16x4_t* lp;
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(p));

@@ -158,17 +158,22 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
 
   // tile fills by pieces (K rows 16 w .. + 7 and + 8 .. + 15, V the same, the chains' keep dwords): piece k of tile
   // tt into stage st. Wave w brings rows 16 w .. 16 w + 15; XOR swizzles applied to the per-lane source addresses.
+  // Addressing: the swizzles depend on the row mod 16 only (tile-invariant); LDS destinations as integer byte
+  // addresses (no pointer conversion per piece); source offsets by 24-bit multiplies (rows < 2^24, strides < 2^23).
+  const unsigned kst_a = lds_addr(kst), vst_a = lds_addr(vst), kbl_a = lds_addr(kbl);
   auto piece = [&](int tt, int st, int k) {
     if (k < 4) {
       const int u = k >> 1, R = 16 * w + 8 * u;
-      const int r = 64 * tt + R + (lane >> 3), pch = lane & 7;
-      const unsigned rr = (unsigned)min(r, a.Lk - 1);
-      if ((k & 1) == 0) dma16_sv(Kb, rr * sk2 + (unsigned)((pch ^ ((r >> 1) & 7)) << 4), kst + st * A7_TB + R * 128);
-      else dma16_sv(Vb, rr * sv2 + (unsigned)((pch ^ vsw(r)) << 4), vst + st * A7_TB + R * 128);
+      const int r0 = R + (lane >> 3), pch = lane & 7;
+      const unsigned rr = (unsigned)min(64 * tt + r0, a.Lk - 1);
+      if ((k & 1) == 0)
+        dma16_so(Kb, __umul24(rr, sk2) + (unsigned)((pch ^ ((r0 >> 1) & 7)) << 4), kst_a + st * A7_TB + R * 128);
+      else
+        dma16_so(Vb, __umul24(rr, sv2) + (unsigned)((pch ^ vsw(r0)) << 4), vst_a + st * A7_TB + R * 128);
     } else {
       const int c = k - 4;
-      dma4_sv(lbits, (unsigned)(lb_dword(bh, nqg, ntiles, min(qg0 + c, nqg - 1), tt) + lane) * 4u,
-              (const unsigned char*)(kbl + st * 512 + (2 * w + c) * 64));
+      dma4_so(lbits, (unsigned)(lb_dword(bh, nqg, ntiles, min(qg0 + c, nqg - 1), tt) + lane) * 4u,
+              kbl_a + (st * 512 + (2 * w + c) * 64) * 4);
     }
   };
   // fill cursor over the active tiles; active tile i goes to stage i % NS. Every span issues exactly NP pieces (past

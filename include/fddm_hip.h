@@ -229,8 +229,10 @@ int fddm_lfd_std_bwd_apply(int zt_dtype, const float* dzt, const void* zt, const
 int fddm_gemm_force_path(int path);
 /* ---- attention kernel-family override for tests and diagnostics: 1 = the 16x16x32-MFMA kernels (fwd6, dq4 / dkv4,
  *      bwd3s) wherever the 32x32x16-MFMA family (csrc/attn7.hip) would run, 2 = the 32x32x16 family without its fused
- *      backward (dq7 + dkv7 at every Lk), 0 = automatic (default). Returns the previous setting. Process-wide; the
- *      train step never sets it. */
+ *      backward (dq7 + dkv7 at every Lk), 3 = the default with every forward on the one-chain fwd7, 4 = the default
+ *      with every forward on the two-chain fwd8 (csrc/attn8.hip), 0 = automatic (default: fwd8 unless its 256-query
+ *      workgroups load the busiest CU with more queries than fwd7's 128-query ones). Returns the previous setting.
+ *      Process-wide; the train step never sets it. */
 int fddm_attn_set_kernels(int v6);
 
 

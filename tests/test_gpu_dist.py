@@ -412,7 +412,9 @@ def test_rccl_world1_forced_dp_step_matches_single_gpu():
     give the single-GPU result). The fp32 kernels' atomics make runs differ by ~1.5e-6 (KL step) and ~1e-5 (L_fd step)
     norm-wise even between two plain runs (tools/probe/rccl_diag.py: gloo vs gloo-bulk 7.7e-6 on the L_fd step), so
     the bar is that spread: gradients within 5e-5 of the gloo run and of the plain single-GPU step (whose L_fd
-    statistics take the local kernels), parameters after AdamW within 1e-5. The two projector biases whose true
+    statistics take the local kernels). Parameters after two AdamW steps within 1e-3 norm-wise: the update g / sqrt(v)
+    has magnitude ~lr whatever |g| is, so elements whose gradient is at the noise level take noise-driven steps (two
+    plain runs already differ by 1.9e-4 .. 2.8e-4 on the worst parameter, measured on MI355X). The two projector biases whose true
     gradient is zero (the L_fd standardisation removes them; NOISE_ONLY) are left out, as in the other DP tests.
     Not a scaling number: SCALE runs on the driver's 8-GPU node."""
     ref_g, ref_p, ref_log = _spawn_one(None)
@@ -435,12 +437,14 @@ def test_rccl_world1_forced_dp_step_matches_single_gpu():
             a, g, r = (torch.from_numpy(x).double() for x in (rc_g[i][n], glo_g[i][n], v))
             exact += int(torch.equal(a, g))
             w_gloo, w_ref = max(w_gloo, rel(a, g)), max(w_ref, rel(a, r))
-    p_gloo, p_ref = 0.0, 0.0
+    p_gloo, p_ref, p_worst = 0.0, 0.0, ""
     for n, v in ref_p.items():
         if n in NOISE_ONLY:
             continue
         a, g, r = (torch.from_numpy(x).double() for x in (rc_p[n], glo_p[n], v))
+        if max(rel(a, g), rel(a, r)) > max(p_gloo, p_ref):
+            p_worst = n
         p_gloo, p_ref = max(p_gloo, rel(a, g)), max(p_ref, rel(a, r))
     print(f"RCCL world-1: {exact} gradient tensors bit-identical to the gloo run; worst gradient rel diff vs gloo "
-          f"{w_gloo:.2e}, vs the single-GPU step {w_ref:.2e}; worst parameter rel diff {p_gloo:.2e} / {p_ref:.2e}")
-    assert w_gloo < 5e-5 and w_ref < 5e-5 and p_gloo < 1e-5 and p_ref < 1e-5
+          f"{w_gloo:.2e}, vs the single-GPU step {w_ref:.2e}; worst parameter rel diff {p_gloo:.2e} / {p_ref:.2e} ({p_worst})")
+    assert w_gloo < 5e-5 and w_ref < 5e-5 and p_gloo < 1e-3 and p_ref < 1e-3

@@ -3,8 +3,8 @@ the producer as the decoder does): "v6" = attention.hip's 16x16x32 kernels (fwd6
 default choice (attn7.hip's 32x32x16 kernels where they apply). Prints us per launch and the fraction of the dense
 bf16 MFMA peak (fwd 4 Lq Lk 64, bwd 10 Lq Lk 64 FLOP per (b, h)), and the max |difference| between the families'
 outputs (bf16 roundings of the same math).
-  python tools/attn7_bench.py [iters] [family,family]   (default families: v6,auto; "fwd7" = the default with the
-  one-chain forward fwd7 instead of the two-chain fwd8)"""
+  python tools/attn7_bench.py [iters] [family,family]   (default families: v6,auto; "fwd7" / "fwd8" = the default with
+  every forward on the one-chain fwd7 / the two-chain fwd8)"""
 import os
 import sys
 
