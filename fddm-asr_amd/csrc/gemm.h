@@ -5,7 +5,9 @@
 
 namespace fddm {
 
-enum { EPI_STORE = 0, EPI_GELU = 1, EPI_ACC_F32 = 2, EPI_GELU_ONLY = 3, EPI_DGELU = 4 };
+// EPI_ROPE_ACC (gemm128, A KC + B MC, f32 out): C += rope_bwd(A B) with the decoder's RoPE pairing (column j with
+// j + N/2, written to columns 2j, 2j+1; misc.hip rope_bwd_kernel), rope tables rcs / rsn [rL][N]
+enum { EPI_STORE = 0, EPI_GELU = 1, EPI_ACC_F32 = 2, EPI_GELU_ONLY = 3, EPI_DGELU = 4, EPI_ROPE_ACC = 5 };
 
 // implicit-conv addressing of a KC A operand: A(m,k) = A + (m/Mi)*sAb + (t*cstride - cpad + k/Cg)*lda + k%Cg,
 // t = m%Mi, zero outside 0 <= time < Tin (WavLM conv feature extractor and grouped positional conv)
@@ -23,6 +25,9 @@ struct GemmArgs {
   long ksplit;                 // K elements per split-K slice (plain GEMM)
   float* colsum;               // optional: colsum[m] += sum_k A(m,k) (MC A operand) — fused bias gradient
   const uint64_t* seed_off;    // graph-replay seed offset (common.h eff_seed) or null
+  const float* rcs = nullptr;  // EPI_ROPE_ACC: cos / sin tables [rL][N] (row m uses position m % rL)
+  const float* rsn = nullptr;
+  long rL = 0;
 };
 
 // KC LDS image: 16-B chunk c of 128-B row r at r*128 + ((c ^ ((r>>1)&7))<<4) — conflict-free ds_read_b128 of

@@ -697,6 +697,19 @@ FDDM_API int fddm_gemm_force_path(int path) {
   return old;
 }
 
+// dx[M][N] += rope_bwd(dy[M][K] @ w[K][N]) — the decoder's self-attention input gradient through RoPE in one launch
+// (gemm128 EPI_ROPE_ACC; replaces linear_dx into an f32 temporary + fddm_rope_bwd, ref models/denoise_decoder.py:
+// 150-156 apply_rope backward). bf16 dy / w, f32 dx and tables [L][N]; N % 128 == 0.
+FDDM_API int fddm_linear_dx_rope(const void* dy, long ldy, const void* w, long ldw, float* dx, long lddx, const float* cs,
+                                 const float* sn, long M, long N, long K, long L, void* hip_stream) {
+  if (M <= 0 || N <= 0) return 0;
+  if (!g128_enabled() || K % 8 || ldy % 8 || ldw % 8 || ((uintptr_t)dy & 15) || ((uintptr_t)w & 15) || ((uintptr_t)dx & 15))
+    return (int)hipErrorInvalidValue;
+  GemmArgs g{dy, ldy, 1L << 62, 0, w, ldw, dx, lddx, nullptr, nullptr, 1.f, M, N, K, 0, 0, 0u, 1.f, ConvGeo{1, 0, 0, 0}, 0, 0, 0, 0, K,
+             nullptr, g_seed_off, cs, sn, L};
+  return gemm128_launch(g, true, false, EPI_ROPE_ACC, FDDM_F32, 1, (hipStream_t)hip_stream);
+}
+
 FDDM_API int fddm_gemm(int dtype, int a_dtype, int a_kc, int b_kc, int epi, int out_dtype, const void* A, long lda,
                        long Mi, long sAb, const void* B, long ldb, void* C, long ldc, void* C2, const float* bias,
                        float alpha, long M, long N, long K, unsigned long long seed, unsigned long long stream,

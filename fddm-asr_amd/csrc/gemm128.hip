@@ -58,8 +58,10 @@ __device__ __forceinline__ int mc_sw(int k) { return ((k & 3) << 1) | (((k >> 3)
 
 // per-lane DMA source byte offsets (tile origin r0 included) of a wave's 2 instructions for one operand image
 // (16 wave-instructions of 1 KB fill a 16-KB image: wave w issues numbers 2w, 2w+1)
+// rope: the MC image's 128 columns are 64 of the first half of the output and their RoPE partners 64 further in the
+// second half (rh = N / 2): logical chunk 8 wc + q holds columns r0 + 32 wc + 8 q (q < 4) or r0 + rh + 32 wc + 8 (q - 4)
 template <bool KC>
-__device__ __forceinline__ void dma_offsets(int (&v)[2], int wid, int lane, int r0, int ld) {
+__device__ __forceinline__ void dma_offsets(int (&v)[2], int wid, int lane, int r0, int ld, int rh = 0) {
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int gi = wid * 2 + u;
@@ -70,7 +72,8 @@ __device__ __forceinline__ void dma_offsets(int (&v)[2], int wid, int lane, int 
     } else {
       const int k = gi * 4 + (lane >> 4);
       const int c = (lane & 15) ^ mc_sw(k);
-      v[u] = (k * ld + r0 + c * 8) * 2;
+      const int col = rh ? r0 + ((c >> 3) << 5) + ((c >> 2) & 1) * rh + ((c & 3) << 3) : r0 + c * 8;
+      v[u] = (k * ld + col) * 2;
     }
   }
 }
@@ -95,7 +98,8 @@ __device__ __forceinline__ void tile128(const GemmArgs& g, unsigned char* smem, 
   const int grp = wid >> 2, w4 = wid & 3, wr = w4 >> 1, wc = w4 & 1;  // grp = k-half of every K-tile
   const int fr = lane & 15, fg = lane >> 4;
   const int M = (int)g.M, N = (int)g.N;
-  const int m0 = min(by * BM, M - BM), n0 = min(bx * BN, N - BN);
+  constexpr bool ROPE = EPI == EPI_ROPE_ACC;
+  const int m0 = min(by * BM, M - BM), n0 = ROPE ? bx * (BN / 2) : min(bx * BN, N - BN);
   const int lda = (int)g.lda, ldb = (int)g.ldb;
   int kbeg = 0, kend = (int)g.K;
   if (nz > 1) {
@@ -111,7 +115,7 @@ __device__ __forceinline__ void tile128(const GemmArgs& g, unsigned char* smem, 
   const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)g.B, 0, (int)recB, SRD_W3);
   int va[2], vb[2];
   dma_offsets<AKC>(va, wid, lane, m0, lda);
-  dma_offsets<BKC>(vb, wid, lane, n0, ldb);
+  dma_offsets<BKC>(vb, wid, lane, n0, ldb, ROPE ? N / 2 : 0);
   auto issue = [&](int kt, int st) {
     const int kk = kbeg + kt * 64;
     const int sa = AKC ? kk * 2 : kk * lda * 2, sb = BKC ? kk * 2 : kk * ldb * 2;
@@ -268,7 +272,7 @@ __device__ __forceinline__ void tile128(const GemmArgs& g, unsigned char* smem, 
     constexpr int G = decltype(gc)::value, I0 = 2 * G, P0 = 2 - 2 * G;  // own / partner's row blocks
     f32x4_t bv[4];
     uint2 pre[2][4];
-    if constexpr (EPI != EPI_ACC_F32) {
+    if constexpr (EPI != EPI_ACC_F32 && !ROPE) {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         bv[j] = g.bias ? *(const f32x4_t*)(g.bias + nw + 16 * j + 4 * fg) : f32x4_t{0.f, 0.f, 0.f, 0.f};
@@ -289,7 +293,39 @@ __device__ __forceinline__ void tile128(const GemmArgs& g, unsigned char* smem, 
     for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[I0 + ii][j] += red[((I0 + ii) * 4 + j) * 64 + lane];
-    if constexpr (EPI == EPI_ACC_F32) {
+    if constexpr (ROPE) {
+      // column block j < 2 holds columns jj = n0 + 32 wc + 16 j + 4 fg + e of the first half, block j + 2 their
+      // partners jj + N/2: dx[m][2 jj] += a cs[p][2 jj] + b sn[p][2 jj], dx[m][2 jj + 1] += -a sn[p][2 jj + 1] +
+      // b cs[p][2 jj + 1] (p = m % rL): 8 consecutive f32 outputs per lane and block pair
+      const int mlo = by * BM;
+      float* C = (float*)g.C;
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii) {
+        const int m = mw + 16 * (I0 + ii) + fr;
+        const long p = m % (int)g.rL;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int c2 = 2 * (n0 + 32 * wc + 16 * j + 4 * fg);
+          const f32x4_t a = acc[I0 + ii][j] * alpha, b = acc[I0 + ii][j + 2] * alpha;
+          const f32x4_t c0 = *(const f32x4_t*)(g.rcs + p * N + c2), c1 = *(const f32x4_t*)(g.rcs + p * N + c2 + 4);
+          const f32x4_t s0 = *(const f32x4_t*)(g.rsn + p * N + c2), s1 = *(const f32x4_t*)(g.rsn + p * N + c2 + 4);
+          f32x4_t* cp = (f32x4_t*)(C + (long)m * ldc + c2);
+          if (m >= mlo) {
+            f32x4_t u = cp[0], v = cp[1];
+            u[0] += a[0] * c0[0] + b[0] * s0[0];
+            u[1] += -a[0] * s0[1] + b[0] * c0[1];
+            u[2] += a[1] * c0[2] + b[1] * s0[2];
+            u[3] += -a[1] * s0[3] + b[1] * c0[3];
+            v[0] += a[2] * c1[0] + b[2] * s1[0];
+            v[1] += -a[2] * s1[1] + b[2] * c1[1];
+            v[2] += a[3] * c1[2] + b[3] * s1[2];
+            v[3] += -a[3] * s1[3] + b[3] * c1[3];
+            cp[0] = u;
+            cp[1] = v;
+          }
+        }
+      }
+    } else if constexpr (EPI == EPI_ACC_F32) {
       // park the finished 32x64 f32 rows in LDS (chunk c of row r at c ^ (r & 15)), then add one 256-B row per
       // instruction: split-K slices atomically, a single slice by read-modify-write
       float* tl = (float*)(smem + 65536) + wid * 2048;
@@ -429,6 +465,9 @@ bool gemm128_ok(const GemmArgs& g, bool akc, bool bkc, int epi, int out_dtype) {
   if (aext * 2 >= (1L << 31) || bext * 2 >= (1L << 31)) return false;
   if (((g.M - 1) * g.ldc + g.N) * 4 >= (1L << 31)) return false;
   if (!akc && bkc) return false;
+  if (epi == EPI_ROPE_ACC)  // whole 128-column tiles of partner pairs, tables and output 16-B aligned
+    return akc && !bkc && out_dtype == FDDM_F32 && g.N % 128 == 0 && g.ldc % 4 == 0 && g.rL > 0 && g.rcs && g.rsn &&
+           !(((uintptr_t)g.rcs | (uintptr_t)g.rsn) & 15);
   if (out_dtype == FDDM_F32) return epi == EPI_STORE || epi == EPI_ACC_F32;
   if (!akc) return false;
   if (!bkc) return epi == EPI_STORE || epi == EPI_DGELU;
@@ -448,6 +487,7 @@ int gemm128_launch(const GemmArgs& g, bool akc, bool bkc, int epi, int out_dtype
     return launch<true, true, EPI_STORE, bf16_t>(g, nz, s);
   }
   if (akc && !bkc) {
+    if (epi == EPI_ROPE_ACC) return nz == 1 ? launch<true, false, EPI_ROPE_ACC, float>(g, nz, s) : (int)hipErrorInvalidValue;
     if (out_dtype == FDDM_F32) return epi == EPI_ACC_F32 ? launch<true, false, EPI_ACC_F32, float>(g, nz, s)
                                                          : launch<true, false, EPI_STORE, float>(g, nz, s);
     if (epi == EPI_DGELU) return launch<true, false, EPI_DGELU, bf16_t>(g, nz, s);

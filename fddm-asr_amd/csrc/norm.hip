@@ -252,7 +252,10 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnBwdArgs a) {
 // the slab adds them with one atomic per column and quantity. CH = 8-column chunks per lane (d <= 512*CH).
 // The device-scope atomics bound the kernel (every slab adds into the same d columns of dgamma/dbeta): at d 512,
 // N 8192, 16-row slabs of 4 waves took 24.0 us, 8 waves 23.4, 32-row slabs 18.5, 64-row slabs 21.8 (occupancy).
-constexpr int LNB_ROWS = 32;
+#ifndef LN_BWD_ROWS
+#define LN_BWD_ROWS 32
+#endif
+constexpr int LNB_ROWS = LN_BWD_ROWS;
 constexpr int LN_FOLD_MAX = 4;  // jobs per fddm_ln_fold launch
 // keep bits of the 8 dropout decisions of elements e0..e0+7 (e0 % 8 == 0): two hash words
 __device__ __forceinline__ unsigned keep8(uint64_t seed, uint64_t stream, uint64_t e0, unsigned thr) {

@@ -366,8 +366,9 @@ class DecoderBlockFn(torch.autograd.Function):
             bwd_s()
         dw_jobs += [(dqk, xr, gsa_w[: 2 * d], gsa_b[: 2 * d]), (dv, xT, gsa_w[2 * d:], gsa_b[2 * d:])]
         ops.linear_dx(dv, W["sa"][2 * d:], out=dx, accumulate=True)
-        dxr = ops.linear_dx(dqk, W["sa"][: 2 * d])
-        ops.rope_bwd(dxr, cos, sin, dx, L)
+        if not ops.linear_dx_rope(dqk, W["sa"][: 2 * d], dx, cos, sin, L):     # dx += rope_bwd(dqk W_qk)
+            dxr = ops.linear_dx(dqk, W["sa"][: 2 * d])
+            ops.rope_bwd(dxr, cos, sin, dx, L)
         lnp.fold()
         _dw_flush(dw_jobs)
         rt.grads_ready(params)

@@ -7,6 +7,7 @@ never sees operands that disagree with its grid.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -160,6 +161,31 @@ def linear_dx(dy2d, w, out=None, accumulate=False, out_dtype=torch.float32, epi=
     e = EPI_ACC if accumulate else (EPI_STORE if epi is None else epi)
     return gemm(dy2d, w, out, M, K, N, a_kc=True, b_kc=False, lda=dy2d.stride(0), ldb=K, ldc=out.stride(0), epi=e,
                 C2=C2, drop_p=drop_p, seed=seed, rng_stream=rng_stream)
+
+
+_NO_ROPE_FUSE = os.environ.get("FDDM_ROPE_FUSE", "1") == "0"     # diagnostic A/B knob (tools/ab.sh)
+
+
+def linear_dx_rope(dy2d, w, dx, cs, sn, L) -> bool:
+    """dx[M,d] += rope_bwd(dy[M,n] @ w[n,d]) in one launch (fddm_linear_dx_rope: the self-attention input gradient
+    through RoPE). Returns False, launching nothing, where the fused kernel does not apply (not bf16, d % 128 != 0,
+    a GEMM-family override): the caller then runs linear_dx into a temporary + rope_bwd."""
+    M, N = dy2d.shape
+    d = w.shape[1]
+    if _NO_ROPE_FUSE:
+        return False
+    if not (dy2d.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and dx.dtype == torch.float32 and d % 128 == 0
+            and w.shape[0] == N and w.is_contiguous() and dy2d.stride(1) == 1 and dx.is_contiguous()
+            and cs.is_contiguous() and sn.is_contiguous() and cs.dtype == torch.float32 and cs.shape[-1] == d):
+        return False
+    rc = lib().fddm_linear_dx_rope(ptr(dy2d), dy2d.stride(0), ptr(w), d, ptr(dx), d, ptr(cs), ptr(sn), M, d, N, L,
+                                   stream())
+    if rc == 1:      # hipErrorInvalidValue: not applicable, nothing launched
+        return False
+    if rc != 0:
+        msg = lib().fddm_error_string(rc)
+        raise RuntimeError(f"fddm_linear_dx_rope failed: hipError {rc} ({msg.decode() if msg else '?'})")
+    return True
 
 
 def linear_dw(dy2d, x2d, out=None, accumulate=False, db=None):

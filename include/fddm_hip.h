@@ -41,6 +41,15 @@ int fddm_gemm(int dtype, int a_dtype, int a_kc, int b_kc, int epi, int out_dtype
               long N, long K, unsigned long long seed, unsigned long long stream, float drop_p, float* colsum,
               void* hip_stream);
 
+/* ---- self-attention input gradient through RoPE: dx[M][N] += rope_bwd(dy[M][K] @ w[K][N]) in one launch (the
+ *      RoPE pairing of fddm_rope_bwd: column j with j + N/2, into columns 2j, 2j+1; tables cs / sn [L][N], row m at
+ *      position m % L). bf16 dy (row stride ldy) and w (stored [K][N], row stride ldw), f32 dx; N % 128 == 0.
+ *      Replaces fddm_gemm (A K-contiguous, B as stored, f32 store) into a temporary followed by fddm_rope_bwd
+ *      (reference: models/denoise_decoder.py:150-156, apply_rope's backward). hipErrorInvalidValue when the shape
+ *      or the kernel override (fddm_gemm_force_path) rules it out: the caller then takes the two-launch path. */
+int fddm_linear_dx_rope(const void* dy, long ldy, const void* w, long ldw, float* dx, long lddx, const float* cs,
+                        const float* sn, long M, long N, long K, long L, void* hip_stream);
+
 /* ---- launch shape of the persistent 256x256 GEMM: at most `cap` workgroups (rounded down to a multiple
  *      of 8; 0 = one per CU). Returns the previous cap. train.py lowers it while it enqueues the frozen
  *      encoder of the next batch on a second stream, so the decoder's launches keep CUs of their own

@@ -755,6 +755,26 @@ def test_ln_fwd_bf16_post_ln_rows(N, d):
     close(rstd, 1 / torch.sqrt(s.var(1, unbiased=False) + 1e-5), rtol=1e-4, what="rstd")
 
 
+@pytest.mark.parametrize("B,L,d,n", [(2, 100, 512, 1024), (1, 256, 256, 512), (3, 50, 128, 256)])
+def test_linear_dx_rope_matches_gemm_then_rope_bwd(B, L, d, n):
+    """fddm_linear_dx_rope (gemm128 EPI_ROPE_ACC: dx += rope_bwd(dy @ w), RoPE partner columns j, j + d/2 loaded into
+    one tile) against float64: dy @ w, then the oracle's RoPE backward by autograd, added to a random dx. Ragged row
+    counts (200, 150) exercise the overlapping last tile."""
+    o = ops()
+    M = B * L
+    inv = O.rope_inv_freq(d)
+    cos, sin = O.rope_cos_sin(L, inv)
+    dy = torch.randn(M, n, generator=g(60)).to(torch.bfloat16)
+    w = (torch.randn(n, d, generator=g(61)) / math.sqrt(n)).to(torch.bfloat16)
+    dx0 = torch.randn(M, d, generator=g(62))
+    dx = dx0.to(dev)
+    assert o.linear_dx_rope(dy.to(dev), w.to(dev), dx, cos.to(dev).contiguous(), sin.to(dev).contiguous(), L)
+    xr = torch.zeros(B, L, d, dtype=torch.float64, requires_grad=True)
+    ref = O.rope_apply(xr, cos.double(), sin.double())
+    ref.backward((dy.double() @ w.double()).view(B, L, d))
+    close(dx, dx0.double() + xr.grad.view(M, d), rtol=1e-5, what="dx += rope_bwd(dy w)")
+
+
 @pytest.mark.parametrize("d", [128, 6])
 def test_rope_and_embedding(d):
     """d = 128: the vectorised kernels (8 columns per thread); d = 6: the scalar forms."""
