@@ -100,6 +100,13 @@ __device__ __forceinline__ void vmwait() {
   } while (0)
 #endif
 
+// LDS: K ring, V ring, keep dwords, 16 B, the key operands [LkP]; then (16-B aligned) 16 KB per wave for the
+// fallback's private tile staging
+__host__ __device__ __forceinline__ int attn8_fwd_fb_off(int Lk) {
+  const int LkP = (Lk + 63) / 64 * 64;
+  return (2 * A8_NS * A7_TB + A8_NS * 512 * 4 + 16 + LkP * 4 + 15) / 16 * 16;
+}
+
 template <int DM, int MK>
 __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
   constexpr bool DROP = DM != 0;
@@ -143,9 +150,13 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
       asm volatile("global_load_ubyte %0, %1, off" : "=v"(kb8[j]) : "v"(a.key_keep + (long)b * a.Lk + k) : "memory");
     }
   }
-  // Q rows of the wave's two chains by LDS-DMA into ring stages 2-3 (free until tile 2's fill): waves 0-1 in the K
-  // ring's stages 2-3, waves 2-3 in the V ring's; the wave's 64 rows (8 KB), chunk c of row r at c ^ (r & 7)
-  unsigned char* qst = sm8 + (w < 2 ? 2 * A7_TB + w * 8192 : 6 * A7_TB + (w - 2) * 8192);
+  // Q rows of the wave's two chains by LDS-DMA into the wave's private 16 KB past the ring (the fallback's staging,
+  // unused until the epilogue): whole 128-B rows per lane group, and no barrier before the reads, since each wave reads
+  // only the rows it brought (its own counted vmcnt covers them). Row r of the wave's 64, chunk c at c ^ (r & 7).
+  // (Direct global loads of the fragments into registers measured slower: each wave-instruction touches 32 rows in
+  // 32-B pieces, and the prologue's fills queued behind them, +2k cycles.)
+  const int qA = qw0 + qi, qB = qw0 + 32 + qi;
+  unsigned char* qst = sm8 + attn8_fwd_fb_off(a.Lk) + w * 16384;
 #pragma unroll
   for (int u = 0; u < 8; ++u) {
     const int r = 8 * u + (lane >> 3), pch = lane & 7;   // row within the wave's 64 queries
@@ -195,7 +206,7 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
     for (int k = 0; k < NP; ++k) piece(t1, 1, k);
   }
   A8ST(11);
-  // key bytes, Q and tile 0 landed; tile 1 in flight (the key bytes' registers named, so no use moves above the wait)
+  // key bytes, Q and tile 0 landed; tile 1 in flight (the loaded registers named, so no use moves above the wait)
   asm volatile("s_waitcnt vmcnt(%4)" : "+v"(kb8[0]), "+v"(kb8[1]), "+v"(kb8[2]), "+v"(kb8[3]) : "n"(NP) : "memory");
   // the keys' fifth-k-step operands (1, 0 or -inf)
   if constexpr (MK != 0) {
@@ -211,11 +222,10 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
   }
   __builtin_amdgcn_s_barrier();                                 // every wave's pieces; the key operands in LDS
   A8ST(1);
-  // the chains' Q fragments (lane: row qi of chain c, chunk 2 ks + hh), pre-scaled by sl2 (scores in log2 units);
-  // rows past Lq are zeroed (never stored)
+  // the chains' Q fragments (lane: row qi of chain c, chunk 2 ks + hh) from the wave's own staging, pre-scaled by sl2
+  // (scores in log2 units); rows past Lq are zeroed (never stored)
   const float sl2 = a.scale * 1.4426950408889634f;
   uint4 qa[4], qb[4];
-  const int qA = qw0 + qi, qB = qw0 + 32 + qi;
   {
     const unsigned zA = qA < a.Lq ? 0xFFFFFFFFu : 0u, zB = qB < a.Lq ? 0xFFFFFFFFu : 0u;
     const int rA = qi, rB = qi + 32;
@@ -227,8 +237,6 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
       qb[ks] = scale_frag(make_uint4(y.x & zB, y.y & zB, y.z & zB, y.w & zB), sl2);
     }
   }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();  // every wave's Q reads done: stages 2-3 may be filled
 
   // per-lane LDS offsets: K row reads (row qi of a 32-key half, chunk 2 ks + hh), V transposed reads
   int koff[4];
@@ -448,7 +456,7 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
     for (int c = 0; c < 4; ++c) rdv(vst, c);
   }
   // ---- tile 0, half 0: each chain's reference comes from this half's scores (computed against 0). This span fills
-  // active tile 2 (stage 2, after the Q reads' barrier): pieces in chunks 1, 4, 7 of both phases
+  // active tile 2 (stage 2): pieces in chunks 1, 4, 7 of both phases
   int fidx = 2, ftile = next_fill_tile();
   auto dm_first = [&](auto base, auto cc) {
     constexpr int c = decltype(cc)::value, k = decltype(base)::value + c / 3;
@@ -566,10 +574,9 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
   }  // nact > 0
 
   A8ST(12);
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __syncthreads();
-  A8ST(13);  // the ring is free: wave w owns bytes [16 KB w, 16 KB (w + 1)) for the fallback and the staging
-  unsigned char* own = sm8 + w * 16384;
+  // no LDS-DMA may land after the workgroup retires (the fills past the last tile are the only ones left)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  A8ST(13);
   float ltA = xsum32(lsA), ltB = xsum32(lsB);  // the row sums (the query's keys sit in lanes l and l ^ 32)
 #ifdef A8_NOFALLBACK  // timing-only ablations below skip the fallback (their sums are not softmax sums)
   if (false) {
@@ -577,9 +584,10 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
   if (nact > 0 && __any(!(ltA <= 0x1p64f && ltA >= 0x1p-40f) || !(ltB <= 0x1p64f && ltB >= 0x1p-40f))) {
 #endif
     // ---- fallback (guard tripped): both chains again, online softmax with rescaling (fwd7's algorithm), each
-    // active tile staged by this wave alone into its own 16 KB (K image 8 KB, V image 8 KB), keep dwords from memory
-    unsigned char* kp = own;
-    unsigned char* vp = own + 8192;
+    // active tile staged by this wave alone into its own 16 KB past the ring (K image 8 KB, V image 8 KB; no other
+    // wave touches it, so no barrier), keep dwords from memory
+    unsigned char* kp = sm8 + attn8_fwd_fb_off(a.Lk) + w * 16384;
+    unsigned char* vp = kp + 8192;
     auto redo = [&](int c, const uint4 (&qX)[4], f32x16_t& o0, f32x16_t& o1, float& l, float& rf) {
       const int qg = min(qg0 + c, nqg - 1);
       float m = -INFINITY;
@@ -639,7 +647,10 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
     redo(0, qa, oA0, oA1, ltA, rfA);
     redo(1, qb, oB0, oB1, ltB, rfB);
   }
-  // ---- normalise, stage the wave's 64 output rows in its own LDS bytes, store whole rows
+  // ---- normalise and store straight from the O^T accumulators: lane (qi, hh) holds d = 8 g + 4 hh + 0..3 of its
+  // query for g = 0..3 (per 32-d half); one v_permlane32_swap per dword pair gives lane hh = 0 the 8 consecutive d
+  // 16 g' .. 16 g' + 7 and lane hh = 1 16 g' + 8 .. + 15 (g' = 0, 1): 16-B stores, the two lanes of a query filling
+  // 32 contiguous bytes (no LDS staging, no barrier)
   bf16_t* Ob = (bf16_t*)a.Out + (long)b * a.Lq * a.so + h * DH;
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
@@ -647,26 +658,26 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
     const float rf = c ? rfB : rfA;
     const float inv = (lt > 0.f) ? (DROP ? a.drop_scale : 1.f) / lt : NAN;
     const int q = qw0 + 32 * c + qi;
+    bf16_t* orow = Ob + (long)min(q, a.Lq - 1) * a.so;
 #pragma unroll
     for (int db = 0; db < 2; ++db) {
+      const f32x16_t& oo = c ? (db ? oB1 : oB0) : (db ? oA1 : oA0);
 #pragma unroll
-      for (int mm = 0; mm < 4; ++mm) {
-        const f32x16_t& oo = c ? (db ? oB1 : oB0) : (db ? oA1 : oA0);
-        uint2 u2;
-        u2.x = pk_bf16(oo[4 * mm] * inv, oo[4 * mm + 1] * inv);
-        u2.y = pk_bf16(oo[4 * mm + 2] * inv, oo[4 * mm + 3] * inv);
-        const int row = 32 * c + qi;
-        *(uint2*)(own + row * 128 + (((4 * db + mm) ^ (row & 7)) << 4) + 8 * hh) = u2;
+      for (int gp = 0; gp < 2; ++gp) {
+        unsigned p0[2], p1[2];  // d groups 2 gp and 2 gp + 1, packed bf16 pairs
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          p0[j] = pk_bf16(oo[8 * gp + 2 * j] * inv, oo[8 * gp + 2 * j + 1] * inv);
+          p1[j] = pk_bf16(oo[8 * gp + 4 + 2 * j] * inv, oo[8 * gp + 4 + 2 * j + 1] * inv);
+        }
+        const auto s0 = __builtin_amdgcn_permlane32_swap(p0[0], p1[0], false, false);
+        const auto s1 = __builtin_amdgcn_permlane32_swap(p0[1], p1[1], false, false);
+        const uint4 v = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+        if (q < a.Lq) *(uint4*)(orow + 32 * db + 16 * gp + 8 * hh) = v;
       }
     }
     if (a.lse && hh == 0 && q < a.Lq)
       a.lse[(long)bh * a.Lq + q] = (lt > 0.f) ? (rf + __log2f(lt)) * 0.69314718055994531f : NAN;
-  }
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int row = (lane >> 3) + 8 * i, c = lane & 7;
-    const uint4 v = *(const uint4*)(own + row * 128 + ((c ^ (row & 7)) << 4));
-    if (qw0 + row < a.Lq) *(uint4*)(Ob + (long)(qw0 + row) * a.so + c * 8) = v;
   }
 #ifdef A8_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -683,8 +694,7 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
 #define A8_LDS_FLOOR 0  // timing probe: a larger LDS request limits the workgroups per CU (tools/build_variant.sh)
 #endif
 size_t attn8_fwd_lds(int Lk) {
-  const int LkP = (Lk + 63) / 64 * 64;
-  const size_t n = (size_t)2 * A8_NS * A7_TB + (size_t)A8_NS * 512 * 4 + 16 + (size_t)LkP * 4;
+  const size_t n = (size_t)attn8_fwd_fb_off(Lk) + 4 * 16384;  // + the 4 waves' fallback staging
   return n > (size_t)A8_LDS_FLOOR ? n : (size_t)A8_LDS_FLOOR;
 }
 

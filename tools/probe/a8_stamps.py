@@ -1,7 +1,8 @@
 """Phase timing of fwd8 from in-kernel s_memtime stamps (timing-only build: tools/build_variant.sh a8st attn8
 -fno-slp-vectorize -DA8_STAMPS, then FDDM_HIP_LIB=abl/a8st.so python tools/probe/a8_stamps.py). Stamps of wave 0 of
 every workgroup overwrite the first output row of its query block: 0 start, 1 tile 0 landed (after the prologue's
-barrier), 2 first half-tile done, 3..10 mid-tile barriers, 12 loop end, 13 epilogue barrier, 14 stores drained;
+barrier), 2 first half-tile done, 3..10 mid-tile barriers, 12 loop end, 13 DMA drained (epilogue start), 14 stores
+drained;
 15 key mask done (before the Q loads), 11 prologue fills issued.
 Prints, per shape, the median cycles between consecutive stamps over the workgroups and the spread of start times."""
 import os
@@ -18,6 +19,7 @@ bf = torch.bfloat16
 
 
 def main():
+    ops.attn_force_kernels("fwd8")     # every shape on fwd8 (auto takes fwd7 at C4)
     cases = [("C2 self", 32, 8, 256, 256, True), ("C2 cross", 32, 8, 256, 499, False),
              ("C4 self", 16, 12, 512, 512, True), ("C4 cross", 16, 12, 512, 499, False)]
     for name, B, H, Lq, Lk, kpm in cases:
