@@ -27,6 +27,12 @@ namespace fddm {
 namespace attn {
 
 constexpr int A8_NS = 4;  // ring stages (tiles in flight: 2 ahead of the one being read)
+// Row sums: A8_RSMFMA 1 = by 32x32x16 MFMAs of a row-selector operand against the undropped packed probabilities (two
+// per phase) into ONE accumulator shared by the chains (rows 0-15: chain A's sums, rows 16-31: chain B's), 0 = f32
+// adds (16 per phase)
+#ifndef A8_RSMFMA
+#define A8_RSMFMA 1
+#endif
 #ifndef A8_WPS
 #define A8_WPS 2  // waves per SIMD the register allocation targets (<= 256 registers: no accumulator-file split)
 #endif
@@ -257,7 +263,13 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
   // rescaling, fwd7's algorithm), exact but slow — not reached by softmax inputs of sane range.
   float rfA = 0.f, rfB = 0.f;
   f32x16_t oA0 = {}, oA1 = {}, oB0 = {}, oB1 = {};
-  float lsA = 0.f, lsB = 0.f;  // the lanes' row sums (relative to rf)
+  constexpr bool RSM = A8_RSMFMA != 0;
+  float lsA = 0.f, lsB = 0.f;  // add row sums (relative to rf): the lane's keys
+  f32x16_t lsum = {};           // MFMA row sums: row r of the accumulator = chain (r >> 4)'s sum for the lane's query
+  uint4 ucar = make_uint4(0, 0, 0, 0);  // MFMA row sums: the previous phase's second packed half, summed a phase late
+  // selector A operands (lane: row l & 31, k 8 hh .. + 7): ones in rows 0-15 (chain A) or 16-31 (chain B)
+  const unsigned one2 = 0x3F803F80u, selA1 = qi < 16 ? one2 : 0u, selB1 = qi < 16 ? 0u : one2;
+  const uint4 selA = make_uint4(selA1, selA1, selA1, selA1), selB = make_uint4(selB1, selB1, selB1, selB1);
   f32x16_t sA, sB;
   uint4 pA[2], pB[2];
   pB[0] = pB[1] = make_uint4(0, 0, 0, 0);
@@ -337,8 +349,8 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
   //   oY0 / oY1 += V^T pY with the current vf; sZ - dZ -> pZ, lsZ: the softmax chain (half KB of the tile: keep bits of
   //   kwZ at lb_bit(KB, .)); rd(c): the LDS reads of chunk c; dm(c): its LDS-DMA pieces of the span's tile fill
   auto phase = [&](f32x16_t& SX, const uint4 (&qX)[4], const uint4& q5X, f32x16_t& oY0, f32x16_t& oY1,
-                   const uint4 (&pY)[2], const f32x16_t& sZ, float dZ, uint4 (&pZ)[2], float& lZ, unsigned kwZ,
-                   auto kbc, auto&& rd, auto&& dm) {
+                   const uint4 (&pY)[2], const f32x16_t& sZ, float dZ, uint4 (&pZ)[2], float& lZ,
+                   const uint4& selZ, const uint4& selP, unsigned kwZ, auto kbc, auto&& rd, auto&& dm) {
     constexpr int KB = decltype(kbc)::value;
     float ex[8], ey[8], la, lb;
     unsigned sh[8], u[8], mk[8];
@@ -364,15 +376,17 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
     // 31 replicated into the low and high halves)
     auto fin = [&](auto ic) {
       constexpr int i = decltype(ic)::value;
-      if constexpr (i == 0) {
-        la = ex[0];
-        lb = ey[0];
-      } else {
-        la += ex[i];
-        lb += ey[i];
+      if constexpr (!RSM) {
+        if constexpr (i == 0) {
+          la = ex[0];
+          lb = ey[0];
+        } else {
+          la += ex[i];
+          lb += ey[i];
+        }
+        pinv(la);
+        pinv(lb);
       }
-      pinv(la);
-      pinv(lb);
       u[i] = pk_bf16(ex[i], ey[i]);
       pinv(u[i]);
       if constexpr (DROP) {
@@ -404,8 +418,16 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
       if constexpr (c >= 2) apply(std::integral_constant<int, c - 2>{});
       if constexpr (c == 8) {
         apply(std::integral_constant<int, 7>{});
-        lZ += la + lb;
+        if constexpr (!RSM) lZ += la + lb;
       }
+    };
+    // MFMA row sums (every row of the accumulator = the query's sum over the 16 keys of the k-step): the previous
+    // phase's second half (its packs written in that phase's last chunk) in chunk 1, this phase's first half (packs of
+    // chunks 1-4) in chunk 6, the second half carried to the next phase
+    auto rsum = [&](auto cc) {
+      constexpr int c = decltype(cc)::value;
+      if constexpr (RSM && c == 1) lsum = mfma32(selP, ucar, lsum);
+      if constexpr (RSM && c == 6) lsum = mfma32(selZ, make_uint4(u[0], u[1], u[2], u[3]), lsum);
     };
     f32x16_t acc = mfma32(k5, q5X, f32x16_t{});
     stages(std::integral_constant<int, 0>{});
@@ -415,6 +437,7 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
     static_for<0, 4>([&](auto kc) {
       constexpr int ks = decltype(kc)::value;
       acc = mfma32(kf[ks], qX[ks], acc);
+      rsum(std::integral_constant<int, ks + 1>{});
       stages(std::integral_constant<int, ks + 1>{});
       rd(std::integral_constant<int, ks + 1>{});
       dm(std::integral_constant<int, ks + 1>{});
@@ -425,11 +448,13 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
       constexpr int pi = decltype(pc)::value;  // PV step s = pi >> 1, d-block pi & 1
       if constexpr ((pi & 1) == 0) oY0 = mfma32(vf[pi >> 1][0], pY[pi >> 1], oY0);
       else oY1 = mfma32(vf[pi >> 1][1], pY[pi >> 1], oY1);
+      rsum(std::integral_constant<int, 5 + pi>{});
       stages(std::integral_constant<int, 5 + pi>{});
       rd(std::integral_constant<int, 5 + pi>{});
       dm(std::integral_constant<int, 5 + pi>{});
       A8_FENCE();
     });
+    if constexpr (RSM) ucar = make_uint4(u[4], u[5], u[6], u[7]);
   };
 
   // the stream of active tiles: active tile i = tile t in stage i % NS; half 0 = keys 64 t .. + 31, half 1 = + 32 ..
@@ -464,7 +489,7 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
   };
   auto dm_none = [&](auto) {};
   first_ref(sA, rfA, q5A);
-  phase(sB, qb, q5B, oB0, oB1, pB, sA, rfA, pA, lsA, kwA, std::integral_constant<int, 0>{},
+  phase(sB, qb, q5B, oB0, oB1, pB, sA, rfA, pA, lsA, selA, selB, kwA, std::integral_constant<int, 0>{},
         [&](auto cc) {  // alpha (see below)
           constexpr int c = decltype(cc)::value;
           if constexpr (c == 1) mk5_read(64 * t + 32);
@@ -473,7 +498,7 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
         },
         [&](auto cc) { dm_first(std::integral_constant<int, 0>{}, cc); });
   first_ref(sB, rfB, q5B);
-  phase(sA, qa, q5A, oA0, oA1, pA, sB, rfB, pB, lsB, kwB, std::integral_constant<int, 0>{},
+  phase(sA, qa, q5A, oA0, oA1, pA, sB, rfB, pB, lsB, selB, selA, kwB, std::integral_constant<int, 0>{},
         [&](auto cc) {  // beta
           constexpr int c = decltype(cc)::value;
           if constexpr (c < 4) rdv(vst, c);
@@ -523,7 +548,7 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
       const unsigned char* kimn = kst + stn * A7_TB;
       const unsigned char* vimg = vst + st * A7_TB;
       // ---- half 1. alpha: S_B(h1), PV_B(h0); softmax A(h1); reads: k5 and K of the next tile's h0
-      phase(sB, qb, q5B, oB0, oB1, pB, sA, 0.f, pA, lsA, kwA, std::integral_constant<int, 1>{},
+      phase(sB, qb, q5B, oB0, oB1, pB, sA, 0.f, pA, lsA, selA, selB, kwA, std::integral_constant<int, 1>{},
             [&](auto cc) {
               constexpr int c = decltype(cc)::value;
               if constexpr (c == 1) mk5_read(64 * tn);
@@ -532,7 +557,7 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
             },
             [&](auto cc) { dm_span(std::integral_constant<int, 0>{}, cc); });
       // beta: V of h1 (chunks 0-3, before its PV in chunks 5-8), S_A(next h0), PV_A(h1); softmax B(h1)
-      phase(sA, qa, q5A, oA0, oA1, pA, sB, 0.f, pB, lsB, kwB, std::integral_constant<int, 1>{},
+      phase(sA, qa, q5A, oA0, oA1, pA, sB, 0.f, pB, lsB, selB, selA, kwB, std::integral_constant<int, 1>{},
             [&](auto cc) {
               constexpr int c = decltype(cc)::value;
               if constexpr (c < 4) rdv(vimg + 32 * 128, c);
@@ -548,7 +573,7 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
       const unsigned char* kimg = kst + st * A7_TB;
       const unsigned char* vimg = vst + st * A7_TB;
       // ---- half 0. alpha: S_B(h0), PV_B(previous h1); softmax A(h0); reads: k5 and K of h1 (after S_B's last K use)
-      phase(sB, qb, q5B, oB0, oB1, pB, sA, 0.f, pA, lsA, kwA, std::integral_constant<int, 0>{},
+      phase(sB, qb, q5B, oB0, oB1, pB, sA, 0.f, pA, lsA, selA, selB, kwA, std::integral_constant<int, 0>{},
             [&](auto cc) {
               constexpr int c = decltype(cc)::value;
               if constexpr (c == 1) mk5_read(64 * t + 32);
@@ -557,7 +582,7 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
             },
             [&](auto cc) { dm_span(std::integral_constant<int, 4>{}, cc); });
       // beta: V of h0, S_A(h1), PV_A(h0); softmax B(h0)
-      phase(sA, qa, q5A, oA0, oA1, pA, sB, 0.f, pB, lsB, kwB, std::integral_constant<int, 0>{},
+      phase(sA, qa, q5A, oA0, oA1, pA, sB, 0.f, pB, lsB, selB, selA, kwB, std::integral_constant<int, 0>{},
             [&](auto cc) {
               constexpr int c = decltype(cc)::value;
               if constexpr (c < 4) rdv(vimg, c);
@@ -565,19 +590,21 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
             dm_none);
     }
   }
-  // pipeline end: PV_B of the last half
+  // pipeline end: PV_B of the last half (and its second half's row sum)
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     oB0 = mfma32(vf[s][0], pB[s], oB0);
     oB1 = mfma32(vf[s][1], pB[s], oB1);
   }
+  if constexpr (RSM) lsum = mfma32(selB, ucar, lsum);
   }  // nact > 0
 
   A8ST(12);
   // no LDS-DMA may land after the workgroup retires (the fills past the last tile are the only ones left)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   A8ST(13);
-  float ltA = xsum32(lsA), ltB = xsum32(lsB);  // the row sums (the query's keys sit in lanes l and l ^ 32)
+  // the row sums (adds: the query's keys sit in lanes l and l ^ 32; MFMA: accumulator rows 0 + 4 hh / 16 + 4 hh)
+  float ltA = RSM ? lsum[0] : xsum32(lsA), ltB = RSM ? lsum[8] : xsum32(lsB);
 #ifdef A8_NOFALLBACK  // timing-only ablations below skip the fallback (their sums are not softmax sums)
   if (false) {
 #else
