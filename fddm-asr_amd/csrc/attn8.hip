@@ -105,6 +105,18 @@ __device__ __forceinline__ void vmwait() {
   do {          \
   } while (0)
 #endif
+// diagnostic: -DA8_FINE=n (with A8_STAMPS) stamps the start and every chunk end of the workgroup's n-th phase call into
+// the second output row (tools/probe/a8_stamps.py --fine)
+#if defined(A8_STAMPS) && defined(A8_FINE)
+#define A8FS(k)                                                  \
+  do {                                                           \
+    if (a8pc_ == A8_FINE) a8fs_[k] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define A8FS(k) \
+  do {          \
+  } while (0)
+#endif
 
 // LDS: K ring, V ring, keep dwords, 16 B, the key operands [LkP]; then (16-B aligned) 16 KB per wave for the
 // fallback's private tile staging
@@ -129,6 +141,10 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
   xcd_tile(bxi, bh);
 #ifdef A8_STAMPS
   unsigned long long a8st_[16] = {};
+#endif
+#if defined(A8_STAMPS) && defined(A8_FINE)
+  unsigned long long a8fs_[16] = {};
+  int a8pc_ = 0;
 #endif
   A8ST(0);
   const int b = bh / a.H, h = bh - b * a.H;
@@ -429,11 +445,16 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
       if constexpr (RSM && c == 1) lsum = mfma32(selP, ucar, lsum);
       if constexpr (RSM && c == 6) lsum = mfma32(selZ, make_uint4(u[0], u[1], u[2], u[3]), lsum);
     };
+#if defined(A8_STAMPS) && defined(A8_FINE)
+    ++a8pc_;
+#endif
+    A8FS(0);
     f32x16_t acc = mfma32(k5, q5X, f32x16_t{});
     stages(std::integral_constant<int, 0>{});
     rd(std::integral_constant<int, 0>{});
     dm(std::integral_constant<int, 0>{});
     A8_FENCE();
+    A8FS(1);
     static_for<0, 4>([&](auto kc) {
       constexpr int ks = decltype(kc)::value;
       acc = mfma32(kf[ks], qX[ks], acc);
@@ -442,6 +463,7 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
       rd(std::integral_constant<int, ks + 1>{});
       dm(std::integral_constant<int, ks + 1>{});
       A8_FENCE();
+      A8FS(ks + 2);
     });
     SX = acc;
     static_for<0, 4>([&](auto pc) {
@@ -453,6 +475,7 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
       rd(std::integral_constant<int, 5 + pi>{});
       dm(std::integral_constant<int, 5 + pi>{});
       A8_FENCE();
+      A8FS(pi + 6);
     });
     if constexpr (RSM) ucar = make_uint4(u[4], u[5], u[6], u[7]);
   };
@@ -713,6 +736,11 @@ __global__ void __launch_bounds__(256, A8_WPS) fwd8_kernel(AttnArgs a) {
     unsigned long long* dst = (unsigned long long*)(Ob + (long)(bxi * 256) * a.so);
 #pragma unroll
     for (int k = 0; k < 16; ++k) dst[k] = a8st_[k];
+#ifdef A8_FINE
+    unsigned long long* dst2 = (unsigned long long*)(Ob + (long)(bxi * 256 + 1) * a.so);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) dst2[k] = a8fs_[k];
+#endif
   }
 #endif
 }

@@ -149,7 +149,7 @@ def _train_two_steps(rank, world, sync):
 
         def rl(*a, **k):
             v = orig(*a, **k)
-            rec.append(float(v))
+            rec.append(float(v.detach() if torch.is_tensor(v) else v))
             return v
 
         T_.lfd_loss = rl

@@ -55,6 +55,16 @@ def main():
         for a_, b_ in zip(pts[:-1], pts[1:]):
             seg.append(f"{a_}->{b_} {float((st[:, b_] - st[:, a_]).median()):.0f}")
         print("   median cycles: " + ", ".join(seg), flush=True)
+        if os.environ.get("A8_FINE"):   # -DA8_FINE build: chunk ends of one phase call in the second row
+            fs = []
+            for b in range(B):
+                for qb in range(0, Lq, 256):
+                    for h in range(H):
+                        fs.append(rows[b, qb + 1, h].contiguous().view(torch.int64)[:16])
+            fs = torch.stack(fs).cpu().double()
+            d = [f"c{k} {float((fs[:, k + 1] - fs[:, k]).median()):.0f}" for k in range(9)]
+            print(f"   phase {os.environ['A8_FINE']} chunk cycles: " + ", ".join(d) +
+                  f" | total {float((fs[:, 9] - fs[:, 0]).median()):.0f}", flush=True)
 
 
 if __name__ == "__main__":
