@@ -2,25 +2,28 @@
 //
 // The decoder's self- and cross-attention (models/denoise_decoder.py:129-130,164,169-176 -> nn.MultiheadAttention:
 // key-padding mask, dropout p on the attention probabilities, head_dim 64), bf16 in / out, fp32 softmax statistics.
-// Same numerics as fwd7 (attn7.hip): pre-scaled Q' = bf16(Q scale log2 e), the softmax reference and the key mask
-// folded into the score MFMA as a fifth k-step, lazy rescale (slow path only when a half-tile's probabilities could
-// exceed 2^8 or no finite reference exists yet), keep bits of layout v4 tested per score, bf16 P into the PV MFMA.
+// Score operands as fwd7 (attn7.hip): pre-scaled Q' = bf16(Q scale log2 e), the softmax reference and the key mask
+// folded into the score MFMA as a fifth k-step, bf16 P into the PV MFMA. Unlike fwd7, each chain's reference is fixed
+// after its first half-tile (no rescale branch in the loop; a guard on the final row sums sends a wave to an exact
+// online-softmax fallback), the keep bits are layout v5 (a score pair's mask by one shift + v_perm), and the row sums
+// come from row-selector MFMAs on the undropped packed probabilities.
 //
 // Why a new structure (profiles/r05e_pmc_attn7_c2.md): fwd7 runs one 32-query chain per wave, so
 // each half-tile is a serial chain — score MFMAs, then ~70 VALU + 16 v_exp on their results, then the PV MFMAs — and
 // its waves sat parked 34-44 % of their cycles with the matrix pipe busy 8-14 %. Here each wave owns TWO independent
 // 32-query chains A and B and software-pipelines them against each other: while the VALU works on one chain's
-// exponentials, the matrix pipe runs the other chain's PV MFMAs and next score MFMAs. One phase = 9 MFMAs:
+// exponentials, the matrix pipe runs the other chain's PV MFMAs and next score MFMAs. One phase = 9 (+2 row-sum) MFMAs:
 //   alpha_j: MFMA { S_B(j) [5], PV_B(j-1) [4] }   VALU { softmax_A(j) }   LDS { K fragments of half j + 1 }
 //   beta_j : MFMA { S_A(j+1) [5], PV_A(j) [4] }   VALU { softmax_B(j) }   LDS { V fragments of half j + 1 }
-// (j = 32-key half-tile). Each phase is written as 9 chunks {one MFMA, one score pair's softmax VALU, an LDS read}
-// fenced by sched_barrier, so the placement is ours, not the scheduler's. Both chains share every K / V fragment
-// (half the LDS reads per MFMA of fwd7).
+// (j = 32-key half-tile). Each phase is written as 9 chunks {one MFMA, three stages of score-pair softmax VALU, an
+// LDS read or DMA piece} fenced by sched_barrier, so the placement is ours, not the scheduler's. Both chains share
+// every K / V fragment (half the LDS reads per MFMA of fwd7). DESIGN.md §4.7 has the measurements.
 //
 // Layout: one workgroup = 4 waves x 64 queries = 256 queries of one (b, h) (C2's Lq 256: one workgroup per (b, h),
-// K / V read once). Register file per wave: 2 x (O 32 + Q' 16 + S 16 + P 8) + 2 K + 2 V fragment sets (64).
-// K / V tiles (64 keys) stream through a 4-stage LDS-DMA ring, two tiles ahead; one counted vmcnt + barrier per tile,
-// placed mid-tile (after the last read of the previous tile's stage, before the first read of the next tile).
+// K / V read once). K / V tiles (64 keys) and the chains' keep dwords stream through a 4-stage LDS-DMA ring, two tiles
+// ahead; one counted vmcnt + barrier per tile, placed mid-tile (after the last read of the previous tile's stage,
+// before the first read of the next tile). Each wave also owns 16 KB past the ring: its Q rows' staging in the
+// prologue, the fallback's tile staging in the epilogue.
 #include "attn7_common.h"
 
 namespace fddm {
@@ -36,14 +39,6 @@ constexpr int A8_NS = 4;  // ring stages (tiles in flight: 2 ahead of the one be
 #ifndef A8_WPS
 #define A8_WPS 2  // waves per SIMD the register allocation targets (<= 256 registers: no accumulator-file split)
 #endif
-
-// one global_load_dwordx4 the compiler does not track (the prologue's Q rows: waited for by the counted vmcnt that
-// also covers the first K / V tiles, instead of a compiler vmcnt(0) that would drain the whole prefetch)
-__device__ __forceinline__ uint4 gload16_asm(const void* p) {
-  u32x4v_t v;
-  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
-  return __builtin_bit_cast(uint4, v);
-}
 
 // pin a value to this point of the instruction stream: its computation cannot sink past the chunk's sched_barrier
 __device__ __forceinline__ void pinv(float& x) { asm volatile("" : "+v"(x)); }
@@ -63,34 +58,6 @@ __device__ __forceinline__ unsigned keep_pack(float x, float y, unsigned kw) {
       : "v"(x), "v"(kw), "v"(y), "i"(B0), "i"(B1));
   return r;
 }
-// score pair P's keep mask applied to its packed bf16 word v (layout v5, attn7_common.h lb_bit): bits 15 - P and 31 - P
-// of kw moved to bits 15 and 31, v_perm_b32 replicates their signs into the low and high halves, one v_and; a single
-// asm statement, so hipcc pads no hazard state between the steps
-template <int P>
-__device__ __forceinline__ unsigned keep_pair(unsigned v, unsigned kw) {
-  unsigned t;
-  if constexpr (P == 0) {
-    asm volatile(
-        "v_perm_b32 %1, %2, %2, %3\n\t"
-        "v_and_b32 %0, %0, %1"
-        : "+v"(v), "=&v"(t)
-        : "v"(kw), "s"(0x09090808u));
-  } else {
-    asm volatile(
-        "v_lshlrev_b32 %1, %4, %2\n\t"
-        "v_perm_b32 %1, %1, %1, %3\n\t"
-        "v_and_b32 %0, %0, %1"
-        : "+v"(v), "=&v"(t)
-        : "v"(kw), "s"(0x09090808u), "i"(P));
-  }
-  return v;
-}
-
-template <int N>
-__device__ __forceinline__ void vmwait() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
 #define A8_FENCE() __builtin_amdgcn_sched_barrier(0)
 
 // Diagnostic build only (-DA8_STAMPS, tools/probe/a8_stamps.py; outputs are overwritten): s_memtime of wave 0 at the

@@ -48,6 +48,23 @@ def main():
     t = timeit(lambda: ops.ln_bwd(dout, s, m, r, g, b, dres=dres, dy_t=dy, dgamma=dg, dbeta=db, drop_p=0.1, seed=1,
                                   rng_stream=2))
     print(f"decoder LN bwd (no FiLM)        {t:6.1f} us  {byt / t / 1e3:6.0f} GB/s", flush=True)
+    # the train step's form: slab sums to partials (one ln_fold per block afterwards) instead of atomics
+    lp = ops.LnPartials()
+    part = lp.add(N, d, dg, db, (dfs, dfh), L)
+
+    def bwd_part():
+        ops.call("fddm_ln_bwd", ops.BF16, ops.ptr(dout), ops.ptr(s), ops.ptr(m), ops.ptr(r), ops.ptr(g), ops.ptr(b),
+                 ops.ptr(fs), ops.ptr(dres), ops.ptr(dy), ops.ptr(dg), ops.ptr(db), ops.ptr(dfs), ops.ptr(dfh), N, d, L,
+                 0.1, 1, 2, ops.ptr(part), ops.stream())
+    t = timeit(bwd_part)
+    print(f"decoder LN bwd (FiLM, partials) {t:6.1f} us  {byt / t / 1e3:6.0f} GB/s  (the step's form)", flush=True)
+    job = lp.jobs[0]
+
+    def fold():
+        lp.jobs = [job]
+        lp.fold()
+    t = timeit(fold)
+    print(f"  + ln_fold of its slab sums    {t:6.1f} us", flush=True)
     N4, d4, L4 = 8192, 768, 512   # C4 decoder LN (d 768): FiLM form and the plain f32 -> f32 + bf16 form
     x4 = torch.randn(N4, d4, device=dev)
     y4 = torch.randn(N4, d4, device=dev, dtype=bf)
