@@ -12,54 +12,71 @@ namespace small {
 constexpr int MAXJ = 16;  // jobs per launch
 
 // ------------------------------------------------------------------------------------------ pooled mean
-// out[b][j] = mean_s x[b][s][j]. Block = one utterance x 512 columns: 64 column groups of 8 (one 16-B load per
-// row) x 16 row slices, each thread's loads independent (unrolled by 4); the 16 slice sums combine in LDS in a
-// fixed order (deterministic).
+// out[b][j] = mean_s x[b][s][j]. Block = one utterance x 64 columns: 8 column groups of 8 (bf16: one 16-B load per
+// row; f32: two) x 32 row slices, each thread's loads independent (unrolled by 4); the 32 slice sums combine in LDS
+// in a fixed order (deterministic). 8x the blocks of a 512-column block: at B 32, d 512 the 32 blocks of that layout
+// kept 32 CUs busy for ~57 us beside the encoder, 256 blocks spread the 16 MB over the chip.
+constexpr int RM_SL = 32;  // row slices per block
+// 8 consecutive elements (bf16: one 16-B load, f32: two) as f32
 template <typename T>
-__global__ void __launch_bounds__(1024) rows_mean_kernel(const T* __restrict__ x, float* __restrict__ out, long S,
-                                                         long d) {
-  constexpr int E = 16 / sizeof(T);  // elements per 16-B load
-  __shared__ float part[16][64 * E + 4];
-  const int cg = threadIdx.x & 63, sl = threadIdx.x >> 6;
-  const long b = blockIdx.y, j0 = (long)blockIdx.x * 64 * E + cg * E;
-  float acc[E];
+__device__ __forceinline__ void rm_ld8(const T* p, float (&v)[8]) {
+  if constexpr (sizeof(T) == 2) {
+    const uint4 u = *(const uint4*)p;
+    const unsigned w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
-  for (int e = 0; e < E; ++e) acc[e] = 0.f;
-  if (j0 + E <= d && (d % E) == 0) {
-    const T* base = x + b * S * d + j0;
-    long s = sl;
-    for (; s + 48 < S; s += 64) {
-      uint4 u[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) u[q] = *(const uint4*)(base + (s + 16 * q) * d);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const T* v = (const T*)&u[q];
-#pragma unroll
-        for (int e = 0; e < E; ++e) acc[e] += ld<T>(v + e);
-      }
-    }
-    for (; s < S; s += 16) {
-      const uint4 u = *(const uint4*)(base + s * d);
-      const T* v = (const T*)&u;
-#pragma unroll
-      for (int e = 0; e < E; ++e) acc[e] += ld<T>(v + e);
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(w[i] << 16);
+      v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
     }
   } else {
-    for (int e = 0; e < E; ++e)
+    const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+}
+template <typename T>
+__global__ void __launch_bounds__(256) rows_mean_kernel(const T* __restrict__ x, float* __restrict__ out, long S,
+                                                        long d) {
+  __shared__ float part[RM_SL][64 + 4];
+  const int cg = threadIdx.x & 7, sl = threadIdx.x >> 3;
+  const long b = blockIdx.y, j0 = (long)blockIdx.x * 64 + cg * 8;
+  float acc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+  if (j0 + 8 <= d && (d % 8) == 0) {
+    const T* base = x + b * S * d + j0;
+    long s = sl;
+    for (; s + 3 * RM_SL < S; s += 4 * RM_SL) {
+      float v[4][8];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) rm_ld8<T>(base + (s + RM_SL * q) * d, v[q]);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += v[q][e];
+    }
+    for (; s < S; s += RM_SL) {
+      float v[8];
+      rm_ld8<T>(base + s * d, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += v[e];
+    }
+  } else {
+    for (int e = 0; e < 8; ++e)
       if (j0 + e < d)
-        for (long s = sl; s < S; s += 16) acc[e] += ld<T>(x + (b * S + s) * d + j0 + e);
+        for (long s = sl; s < S; s += RM_SL) acc[e] += ld<T>(x + (b * S + s) * d + j0 + e);
   }
 #pragma unroll
-  for (int e = 0; e < E; ++e) part[sl][cg * E + e] = acc[e];
+  for (int e = 0; e < 8; ++e) part[sl][cg * 8 + e] = acc[e];
   __syncthreads();
-  for (int c = threadIdx.x; c < 64 * E; c += 1024) {
-    const long j = (long)blockIdx.x * 64 * E + c;
-    if (j >= d) continue;
-    float a = 0.f;
+  if (threadIdx.x < 64) {
+    const int c = threadIdx.x;
+    const long j = (long)blockIdx.x * 64 + c;
+    if (j < d) {
+      float a = 0.f;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) a += part[q][c];
-    out[b * d + j] = a / (float)S;
+      for (int q = 0; q < RM_SL; ++q) a += part[q][c];
+      out[b * d + j] = a / (float)S;
+    }
   }
 }
 
@@ -284,13 +301,12 @@ using namespace fddm::small;
 
 FDDM_API int fddm_rows_mean(int dtype, const void* x, float* out, long B, long S, long d, void* hs) {
   if (B <= 0 || d <= 0) return 0;
-  const long cols = dtype == FDDM_BF16 ? 512 : 256;  // columns per block: 64 groups x one 16-B load
-  dim3 g((unsigned)((d + cols - 1) / cols), (unsigned)B);
+  dim3 g((unsigned)((d + 63) / 64), (unsigned)B);  // 64 columns per block
   if (((uintptr_t)x) & 15) return (int)hipErrorInvalidValue;
   if (dtype == FDDM_BF16)
-    hipLaunchKernelGGL(rows_mean_kernel<bf16_t>, g, dim3(1024), 0, (hipStream_t)hs, (const bf16_t*)x, out, S, d);
+    hipLaunchKernelGGL(rows_mean_kernel<bf16_t>, g, dim3(256), 0, (hipStream_t)hs, (const bf16_t*)x, out, S, d);
   else
-    hipLaunchKernelGGL(rows_mean_kernel<float>, g, dim3(1024), 0, (hipStream_t)hs, (const float*)x, out, S, d);
+    hipLaunchKernelGGL(rows_mean_kernel<float>, g, dim3(256), 0, (hipStream_t)hs, (const float*)x, out, S, d);
   return (int)hipGetLastError();
 }
 

@@ -158,9 +158,11 @@ class FusedAdamW(torch.optim.Optimizer):
         return self._skipped
 
     @torch.no_grad()
-    def clip_and_step(self, max_norm: float | None = None, zero_grads: bool = False, grad_scale: float = 1.0):
+    def clip_and_step(self, max_norm: float | None = None, zero_grads: bool = False, grad_scale: float = 1.0,
+                      return_norm: bool = True):
         """clip_grad_norm_(all params with grads, max_norm) followed by AdamW.step(); returns the
-        (device) total gradient norm. zero_grads: the step also zeroes every gradient it reads (the train loop's
+        (device) total gradient norm (return_norm=False: None, and no sqrt launch — the sum of squares stays in
+        last_total_sq). zero_grads: the step also zeroes every gradient it reads (the train loop's
         next zero_grad then has no arena fill to do; .grad reads as zero after the call). grad_scale: every gradient
         is multiplied by it before the clip and the update (data parallelism: the all-reduce leaves the ranks' sum,
         grad_scale = 1/W averages it inside the kernel instead of a pass over the gradients)."""
@@ -205,6 +207,8 @@ class FusedAdamW(torch.optim.Optimizer):
                 a.views_zero = bool(zero_grads) and all(
                     p.grad is not None and p.grad.data_ptr() == v.data_ptr() for p, v in zip(a.params, a.views))
         self.last_total_sq = total
+        if not return_norm:
+            return None
         return total.sqrt() * grad_scale if grad_scale != 1.0 else total.sqrt()
 
     @torch.no_grad()
