@@ -211,6 +211,141 @@ __global__ void __launch_bounds__(1024) linear4_kernel(const float* __restrict__
   }
 }
 
+// Round 6: a 32 x 32 output tile (32 rows of one job's 32 columns) per 512-thread block; the 8 waves split K (64-wide
+// chunks c = w, w + 8, ...), each lane keeps a 4 x 4 register tile (rows rg + 8 i, columns cg + 8 j), operands staged
+// per wave in its own LDS (no barrier inside the K walk), the 8 partial tiles added in a fixed order (deterministic).
+// Round 2's 32 x 8 tile re-read the whole [32, K] input per 8 columns (82 KB of LDS per block, one block per CU): the
+// 12 FiLM projections took 28 us alone and 73 us beside the encoder; here each weight element is read once.
+constexpr int LR_TC = 32, LR_KC = 64, LR_NW = 8, LR_LD = LR_KC + 4;  // tile columns, K chunk, waves, LDS row (floats)
+constexpr int LR_WAVE_FLOATS = 2 * 32 * LR_LD;                       // input + weight chunk of one wave
+constexpr size_t LR_LDS = (size_t)LR_NW * LR_WAVE_FLOATS * 4;         // 139 264 B (the partial tiles reuse it)
+template <bool TW>
+__global__ void __launch_bounds__(512) linrt_kernel(const float* __restrict__ in, long ldi, LinJobs J, long ldw,
+                                                    long ldo, const float* __restrict__ aux, long R, long N, long K,
+                                                    int act) {
+  extern __shared__ __attribute__((aligned(16))) float lrs[];
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, rg = lane >> 3, cg = lane & 7;
+  const long n0 = (long)blockIdx.x * LR_TC, r0 = (long)blockIdx.z * 32;
+  const int j = blockIdx.y;
+  const float* W = J.W[j];
+  float* Is = lrs + w * LR_WAVE_FLOATS;  // [32 rows][LR_LD]
+  float* Ws = Is + 32 * LR_LD;           // [32 columns][LR_LD]
+  float acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) acc[i][jj] = 0.f;
+  const long nch = (K + LR_KC - 1) / LR_KC;
+  for (long c = w; c < nch; c += LR_NW) {
+    const long k0 = c * LR_KC;
+    // input chunk [32 rows][64 k]: 512 float4, 8 per lane (lane-consecutive k: coalesced rows)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int e = lane + 64 * q, ri = e >> 4, k4 = e & 15;
+      const long r = r0 + ri, k = k0 + 4 * k4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (r < R) {
+        const float* src = in + r * ldi + k;
+        if (k + 3 < K && (((uintptr_t)src) & 15) == 0) {
+          v = *(const float4*)src;
+        } else {
+          if (k < K) v.x = src[0];
+          if (k + 1 < K) v.y = src[1];
+          if (k + 2 < K) v.z = src[2];
+          if (k + 3 < K) v.w = src[3];
+        }
+      }
+      *(float4*)&Is[ri * LR_LD + 4 * k4] = v;
+    }
+    // weight chunk as [32 columns][64 k]
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int e = lane + 64 * q;
+      if (!TW) {  // W[n][k]: rows of k, like the input
+        const int ci = e >> 4, k4 = e & 15;
+        const long n = n0 + ci, k = k0 + 4 * k4;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (n < N) {
+          const float* src = W + n * ldw + k;
+          if (k + 3 < K && (((uintptr_t)src) & 15) == 0) {
+            v = *(const float4*)src;
+          } else {
+            if (k < K) v.x = src[0];
+            if (k + 1 < K) v.y = src[1];
+            if (k + 2 < K) v.z = src[2];
+            if (k + 3 < K) v.w = src[3];
+          }
+        }
+        *(float4*)&Ws[ci * LR_LD + 4 * k4] = v;
+      } else {    // W[k][n] (in @ W): rows of n, transposed into the column-major chunk
+        const int ki = e >> 3, n4 = e & 7;
+        const long k = k0 + ki, n = n0 + 4 * n4;
+        float v[4] = {0.f, 0.f, 0.f, 0.f};
+        if (k < K) {
+          const float* src = W + k * ldw + n;
+          if (n + 3 < N && (((uintptr_t)src) & 15) == 0) {
+            const float4 t = *(const float4*)src;
+            v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+          } else {
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              if (n + u < N) v[u] = src[u];
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) Ws[(4 * n4 + u) * LR_LD + ki] = v[u];
+      }
+    }
+    // (one wave writes and reads its own chunk: LDS executes a wave's instructions in order)
+#pragma unroll 4
+    for (int kk = 0; kk < LR_KC; kk += 4) {
+      float4 a[4], bw[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = *(const float4*)&Is[(rg + 8 * i) * LR_LD + kk];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) bw[jj] = *(const float4*)&Ws[(cg + 8 * jj) * LR_LD + kk];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          acc[i][jj] = fmaf(a[i].x, bw[jj].x, acc[i][jj]);
+          acc[i][jj] = fmaf(a[i].y, bw[jj].y, acc[i][jj]);
+          acc[i][jj] = fmaf(a[i].z, bw[jj].z, acc[i][jj]);
+          acc[i][jj] = fmaf(a[i].w, bw[jj].w, acc[i][jj]);
+        }
+    }
+  }
+  // the 8 waves' partial tiles, added in wave order
+  __syncthreads();
+  float* red = lrs;  // [8 waves][32 rows][32 columns]
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) red[w * 1024 + (rg + 8 * i) * 32 + cg + 8 * jj] = acc[i][jj];
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int o = tid + 512 * h, ri = o >> 5, ci = o & 31;
+    float v = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < LR_NW; ++ww) v += red[ww * 1024 + o];
+    const long n = n0 + ci, r = r0 + ri;
+    if (n >= N || r >= R) continue;
+    const float bias = J.b[j] ? J.b[j][n] : 0.f;
+    const float pre = v + bias;
+    if (act == 1) {
+      J.out[j][r * ldo + n] = pre;
+      J.out2[j][r * ldo + n] = pre / (1.f + expf(-pre));
+    } else if (act == 2) {
+      const float x = aux[r * ldo + n];
+      const float sg = 1.f / (1.f + expf(-x));
+      J.out[j][r * ldo + n] = v * (sg * (1.f + x * (1.f - sg)));
+    } else {
+      J.out[j][r * ldo + n] = pre;
+    }
+  }
+}
+
 // Job j: dW_j[n][k] += sum_r dy_j[r][n] * x_j[r][k];  db_j[n] += sum_r dy_j[r][n]   (accumulating: gradient slots)
 struct DwJobs {
   const float* dy[MAXJ];
@@ -220,42 +355,64 @@ struct DwJobs {
   long N[MAXJ], K[MAXJ], lddy[MAXJ], ldx[MAXJ];
 };
 
+// tile 32 (n) x 64 (k) per 256-thread block: thread (n = n0 + (tid >> 3), k = k0 + 8 (tid & 7) + 0..7), rows staged in
+// chunks of 32; the dW rows are read-modified-written as two float4 per thread (round 2's 32 x 32 tile with one
+// scalar per thread and row ran the FiLM weight gradients at ~1.3 TB/s of dW traffic)
 __global__ void __launch_bounds__(256) dw_kernel(DwJobs J, long R) {
-  // tile 32 (n) x 32 (k); rows staged in chunks of 32
   __shared__ float Ds[32][33];
-  __shared__ float Xs[32][33];
+  __shared__ __attribute__((aligned(16))) float Xs[32][64 + 4];
   const int j = blockIdx.z;
   const long N = J.N[j], K = J.K[j];
-  const long n0 = (long)blockIdx.y * 32, k0 = (long)blockIdx.x * 32;
+  const long n0 = (long)blockIdx.y * 32, k0 = (long)blockIdx.x * 64;
   if (n0 >= N || k0 >= K) return;
-  const int tid = threadIdx.x, kc = tid & 31, ng = tid >> 5;  // thread: column k0+kc, rows n0 + 4*ng .. +3
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  const int tid = threadIdx.x, ty = tid >> 3, tx = tid & 7;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   float bacc = 0.f;
+  const bool dob = J.db[j] && blockIdx.x == 0 && tx == 0;
   for (long rr0 = 0; rr0 < R; rr0 += 32) {
     for (int e = tid; e < 32 * 32; e += 256) {
       const int rr = e >> 5, cc = e & 31;
       const long r = rr0 + rr;
       Ds[rr][cc] = (r < R && n0 + cc < N) ? J.dy[j][r * J.lddy[j] + n0 + cc] : 0.f;
+    }
+    for (int e = tid; e < 32 * 64; e += 256) {
+      const int rr = e >> 6, cc = e & 63;
+      const long r = rr0 + rr;
       Xs[rr][cc] = (r < R && k0 + cc < K) ? J.x[j][r * J.ldx[j] + k0 + cc] : 0.f;
     }
     __syncthreads();
 #pragma unroll 8
     for (int rr = 0; rr < 32; ++rr) {
-      const float xv = Xs[rr][kc];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) acc[i] = fmaf(Ds[rr][4 * ng + i], xv, acc[i]);
+      const float dv = Ds[rr][ty];
+      const float4 x0 = *(const float4*)&Xs[rr][8 * tx], x1 = *(const float4*)&Xs[rr][8 * tx + 4];
+      acc[0] = fmaf(dv, x0.x, acc[0]);
+      acc[1] = fmaf(dv, x0.y, acc[1]);
+      acc[2] = fmaf(dv, x0.z, acc[2]);
+      acc[3] = fmaf(dv, x0.w, acc[3]);
+      acc[4] = fmaf(dv, x1.x, acc[4]);
+      acc[5] = fmaf(dv, x1.y, acc[5]);
+      acc[6] = fmaf(dv, x1.z, acc[6]);
+      acc[7] = fmaf(dv, x1.w, acc[7]);
+      if (dob) bacc += dv;
     }
-    if (J.db[j] && blockIdx.x == 0 && tid < 32)
-      for (int rr = 0; rr < 32; ++rr) bacc += Ds[rr][tid];
     __syncthreads();
   }
-  const long k = k0 + kc;
+  const long n = n0 + ty, k = k0 + 8 * tx;
+  if (n < N && k < K) {
+    float* dst = J.dW[j] + n * K + k;
+    if (k + 7 < K && (((uintptr_t)dst) & 15) == 0) {
+      float4 u = *(float4*)dst, v = *(float4*)(dst + 4);
+      u.x += acc[0]; u.y += acc[1]; u.z += acc[2]; u.w += acc[3];
+      v.x += acc[4]; v.y += acc[5]; v.z += acc[6]; v.w += acc[7];
+      *(float4*)dst = u;
+      *(float4*)(dst + 4) = v;
+    } else {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const long n = n0 + 4 * ng + i;
-    if (n < N && k < K) J.dW[j][n * K + k] += acc[i];
+      for (int e = 0; e < 8; ++e)
+        if (k + e < K) dst[e] += acc[e];
+    }
   }
-  if (J.db[j] && blockIdx.x == 0 && tid < 32 && n0 + tid < N) J.db[j][n0 + tid] += bacc;
+  if (dob && n < N) J.db[j][n] += bacc;
 }
 
 // ------------------------------------------------------------------------------------------ KL reduction
@@ -332,11 +489,27 @@ FDDM_API int fddm_small_linear(const float* in, long ldi, int njobs, const float
     if (act == 1 && !J.out2[j]) return (int)hipErrorInvalidValue;
   }
   if (act == 2 && !aux) return (int)hipErrorInvalidValue;
-  dim3 g((unsigned)((N + LNC - 1) / LNC), (unsigned)njobs, (unsigned)((R + 31) / 32));
+  // the register-tile kernel where its 32-column tiles make >= 128 blocks (the 12 FiLM projections: 192; 28 -> ~21 us
+  // alone, 73 -> 22-37 us beside the encoder); narrower launches (the time MLP, the input gradients: 16-64 tiles)
+  // keep round 2's 8-column blocks, whose 4 K-quarters give them 4-16x the waves (measured faster there in the step)
+  const long rt_blocks = ((N + LR_TC - 1) / LR_TC) * njobs * ((R + 31) / 32);
+  if (rt_blocks < 128) {
+    dim3 g4((unsigned)((N + LNC - 1) / LNC), (unsigned)njobs, (unsigned)((R + 31) / 32));
+    if (transpose_w)
+      hipLaunchKernelGGL(linear4_kernel<true>, g4, dim3(1024), 0, (hipStream_t)hs, in, ldi, J, ldw, ldo, aux, R, N, K,
+                         act);
+    else
+      hipLaunchKernelGGL(linear4_kernel<false>, g4, dim3(1024), 0, (hipStream_t)hs, in, ldi, J, ldw, ldo, aux, R, N, K,
+                         act);
+    return (int)hipGetLastError();
+  }
+  dim3 g((unsigned)((N + LR_TC - 1) / LR_TC), (unsigned)njobs, (unsigned)((R + 31) / 32));
   if (transpose_w)
-    hipLaunchKernelGGL(linear4_kernel<true>, g, dim3(1024), 0, (hipStream_t)hs, in, ldi, J, ldw, ldo, aux, R, N, K, act);
+    hipLaunchKernelGGL(linrt_kernel<true>, g, dim3(512), LR_LDS, (hipStream_t)hs, in, ldi, J, ldw, ldo, aux, R, N, K,
+                       act);
   else
-    hipLaunchKernelGGL(linear4_kernel<false>, g, dim3(1024), 0, (hipStream_t)hs, in, ldi, J, ldw, ldo, aux, R, N, K, act);
+    hipLaunchKernelGGL(linrt_kernel<false>, g, dim3(512), LR_LDS, (hipStream_t)hs, in, ldi, J, ldw, ldo, aux, R, N, K,
+                       act);
   return (int)hipGetLastError();
 }
 
@@ -357,7 +530,7 @@ FDDM_API int fddm_small_dw(int njobs, const float* const* dy, const long* lddy, 
     nmax = N[j] > nmax ? N[j] : nmax;
     kmax = K[j] > kmax ? K[j] : kmax;
   }
-  dim3 g((unsigned)((kmax + 31) / 32), (unsigned)((nmax + 31) / 32), (unsigned)njobs);
+  dim3 g((unsigned)((kmax + 63) / 64), (unsigned)((nmax + 31) / 32), (unsigned)njobs);
   hipLaunchKernelGGL(dw_kernel, g, dim3(256), 0, (hipStream_t)hs, J, R);
   return (int)hipGetLastError();
 }

@@ -1122,6 +1122,24 @@ def test_small_linear_and_dw_match_torch():
     o.small_linear(dy.to(dev), [Ws[1].to(dev)], None, [dxs], act=2, aux=aux.to(dev), transpose_w=True)
     sg = torch.sigmoid(aux.double())
     close(dxs, (dy.double() @ Ws[1].double()) * sg * (1 + aux.double() * (1 - sg)), rtol=1e-5, what="dsilu")
+    # >= 128 tiles of 32 columns: the register-tile kernel (linrt), with ragged rows (45), K (96) and columns (400)
+    R3, K3, N3, nj = 45, 96, 400, 12
+    x3 = torch.randn(R3, K3, generator=gen)
+    W3 = [torch.randn(N3, K3, generator=gen) / 10 for _ in range(nj)]
+    b3 = [torch.randn(N3, generator=gen) for _ in range(nj)]
+    o3, o3s = [torch.empty(R3, N3, device=dev) for _ in range(nj)], [torch.empty(R3, N3, device=dev) for _ in range(nj)]
+    o.small_linear(x3.to(dev), [w.to(dev) for w in W3], [b.to(dev) for b in b3], o3, o3s, act=1)
+    for w, b, out, outs in zip(W3, b3, o3, o3s):
+        ref = x3.double() @ w.double().T + b.double()
+        close(out, ref, rtol=1e-5, what="small_linear (tiles)")
+        close(outs, torch.nn.functional.silu(ref), rtol=1e-5, what="silu (tiles)")
+    WT = [torch.randn(K3, N3, generator=gen) / 10 for _ in range(nj)]
+    aux3 = torch.randn(R3, N3, generator=gen)
+    oT = [torch.empty(R3, N3, device=dev) for _ in range(nj)]
+    o.small_linear(x3.to(dev), [w.to(dev) for w in WT], None, oT, act=2, aux=aux3.to(dev), transpose_w=True)
+    sg3 = torch.sigmoid(aux3.double())
+    for w, out in zip(WT, oT):
+        close(out, (x3.double() @ w.double()) * sg3 * (1 + aux3.double() * (1 - sg3)), rtol=1e-5, what="dsilu (tiles)")
     dW = [torch.full((N, K), 0.5, device=dev) for _ in range(2)]
     db = [torch.full((N,), 0.25, device=dev) for _ in range(2)]
     xs = [torch.randn(R, K, generator=gen) for _ in range(2)]
