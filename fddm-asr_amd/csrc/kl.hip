@@ -369,8 +369,11 @@ __device__ __forceinline__ float4 block_sum4(float a, float b, float c, float d,
   return r;
 }
 
+#ifndef KL_WPE
+#define KL_WPE 4  // waves per SIMD the fused KL targets: 128 VGPRs (1: 132 VGPRs, 3 waves, 97 us; 4: 86 us; 5 spills: 127 us)
+#endif
 template <int NV, typename OT, int NT>
-__global__ void __launch_bounds__(NT) kl4_fused_kernel(const float* __restrict__ logits, const long* __restrict__ xt_,
+__global__ void __launch_bounds__(NT, KL_WPE) kl4_fused_kernel(const float* __restrict__ logits, const long* __restrict__ xt_,
                                                         const long* __restrict__ x0_, const long* __restrict__ t_,
                                                         const float* __restrict__ betas,
                                                         const unsigned char* __restrict__ mask,
@@ -396,12 +399,16 @@ __global__ void __launch_bounds__(NT) kl4_fused_kernel(const float* __restrict__
     v[i][0] = f.x; v[i][1] = f.y; v[i][2] = f.z; v[i][3] = f.w;
     mt = fmaxf(mt, fmaxf(fmaxf(f.x, f.y), fmaxf(f.z, f.w)));
   }
+  // exp(v - mt) as one exp2 of an FMA; a thread whose elements are all padding (-inf) has mt = -inf: subtracting 0
+  // instead gives its exps exactly 0 without a select per element
+  constexpr float L2E = 1.4426950408889634f;
+  const float mtl = (mt == -INFINITY) ? 0.f : mt * L2E;
   float st_ = 0.f;
 #pragma unroll
   for (int i = 0; i < NV; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      v[i][j] = (mt == -INFINITY) ? 0.f : __expf(v[i][j] - mt);
+      v[i][j] = __builtin_amdgcn_exp2f(fmaf(v[i][j], L2E, -mtl));
       st_ += v[i][j];
     }
   const float2 ms = block_maxsum(mt, st_, red);
@@ -418,39 +425,48 @@ __global__ void __launch_bounds__(NT) kl4_fused_kernel(const float* __restrict__
     Q = M * ((k == x0 ? c.a_p : 0.f) + c.b_p) * c.inv_dq;
     P = M * (c.a_p * xh + c.b_p) * inv_dp;
   };
-  const float pa = c.b_t * c.a_p * inv_dp, pb = c.b_t * c.b_p * inv_dp;
+  const float pa = c.b_t * c.a_p * inv_dp, pb = c.b_t * c.b_p * inv_dp, pbe = pb + eps;
   const long ks[2] = {xt, x0};
   const float xs[2] = {xhat_xt, xhat_x0};
   const int nsp = (xt == x0) ? 1 : 2;
 
   // one row pass: the KL's generic log terms and the gradient's two sums; the mask count of this utterance rides
-  // in the same block reduction
-  // VALU budget: the pass is as long as the row's HBM time, so per element one exp (above), one rcp (kept in
-  // registers for the output pass) and a quarter of a log: sum_k log(P_k + eps) is taken as log of the product of
-  // each float4's four factors (each >= eps = 1e-8, so a product >= 1e-32 stays a normal f32)
-  float acc = 0.f, a1 = 0.f, a2 = 0.f, cnt = 0.f;
+  // in the same block reduction. Per element one exp (above), one rcp (kept in registers for the output pass) and a
+  // quarter of a log: sum_k log(P_k + eps) is taken as log of the product of each float4's four factors (each >= eps =
+  // 1e-8, so a product >= 1e-32 stays a normal f32). sum_k P_k / (P_k + eps) = V - eps sum_k 1 / (P_k + eps): one
+  // add per element instead of a subtract and an FMA. Chunks whose every lane is inside the row skip the validity
+  // selects (a uniform branch per chunk).
+  float acc = 0.f, sr = 0.f, a2 = 0.f, cnt = 0.f;
   float r[NV][4];
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
-    const bool ok = tid + (long)NT * i < V4;
-    float prod = 1.f;
+    float prod = 1.f, sri = 0.f, a2i = 0.f;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const float xh = v[i][j] * resc;
       v[i][j] = xh;
-      const float Pe = fmaf(pa, xh, pb) + eps;
+      const float Pe = fmaf(pa, xh, pbe);
       r[i][j] = __builtin_amdgcn_rcpf(Pe);
       prod *= Pe;
-      if (ok) {
-        a1 += (Pe - eps) * r[i][j];
-        a2 += xh * r[i][j];
-      }
+      sri += r[i][j];
+      a2i = fmaf(xh, r[i][j], a2i);
     }
-    if (ok) acc += 4.f * LQg - __logf(prod);
+    // prod >= eps^4 = 1e-32, a normal f32: the raw log2 instruction (no denormal scaling), times ln 2
+    const float lt = fmaf(-0.6931471805599453f, __builtin_amdgcn_logf(prod), 4.f * LQg);
+    if ((long)NT * (i + 1) <= V4) {  // uniform: every lane's float4 is in the row
+      acc += lt;
+      sr += sri;
+      a2 += a2i;
+    } else if (tid + (long)NT * i < V4) {
+      acc += lt;
+      sr += sri;
+      a2 += a2i;
+    }
   }
   if (mask)
     for (long l = tid; l < L; l += NT) cnt += mask[b * L + l] ? 1.f : 0.f;
-  const float4 sums = block_sum4(acc, a1, a2, cnt, red + 2 * (NT / 64));
+  const float4 sums0 = block_sum4(acc, sr, a2, cnt, red + 2 * (NT / 64));
+  const float4 sums = make_float4(sums0.x, (float)V - eps * sums0.y, sums0.z, sums0.w);
   if (tid == 0) {
     float kl = Qg * sums.x;
     for (int j = 0; j < nsp; ++j) {
@@ -472,6 +488,7 @@ __global__ void __launch_bounds__(NT) kl4_fused_kernel(const float* __restrict__
   const float gxt = c.a_t * s1 * inv_dp;
   const float G = g0s + xhat_xt * gxt;
   const float wr = mask ? ((mask[row] ? 1.f : 0.f) / (sums.w + eps) / (float)B) : 1.f / ((float)L * (float)B);
+  const float wgc = wr * gc, wG = wr * G;
   OT* out = dz + row * V;
   const int qxt = (int)(xt >> 2), qx0 = (int)(x0 >> 2), iv4 = (int)V4;
 #pragma unroll
@@ -480,7 +497,7 @@ __global__ void __launch_bounds__(NT) kl4_fused_kernel(const float* __restrict__
     if (q < iv4) {
       float o[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = wr * v[i][j] * (gc * r[i][j] - G);
+      for (int j = 0; j < 4; ++j) o[j] = v[i][j] * fmaf(wgc, r[i][j], -wG);
       if (q == qxt || q == qx0) {
         for (int j = 0; j < 4; ++j) {
           const long k = 4L * q + j;
@@ -803,6 +820,9 @@ FDDM_API int fddm_kl_fused(const float* logits, const long* xt, const long* x0, 
   hipStream_t s = (hipStream_t)hs;
   // 256-thread rows (measured against 128 / 1024, round 2); 512 threads for vocabularies beyond 16 x 4 x 256
   KLF_LAUNCH(2, 256)
+#ifdef KL_PREFER512  // timing variant (tools/build_variant.sh): 512-thread rows from V > 2048
+  KLF_LAUNCH(4, 512)
+#endif
   KLF_LAUNCH(8, 256)
   KLF_LAUNCH(16, 256)
   KLF_LAUNCH(1, 512)

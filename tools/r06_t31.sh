@@ -1,0 +1,8 @@
+#!/bin/bash
+# fused KL with fewer VALU per element: KL tests, timing alone
+set -o pipefail
+cd "$(dirname "$0")/.."
+export PYTHONPATH=$PWD:$PWD/fddm-asr_amd:$PWD/tests
+timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_models.py -x -q -k "kl" --timeout 120 --timeout-method thread > gpurun_out/r06_t31_k.log 2>&1 || exit 1
+timeout -k 10 120 python -u tools/kl_time.py > gpurun_out/r06_t31_kl.txt 2>&1 || exit 1
+echo done
