@@ -546,8 +546,11 @@ __global__ void __launch_bounds__(256, ATTN_FWD_WPS) fwd2_kernel(AttnArgs a) {
 // reads; each tile waits for its own pieces with a counted vmcnt (every wave issues exactly 4 DMA instructions per
 // tile — past the end the last tile is re-read into a free stage — and no other vector-memory instruction in the
 // loop), then a barrier; the stage of tile t-1 is refilled after it. WavLM attention 56.5 -> 52 us at C2.
+#ifndef FWD5_WPS
+#define FWD5_WPS 2  // waves per SIMD the NG = 2 build's register allocation targets (timing variants: 3, 4)
+#endif
 template <bool MASK, int NST = 2, int NG = 2>
-__global__ void __launch_bounds__(256, NG == 1 ? 4 : 2) fwd5_kernel(AttnArgs a) {
+__global__ void __launch_bounds__(256, NG == 1 ? 4 : FWD5_WPS) fwd5_kernel(AttnArgs a) {
   constexpr int QW = 64 * NG, TB = 64 * 128, RB = 128;
   constexpr bool DROP = false, REL = true;
   extern __shared__ __attribute__((aligned(16))) unsigned char sm5[];
