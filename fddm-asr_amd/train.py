@@ -284,7 +284,7 @@ def train_one_epoch(encoder, decoder, s_proj, t_embed, t_proj, scheduler, loader
     pbar = loader
     if tqdm is not None and print_epoch_summary:
         pbar = tqdm(loader, desc=f"Epoch {epoch} [train]", leave=False)
-    losses = []     # the steps' device losses, summed once at the end (no add launch per step)
+    loss_sum = torch.zeros((), device=device)   # accumulated per step: a replayed graph's loss is a static buffer
     nsteps = 0
     aux = [p for m in (s_proj, t_embed, t_proj) for p in m.parameters() if p.requires_grad]
     if (arena is not None and getattr(optimizer, "aux_arena", 1) is None and aux and
@@ -360,7 +360,7 @@ def train_one_epoch(encoder, decoder, s_proj, t_embed, t_proj, scheduler, loader
                                step_args)
         else:
             loss, loss_diff, loss_fd = step(c, c_mask, x0, t, xt, fd)
-        losses.append(loss.detach())
+        loss_sum += loss.detach()
         nsteps += 1
         if tqdm is not None and print_epoch_summary and (global_step % log_every == 0):
             post = {"step": global_step, "loss": f"{float(loss):.3f}", "diff": f"{float(loss_diff):.3f}"}
@@ -370,7 +370,7 @@ def train_one_epoch(encoder, decoder, s_proj, t_embed, t_proj, scheduler, loader
         global_step += 1
     global LAST_ENQUEUE_DONE
     LAST_ENQUEUE_DONE = time.perf_counter()     # host finished enqueueing the epoch (bench.py: host-bound check)
-    avg = float(torch.stack(losses).sum()) / max(1, nsteps) if losses else 0.0
+    avg = float(loss_sum) / max(1, nsteps)
     if print_epoch_summary:
         logging.info(f"[Summary] Epoch {epoch} Avg Train Loss: {avg:.4f}")
     return global_step, avg
