@@ -47,17 +47,38 @@ struct DmArgs {
 };
 
 // One workgroup per (b, h, site): the site's three 4096-entry draw tables in LDS (one splitmix64 per 4 entries, as
-// dbits_kernel), then each wave takes 32-query groups; per group and key tile, lane l draws the 4 keys 64 t + 32 kb + 8 m
-// + 4 (l >> 5) + 0..3 of query 32 qg + (l & 31) from one 8-byte entry of each table, and the wave's compare of draw e
-// IS the word of slot 16 kb + 4 m + e (a ballot), gathered into lane j by v_writelane and stored as 256 B.
+// dbits_kernel), each followed by a copy of its first 64 entries so that a tile's 64 keys never wrap; then each wave
+// takes 32-query groups. Per group and key tile, lane l draws the 4 keys 64 t + 32 kb + 8 m + 4 (l >> 5) + 0..3 of query
+// 32 qg + (l & 31) from one 8-byte entry of each table (one base address per table and tile, the rest immediate
+// offsets), and builds its layout-v5 dword directly: the 32 compares are taken in the order of falling bit position
+// (lb_bit), each one shifted in as the carry of lw + lw (v_cmp + v_addc per draw). The lane-mask words (layout v3) are
+// the transpose of those dwords over each 32-lane half: a 32 x 32 bit transpose in five lane-exchange / rotate / bfi
+// stages leaves in lane j of half h the keep bits of lanes 32 h .. 32 h + 31 for bit position j, i.e. one 32-bit half
+// of the word of the slot whose bit is j, stored straight to it (the partner moves by DPP / v_permlane16_swap). Per tile and wave ~100 VALU instead of the ~230 of a
+// ballot + two v_writelane per draw.
+__device__ __forceinline__ int lb_slot(int j) {  // the slot 16 kb + r whose layout-v5 bit position is j (lb_bit^-1)
+  const int odd = j >> 4, P = odd ? 31 - j : 15 - j;
+  return 16 * (P >> 3) + 2 * (P & 7) + odd;
+}
+constexpr int DM_TABW = ATTN_R / 4 + 16;  // 8-byte words per table: 4096 entries + the first 64 again
+typedef unsigned dm_u32x2 __attribute__((ext_vector_type(2)));
+template <int OFF>
+__device__ __forceinline__ dm_u32x2 lds_read64_at(unsigned a) {  // not tracked by hipcc: the caller waits lgkmcnt
+  dm_u32x2 v;
+  asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(v) : "v"(a), "n"(OFF));
+  return v;
+}
+
 __global__ void __launch_bounds__(256) dmask_kernel(DmArgs d) {
-  __shared__ __attribute__((aligned(16))) uint64_t tab[3 * ATTN_R / 4];
+  __shared__ __attribute__((aligned(16))) uint64_t tab[3 * DM_TABW];
   const int bh = blockIdx.x, site = blockIdx.y, tid = threadIdx.x;
   const uint64_t stream = d.stream0 + (uint64_t)site * d.stream_step;
   const uint64_t seed = eff_seed(d.seed, d.seed_off);
   for (int wi = tid; wi < 3 * ATTN_R / 4; wi += 256) {
     const int tau = wi / (ATTN_R / 4), jw = wi % (ATTN_R / 4);
-    tab[wi] = mix64(seed, stream, ATTN_TAB0 + ((uint64_t)bh * 3 + tau) * (ATTN_R / 4) + jw);
+    const uint64_t v = mix64(seed, stream, ATTN_TAB0 + ((uint64_t)bh * 3 + tau) * (ATTN_R / 4) + jw);
+    tab[tau * DM_TABW + jw] = v;
+    if (jw < 16) tab[tau * DM_TABW + ATTN_R / 4 + jw] = v;
   }
   __syncthreads();
   const int ntiles = (d.Lk + 63) >> 6, nqg = (d.Lq + 31) >> 5;
@@ -65,32 +86,74 @@ __global__ void __launch_bounds__(256) dmask_kernel(DmArgs d) {
   uint64_t* out = d.out + (long)site * d.site_words;
   const unsigned char* tb = (const unsigned char*)tab;
   unsigned* lbits = (unsigned*)(out + (long)d.BH * nqg * ntiles * 32);  // the per-lane dwords after the lane masks
+  // transpose stage constants: stage s pairs lane l with l ^ s; the lane's partner word rotated right by rot[i] and
+  // merged under msk[i] (kept bits of its own word)
+  unsigned rot[5], msk[5];
+  static_for<0, 5>([&](auto ic) {
+    constexpr int i = decltype(ic)::value, s = 16 >> i;
+    constexpr unsigned ms = i == 0 ? 0x0000FFFFu : i == 1 ? 0x00FF00FFu : i == 2 ? 0x0F0F0F0Fu : i == 3 ? 0x33333333u
+                                                                                                        : 0x55555555u;
+    const bool up = (lane & s) != 0;
+    rot[i] = up ? s : 32 - s;
+    msk[i] = up ? ~ms : ms;
+  });
+  const int wslot = 2 * lb_slot(qi) + hh;  // the dword of the lane-mask words this lane stores
+  const unsigned thm1 = ((d.thr16 - 1) & 0xFFFFu) * 0x00010001u;  // both u16 halves thr16 - 1: keep iff draw > it
   for (int qg = w; qg < nqg; qg += 4) {
     const uint64_t off = mix64(seed, stream, ATTN_OFF0 + (uint64_t)bh * d.Lq + 32 * qg + qi);
     const unsigned o0 = (unsigned)(off & 0xFFCu), o1 = (unsigned)((off >> 16) & 0xFFCu),
                    o2 = (unsigned)((off >> 32) & 0xFFCu);
     for (int t = 0; t < ntiles; ++t) {
-      unsigned lo = 0, hi = 0, lw = 0;
-      static_for<0, 2>([&](auto kbc) {
-        constexpr int kb = decltype(kbc)::value;
-        static_for<0, 4>([&](auto mc) {
-          constexpr int m = decltype(mc)::value;
-          const unsigned kq = 64 * t + 32 * kb + 8 * m + 4 * hh;
-          const uint64_t wd = *(const uint64_t*)(tb + (((o0 + kq) & (ATTN_R - 1)) << 1)) ^
-                              *(const uint64_t*)(tb + ATTN_R * 2 + (((o1 + kq) & (ATTN_R - 1)) << 1)) ^
-                              *(const uint64_t*)(tb + ATTN_R * 4 + (((o2 + kq) & (ATTN_R - 1)) << 1));
-          static_for<0, 4>([&](auto ec) {
-            constexpr int e = decltype(ec)::value;
-            const bool keep = ((unsigned)(wd >> (16 * e)) & 0xFFFFu) >= d.thr16;
-            const unsigned long long bm = __ballot(keep);
-            writelane<16 * kb + 4 * m + e>(lo, (unsigned)bm);
-            writelane<16 * kb + 4 * m + e>(hi, (unsigned)(bm >> 32));
-            lw |= (keep ? 1u : 0u) << lb_bit(kb, 4 * m + e);
-          });
-        });
+      const unsigned kq = 64 * t + 4 * hh;
+      // the tile's 24 table reads as single ds_read_b64 by hand: hipcc pairs them into ds_read2_b64, which the LDS
+      // serves at half the rate with 32-bank conflict groups (MI355X_MICROARCH.md, LDS table) -- on these random
+      // gathers the bank conflicts, not the VALU, bound the kernel
+      const unsigned tl = lds_addr(tb);
+      const unsigned a0 = tl + (((o0 + kq) & (ATTN_R - 1)) << 1);
+      const unsigned a1 = tl + DM_TABW * 8 + (((o1 + kq) & (ATTN_R - 1)) << 1);
+      const unsigned a2 = tl + DM_TABW * 16 + (((o2 + kq) & (ATTN_R - 1)) << 1);
+      dm_u32x2 rd[3][8];  // [table][4 kb + m]
+      static_for<0, 8>([&](auto jc) {
+        constexpr int j = decltype(jc)::value, ob = 64 * (j >> 2) + 16 * (j & 3);
+        rd[0][j] = lds_read64_at<ob>(a0);
+        rd[1][j] = lds_read64_at<ob>(a1);
+        rd[2][j] = lds_read64_at<ob>(a2);
       });
-      if (lane < 32) out[lm_word(bh, nqg, ntiles, qg, t) + lane] = ((uint64_t)hi << 32) | lo;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(rd[0][j]), "+v"(rd[1][j]), "+v"(rd[2][j]));
+      // dword h of the (kb, m) entry holds the draws of registers r = 4 m + 2 h (low half) and r + 1 (high half): score
+      // pair p = 8 kb + 2 m + h, whose bits are 15 - p and 31 - p. Saturating u16 subtract of thr - 1 and a min with 1
+      // (two packed ops) leave keep as 0 / 1 in bits 0 and 16; shifted left by 15 - p they are the pair's two bits.
+      unsigned lw = 0;
+      static_for<0, 16>([&](auto ic) {
+        constexpr int i = decltype(ic)::value, j = i >> 1, h = i & 1, p = 8 * (j >> 2) + 2 * (j & 3) + h;
+        unsigned k;  // as packed VALU by hand (hipcc turns the builtins into two compares and selects)
+        asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96\n\tv_pk_sub_u16 %0, %0, %4 clamp\n\tv_pk_min_u16 %0, %0, %5"
+            : "=&v"(k)
+            : "v"(rd[0][j][h]), "v"(rd[1][j][h]), "v"(rd[2][j][h]), "s"(thm1), "s"(0x00010001u));
+        lw |= k << (15 - p);
+      });
+      if (d.thr16 == 0) lw = 0xFFFFFFFFu;  // p < 2^-17: every score kept
       lbits[lb_dword(bh, nqg, ntiles, qg, t) + lane] = lw;
+      unsigned x = lw;
+      static_for<0, 5>([&](auto ic) {
+        constexpr int i = decltype(ic)::value, s = 16 >> i;
+        unsigned y;  // x of lane l ^ s: cross-lane moves on the VALU (no LDS round trip in the chain)
+        if constexpr (s == 16) {
+          const auto sw = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+          y = (lane & 16) ? sw[0] : sw[1];
+        } else if constexpr (s == 8) {
+          y = (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0x128, 0xF, 0xF, false);  // row_ror:8
+        } else if constexpr (s == 4) {  // lanes with bit 2 clear read l + 4 (row_ror:12), the others l - 4 (row_ror:4)
+          y = (unsigned)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x12C, 0xF, 0x5, false);
+          y = (unsigned)__builtin_amdgcn_update_dpp((int)y, (int)x, 0x124, 0xF, 0xA, false);
+        } else {
+          y = (unsigned)__builtin_amdgcn_mov_dpp((int)x, s == 2 ? 0x4E : 0xB1, 0xF, 0xF, false);  // quad_perm
+        }
+        x = (msk[i] & x) | (~msk[i] & __builtin_rotateright32(y, rot[i]));
+      });
+      ((unsigned*)(out + lm_word(bh, nqg, ntiles, qg, t)))[wslot] = x;
     }
   }
 }
