@@ -2392,7 +2392,8 @@ __global__ void __launch_bounds__(1024, 1) bwd3s_kernel(AttnArgs a) {
 }
 
 // Kernel choice per launch shape (bf16; the fp32 parity mode runs the generic kernels):
-//  forward  WavLM gated rel-pos bias: fwd5 (streamed ring, bias slice staged; gate from a precomputed row, from the
+//  forward  WavLM gated rel-pos bias, Lk <= 1024: fwd7 with the bias (attn7.hip REL, round 6); longer, or under
+//           fddm_attn_set_kernels(1 / 5): fwd5 (streamed ring, bias slice staged; gate from a precomputed row, from the
 //           projection's extra columns, or from the attention input); decoder, Lk <= 1024: fwd8 (attn8.hip, two
 //           32-query chains per wave on 32x32x16 MFMAs; keep bits from the producer); Lk > 1024: fwd2.
 //  backward decoder, recorded bits or no dropout: Lq <= 256 and Lk <= 512: bwdf7 (attn7.hip, one fused launch per
@@ -2400,7 +2401,8 @@ __global__ void __launch_bounds__(1024, 1) bwd3s_kernel(AttnArgs a) {
 //           dq2 + dkv2. Under fddm_attn_set_kernels(1) the round-4 kernels: bwd3s (Lq == Lk <= 256), dq4 + dkv4.
 // fddm_attn_set_kernels (tests / tools only): 1 selects the round-4 16x16x32 kernels (fwd6 / dq4 / dkv4 / bwd3s)
 // where the 32x32x16 family (attn7.hip) would run; 0 (default) the 32x32x16 family with the two-chain forward fwd8
-// (attn8.hip); 2 the same without the fused backward (dq7 + dkv7 at every Lk); 3 the default with fwd7 as the forward
+// (attn8.hip); 2 the same without the fused backward (dq7 + dkv7 at every Lk); 3 the default with fwd7 as the forward;
+// 4 fwd8 at every decoder shape; 5 the default with WavLM's biased attention on fwd5 instead of fwd7 (REL)
 static int g_attn_v6 = 0;
 #ifndef A7_FUSED_MAXLQ
 #define A7_FUSED_MAXLQ 256  // fused backward up to this many queries, one or two key passes (more: one workgroup per
@@ -2431,6 +2433,9 @@ static int run(int which, AttnArgs& a, hipStream_t s) {
       const int LkP = (a.Lk + 63) / 64 * 64;
       if (rel) {
         if (drop) return (int)hipErrorInvalidValue;    // WavLM attention has no dropout in the frozen encoder
+        // round 6: fwd7 with the bias (attn7.hip REL) where the keys fit its key-mask staging; fwd5 under the round-4
+        // kernel selection (fddm_attn_set_kernels(1)) and for longer key ranges
+        if (attn7_enabled() && a.Lk <= 1024 && g_attn_v6 != 5) return attn7_fwd(a, s);
         const size_t lds5 = (size_t)2 * 2 * 64 * 128 + (size_t)LkP * 4 + (size_t)(LkP + 128) * 4;
         dim3 grid5((a.Lq + 127) / 128, a.B * a.H);
         if (mask) hipLaunchKernelGGL((fwd5_kernel<true, 2, 2>), grid5, dim3(256), lds5, s, a);
@@ -2584,7 +2589,7 @@ FDDM_API int fddm_attn_stamps_clear() {
 
 FDDM_API int fddm_attn_set_kernels(int v6) {
   const int old = g_attn_v6;
-  g_attn_v6 = (v6 >= 1 && v6 <= 4) ? v6 : 0;
+  g_attn_v6 = (v6 >= 1 && v6 <= 5) ? v6 : 0;
   return old;
 }
 

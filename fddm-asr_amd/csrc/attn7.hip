@@ -170,19 +170,31 @@ long attn7_drop_words(int B, int H, int Lq, int Lk) {  // lane masks + per-lane 
 
 // DM: 0 no dropout, 1 keep bits from the words fddm_attn_drop_bits wrote (word (bh, t, q), bit = key - 64 t).
 // MK: 0 no mask, 1 the ragged last tile only (Lk % 64 != 0, no key-padding mask), 2 key-padding mask on every tile.
+// REL: WavLM's gated relative-position bias (HF modeling_wavlm.py:474-513, 569-596; round 6, replacing fwd5 of
+// attention.hip): score += gate(q) * table[h][k - q + Lk - 1], added in log2 units (g2 = gate log2 e) to the score
+// accumulators before the softmax. The workgroup's slice of the table row (keys 0 .. LkP + 127 relative to its 128
+// queries) is staged in LDS as two copies shifted by 0 / 1 entries, so that a lane's 4 consecutive keys of an
+// accumulator quad are two aligned ds_read_b64 (copy jq & 1 of lane offset jq = qbase + 127 - q); copies are
+// LkP + 160 floats apart (= 128 B mod 256), which spreads a 32-lane read group over all 64 banks, and the workgroup
+// fits 40 KB of LDS (no keep-bit stage without dropout): four workgroups per CU (four copies and ds_read_b128: three,
+// 46-47 us at the C2 encoder shape). The gate per query
+// comes from a precomputed row, from the Q|K|V projection's 8 extra columns, or from the attention input x through
+// the folded GRU weights (lanes l and l ^ 32 each take 32 of the head's 64 inputs).
 #ifndef A7_FWD_WPS
 #define A7_FWD_WPS 3  // waves per SIMD the forward's register allocation targets
 #endif
-template <int DM, int MK>
+template <int DM, int MK, bool REL = false>
 __global__ void __launch_bounds__(256, A7_FWD_WPS) fwd7_kernel(AttnArgs a) {
   constexpr bool DROP = DM != 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char sm7[];
   const int ntiles = (a.Lk + 63) >> 6, LkP = ntiles * 64;
   unsigned char* kst = sm7;                             // [2][64 rows][128 B] K, KC swizzle
   unsigned char* vst = sm7 + 2 * A7_TB;                 // [2][64 rows][128 B] V, vsw swizzle
+  constexpr int KBL = DROP ? 2048 : 0;                   // the keep-bit stage only with dropout (REL: 4 WGs per CU)
   unsigned* kbl = (unsigned*)(sm7 + 4 * A7_TB);         // [2][4 waves][64 lanes] keep bits of the tile (v4 dwords)
-  unsigned* tact = (unsigned*)(sm7 + 4 * A7_TB + 2048);  // [4] active-tile nibbles per wave (MK 2)
-  unsigned* mpk = (unsigned*)(sm7 + 4 * A7_TB + 2064);   // [LkP] bf16 pair (1, mask): the key's fifth-k-step operand
+  unsigned* tact = (unsigned*)(sm7 + 4 * A7_TB + KBL);   // [4] active-tile nibbles per wave (MK 2)
+  unsigned* mpk = (unsigned*)(sm7 + 4 * A7_TB + KBL + 16);  // [LkP] bf16 pair (1, mask): the key's fifth-k-step operand
+  float* bcp = (float*)(sm7 + 4 * A7_TB + KBL + 16 + LkP * 4);  // REL: [2][LkP + 160] bias slices shifted by 0 / 1
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hh = lane >> 5, qi = lane & 31;
   int bxi, bh;
@@ -227,6 +239,58 @@ __global__ void __launch_bounds__(256, A7_FWD_WPS) fwd7_kernel(AttnArgs a) {
       const uint4 x = *(const uint4*)(Qb + qc * a.sq + 16 * ks + 8 * hh);
       qf[ks] = scale_frag(make_uint4(x.x & zm, x.y & zm, x.z & zm, x.w & zm), sl2);
     }
+  }
+  float g2 = 0.f;  // REL: the query's gate in log2 units
+  int boff = 0;    // REL: the lane's float offset of its bias quads in the shifted copies (key offset 0)
+  if constexpr (REL) {
+    float gate = 0.f;
+    if (a.gate) {
+      gate = qv ? a.gate[(long)bh * a.Lq + q] : 0.f;
+    } else if (a.graw) {  // gate from the 8 pre-activations the Q|K|V projection appended (HF modeling_wavlm.py:177-186)
+      const long qc = min(q, a.Lq - 1);
+      const uint4 u = *(const uint4*)((const bf16_t*)a.graw + ((long)b * a.Lq + qc) * a.sgr + h * 8);
+      const float ra = __uint_as_float(u.x << 16) + __uint_as_float(u.x & 0xFFFF0000u) + __uint_as_float(u.y << 16) +
+                       __uint_as_float(u.y & 0xFFFF0000u);
+      const float rb = __uint_as_float(u.z << 16) + __uint_as_float(u.z & 0xFFFF0000u) + __uint_as_float(u.w << 16) +
+                       __uint_as_float(u.w & 0xFFFF0000u);
+      const float ga = 1.f / (1.f + __expf(-ra)), gb = 1.f / (1.f + __expf(-rb));
+      gate = ga * (gb * a.gconst[h] - 1.f) + 2.f;
+    } else {  // gate from the attention input x through the folded GRU weights: lane half hh takes inputs 32 hh ..
+      const long qc = min(q, a.Lq - 1);
+      const bf16_t* xr = (const bf16_t*)a.gx + ((long)b * a.Lq + qc) * a.sgx + h * DH + 32 * hh;
+      const float4* wa = (const float4*)(a.gw + 32 * hh);
+      const float4* wb = (const float4*)(a.gw + 64 + 32 * hh);
+      float sa = 0.f, sb = 0.f;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const uint4 xv = *(const uint4*)(xr + 8 * c);
+        const unsigned xs[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const float4 A = wa[2 * c + j], Bw = wb[2 * c + j];
+          const float e0 = __uint_as_float(xs[2 * j] << 16), e1 = __uint_as_float(xs[2 * j] & 0xFFFF0000u);
+          const float e2 = __uint_as_float(xs[2 * j + 1] << 16), e3 = __uint_as_float(xs[2 * j + 1] & 0xFFFF0000u);
+          sa = fmaf(e0, A.x, fmaf(e1, A.y, fmaf(e2, A.z, fmaf(e3, A.w, sa))));
+          sb = fmaf(e0, Bw.x, fmaf(e1, Bw.y, fmaf(e2, Bw.z, fmaf(e3, Bw.w, sb))));
+        }
+      }
+      sa = xsum32(sa) + a.gw[128];
+      sb = xsum32(sb) + a.gw[129];
+      const float ga = 1.f / (1.f + __expf(-sa)), gb = 1.f / (1.f + __expf(-sb));
+      gate = qv ? ga * (gb * a.gconst[h] - 1.f) + 2.f : 0.f;
+    }
+    g2 = gate * 1.4426950408889634f;
+    // copy c, entry i = table[h][off0 + i + c], off0 = (Lk - 1) - (qbase + 127); zero outside the row
+    const int CL = LkP + 160, qbase = bxi * 128;
+    const float* tabh = a.table + (long)h * (2 * a.Lk - 1);
+    const long off0 = (long)(a.Lk - 1) - (qbase + 127);
+    for (int i = tid; i < 2 * CL; i += 256) {
+      const int c = i >= CL ? 1 : 0;
+      const long ti = off0 + (i - c * CL) + c;
+      bcp[i] = (ti >= 0 && ti < 2L * a.Lk - 1) ? tabh[ti] : 0.f;
+    }
+    const int jq = qbase + 127 - q;  // key k of this query sits at slice entry k + jq
+    boff = (jq & 1) * CL + (jq & ~1) + 4 * hh;
   }
   unsigned tmask = ntiles >= 32 ? 0xFFFFFFFFu : ((1u << ntiles) - 1u);
   if constexpr (MK != 0) {
@@ -295,12 +359,27 @@ __global__ void __launch_bounds__(256, A7_FWD_WPS) fwd7_kernel(AttnArgs a) {
       f32x16_t sc = mfma32(k5, q5, f32x16_t{});
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) sc = mfma32(*(const uint4*)(kimg + koff[ks] + kb * 32 * 128), qf[ks], sc);
+      if constexpr (REL) {  // + g2 * bias: register r is key 32 kb + 8 (r >> 2) + 4 hh + (r & 3) of tile t
+        const float* bp = bcp + boff + 64 * t + 32 * kb;
+#pragma unroll
+        for (int rq = 0; rq < 4; ++rq) {  // as packed FMAs (v_pk_fma_f32 on register pairs)
+          const f32x2_t b01 = *(const f32x2_t*)(bp + 8 * rq), b23 = *(const f32x2_t*)(bp + 8 * rq + 2);
+          const f32x4_t bv = {b01[0], b01[1], b23[0], b23[1]};
+#pragma unroll
+          for (int e = 0; e < 4; e += 2) {
+            const f32x2_t r2 = __builtin_elementwise_fma(f32x2_t{g2, g2}, f32x2_t{bv[e], bv[e + 1]},
+                                                         f32x2_t{sc[4 * rq + e], sc[4 * rq + e + 1]});
+            sc[4 * rq + e] = r2[0];
+            sc[4 * rq + e + 1] = r2[1];
+          }
+        }
+      }
       // exponentials 2^(sc - d), the lane's row sum (before dropout), the keep-mask select and the bf16 pack into
       // the PV operands bq[s]
       uint4 bq[2];
       float ls;
       auto expall = [&](float d) {
-        float la = 0.f, lb = 0.f;
+        f32x2_t lab = {0.f, 0.f};  // the two partial row sums as one packed add per pair
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
           unsigned bw[4];
@@ -309,8 +388,7 @@ __global__ void __launch_bounds__(256, A7_FWD_WPS) fwd7_kernel(AttnArgs a) {
             const int r = 8 * s + 2 * jj;
             float x = __builtin_amdgcn_exp2f(sc[r] - d);
             float y = __builtin_amdgcn_exp2f(sc[r + 1] - d);
-            la += x;
-            lb += y;
+            lab += f32x2_t{x, y};
             if constexpr (DROP) {  // keep bit lb_bit(kb, r) of the lane's dword as an AND mask (v_bfe_i32)
               x = __uint_as_float(__float_as_uint(x) & (unsigned)__builtin_amdgcn_sbfe((int)kw, lb_bit(kb, r), 1));
               y = __uint_as_float(__float_as_uint(y) & (unsigned)__builtin_amdgcn_sbfe((int)kw, lb_bit(kb, r + 1), 1));
@@ -319,7 +397,7 @@ __global__ void __launch_bounds__(256, A7_FWD_WPS) fwd7_kernel(AttnArgs a) {
           }
           bq[s] = make_uint4(bw[0], bw[1], bw[2], bw[3]);
         }
-        ls = la + lb;
+        ls = lab[0] + lab[1];
       };
       // fast path: 2^sc against the current reference; slow path (a query block's first half-tile, or a lane sum
       // above 2^8 / inf / NaN): the half's maximum, a new bf16 reference, O and l rescaled, 2^(sc - (rf' - rf))
@@ -1118,11 +1196,17 @@ int attn7_fwd(AttnArgs& a, hipStream_t s) {
   const int dm = a.thr16 == 0 ? 0 : 1;
   const int mk = a.key_keep != nullptr ? 2 : (a.Lk % 64) != 0 ? 1 : 0;
   const int ntiles = (a.Lk + 63) / 64;
-  const size_t lds = (size_t)4 * A7_TB + 2064 + (size_t)ntiles * 64 * 4;
+  const bool rel = a.table != nullptr;  // the caller checked a gate source (fddm_attn_fwd dispatch)
+  if (ntiles > 16 || (rel && dm)) return (int)hipErrorInvalidValue;  // LkP <= 1024; WavLM has no dropout
+  const size_t lds = (size_t)4 * A7_TB + (dm ? 2048 : 0) + 16 + (size_t)ntiles * 64 * 4 +
+                     (rel ? (size_t)2 * (ntiles * 64 + 160) * 4 : 0);
   dim3 grid((a.Lq + 127) / 128, a.B * a.H);
 #define FWD7(D, M) hipLaunchKernelGGL((fwd7_kernel<D, M>), grid, dim3(256), lds, s, a)
-  if (dm) { if (mk == 2) FWD7(1, 2); else if (mk == 1) FWD7(1, 1); else FWD7(1, 0); }
+#define FWD7R(M) hipLaunchKernelGGL((fwd7_kernel<0, M, true>), grid, dim3(256), lds, s, a)
+  if (rel) { if (mk == 2) FWD7R(2); else if (mk == 1) FWD7R(1); else FWD7R(0); }
+  else if (dm) { if (mk == 2) FWD7(1, 2); else if (mk == 1) FWD7(1, 1); else FWD7(1, 0); }
   else { if (mk == 2) FWD7(0, 2); else if (mk == 1) FWD7(0, 1); else FWD7(0, 0); }
+#undef FWD7R
 #undef FWD7
   return (int)hipGetLastError();
 }

@@ -82,10 +82,10 @@ def lib():
             f.restype = res
             f.argtypes = args
         _lib = L
-        # diagnostic A/B knob (tools/ab.sh): FDDM_ATTN_KERNELS = auto | v6 | nofused | fwd7 | fwd8 (ops.ATTN_KERNELS)
+        # diagnostic A/B knob (tools/ab.sh): FDDM_ATTN_KERNELS = auto | v6 | nofused | fwd7 | fwd8 | relfwd5 (ops.ATTN_KERNELS)
         ak = os.environ.get("FDDM_ATTN_KERNELS")
         if ak:
-            L.fddm_attn_set_kernels({"auto": 0, "v6": 1, "nofused": 2, "fwd7": 3, "fwd8": 4}[ak])
+            L.fddm_attn_set_kernels({"auto": 0, "v6": 1, "nofused": 2, "fwd7": 3, "fwd8": 4, "relfwd5": 5}[ak])
     return _lib
 
 

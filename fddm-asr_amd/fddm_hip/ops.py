@@ -105,16 +105,16 @@ def gemm_force_path(name: str) -> str:
     return {v: k for k, v in GEMM_PATHS.items()}[old]
 
 
-ATTN_KERNELS = {"auto": 0, "v6": 1, "nofused": 2, "fwd7": 3, "fwd8": 4}
+ATTN_KERNELS = {"auto": 0, "v6": 1, "nofused": 2, "fwd7": 3, "fwd8": 4, "relfwd5": 5}
 
 
 def attn_force_kernels(name: str) -> str:
     """Select the attention kernel family for every following launch (tests and diagnostics): "v6" = the
     16x16x32-MFMA kernels of attention.hip where the 32x32x16 family (attn7.hip) would run, "nofused" = the 32x32x16
     family without its fused backward (dq7 + dkv7 at every key length), "fwd7" = the default with the one-chain forward
-    fwd7 everywhere, "fwd8" = the default with the two-chain fwd8 (attn8.hip) everywhere, "auto" = the default choice
-    (fwd8 unless its 256-query workgroups load the busiest CU with more queries than fwd7's). Returns the previous
-    setting's name."""
+    fwd7 everywhere, "fwd8" = the default with the two-chain fwd8 (attn8.hip) everywhere, "relfwd5" = the default with
+    WavLM's biased attention on the round-2 fwd5 instead of fwd7's REL build, "auto" = the default choice (fwd8 unless
+    its 256-query workgroups load the busiest CU with more queries than fwd7's). Returns the previous setting's name."""
     from ._lib import lib
     old = lib().fddm_attn_set_kernels(ATTN_KERNELS[name])
     return {v: k for k, v in ATTN_KERNELS.items()}[old]

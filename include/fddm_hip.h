@@ -239,8 +239,10 @@ int fddm_gemm_force_path(int path);
 /* ---- attention kernel-family override for tests and diagnostics: 1 = the 16x16x32-MFMA kernels (fwd6, dq4 / dkv4,
  *      bwd3s) wherever the 32x32x16-MFMA family (csrc/attn7.hip) would run, 2 = the 32x32x16 family without its fused
  *      backward (dq7 + dkv7 at every Lk), 3 = the default with every forward on the one-chain fwd7, 4 = the default
- *      with every forward on the two-chain fwd8 (csrc/attn8.hip), 0 = automatic (default: fwd8 unless its 256-query
- *      workgroups load the busiest CU with more queries than fwd7's 128-query ones). Returns the previous setting.
+ *      with every forward on the two-chain fwd8 (csrc/attn8.hip), 5 = the default with WavLM's gated relative-position
+ *      attention on the round-2 fwd5 instead of fwd7's bias build, 0 = automatic (default: fwd8 unless its 256-query
+ *      workgroups load the busiest CU with more queries than fwd7's 128-query ones; WavLM attention with Lk <= 1024 on
+ *      fwd7 with the bias). Returns the previous setting.
  *      Process-wide; the train step never sets it. */
 int fddm_attn_set_kernels(int v6);
 

@@ -653,6 +653,72 @@ def test_attention_relgate_x_matches_gate_kernel_path(S):
     close(out.float(), ref.transpose(1, 2).reshape(B * S, E), rtol=2e-2, what="relgate_x vs float64")
 
 
+@pytest.mark.parametrize("S,src,masked", [(499, "gate", False), (499, "graw", False), (499, "gx", False),
+                                          (70, "gx", False), (1000, "gate", False), (203, "gate", True)])
+def test_wavlm_attention_fwd7_bias_matches_fwd5_and_float64(S, src, masked):
+    """Round 6: WavLM's gated relative-position attention on fwd7's bias build (csrc/attn7.hip REL: the bias slice in
+    four shifted LDS copies, the gate from a precomputed row / the projection's 8 extra columns / the attention input)
+    against the round-2 fwd5 (fddm_attn_set_kernels(5)) and float64 torch on the same bf16 inputs, for each gate
+    source, a ragged key count (70, 203), two key passes past 512 (1000) and a key-padding mask."""
+    o = ops()
+    from models.wavlm import _fold_gate
+    B, H, E = 2, 12, 768
+    gen = torch.Generator(device=dev).manual_seed(43 + S)
+    x = torch.randn(B * S, E, device=dev, generator=gen).bfloat16()
+    qkv = (torch.randn(B * S, 3 * E, device=dev, generator=gen) * 1.5).bfloat16()
+    lin = torch.nn.Linear(64, 8).to(dev)
+    with torch.no_grad():
+        lin.weight.copy_(torch.randn(8, 64, device=dev, generator=gen) * 0.2)
+        lin.bias.copy_(torch.randn(8, device=dev, generator=gen) * 0.1)
+    cst = torch.rand(H, device=dev, generator=gen) + 0.5
+    table = torch.randn(H, 2 * S - 1, device=dev, generator=gen) * 2.0
+    keep = None
+    if masked:
+        keep = torch.ones(B, S, device=dev, dtype=torch.uint8)
+        keep[0, S - 37:] = 0
+        keep[1, :5] = 0
+    gate = o.wavlm_gate(x, lin.weight.detach(), lin.bias.detach(), cst, B, S, H)      # [B*H, S]
+    graw = torch.einsum("nhd,od->nho", x.float().view(B * S, H, 64), lin.weight.detach()) + lin.bias.detach()
+    buf = torch.zeros(B * S, 3 * E + 8 * H + 8, device=dev, dtype=torch.bfloat16)
+    buf[:, :3 * E] = qkv
+    buf[:, 3 * E:3 * E + 8 * H] = graw.reshape(B * S, 8 * H).bfloat16()
+
+    def run():
+        out = torch.empty(B * S, E, device=dev, dtype=torch.bfloat16)
+        if src == "gate":
+            o.attn_fwd(qkv, qkv[:, E:], qkv[:, 2 * E:], out, None, B, H, S, S, key_keep=keep, gate=gate, table=table)
+        elif src == "graw":
+            o.attn_fwd_relgate(buf, buf[:, E:], buf[:, 2 * E:], out, buf[:, 3 * E:], cst, table, B, H, S)
+        else:
+            o.attn_fwd_relgate_x(qkv, qkv[:, E:], qkv[:, 2 * E:], out, x, _fold_gate(lin), cst, table, B, H, S)
+        return out
+
+    new = run()
+    old_fam = o.attn_force_kernels("relfwd5")
+    try:
+        old = run()
+    finally:
+        o.attn_force_kernels(old_fam)
+    close(new.float(), old.float(), rtol=2e-2, what=f"fwd7 bias vs fwd5 ({src})")
+    if src == "graw":
+        r = buf[:, 3 * E:3 * E + 8 * H].double().view(B, S, H, 8)
+    else:
+        r = (torch.einsum("nhd,od->nho", x.double().view(B * S, H, 64), lin.weight.detach().double()) +
+             lin.bias.detach().double()).view(B, S, H, 8)
+    ga, gb = torch.sigmoid(r[..., :4].sum(-1)), torch.sigmoid(r[..., 4:].sum(-1))
+    gref = (ga * (gb * cst.double() - 1) + 2).permute(0, 2, 1)                      # [B, H, S]
+    if src == "gate":
+        gref = gate.double().view(B, H, S)
+    hv = lambda t: t.double().view(B, S, H, 64).transpose(1, 2)  # noqa: E731
+    q_, k_, v_ = hv(qkv[:, :E]), hv(qkv[:, E:2 * E]), hv(qkv[:, 2 * E:])
+    rel = torch.arange(S, device=dev)[None, :] - torch.arange(S, device=dev)[:, None] + S - 1   # key - query + S-1
+    sc = q_ @ k_.transpose(-1, -2) / 8.0 + gref[..., None] * table.double()[:, rel][None]
+    if keep is not None:
+        sc = sc.masked_fill(keep[:, None, None, :] == 0, float("-inf"))
+    ref = torch.softmax(sc, -1) @ v_
+    close(new.float(), ref.transpose(1, 2).reshape(B * S, E), rtol=2e-2, what=f"fwd7 bias vs float64 ({src})")
+
+
 # ----------------------------------------------------------------------------- LN / RoPE / embed
 @pytest.mark.parametrize("fold", [False, True])
 @pytest.mark.parametrize("film", [False, True])
