@@ -177,7 +177,8 @@ long attn7_drop_words(int B, int H, int Lq, int Lk) {  // lane masks + per-lane 
 // accumulator quad are two aligned ds_read_b64 (copy jq & 1 of lane offset jq = qbase + 127 - q); copies are
 // LkP + 160 floats apart (= 128 B mod 256), which spreads a 32-lane read group over all 64 banks, and the workgroup
 // fits 40 KB of LDS (no keep-bit stage without dropout): four workgroups per CU (four copies and ds_read_b128: three,
-// 46-47 us at the C2 encoder shape). The gate per query
+// 46-47 us at the C2 encoder shape; v_pk_fma_f32 / v_pk_add_f32 for the bias and the row sums measured 2-3 % slower than
+// scalar f32, here and in the decoder's fwd7, tools/r06_t48.sh). The gate per query
 // comes from a precomputed row, from the Q|K|V projection's 8 extra columns, or from the attention input x through
 // the folded GRU weights (lanes l and l ^ 32 each take 32 of the head's 64 inputs).
 #ifndef A7_FWD_WPS
@@ -362,16 +363,11 @@ __global__ void __launch_bounds__(256, A7_FWD_WPS) fwd7_kernel(AttnArgs a) {
       if constexpr (REL) {  // + g2 * bias: register r is key 32 kb + 8 (r >> 2) + 4 hh + (r & 3) of tile t
         const float* bp = bcp + boff + 64 * t + 32 * kb;
 #pragma unroll
-        for (int rq = 0; rq < 4; ++rq) {  // as packed FMAs (v_pk_fma_f32 on register pairs)
+        for (int rq = 0; rq < 4; ++rq) {  // scalar FMAs: v_pk_fma_f32 measured 2-3 % slower
           const f32x2_t b01 = *(const f32x2_t*)(bp + 8 * rq), b23 = *(const f32x2_t*)(bp + 8 * rq + 2);
           const f32x4_t bv = {b01[0], b01[1], b23[0], b23[1]};
 #pragma unroll
-          for (int e = 0; e < 4; e += 2) {
-            const f32x2_t r2 = __builtin_elementwise_fma(f32x2_t{g2, g2}, f32x2_t{bv[e], bv[e + 1]},
-                                                         f32x2_t{sc[4 * rq + e], sc[4 * rq + e + 1]});
-            sc[4 * rq + e] = r2[0];
-            sc[4 * rq + e + 1] = r2[1];
-          }
+          for (int e = 0; e < 4; ++e) sc[4 * rq + e] = fmaf(g2, bv[e], sc[4 * rq + e]);
         }
       }
       // exponentials 2^(sc - d), the lane's row sum (before dropout), the keep-mask select and the bf16 pack into
@@ -379,7 +375,7 @@ __global__ void __launch_bounds__(256, A7_FWD_WPS) fwd7_kernel(AttnArgs a) {
       uint4 bq[2];
       float ls;
       auto expall = [&](float d) {
-        f32x2_t lab = {0.f, 0.f};  // the two partial row sums as one packed add per pair
+        float la = 0.f, lb = 0.f;
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
           unsigned bw[4];
@@ -388,7 +384,8 @@ __global__ void __launch_bounds__(256, A7_FWD_WPS) fwd7_kernel(AttnArgs a) {
             const int r = 8 * s + 2 * jj;
             float x = __builtin_amdgcn_exp2f(sc[r] - d);
             float y = __builtin_amdgcn_exp2f(sc[r + 1] - d);
-            lab += f32x2_t{x, y};
+            la += x;
+            lb += y;
             if constexpr (DROP) {  // keep bit lb_bit(kb, r) of the lane's dword as an AND mask (v_bfe_i32)
               x = __uint_as_float(__float_as_uint(x) & (unsigned)__builtin_amdgcn_sbfe((int)kw, lb_bit(kb, r), 1));
               y = __uint_as_float(__float_as_uint(y) & (unsigned)__builtin_amdgcn_sbfe((int)kw, lb_bit(kb, r + 1), 1));
@@ -397,7 +394,7 @@ __global__ void __launch_bounds__(256, A7_FWD_WPS) fwd7_kernel(AttnArgs a) {
           }
           bq[s] = make_uint4(bw[0], bw[1], bw[2], bw[3]);
         }
-        ls = lab[0] + lab[1];
+        ls = la + lb;
       };
       // fast path: 2^sc against the current reference; slow path (a query block's first half-tile, or a lane sum
       // above 2^8 / inf / NaN): the half's maximum, a new bf16 reference, O and l rescaled, 2^(sc - (rf' - rf))
