@@ -48,14 +48,16 @@ struct DmArgs {
 
 // One workgroup per (b, h, site): the site's three 4096-entry draw tables in LDS (one splitmix64 per 4 entries, as
 // dbits_kernel), each followed by a copy of its first 64 entries so that a tile's 64 keys never wrap; then each wave
-// takes 32-query groups. Per group and key tile, lane l draws the 4 keys 64 t + 32 kb + 8 m + 4 (l >> 5) + 0..3 of query
-// 32 qg + (l & 31) from one 8-byte entry of each table (one base address per table and tile, the rest immediate
-// offsets), and builds its layout-v5 dword directly: the 32 compares are taken in the order of falling bit position
-// (lb_bit), each one shifted in as the carry of lw + lw (v_cmp + v_addc per draw). The lane-mask words (layout v3) are
-// the transpose of those dwords over each 32-lane half: a 32 x 32 bit transpose in five lane-exchange / rotate / bfi
-// stages leaves in lane j of half h the keep bits of lanes 32 h .. 32 h + 31 for bit position j, i.e. one 32-bit half
-// of the word of the slot whose bit is j, stored straight to it (the partner moves by DPP / v_permlane16_swap). Per tile and wave ~100 VALU instead of the ~230 of a
-// ballot + two v_writelane per draw.
+// takes 32-query groups. Per group and key tile, lane l draws the 4 keys 64 t + 32 kb + 8 m + 4 (l >> 5) + 0..3 of
+// query 32 qg + (l & 31) from one 8-byte entry of each table (one base address per table and tile, the rest immediate
+// offsets; single ds_read_b64, see below) and builds its layout-v5 dword directly: per dword of draws one XOR of the
+// three tables (v_bitop3), a saturating packed u16 subtract of thr - 1 and a packed min with 1 (keep as 0 / 1 in bits
+// 0 and 16), shifted to the pair's bits. The lane-mask words (layout v3) are the transpose of those dwords over each
+// 32-lane half: a 32 x 32 bit transpose in five lane-exchange (DPP / v_permlane16_swap) / rotate / bit-select stages
+// leaves in lane j of half h the keep bits of lanes 32 h .. 32 h + 31 for bit position j, i.e. one 32-bit half of the
+// word of the slot whose bit is j, stored straight to it. Per tile and wave ~106 VALU and 24 LDS gathers instead of
+// ~230 VALU (a ballot and two v_writelane per draw); the random gathers' bank conflicts bound it
+// (profiles/r06i_dmask.md).
 __device__ __forceinline__ int lb_slot(int j) {  // the slot 16 kb + r whose layout-v5 bit position is j (lb_bit^-1)
   const int odd = j >> 4, P = odd ? 31 - j : 15 - j;
   return 16 * (P >> 3) + 2 * (P & 7) + odd;
