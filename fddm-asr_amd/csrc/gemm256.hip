@@ -269,27 +269,27 @@ __global__ void __launch_bounds__(512) gemm256_kernel(GemmArgs g) {
   // x0 / x1 hold row fr of column group 0 / 1; after the exchange (lane bit 0 <-> register) x0 holds the even
   // and x1 the odd rows of the block, lane bit 0 selecting the column group. Lanes fr and fr ^ 1 trade through
   // DPP quad_perm [1,0,3,2].
+  // (each select reads its partner's register through DPP: hipcc folds the quad_perm into the v_cndmask, two VALU per
+  // dword instead of a select, a DPP move and two selects)
   auto xchg1 = [&](u32x4_t& x0, u32x4_t& x1) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const unsigned y = odd_r ? x0[e] : x1[e];
-      const unsigned z = (unsigned)__builtin_amdgcn_mov_dpp((int)y, 0xb1, 0xf, 0xf, false);
-      x0[e] = odd_r ? z : x0[e];
-      x1[e] = odd_r ? x1[e] : z;
+      const unsigned a = x0[e], b = x1[e];
+      const unsigned pb = (unsigned)__builtin_amdgcn_mov_dpp((int)b, 0xb1, 0xf, 0xf, false);  // x1 of lane ^ 1
+      const unsigned pa = (unsigned)__builtin_amdgcn_mov_dpp((int)a, 0xb1, 0xf, 0xf, false);  // x0 of lane ^ 1
+      x0[e] = odd_r ? pb : a;
+      x1[e] = odd_r ? b : pa;
     }
   };
   // bf16: the two lanes 16 apart (fg, fg^1) trade packed halves (v_permlane16_swap) so that each lane holds 8
-  // consecutive columns (16 B) of a 32-column pair; odd-fg lanes hold the second block of the pair
-  const bool odd = fg & 1;
+  // consecutive columns (16 B) of a 32-column pair; odd-fg lanes hold the second block of the pair.
+  // v_permlane16_swap(pa, pb) swaps the odd 16-lane rows of pa with the even rows of pb: an even-row lane keeps its pa
+  // and gets the pa of lane + 16 in pb's place, an odd-row lane gets the pb of lane - 16 in pa's place and keeps its pb
+  // — exactly {pa, pa'} / {pb', pb}, no lane-parity selects
   auto chunk16 = [&](const f32x4_t& a, const f32x4_t& b) -> u32x4_t {
-    const u32x2_t pa = {pk_bf16(a[0], a[1]), pk_bf16(a[2], a[3])};
-    const u32x2_t pb = {pk_bf16(b[0], b[1]), pk_bf16(b[2], b[3])};
-    const u32x2_t x = odd ? pa : pb;
-    // v_permlane16_swap(x, x): odd 16-lane rows get x of lane-16 in [0], even rows x of lane+16 in [1]
-    const auto s0 = __builtin_amdgcn_permlane16_swap(x[0], x[0], false, false);
-    const auto s1 = __builtin_amdgcn_permlane16_swap(x[1], x[1], false, false);
-    const u32x2_t y = odd ? u32x2_t{s0[0], s1[0]} : u32x2_t{s0[1], s1[1]};
-    return odd ? u32x4_t{y[0], y[1], pb[0], pb[1]} : u32x4_t{pa[0], pa[1], y[0], y[1]};
+    const auto s0 = __builtin_amdgcn_permlane16_swap(pk_bf16(a[0], a[1]), pk_bf16(b[0], b[1]), false, false);
+    const auto s1 = __builtin_amdgcn_permlane16_swap(pk_bf16(a[2], a[3]), pk_bf16(b[2], b[3]), false, false);
+    return u32x4_t{s0[0], s1[0], s0[1], s1[1]};
   };
   // one bf16 row block (4 column blocks v) -> 2 whole-line stores
   auto emit_bf16 = [&](const f32x4_t (&v)[4], const i32x4_t& r, int so) {
