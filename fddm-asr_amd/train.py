@@ -226,9 +226,9 @@ def _step_graph_ok(device, scaler, optimizer, arena) -> bool:
 
     Refused under DEBUG_HIP_FORCE_GRAPH_QUEUES=0: round 4's A/B arm that differed from its neighbours only by that
     setting died with SIGFPE (gpurun_out/ab_g.log: bash reports `Floating point exception` for bench.py; its stderr
-    holds no Python traceback, so the signal came from native code). SIGFPE on x86 is an integer divide by zero;
-    the HIP runtime spreads a graph's launches over the number of queues that knob forces, so zero queues makes that
-    count a divisor. The cause is the runtime's knob, not this code; the arm is gone from
+    holds no Python traceback, so the signal came from native code). Hypothesis, not verified: SIGFPE on x86 is an
+    integer divide by zero, and if the HIP runtime spreads a graph's launches over the number of queues that knob
+    forces, zero queues would make that count a divisor. Either way the arm is gone from
     tools/ab_graph.sh and this check keeps the graph path off under that setting."""
     if os.environ.get("DEBUG_HIP_FORCE_GRAPH_QUEUES", None) == "0":
         return False
