@@ -363,13 +363,26 @@ __global__ void __launch_bounds__(256, A7_FWD_WPS) fwd7_kernel(AttnArgs a) {
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) sc = mfma32(*(const uint4*)(kimg + koff[ks] + kb * 32 * 128), qf[ks], sc);
       if constexpr (REL) {  // + g2 * bias: register r is key 32 kb + 8 (r >> 2) + 4 hh + (r & 3) of tile t
-        const float* bp = bcp + boff + 64 * t + 32 * kb;
+        // the 8 bias pairs as single ds_read_b64 by hand: hipcc pairs them into ds_read2_b64 (16-lane groups over 32
+        // banks, where the two shifted copies collide), the same trap as the keep-bit producer's gathers
+        const unsigned bl = lds_addr(bcp) + 4u * (unsigned)(boff + 64 * t + 32 * kb);
+        dm_u32x2 bw[8];
+        bw[0] = lds_read64_at<0>(bl);
+        bw[1] = lds_read64_at<8>(bl);
+        bw[2] = lds_read64_at<32>(bl);
+        bw[3] = lds_read64_at<40>(bl);
+        bw[4] = lds_read64_at<64>(bl);
+        bw[5] = lds_read64_at<72>(bl);
+        bw[6] = lds_read64_at<96>(bl);
+        bw[7] = lds_read64_at<104>(bl);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(bw[j]));
 #pragma unroll
         for (int rq = 0; rq < 4; ++rq) {  // scalar FMAs: v_pk_fma_f32 measured 2-3 % slower
-          const f32x2_t b01 = *(const f32x2_t*)(bp + 8 * rq), b23 = *(const f32x2_t*)(bp + 8 * rq + 2);
-          const f32x4_t bv = {b01[0], b01[1], b23[0], b23[1]};
 #pragma unroll
-          for (int e = 0; e < 4; ++e) sc[4 * rq + e] = fmaf(g2, bv[e], sc[4 * rq + e]);
+          for (int e = 0; e < 4; ++e)
+            sc[4 * rq + e] = fmaf(g2, __uint_as_float(bw[2 * rq + (e >> 1)][e & 1]), sc[4 * rq + e]);
         }
       }
       // exponentials 2^(sc - d), the lane's row sum (before dropout), the keep-mask select and the bf16 pack into
