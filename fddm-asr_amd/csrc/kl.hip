@@ -8,6 +8,7 @@
 //                         one write). Closed form: SURVEY §8(a) "KL closed form".
 //  * fddm_softmax_rows / fddm_softmax_bwd_rows — TextEmbedding (models/projection.py:41-47).
 #include "common.h"
+#include <type_traits>
 #include <cstdlib>
 
 namespace fddm {
@@ -168,18 +169,44 @@ __global__ void __launch_bounds__(256) kl_kernel(const float* __restrict__ logit
   }
 }
 
+// Lane partner of all-reduce step S (0..5) on the VALU instead of a ds_bpermute per step (__shfl_xor): quad_perm
+// [1,0,3,2] and [2,3,0,1], then row_half_mirror (quad <-> quad within 8 lanes) and row_mirror (8 <-> 8 within 16),
+// which pair whole groups once every lane of a group holds the same value, then v_permlane16_swap / 32_swap.
+template <int S>
+__device__ __forceinline__ float xpartner(float v) {
+  const int u = __float_as_int(v);
+  if constexpr (S == 0) return __int_as_float(__builtin_amdgcn_mov_dpp(u, 0xB1, 0xF, 0xF, false));
+  else if constexpr (S == 1) return __int_as_float(__builtin_amdgcn_mov_dpp(u, 0x4E, 0xF, 0xF, false));
+  else if constexpr (S == 2) return __int_as_float(__builtin_amdgcn_mov_dpp(u, 0x141, 0xF, 0xF, false));
+  else if constexpr (S == 3) return __int_as_float(__builtin_amdgcn_mov_dpp(u, 0x140, 0xF, 0xF, false));
+  else if constexpr (S == 4) {
+    const auto r = __builtin_amdgcn_permlane16_swap((unsigned)u, (unsigned)u, false, false);
+    return __uint_as_float((threadIdx.x & 16) ? r[0] : r[1]);
+  } else {
+    const auto r = __builtin_amdgcn_permlane32_swap((unsigned)u, (unsigned)u, false, false);
+    return __uint_as_float((threadIdx.x & 32) ? r[0] : r[1]);
+  }
+}
+template <int B, int E, typename F>
+__device__ __forceinline__ void kl_static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    kl_static_for<B + 1, E>(f);
+  }
+}
+
 // Vectorised variant for V % 4 == 0 (the train step: V = 8000): 16-B loads, 8-B (bf16) / 16-B (f32) stores, the
 // row max and sum in one block reduction (per-thread max, exp relative to it, rescaled once the row max is
 // known), and the two backward sums in one. NV = float4 chunks per thread (V <= 1024 * NV).
 __device__ __forceinline__ float2 block_maxsum(float m, float s, float* red) {
   // combine (m, s) pairs: m = max, s = sum of exp(v - m)
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float mo = __shfl_xor(m, o, 64), so = __shfl_xor(s, o, 64);
+  kl_static_for<0, 6>([&](auto sc) {
+    constexpr int S = decltype(sc)::value;
+    const float mo = xpartner<S>(m), so = xpartner<S>(s);
     const float mn = fmaxf(m, mo);
     s = (mn == -INFINITY) ? 0.f : s * __expf(m - mn) + so * __expf(mo - mn);
     m = mn;
-  }
+  });
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
   __syncthreads();
   if (lane == 0) { red[2 * w] = m; red[2 * w + 1] = s; }
@@ -191,11 +218,11 @@ __device__ __forceinline__ float2 block_maxsum(float m, float s, float* red) {
   return make_float2(M, S);
 }
 __device__ __forceinline__ float2 block_sum2(float a, float b, float* red) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    a += __shfl_xor(a, o, 64);
-    b += __shfl_xor(b, o, 64);
-  }
+  kl_static_for<0, 6>([&](auto sc) {
+    constexpr int S = decltype(sc)::value;
+    a += xpartner<S>(a);
+    b += xpartner<S>(b);
+  });
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
   __syncthreads();
   if (lane == 0) { red[2 * w] = a; red[2 * w + 1] = b; }
@@ -353,13 +380,13 @@ __global__ void __launch_bounds__(NT) kl4_kernel(const float* __restrict__ logit
 // (the train step: loss = kl + ...). 393 MB of HBM per step at V = 8000, B*L = 8192 (f32 in, bf16 out) instead of
 // 262 + 393 MB for the separate forward and backward passes.
 __device__ __forceinline__ float4 block_sum4(float a, float b, float c, float d, float* red) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    a += __shfl_xor(a, o, 64);
-    b += __shfl_xor(b, o, 64);
-    c += __shfl_xor(c, o, 64);
-    d += __shfl_xor(d, o, 64);
-  }
+  kl_static_for<0, 6>([&](auto sc) {
+    constexpr int S = decltype(sc)::value;
+    a += xpartner<S>(a);
+    b += xpartner<S>(b);
+    c += xpartner<S>(c);
+    d += xpartner<S>(d);
+  });
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
   __syncthreads();
   if (lane == 0) { red[4 * w] = a; red[4 * w + 1] = b; red[4 * w + 2] = c; red[4 * w + 3] = d; }
